@@ -1,0 +1,83 @@
+"""ctypes binding of libkwmatch.so (include/kwmatch.h).
+
+The library is built in-tree (``advanced_scrapper_amd/lib/``) by
+``advanced_scrapper_amd.build`` / ``__graft_entry__.build()``.  There is no
+fallback: if the library is missing or fails to load, every GPU entry point
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib')
+LIB_PATH = os.path.join(LIB_DIR, 'libkwmatch.so')
+
+KW_OK = 0
+KW_EINVAL = -1
+KW_EUNSUPPORTED = -2
+KW_EHIP = -3
+KW_EOVERFLOW = -4
+KW_ESTATE = -5
+KW_NOPOS = 0xFFFFFFFF
+
+HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('field', '<u4')])
+
+# every symbol include/kwmatch.h declares
+EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
+           'kw_last_error', 'kw_destroy')
+
+
+class KwError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libkwmatch error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libkwmatch.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.kw_compile.argtypes = [vp, vp, vp, i32, vp, vp, vp, i32, ctypes.POINTER(vp)]
+    L.kw_compile.restype = ctypes.c_int
+    L.kw_scan.argtypes = [vp, vp, vp, i64, vp]
+    L.kw_scan.restype = ctypes.c_int
+    L.kw_hits.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(vp)]
+    L.kw_hits.restype = ctypes.c_int
+    L.kw_hits_copy.argtypes = [vp, vp, i64, ctypes.POINTER(i64), vp]
+    L.kw_hits_copy.restype = ctypes.c_int
+    L.kw_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.kw_stats.restype = ctypes.c_int
+    L.kw_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    L.kw_last_kernel_ms.restype = ctypes.c_int
+    L.kw_last_error.argtypes = [vp]
+    L.kw_last_error.restype = ctypes.c_char_p
+    L.kw_destroy.argtypes = [vp]
+    L.kw_destroy.restype = ctypes.c_int
+    _LIB = L
+    return L
+
+
+def check(rc: int, handle=None) -> None:
+    if rc != KW_OK:
+        msg = lib().kw_last_error(handle)
+        raise KwError(rc, msg.decode('utf-8', 'replace') if msg else '')
+
+
+def ptr(a) -> ctypes.c_void_p:
+    """Raw pointer of a numpy array or torch tensor."""
+    if a is None:
+        return ctypes.c_void_p(0)
+    if isinstance(a, np.ndarray):
+        return ctypes.c_void_p(a.ctypes.data)
+    return ctypes.c_void_p(a.data_ptr())

@@ -1,0 +1,61 @@
+"""Build the in-tree native libraries (no JIT cache, nothing pip-installed).
+
+* ``lib/libkwmatch.so`` — HIP kernels + C-ABI, ``hipcc --offload-arch=gfx950``
+* ``lib/libsynth.so``   — host C corpus generator (bench/test data)
+
+Run ``python -m advanced_scrapper_amd.build``.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+LIB = os.path.join(HERE, 'lib')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = os.environ.get('KW_OFFLOAD_ARCH', 'gfx950')
+
+
+def _run(cmd):
+    print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def build_kwmatch(force: bool = False) -> str:
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, 'libkwmatch.so')
+    srcs = [os.path.join(CSRC, f) for f in ('kwmatch.hip', 'kwmatch_kernels.hpp', 'kwmatch_device.hpp',
+                                             'dedup.hip')]
+    srcs.append(os.path.join(HERE, '..', 'include', 'kwmatch.h'))
+    srcs = [s for s in srcs if os.path.exists(s)]
+    if force or _stale(out, srcs):
+        units = [s for s in srcs if s.endswith('.hip')]
+        _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',
+              '-o', out] + units)
+    return out
+
+
+def build_synth(force: bool = False) -> str:
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, 'libsynth.so')
+    src = os.path.join(CSRC, 'synth.c')
+    if force or _stale(out, [src]):
+        _run(['gcc', '-O2', '-fopenmp', '-fPIC', '-shared', '-Wall', '-o', out, src])
+    return out
+
+
+def build_all(force: bool = False):
+    return build_kwmatch(force), build_synth(force)
+
+
+if __name__ == '__main__':
+    build_all(force='--force' in sys.argv)

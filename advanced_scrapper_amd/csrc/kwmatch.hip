@@ -1,0 +1,620 @@
+// libkwmatch: host side of the C-ABI declared in include/kwmatch.h.
+//
+// kw_compile turns the active names of the knowledge base into the device
+// tables the scan kernel walks (anchor strings and their uses, the LDS filter,
+// the global anchor hash table, bit-parallel match vectors, regex atom
+// programs, the short-field substring table).  kw_scan launches the fused
+// scan/resolve kernel plus a two-kernel compaction of the per-wave result
+// regions.  Reference: match_keywords.py:148-192 (the loops this replaces).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "kwmatch_kernels.hpp"
+
+using namespace kw;
+
+struct kw_handle {
+    int device = 0;
+    DevTables T{};
+    void *d_tables = nullptr;
+    size_t tables_bytes = 0;
+    // scratch
+    int n_waves = 0;
+    uint32_t out_cap = 0;
+    DevScratch S{};
+    void *d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    void *d_small = nullptr;       // status, stats, out_cnt, offsets
+    unsigned long long *d_offs = nullptr;
+    kw_hit *d_hits = nullptr;
+    size_t hits_cap = 0;
+    // last scan
+    const uint8_t *arena = nullptr;
+    const int64_t *doc_off = nullptr;
+    int64_t n_docs = 0;
+    hipStream_t stream = nullptr;
+    bool scanned = false;
+    bool fetched = false;
+    int64_t n_hits = 0;
+    unsigned long long stats[3] = {0, 0, 0};
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    int cus = 256;
+    int blocks_per_cu = 2;
+    std::string err;
+    int n_pat = 0;
+    int launched_waves = 0;
+};
+
+static thread_local std::string g_err;
+
+#define HIPCHK(h, x)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            (h)->err = std::string("HIP error ") + hipGetErrorString(e_) + " at " #x; \
+            return KW_EHIP;                                                            \
+        }                                                                              \
+    } while (0)
+
+// ------------------------------------------------------------------ host tables
+namespace {
+
+bool utf8_decode(const uint8_t *s, size_t n, std::vector<uint32_t> &out)
+{
+    out.clear();
+    size_t i = 0;
+    while (i < n) {
+        uint32_t b = s[i];
+        uint32_t len, cp;
+        if (b < 0x80) { len = 1; cp = b; }
+        else if ((b & 0xE0) == 0xC0) { len = 2; cp = b & 0x1F; }
+        else if ((b & 0xF0) == 0xE0) { len = 3; cp = b & 0x0F; }
+        else if ((b & 0xF8) == 0xF0) { len = 4; cp = b & 0x07; }
+        else return false;
+        if (i + len > n) return false;
+        for (uint32_t k = 1; k < len; ++k) {
+            if ((s[i + k] & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (s[i + k] & 0x3F);
+        }
+        out.push_back(cp);
+        i += len;
+    }
+    return true;
+}
+
+size_t utf8_offset(const std::vector<uint32_t> &cps, size_t upto)
+{
+    size_t b = 0;
+    for (size_t i = 0; i < upto; ++i) b += cps[i] < 0x80 ? 1 : cps[i] < 0x800 ? 2 : cps[i] < 0x10000 ? 3 : 4;
+    return b;
+}
+
+uint32_t kfull_h(uint32_t m)
+{
+    uint32_t k = 0;
+    while (20u * (k + 1) < m) ++k;
+    return k;
+}
+
+// largest indel distance any window of the partial_ratio family may have and
+// still pass 20*d < m+|W|: full windows d = 2k, edge
+// windows |W| = m-1 give floor((2m-2)/20).
+uint32_t dmax_h(uint32_t m)
+{
+    uint32_t a = 2 * kfull_h(m);
+    uint32_t b = m >= 1 ? (2 * m - 2) / 20 : 0;
+    return a > b ? a : b;
+}
+
+bool is_word_h(const uint32_t *bits, uint32_t c)
+{
+    if (c >= 0x110000u) return false;
+    return (bits[c >> 5] >> (c & 31)) & 1u;
+}
+
+template <class T>
+size_t push_array(std::vector<uint8_t> &blob, const std::vector<T> &v)
+{
+    size_t off = (blob.size() + 255) & ~size_t(255);
+    blob.resize(off + v.size() * sizeof(T) + 16);
+    if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+}  // namespace
+
+extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, const uint8_t *pat_class, int32_t n_pat,
+                          const int32_t *rx_atoms, const int64_t *rx_off, const uint32_t *word_bitmap, int32_t device,
+                          kw_handle **out)
+{
+    if (!out) return KW_EINVAL;
+    *out = nullptr;
+    kw_handle *h = new kw_handle();
+    auto fail = [&](int code, const std::string &msg) {
+        g_err = msg;
+        h->err = msg;
+        *out = h;   // caller can read kw_last_error, then kw_destroy
+        return code;
+    };
+    if (n_pat < 0 || (n_pat > 0 && (!pat_bytes || !pat_off || !pat_class)) || !word_bitmap)
+        return fail(KW_EINVAL, "kw_compile: null argument");
+    if (n_pat >= (1 << 20)) return fail(KW_EUNSUPPORTED, "kw_compile: more than 2^20 patterns");
+    h->device = device;
+    h->n_pat = n_pat;
+
+    // ---- patterns
+    std::vector<std::vector<uint32_t>> cps(n_pat);
+    std::vector<uint32_t> pat_info(n_pat), pat_cp_off(n_pat + 1), pat_cps;
+    int f_first = n_pat, empty_pat = -1;
+    int prev_m = 1 << 30;
+    for (int i = 0; i < n_pat; ++i) {
+        const uint8_t *s = pat_bytes + pat_off[i];
+        size_t bl = (size_t)(pat_off[i + 1] - pat_off[i]);
+        if (!utf8_decode(s, bl, cps[i])) return fail(KW_EINVAL, "kw_compile: pattern " + std::to_string(i) + " is not valid UTF-8");
+        uint32_t m = (uint32_t)cps[i].size();
+        const bool fuzzy = pat_class[i] == KW_CLASS_FUZZY;
+        if (!fuzzy && pat_class[i] != KW_CLASS_UPPER) return fail(KW_EINVAL, "kw_compile: bad class of pattern " + std::to_string(i));
+        if (fuzzy) {
+            if (f_first == n_pat) f_first = i;
+            if ((int)m > prev_m) return fail(KW_EINVAL, "kw_compile: fuzzy patterns must be sorted by length, longest first");
+            prev_m = (int)m;
+            if (m > (uint32_t)MAXM)
+                return fail(KW_EUNSUPPORTED, "kw_compile: fuzzy name longer than 64 code points (rapidfuzz long-needle path is not restated)");
+            if (bl == 1) return fail(KW_EUNSUPPORTED, "kw_compile: one-byte fuzzy names are not supported");
+            if (m == 0) empty_pat = i;
+        } else {
+            if (f_first != n_pat) return fail(KW_EINVAL, "kw_compile: uppercase patterns must precede fuzzy ones");
+            if (m < 2) return fail(KW_EINVAL, "kw_compile: uppercase names have at least 2 code points");
+            if (m > 255) return fail(KW_EUNSUPPORTED, "kw_compile: uppercase name longer than 255 code points");
+        }
+        if (bl > 65535) return fail(KW_EUNSUPPORTED, "kw_compile: name longer than 65535 bytes");
+        uint32_t pi = (fuzzy ? PI_FUZZY : 0u) | (m << 8) | ((uint32_t)bl << 16);
+        if (!fuzzy) {
+            if (is_word_h(word_bitmap, cps[i].front())) pi |= PI_WORD_FIRST;
+            if (is_word_h(word_bitmap, cps[i].back())) pi |= PI_WORD_LAST;
+        }
+        pat_info[i] = pi;
+        pat_cp_off[i] = (uint32_t)pat_cps.size();
+        pat_cps.insert(pat_cps.end(), cps[i].begin(), cps[i].end());
+    }
+    pat_cp_off[n_pat] = (uint32_t)pat_cps.size();
+
+    // ---- regex programs
+    std::vector<int4> atoms;
+    std::vector<uint32_t> rxo(n_pat + 1, 0);
+    for (int i = 0; i < n_pat; ++i) {
+        rxo[i] = (uint32_t)atoms.size();
+        const bool fuzzy = pat_info[i] & PI_FUZZY;
+        int64_t a0 = rx_off ? rx_off[i] : 0, a1 = rx_off ? rx_off[i + 1] : 0;
+        if (!fuzzy || a1 <= a0 || !rx_atoms) {
+            if (fuzzy) pat_info[i] |= PI_LITERAL;
+            continue;
+        }
+        int nq = 0, minsum = 0;
+        for (int64_t a = a0; a < a1; ++a) {
+            int4 t;
+            t.x = rx_atoms[4 * a]; t.y = rx_atoms[4 * a + 1]; t.z = rx_atoms[4 * a + 2]; t.w = rx_atoms[4 * a + 3];
+            if ((t.x != KW_RX_LIT && t.x != KW_RX_ANY) || t.z < 0 || (t.w >= 0 && t.w < t.z))
+                return fail(KW_EUNSUPPORTED, "kw_compile: bad regex atom in pattern " + std::to_string(i));
+            if (!(t.z == 1 && t.w == 1)) ++nq;
+            minsum += t.z;
+            atoms.push_back(t);
+        }
+        if (nq > RX_MAX_QUANT) return fail(KW_EUNSUPPORTED, "kw_compile: too many quantified atoms in pattern " + std::to_string(i));
+        if (minsum == 0) return fail(KW_EUNSUPPORTED, "kw_compile: regex that can match the empty string in pattern " + std::to_string(i));
+    }
+    rxo[n_pat] = (uint32_t)atoms.size();
+    if (atoms.empty()) atoms.push_back(int4{0, 0, 1, 1});
+
+    // ---- anchor strings and their uses
+    std::unordered_map<std::string, uint32_t> as_id;
+    std::vector<std::string> as_str;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> as_uses;   // (pat, info)
+    auto add_use = [&](const std::string &a, uint32_t pat, uint32_t info) {
+        auto it = as_id.find(a);
+        uint32_t id;
+        if (it == as_id.end()) {
+            id = (uint32_t)as_str.size();
+            as_id.emplace(a, id);
+            as_str.push_back(a);
+            as_uses.emplace_back();
+        } else {
+            id = it->second;
+        }
+        as_uses[id].emplace_back(pat, info);
+    };
+    for (int i = 0; i < n_pat; ++i) {
+        const std::string full((const char *)pat_bytes + pat_off[i], (size_t)(pat_off[i + 1] - pat_off[i]));
+        const uint32_t m = (uint32_t)cps[i].size();
+        if (!(pat_info[i] & PI_FUZZY)) {
+            add_use(full, (uint32_t)i, USE_UPPER | (m << 16));
+            continue;
+        }
+        if (m == 0) continue;
+        add_use(full, (uint32_t)i, USE_FULL | (m << 16));
+        uint32_t dm = dmax_h(m);
+        if (dm == 0) continue;
+        uint32_t K = dm + 1;
+        for (uint32_t k = 0; k < K; ++k) {
+            uint32_t b = (k * m) / K, e = ((k + 1) * m) / K;
+            size_t bb = utf8_offset(cps[i], b), be = utf8_offset(cps[i], e);
+            std::string piece = full.substr(bb, be - bb);
+            if (piece.size() < 2) return fail(KW_EUNSUPPORTED, "kw_compile: piece shorter than 2 bytes");
+            add_use(piece, (uint32_t)i, USE_PIECE | (b << 8) | ((e - b) << 16));
+        }
+    }
+    const uint32_t n_as = (uint32_t)as_str.size();
+    std::vector<uint64_t> as_head(n_as);
+    std::vector<uint32_t> as_off(n_as), as_len(n_as), as_use_begin(n_as), as_use_cnt(n_as), use_pat, use_info;
+    std::vector<uint8_t> as_bytes;
+    for (uint32_t a = 0; a < n_as; ++a) {
+        const std::string &s = as_str[a];
+        uint64_t hd = 0;
+        for (size_t k = 0; k < s.size() && k < 8; ++k) hd |= (uint64_t)(uint8_t)s[k] << (8 * k);
+        as_head[a] = hd;
+        as_off[a] = (uint32_t)as_bytes.size();
+        as_len[a] = (uint32_t)s.size();
+        as_bytes.insert(as_bytes.end(), s.begin(), s.end());
+        as_use_begin[a] = (uint32_t)use_pat.size();
+        as_use_cnt[a] = (uint32_t)as_uses[a].size();
+        for (auto &u : as_uses[a]) { use_pat.push_back(u.first); use_info.push_back(u.second); }
+    }
+    if (use_pat.size() > IT_USE_MASK) return fail(KW_EUNSUPPORTED, "kw_compile: more than 2^19 anchor uses");
+
+    // ---- 3-byte keys: LDS filter bits + global hash table key -> anchor list
+    std::map<uint32_t, std::vector<uint32_t>> key_anchors;
+    for (uint32_t a = 0; a < n_as; ++a) {
+        const std::string &s = as_str[a];
+        uint32_t b0 = (uint8_t)s[0], b1 = (uint8_t)s[1];
+        if (s.size() >= 3) {
+            key_anchors[b0 | (b1 << 8) | ((uint32_t)(uint8_t)s[2] << 16)].push_back(a);
+        } else {
+            for (uint32_t x = 0; x < 256; ++x) key_anchors[b0 | (b1 << 8) | (x << 16)].push_back(a);
+        }
+    }
+    std::vector<uint32_t> filt(FILT_WORDS, 0);
+    uint32_t ht_size = 1024;
+    while (ht_size < 2 * key_anchors.size()) ht_size <<= 1;
+    int ht_log = 0;
+    while ((1u << ht_log) < ht_size) ++ht_log;
+    std::vector<uint32_t> ht_key(ht_size, 0xFFFFFFFFu), ht_begin(ht_size, 0), ht_cnt(ht_size, 0), kl_anchor;
+    for (auto &kv : key_anchors) {
+        uint32_t key = kv.first;
+        uint32_t hb = (key * HASH_MUL) >> (32 - FILT_BITS);
+        filt[hb >> 5] |= 1u << (hb & 31);
+        uint32_t slot = (key * HASH_MUL) >> (32 - ht_log);
+        while (ht_key[slot] != 0xFFFFFFFFu) slot = (slot + 1) & (ht_size - 1);
+        ht_key[slot] = key;
+        ht_begin[slot] = (uint32_t)kl_anchor.size();
+        ht_cnt[slot] = (uint32_t)kv.second.size();
+        kl_anchor.insert(kl_anchor.end(), kv.second.begin(), kv.second.end());
+    }
+    if (kl_anchor.empty()) kl_anchor.push_back(0);
+
+    // ---- bit-parallel match vectors (needle = name)
+    std::vector<uint64_t> pm_ascii((size_t)std::max(n_pat, 1) * 128, 0);
+    std::vector<uint32_t> pm_ext_off(n_pat + 1, 0), pm_ext_cp;
+    std::vector<uint64_t> pm_ext_mask;
+    for (int i = 0; i < n_pat; ++i) {
+        pm_ext_off[i] = (uint32_t)pm_ext_cp.size();
+        if (!(pat_info[i] & PI_FUZZY)) continue;
+        const auto &c = cps[i];
+        size_t ext0 = pm_ext_cp.size();
+        for (size_t j = 0; j < c.size(); ++j) {
+            if (c[j] < 128) { pm_ascii[(size_t)i * 128 + c[j]] |= 1ull << j; continue; }
+            size_t k = ext0;
+            while (k < pm_ext_cp.size() && pm_ext_cp[k] != c[j]) ++k;
+            if (k == pm_ext_cp.size()) { pm_ext_cp.push_back(c[j]); pm_ext_mask.push_back(0); }
+            pm_ext_mask[k] |= 1ull << j;
+        }
+    }
+    pm_ext_off[n_pat] = (uint32_t)pm_ext_cp.size();
+    if (pm_ext_cp.empty()) { pm_ext_cp.push_back(0); pm_ext_mask.push_back(0); }
+
+    // ---- short fields: substrings (<= SHORT_EXACT_MAX code points) of fuzzy names
+    std::unordered_map<uint64_t, std::vector<uint32_t>> subs;
+    for (int i = f_first; i < n_pat; ++i) {
+        const auto &c = cps[i];
+        for (size_t s0 = 0; s0 < c.size(); ++s0) {
+            uint64_t hh = 0;
+            for (size_t l = 1; l <= (size_t)SHORT_EXACT_MAX && s0 + l <= c.size(); ++l) {
+                hh = hh * SUB_B + c[s0 + l - 1];
+                uint64_t key = (hh + (uint64_t)l * 0x9E3779B97F4A7C15ull) | 1ull;
+                auto &v = subs[key];
+                if (v.empty() || v.back() != (uint32_t)i) v.push_back((uint32_t)i);
+            }
+        }
+    }
+    uint32_t sub_size = 1024;
+    while (sub_size < 2 * subs.size()) sub_size <<= 1;
+    std::vector<uint64_t> sub_key(sub_size, 0);
+    std::vector<uint32_t> sub_begin(sub_size, 0), sub_cnt(sub_size, 0), sub_pat;
+    for (auto &kv : subs) {
+        uint32_t slot = (uint32_t)(kv.first >> 32) & (sub_size - 1);
+        while (sub_key[slot] != 0) slot = (slot + 1) & (sub_size - 1);
+        sub_key[slot] = kv.first;
+        sub_begin[slot] = (uint32_t)sub_pat.size();
+        sub_cnt[slot] = (uint32_t)kv.second.size();
+        sub_pat.insert(sub_pat.end(), kv.second.begin(), kv.second.end());
+    }
+    if (sub_pat.empty()) sub_pat.push_back(0);
+
+    std::vector<int32_t> f_count_ge(MAXM + 2, 0);
+    for (int n = 0; n <= MAXM + 1; ++n) {
+        int c = 0;
+        for (int i = f_first; i < n_pat; ++i) c += ((int)cps[i].size() >= n);
+        f_count_ge[n] = c;
+    }
+    std::vector<uint32_t> wb(word_bitmap, word_bitmap + 0x110000 / 32);
+    if (pat_info.empty()) pat_info.push_back(0);
+    if (pat_cps.empty()) pat_cps.push_back(0);
+    if (use_pat.empty()) { use_pat.push_back(0); use_info.push_back(0); }
+    if (as_head.empty()) { as_head.push_back(0); as_off.push_back(0); as_len.push_back(0); as_use_begin.push_back(0); as_use_cnt.push_back(0); }
+    if (as_bytes.empty()) as_bytes.push_back(0);
+
+    // ---- one device blob
+    std::vector<uint8_t> blob;
+    size_t o_filt = push_array(blob, filt), o_htk = push_array(blob, ht_key), o_htb = push_array(blob, ht_begin),
+           o_htc = push_array(blob, ht_cnt), o_kl = push_array(blob, kl_anchor), o_ash = push_array(blob, as_head),
+           o_aso = push_array(blob, as_off), o_asl = push_array(blob, as_len), o_asub = push_array(blob, as_use_begin),
+           o_asuc = push_array(blob, as_use_cnt), o_asb = push_array(blob, as_bytes), o_up = push_array(blob, use_pat),
+           o_ui = push_array(blob, use_info), o_pi = push_array(blob, pat_info), o_pco = push_array(blob, pat_cp_off),
+           o_pc = push_array(blob, pat_cps), o_pma = push_array(blob, pm_ascii), o_peo = push_array(blob, pm_ext_off),
+           o_pec = push_array(blob, pm_ext_cp), o_pem = push_array(blob, pm_ext_mask), o_rxo = push_array(blob, rxo),
+           o_rxa = push_array(blob, atoms), o_wb = push_array(blob, wb), o_fc = push_array(blob, f_count_ge),
+           o_sk = push_array(blob, sub_key), o_sb = push_array(blob, sub_begin), o_sc = push_array(blob, sub_cnt),
+           o_sp = push_array(blob, sub_pat);
+
+    HIPCHK(h, hipSetDevice(device));
+    HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
+    HIPCHK(h, hipMemcpy(h->d_tables, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    h->tables_bytes = blob.size();
+    uint8_t *B = (uint8_t *)h->d_tables;
+    DevTables &T = h->T;
+    T.filt = (const uint32_t *)(B + o_filt);
+    T.ht_key = (const uint32_t *)(B + o_htk);
+    T.ht_begin = (const uint32_t *)(B + o_htb);
+    T.ht_cnt = (const uint32_t *)(B + o_htc);
+    T.ht_mask = ht_size - 1;
+    T.ht_shift = 32 - ht_log;
+    T.kl_anchor = (const uint32_t *)(B + o_kl);
+    T.as_head = (const uint64_t *)(B + o_ash);
+    T.as_off = (const uint32_t *)(B + o_aso);
+    T.as_len = (const uint32_t *)(B + o_asl);
+    T.as_use_begin = (const uint32_t *)(B + o_asub);
+    T.as_use_cnt = (const uint32_t *)(B + o_asuc);
+    T.as_bytes = (const uint8_t *)(B + o_asb);
+    T.use_pat = (const uint32_t *)(B + o_up);
+    T.use_info = (const uint32_t *)(B + o_ui);
+    T.pat_info = (const uint32_t *)(B + o_pi);
+    T.pat_cp_off = (const uint32_t *)(B + o_pco);
+    T.pat_cps = (const uint32_t *)(B + o_pc);
+    T.pm_ascii = (const uint64_t *)(B + o_pma);
+    T.pm_ext_off = (const uint32_t *)(B + o_peo);
+    T.pm_ext_cp = (const uint32_t *)(B + o_pec);
+    T.pm_ext_mask = (const uint64_t *)(B + o_pem);
+    T.rx_off = (const uint32_t *)(B + o_rxo);
+    T.rx_atoms = (const int4 *)(B + o_rxa);
+    T.word_bits = (const uint32_t *)(B + o_wb);
+    T.f_count_ge = (const int32_t *)(B + o_fc);
+    T.sub_key = (const uint64_t *)(B + o_sk);
+    T.sub_begin = (const uint32_t *)(B + o_sb);
+    T.sub_cnt = (const uint32_t *)(B + o_sc);
+    T.sub_pat = (const uint32_t *)(B + o_sp);
+    T.sub_mask = sub_size - 1;
+    T.n_pat = n_pat;
+    T.f_first = f_first;
+    T.empty_pat = empty_pat;
+
+    hipDeviceProp_t prop;
+    HIPCHK(h, hipGetDeviceProperties(&prop, device));
+    h->cus = prop.multiProcessorCount;
+    int bpc = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_scan_kernel, BLOCK, kScanLds));
+    h->blocks_per_cu = bpc > 0 ? bpc : 1;
+    HIPCHK(h, hipEventCreate(&h->ev0));
+    HIPCHK(h, hipEventCreate(&h->ev1));
+    HIPCHK(h, hipEventCreate(&h->ev2));
+    *out = h;
+    return KW_OK;
+}
+
+// (re)allocate scratch for n_waves waves with out_cap records per wave
+static int ensure_scratch(kw_handle *h, int n_waves, uint32_t out_cap)
+{
+    if (h->d_scratch && n_waves <= h->n_waves && out_cap <= h->out_cap) return KW_OK;
+    n_waves = std::max(n_waves, h->n_waves);
+    out_cap = std::max(out_cap, h->out_cap);
+    if (h->d_scratch) { (void)hipFree(h->d_scratch); h->d_scratch = nullptr; }
+    if (h->d_small) { (void)hipFree(h->d_small); h->d_small = nullptr; }
+    if (h->d_hits) { (void)hipFree(h->d_hits); h->d_hits = nullptr; }
+    const size_t per_items = (size_t)2 * ITEM_CAP * sizeof(uint64_t);
+    const size_t per_cps = (size_t)CP_CAP * sizeof(uint32_t);
+    const size_t per_blk = (size_t)(CP_CAP / 16 + 2) * sizeof(uint32_t);
+    const size_t per_out = (size_t)out_cap * sizeof(kw_hit);
+    size_t total = (size_t)n_waves * (per_items + per_cps + per_blk + per_out) + 4096;
+    HIPCHK(h, hipMalloc(&h->d_scratch, total));
+    uint8_t *p = (uint8_t *)h->d_scratch;
+    h->S.items = (uint64_t *)p; p += (size_t)n_waves * per_items;
+    h->S.cps = (uint32_t *)p; p += (size_t)n_waves * per_cps;
+    h->S.blkcnt = (uint32_t *)p; p += (size_t)n_waves * per_blk;
+    p = (uint8_t *)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    h->S.out = (kw_hit *)p;
+    size_t small = 256 + (size_t)n_waves * 4 + 256 + (size_t)(n_waves + 1) * 8 + 256;
+    HIPCHK(h, hipMalloc(&h->d_small, small));
+    uint8_t *q = (uint8_t *)h->d_small;
+    h->S.status = (uint32_t *)q;                       // 4 x u32
+    h->S.stats = (unsigned long long *)(q + 64);       // 3 x u64
+    h->S.out_cnt = (uint32_t *)(q + 256);
+    h->d_offs = (unsigned long long *)(q + 256 + (((size_t)n_waves * 4 + 255) & ~(size_t)255));
+    h->S.out_cap = out_cap;
+    h->n_waves = n_waves;
+    h->out_cap = out_cap;
+    h->hits_cap = (size_t)n_waves * out_cap;
+    HIPCHK(h, hipMalloc(&h->d_hits, h->hits_cap * sizeof(kw_hit) + 16));
+    h->scratch_bytes = total;
+    return KW_OK;
+}
+
+static int launch_scan(kw_handle *h)
+{
+    hipStream_t st = h->stream;
+    int64_t n_docs = h->n_docs;
+    int n_blocks = (int)std::min<int64_t>((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK,
+                                          (int64_t)h->cus * h->blocks_per_cu);
+    if (n_blocks < 1) n_blocks = 1;
+    const int n_waves = n_blocks * WAVES_PER_BLOCK;
+    int64_t docs_per_wave = (n_docs + n_waves - 1) / n_waves;
+    uint32_t want_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_wave * 48), (int64_t)1 << 26);
+    int rc = ensure_scratch(h, n_waves, std::max(want_cap, h->out_cap));
+    if (rc) return rc;
+    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
+    HIPCHK(h, hipEventRecord(h->ev0, st));
+    if (n_docs > 0) {
+        hipLaunchKernelGGL(kw_scan_kernel, dim3(n_blocks), dim3(BLOCK), kScanLds, st, h->T, h->arena, h->doc_off,
+                           n_docs, h->S);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->ev1, st));
+    // compaction of the per-wave regions
+    if (n_docs > 0) {
+        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->S.out_cnt, n_waves, h->S.out_cap,
+                           h->d_offs);
+        hipLaunchKernelGGL(kw_gather_kernel, dim3(n_waves), dim3(256), 0, st, h->S.out, h->S.out_cap, h->S.out_cnt,
+                           h->d_offs, h->d_hits);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->ev2, st));
+    h->launched_waves = n_waves;
+    return KW_OK;
+}
+
+extern "C" int kw_scan(kw_handle *h, const uint8_t *d_arena, const int64_t *d_doc_off, int64_t n_docs, void *stream)
+{
+    if (!h) return KW_EINVAL;
+    if (n_docs < 0 || (n_docs > 0 && (!d_arena || !d_doc_off))) { h->err = "kw_scan: bad arguments"; return KW_EINVAL; }
+    if (((uintptr_t)d_arena & 15) != 0) { h->err = "kw_scan: arena must be 16-byte aligned"; return KW_EINVAL; }
+    HIPCHK(h, hipSetDevice(h->device));
+    h->arena = d_arena;
+    h->doc_off = d_doc_off;
+    h->n_docs = n_docs;
+    h->stream = (hipStream_t)stream;
+    h->scanned = true;
+    h->fetched = false;
+    return launch_scan(h);
+}
+
+static int finish(kw_handle *h)
+{
+    if (!h->scanned) { h->err = "kw_hits: no scan"; return KW_ESTATE; }
+    if (h->fetched) return KW_OK;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        uint32_t status[4];
+        HIPCHK(h, hipMemcpy(status, h->S.status, sizeof(status), hipMemcpyDeviceToHost));
+        if (h->n_docs == 0) { h->n_hits = 0; h->fetched = true; return KW_OK; }
+        if (status[0] & (ST_ITEM_OVERFLOW | ST_CP_OVERFLOW | ST_FIELD_TOO_LONG)) {
+            char buf[256];
+            snprintf(buf, sizeof(buf), "kw_scan: device work buffer overflow (status 0x%x: %s%s%s)", status[0],
+                     (status[0] & ST_ITEM_OVERFLOW) ? "more than 16384 anchor occurrences in one field; " : "",
+                     (status[0] & ST_CP_OVERFLOW) ? "non-ASCII field longer than 65536 code points; " : "",
+                     (status[0] & ST_FIELD_TOO_LONG) ? "field longer than 8 MiB; " : "");
+            h->err = buf;
+            return KW_EOVERFLOW;
+        }
+        if (status[0] & ST_OUT_OVERFLOW) {
+            // grow the per-wave result regions to the largest count seen and rescan
+            std::vector<uint32_t> cnt(h->launched_waves);
+            HIPCHK(h, hipMemcpy(cnt.data(), h->S.out_cnt, cnt.size() * 4, hipMemcpyDeviceToHost));
+            uint32_t mx = 0;
+            for (uint32_t c : cnt) mx = std::max(mx, c);
+            int rc = ensure_scratch(h, h->n_waves, mx + 1024);
+            if (rc) return rc;
+            rc = launch_scan(h);
+            if (rc) return rc;
+            continue;
+        }
+        unsigned long long tot = 0;
+        HIPCHK(h, hipMemcpy(&tot, h->d_offs + h->launched_waves, sizeof(tot), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(h->stats, h->S.stats, sizeof(h->stats), hipMemcpyDeviceToHost));
+        h->n_hits = (int64_t)tot;
+        h->fetched = true;
+        return KW_OK;
+    }
+    h->err = "kw_hits: result buffer kept overflowing";
+    return KW_EOVERFLOW;
+}
+
+extern "C" int kw_hits(kw_handle *h, int64_t *n_hits, const kw_hit **d_hits)
+{
+    if (!h || !n_hits || !d_hits) return KW_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = finish(h);
+    if (rc) return rc;
+    *n_hits = h->n_hits;
+    *d_hits = h->d_hits;
+    return KW_OK;
+}
+
+extern "C" int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void *stream)
+{
+    if (!h || !n_hits) return KW_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = finish(h);
+    if (rc) return rc;
+    *n_hits = h->n_hits;
+    if (h->n_hits > cap) { h->err = "kw_hits_copy: destination too small"; return KW_EINVAL; }
+    if (h->n_hits > 0)
+        HIPCHK(h, hipMemcpyAsync(d_dst, h->d_hits, (size_t)h->n_hits * sizeof(kw_hit), hipMemcpyDeviceToDevice,
+                                 (hipStream_t)stream));
+    return KW_OK;
+}
+
+extern "C" int kw_stats(kw_handle *h, int64_t *candidates, int64_t *anchor_hits, int64_t *windows)
+{
+    if (!h) return KW_EINVAL;
+    int rc = finish(h);
+    if (rc) return rc;
+    if (candidates) *candidates = (int64_t)h->stats[0];
+    if (anchor_hits) *anchor_hits = (int64_t)h->stats[1];
+    if (windows) *windows = (int64_t)h->stats[2];
+    return KW_OK;
+}
+
+extern "C" int kw_last_kernel_ms(kw_handle *h, float *scan_ms, float *total_ms)
+{
+    if (!h) return KW_EINVAL;
+    int rc = finish(h);
+    if (rc) return rc;
+    if (scan_ms) HIPCHK(h, hipEventElapsedTime(scan_ms, h->ev0, h->ev1));
+    if (total_ms) HIPCHK(h, hipEventElapsedTime(total_ms, h->ev0, h->ev2));
+    return KW_OK;
+}
+
+extern "C" const char *kw_last_error(kw_handle *h)
+{
+    if (!h) return g_err.c_str();
+    return h->err.c_str();
+}
+
+extern "C" int kw_destroy(kw_handle *h)
+{
+    if (!h) return KW_OK;
+    (void)hipSetDevice(h->device);
+    if (h->d_tables) (void)hipFree(h->d_tables);
+    if (h->d_scratch) (void)hipFree(h->d_scratch);
+    if (h->d_small) (void)hipFree(h->d_small);
+    if (h->d_hits) (void)hipFree(h->d_hits);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->ev2) (void)hipEventDestroy(h->ev2);
+    delete h;
+    return KW_OK;
+}

@@ -1,0 +1,194 @@
+"""Drop-in replacement of the reference's ``match_keywords.py`` (MI355X build).
+
+Same public functions, arguments, side effects and CSV schema as
+match_keywords.py:17-246 of lwowlwowl/advanced_scrapper:
+
+* ``is_within_period``, ``extract_time_periods``, ``process_json_data``,
+  ``read_and_process_json_files``   (re-exported from :mod:`.kb`)
+* ``append_to_csv(source_name, ticker, matched_names, article)``   :128-146
+* ``process_chunk(source_name, chunk, processed_data)``            :148-192
+* ``sort_matched_csv(file_path)``                                  :195-217
+* ``main()`` / ``python -m advanced_scrapper_amd.match_keywords``   :220-246
+
+What changes is where the per-article x per-name loop runs: ``process_chunk``
+packs the chunk's ``article_text``/``title`` strings into one byte arena, and
+the hand-written HIP kernels of libkwmatch compute every
+(article, field, name) result on the GPU.  The host then applies the period
+filter, builds the same ``ticker_matches`` dicts and appends the same rows.
+``process_chunk`` runs in-process (forking after HIP initialisation is
+unsafe), one call per chunk instead of one per CPU sub-chunk.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+from typing import Dict, List, Optional
+
+import pandas as pd
+from dateutil import parser
+
+from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
+                 process_json_data, read_and_process_json_files)
+from .matcher import GpuMatcher, assemble_ticker_matches, field_str, group_hits, pack_fields
+
+OUTPUT_COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source',
+                  'source_url', 'article_text')
+
+
+def _output_path(source_name, ticker):
+    return f'{source_name}_ticker_matched_articles/{ticker}_match.csv'
+
+
+def _csv_row(matched_names, article):
+    """One output row (match_keywords.py:131-144)."""
+    stamp = int(parser.parse(article['date_time']).timestamp())
+    return {
+        'time_unix': stamp,
+        'date_time': article['date_time'],
+        'text_matches': json.dumps(matched_names['text']),
+        'title_matches': json.dumps(matched_names['title']),
+        'title': article['title'],
+        'url': article['url'],
+        'source': article['source'],
+        'source_url': article['source_url'],
+        'article_text': article['article_text'],
+    }
+
+
+def append_to_csv(source_name, ticker, matched_names, article):
+    """Append one matched article to ``{source}_ticker_matched_articles/{ticker}_match.csv``."""
+    _append_rows(source_name, ticker, [_csv_row(matched_names, article)])
+
+
+def _append_rows(source_name, ticker, rows):
+    path = _output_path(source_name, ticker)
+    header = not os.path.exists(path)
+    pd.DataFrame(rows).to_csv(path, mode='a', index=False, header=header)
+
+
+# --------------------------------------------------------------------- matcher cache
+_MATCHERS: Dict[tuple, GpuMatcher] = {}
+
+
+def _kb_fingerprint(processed_data) -> str:
+    h = hashlib.sha1()
+    for ticker, attrs in processed_data.items():
+        h.update(repr(ticker).encode())
+        for attr, names in attrs.items():
+            h.update(repr(attr).encode())
+            for name, period in names.items():
+                h.update(repr((name, period)).encode())
+    return h.hexdigest()
+
+
+def get_matcher(processed_data, device: Optional[int] = None) -> GpuMatcher:
+    """Compile (once) the knowledge base into a libkwmatch handle."""
+    key = (id(processed_data), _kb_fingerprint(processed_data), device)
+    m = _MATCHERS.get(key)
+    if m is None:
+        m = GpuMatcher(compile_kb(processed_data), device)
+        _MATCHERS.clear()
+        _MATCHERS[key] = m
+    return m
+
+
+# --------------------------------------------------------------------- process_chunk
+def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
+    """``ticker_matches`` of every row of ``chunk`` (list aligned with the rows).
+
+    Raises the reference's exceptions: a row whose ``date_time`` does not parse
+    raises after the rows before it were matched (the returned ``error`` lets
+    ``process_chunk`` write those rows first, as the reference's row loop does).
+    """
+    n = len(chunk)
+    if n == 0:
+        return [], None
+    texts = [field_str(v) for v in chunk['article_text'].tolist()]
+    titles = [field_str(v) for v in chunk['title'].tolist()]
+    dates: List = []
+    error = None
+    for v in chunk['date_time'].tolist():
+        try:
+            dates.append(parser.parse(str(v)) if pd.notna(v) else None)
+        except Exception as exc:   # match_keywords.py:152 raises here for this row
+            error = exc
+            break
+    n_ok = len(dates)
+    matcher = matcher or get_matcher(processed_data)
+    results: List[dict] = [{} for _ in range(n_ok)]
+    if n_ok:
+        hits = matcher.match_strings(texts[:n_ok], titles[:n_ok])
+        for doc, fields in group_hits(hits).items():
+            results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
+    return results, error
+
+
+def process_chunk(source_name, chunk, processed_data):
+    """Match every row of ``chunk`` and append the per-ticker CSV rows (match_keywords.py:148-192)."""
+    results, error = match_chunk(chunk, processed_data)
+    if results:
+        rows_by_ticker: Dict[str, list] = {}
+        for i, ticker_matches in enumerate(results):
+            if not ticker_matches:
+                continue
+            row = chunk.iloc[i]
+            for ticker, matched in ticker_matches.items():
+                rows_by_ticker.setdefault(ticker, []).append(_csv_row(matched, row))
+        for ticker, rows in rows_by_ticker.items():
+            _append_rows(source_name, ticker, rows)
+    if error is not None:
+        raise error
+
+
+# --------------------------------------------------------------------- sort
+def sort_matched_csv(file_path):
+    """Re-read, sort by ``time_unix`` (pandas default quicksort) and rewrite (match_keywords.py:195-217)."""
+    try:
+        frame = pd.read_csv(file_path)
+        if 'time_unix' not in frame.columns:
+            frame['date_time'] = frame['date_time'].apply(parser.parse)
+            frame['time_unix'] = frame['date_time'].apply(lambda d: int(d.timestamp()))
+        ordered = frame.sort_values('time_unix', ascending=True)
+        ordered['time_unix'] = ordered['time_unix'].astype(int)
+        ordered.to_csv(file_path, index=False)
+        print(f"Sorted and saved: {file_path}")
+    except Exception as exc:  # noqa: BLE001 - mirrors the reference
+        print(f"Error processing {file_path}: {str(exc)}")
+
+
+# --------------------------------------------------------------------- CLI
+def main(argv=None):
+    """The reference's ``__main__`` (match_keywords.py:220-246) with its constants as defaults."""
+    ap = argparse.ArgumentParser(description=__doc__.split('\n')[0])
+    ap.add_argument('--source', default='yahoo')
+    ap.add_argument('--info-dir', default='info/Icahn_filter')
+    ap.add_argument('--articles', default='datasets/yahoo_articles_all_20250605.csv')
+    ap.add_argument('--chunksize', type=int, default=20000)
+    ap.add_argument('--device', type=int, default=None)
+    args = ap.parse_args(argv)
+    processed = read_and_process_json_files(args.info_dir)
+    out_dir = f'{args.source}_ticker_matched_articles'
+    os.makedirs(out_dir, exist_ok=True)
+    matcher = get_matcher(processed, args.device)
+    for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
+        results, error = match_chunk(chunk, processed, matcher)
+        rows_by_ticker: Dict[str, list] = {}
+        for i, tm in enumerate(results):
+            for ticker, matched in tm.items():
+                rows_by_ticker.setdefault(ticker, []).append(_csv_row(matched, chunk.iloc[i]))
+        for ticker, rows in rows_by_ticker.items():
+            _append_rows(args.source, ticker, rows)
+        if error is not None:
+            raise error
+    print("All matched CSV files have been processed.")
+    for name in os.listdir(out_dir):
+        sort_matched_csv(f"{out_dir}/{name}")
+    print("All matched CSV files have been sorted by date and time.")
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

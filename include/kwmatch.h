@@ -1,0 +1,116 @@
+/*
+ * kwmatch.h — C-ABI of libkwmatch.so, the MI355X (gfx950) ticker<->news
+ * keyword matcher.
+ *
+ * What it replaces.  The reference has no FFI on this path: its operator
+ * boundary is the Python function
+ *     process_chunk(source_name, chunk, processed_data)   match_keywords.py:148
+ * whose inner loops (match_keywords.py:159-180) run, per article and per name,
+ *   - the uppercase branch  re.finditer(r'\b'+re.escape(name)+r'\b', s)      :165-173
+ *   - the fuzzy branch      rapidfuzz.fuzz.partial_ratio(s, name) > 95        :174-176
+ *                           followed by re.finditer(name, s)                  :177-180
+ * on s = article_text and s = title (:150-151).  This library computes exactly
+ * those per-(article, field, name) results on the GPU.  Everything around them
+ * (knowledge-base loading :40-120, the period filter :17-37/:164, the
+ * per-ticker dict assembly :159-187, CSV egress :128-146/:195-217) stays in the
+ * host module advanced_scrapper_amd/match_keywords.py, which is the drop-in
+ * replacement of the reference script and binds this header with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions: every function returns 0 on success or a negative KW_E* code;
+ * kw_last_error(h) gives a message.  Handles are not thread-safe: use one
+ * handle per device and per host thread.  Device pointers passed to kw_scan are
+ * caller-owned (e.g. torch uint8/int64 tensors); kw_scan is asynchronous on the
+ * given HIP stream.
+ */
+#ifndef KWMATCH_H
+#define KWMATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes */
+#define KW_OK 0
+#define KW_EINVAL -1        /* bad argument */
+#define KW_EUNSUPPORTED -2  /* pattern outside the supported subset (see kw_compile) */
+#define KW_EHIP -3          /* HIP runtime error */
+#define KW_EOVERFLOW -4     /* a device work buffer overflowed; see kw_last_error */
+#define KW_ESTATE -5        /* call out of order (e.g. kw_hits before kw_scan) */
+
+/* pattern classes (match_keywords.py:165-174) */
+#define KW_CLASS_UPPER 'U'  /* name.isupper() and len(name) > 1: \b-bounded literal */
+#define KW_CLASS_FUZZY 'F'  /* the fuzzy branch: partial_ratio > 95, then re.finditer */
+
+/* regex atom program of a fuzzy-class name, used for the positions of
+ * re.finditer(name, s) (match_keywords.py:177-180).  Four int32 per atom:
+ * {op, value, min, max}; op 0 = literal code point `value`, op 1 = '.'
+ * (any code point except '\n'); the atom repeats greedily min..max times
+ * (max = -1: unbounded).  A pattern with rx_off[i] == rx_off[i+1] is matched
+ * literally (its atoms are its code points). */
+#define KW_RX_LIT 0
+#define KW_RX_ANY 1
+
+typedef struct kw_handle kw_handle;
+
+/* One result record.  pos is a code-point offset (str index) of a match start
+ * in the field; KW_NOPOS marks a fuzzy-branch match whose re.finditer found
+ * no position (the reference stores `name: []`, match_keywords.py:177-180). */
+typedef struct {
+    uint32_t doc;      /* document index within the scanned batch */
+    uint32_t pattern;  /* pattern index as passed to kw_compile */
+    uint32_t pos;      /* code-point offset or KW_NOPOS */
+    uint32_t field;    /* 0 = article_text, 1 = title */
+} kw_hit;
+#define KW_NOPOS 0xFFFFFFFFu
+
+/* Compile the active names into device tables on `device`.
+ *   pat_bytes/pat_off : UTF-8 of n_pat names, name i = pat_bytes[pat_off[i]:pat_off[i+1]]
+ *   pat_class         : KW_CLASS_UPPER or KW_CLASS_FUZZY per name.  Names of the
+ *                       other two reference classes (single uppercase char,
+ *                       lowercase-alpha) never match and must not be passed.
+ *                       Order: all 'U' names first, then the 'F' names sorted by
+ *                       code-point length, longest first.
+ *   rx_atoms/rx_off   : regex programs (see KW_RX_*), rx_off has n_pat+1 entries;
+ *                       may be NULL (all names literal).
+ *   word_bitmap       : 0x110000 bits, bit c set iff chr(c).isalnum() or c == '_'
+ *                       (CPython's \b word class, Unicode database of the host).
+ * Fuzzy names longer than 64 code points or one byte long are KW_EUNSUPPORTED
+ * (rapidfuzz switches algorithm above 64). */
+int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, const uint8_t *pat_class, int32_t n_pat,
+               const int32_t *rx_atoms, const int64_t *rx_off, const uint32_t *word_bitmap, int32_t device,
+               kw_handle **out);
+
+/* Scan n_docs documents.  d_arena: UTF-8 bytes; d_doc_off: 2*n_docs+1 int64
+ * byte offsets, text of doc d = [off[2d], off[2d+1]), title = [off[2d+1],
+ * off[2d+2]).  The host has already applied the str()/NaN rules of
+ * match_keywords.py:150-151 (NaN -> "nan").  stream: a hipStream_t (NULL =
+ * default stream).  Asynchronous. */
+int kw_scan(kw_handle *h, const uint8_t *d_arena, const int64_t *d_doc_off, int64_t n_docs, void *stream);
+
+/* Wait for the last scan and return its records (device memory owned by the
+ * library, valid until the next kw_scan or kw_destroy).  Records are grouped
+ * by document but not sorted. */
+int kw_hits(kw_handle *h, int64_t *n_hits, const kw_hit **d_hits);
+
+/* Copy the last scan's records into a caller-owned device buffer of capacity
+ * `cap` records (asynchronous on `stream`); *n_hits receives the count. */
+int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void *stream);
+
+/* Scan statistics of the last kw_scan (after kw_hits): candidate positions that
+ * passed the LDS filter, anchor occurrences, verified windows. */
+int kw_stats(kw_handle *h, int64_t *candidates, int64_t *anchor_hits, int64_t *windows);
+
+/* Device time (ms) of the scan kernel of the last kw_scan, measured with HIP
+ * events on the scan's stream (valid after kw_hits). */
+int kw_last_kernel_ms(kw_handle *h, float *scan_ms, float *total_ms);
+
+const char *kw_last_error(kw_handle *h);
+int kw_destroy(kw_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,178 @@
+"""GPU parity: libkwmatch (HIP, gfx950) vs the CPU oracle and the reference's golden outputs.
+
+Bar: bit-exact — the same (doc, field, name) set with the same code-point
+positions as the oracle, the same ticker_matches dicts as the reference, and
+byte-identical per-ticker CSV files.
+"""
+import io
+import os
+import random
+
+import numpy as np
+import pandas as pd
+import pytest
+from dateutil import parser
+
+from tests import oracle_pool
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def env(golden):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    processed = golden.kb_processed()
+    ckb = compile_kb(processed)
+    return {'processed': processed, 'ckb': ckb, 'm': GpuMatcher(ckb)}
+
+
+def _field_str(v):
+    return str(v) if v else ""
+
+
+def _golden_rows(golden):
+    frame = golden.articles_frame()
+    texts = [_field_str(v) for v in frame['article_text'].tolist()]
+    titles = [_field_str(v) for v in frame['title'].tolist()]
+    dates = [parser.parse(str(v)) if pd.notna(v) else None for v in frame['date_time'].tolist()]
+    return texts, titles, dates
+
+
+def _gpu_maps(m, texts, titles):
+    from advanced_scrapper_amd.matcher import group_hits
+    hits = m.match_strings(texts, titles)
+    g = group_hits(hits)
+    names = m.ckb.names
+    out = []
+    for d in range(len(texts)):
+        f = g.get(d, {})
+        out.append(({names[p]: v for p, v in f.get(0, {}).items()}, {names[p]: v for p, v in f.get(1, {}).items()}))
+    return out
+
+
+def _compare(processed, texts, titles, got):
+    want_t = oracle_pool.field_results(processed, texts)
+    want_i = oracle_pool.field_results(processed, titles)
+    bad = []
+    for d in range(len(texts)):
+        if got[d][0] != want_t[d] or got[d][1] != want_i[d]:
+            bad.append((d, sorted(set(got[d][0].items()) ^ set((k, tuple(v)) for k, v in want_t[d].items()))
+                        if False else None))
+            if len(bad) < 4:
+                gt, wt = got[d][0], want_t[d]
+                gi, wi = got[d][1], want_i[d]
+                diff_t = {k: (gt.get(k), wt.get(k)) for k in set(gt) | set(wt) if gt.get(k) != wt.get(k)}
+                diff_i = {k: (gi.get(k), wi.get(k)) for k in set(gi) | set(wi) if gi.get(k) != wi.get(k)}
+                print(f"doc {d}: text diff {diff_t} title diff {diff_i}")
+    return [b[0] for b in bad]
+
+
+def test_golden_pattern_level(env, golden):
+    texts, titles, _dates = _golden_rows(golden)
+    got = _gpu_maps(env['m'], texts, titles)
+    bad = _compare(env['processed'], texts, titles, got)
+    assert not bad, f"GPU differs from the oracle on docs {bad[:20]}"
+
+
+def test_golden_ticker_level(env, golden):
+    from advanced_scrapper_amd.matcher import assemble_ticker_matches, group_hits
+    texts, titles, dates = _golden_rows(golden)
+    m = env['m']
+    g = group_hits(m.match_strings(texts, titles))
+    want = golden.matches()
+    for d in range(len(texts)):
+        got = assemble_ticker_matches(m.ckb, g.get(d, {}), dates[d])
+        assert got == want[d], d
+        assert list(got) == list(want[d]), d
+        for t in got:
+            assert list(got[t]['text']) == list(want[d][t]['text']), (d, t)
+            assert list(got[t]['title']) == list(want[d][t]['title']), (d, t)
+
+
+def test_dropin_process_chunk_csv_bytes(env, golden, tmp_path, monkeypatch):
+    """The drop-in driver writes byte-identical per-ticker CSVs (after the sort)."""
+    from advanced_scrapper_amd import match_keywords as mk
+    monkeypatch.chdir(tmp_path)
+    os.makedirs('yahoo_ticker_matched_articles')
+    processed = env['processed']
+    for chunk in pd.read_csv(io.BytesIO(golden.articles_csv_bytes()), chunksize=golden.chunksize()):
+        mk.process_chunk('yahoo', chunk, processed)
+    for fn in os.listdir('yahoo_ticker_matched_articles'):
+        mk.sort_matched_csv(f'yahoo_ticker_matched_articles/{fn}')
+    want = golden.outputs()
+    got = {fn: open(os.path.join('yahoo_ticker_matched_articles', fn), 'rb').read()
+           for fn in os.listdir('yahoo_ticker_matched_articles')}
+    assert sorted(got) == sorted(want)
+    for fn in want:
+        assert got[fn] == want[fn], fn
+
+
+@pytest.mark.parametrize('seed', [7, 11])
+def test_random_corpus_vs_oracle(env, seed):
+    from advanced_scrapper_amd import synth
+    names, kinds = synth.injectable_names(env['ckb'])
+    c = synth.generate(400, names, kinds, seed=seed, doc_base=seed * 1000)
+    texts, titles = c.texts(), c.titles()
+    got = _gpu_maps(env['m'], texts, titles)
+    bad = _compare(env['processed'], texts, titles, got)
+    assert not bad, f"seed {seed}: GPU differs from the oracle on docs {bad[:20]}"
+
+
+def _adversarial_strings(ckb):
+    rng = random.Random(5)
+    fz = [n for n, c in zip(ckb.names, ckb.classes) if c == 'F' and n]
+    up = [n for n, c in zip(ckb.names, ckb.classes) if c == 'U']
+    texts, titles = [], []
+    # empty fields, names as whole fields, names with one edit, glued uppercase names
+    texts += ['', 'nan', 'a', 'é', '\n', '中文']
+    titles += ['', '', 'nan', 'x', '', 'é']
+    for n in rng.sample(fz, 60):
+        texts.append(n)
+        titles.append(n[1:] if len(n) > 1 else n)
+        k = rng.randrange(len(n))
+        texts.append(n[:k] + n[k + 1:])
+        titles.append(n[:k] + 'x' + n[k:])
+        texts.append('é ' * 40 + n[:k] + n[k + 1:] + ' ’' * 30)
+        titles.append(n + ' ' + n)
+    for n in rng.sample(up, 40):
+        for glue in ('x', '_', '7', 'é', 'É', '中', '.', ' ', '+', '’'):
+            texts.append(f"{glue}{n}{glue} {n}{glue}{n} {glue}{n}")
+            titles.append(n + glue)
+    long_na = ' '.join(rng.choice(fz) + rng.choice([' ', 'é ', '—', '\n']) for _ in range(400))
+    texts.append(long_na)
+    titles.append(long_na[:63])
+    return texts, titles
+
+
+def test_adversarial_strings_vs_oracle(env):
+    texts, titles = _adversarial_strings(env['ckb'])
+    got = _gpu_maps(env['m'], texts, titles)
+    bad = _compare(env['processed'], texts, titles, got)
+    assert not bad, f"GPU differs from the oracle on adversarial docs {bad[:20]}"
+
+
+def test_batch_invariance_and_determinism(env):
+    """Results of a doc do not depend on its batch or on the run (size-independent property)."""
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.matcher import group_hits
+    names, kinds = synth.injectable_names(env['ckb'])
+    c = synth.generate(3000, names, kinds, seed=99)
+    m = env['m']
+    d_arena, d_off = m.upload(c.arena, c.off)
+    m.scan(d_arena, d_off, c.n_docs)
+    full = np.sort(m.fetch(), order=['doc', 'field', 'pattern', 'pos'])
+    m.scan(d_arena, d_off, c.n_docs)
+    again = np.sort(m.fetch(), order=['doc', 'field', 'pattern', 'pos'])
+    assert np.array_equal(full, again)
+    half = c.n_docs // 2
+    c2 = synth.generate(c.n_docs - half, names, kinds, seed=99, doc_base=half)
+    a2, o2 = m.upload(c2.arena, c2.off)
+    m.scan(a2, o2, c2.n_docs)
+    tail = m.fetch()
+    tail['doc'] += half
+    tail = np.sort(tail, order=['doc', 'field', 'pattern', 'pos'])
+    assert np.array_equal(full[full['doc'] >= half], tail)

@@ -1,0 +1,270 @@
+"""CPU tests of the host side: KB loading, classification, regex atoms, assembly, CSV egress, C-ABI."""
+import io
+import os
+import random
+import re
+import subprocess
+
+import numpy as np
+import pandas as pd
+import pytest
+from dateutil import parser
+
+from advanced_scrapper_amd import kb
+from advanced_scrapper_amd.kb import compile_kb
+
+
+# ------------------------------------------------------------------ KB loading (a1-a3)
+def test_kb_loader_matches_reference(golden, tmp_path):
+    order = golden.materialize_kb(str(tmp_path / 'ticker'))
+    got = kb.read_and_process_json_files(str(tmp_path / 'ticker'), _listdir=lambda _p: order)
+    want = golden.kb_processed()
+    assert list(got) == list(want)
+    for t in want:
+        assert list(got[t]) == list(want[t])
+        for a in want[t]:
+            assert list(got[t][a].items()) == list(want[t][a].items()), (t, a)
+
+
+def test_kb_loader_error_paths(tmp_path, capsys):
+    d = tmp_path / 'kb'
+    d.mkdir()
+    (d / 'A_info.json').write_text('[{"ticker": "AAA", "country": ["United States"], "aliases": ["Aaa Corp"]}]')
+    (d / 'B_info.json').write_text('[{"ticker": "BBB"}, {"ticker": "CCC"}]')       # KeyError: skipped
+    (d / 'C_info.json').write_bytes('[{"ticker": "DDD", "aliases": ["Ca\xe9"]}]'.encode('latin1'))  # not utf-8
+    (d / 'notes.txt').write_text('ignored')
+    got = kb.read_and_process_json_files(str(d), _listdir=lambda p: sorted(os.listdir(p)))
+    assert list(got) == ['AAA', 'DDD']
+    assert 'Aaa Corp' in got['AAA']['aliases']
+
+
+def test_extract_time_periods_rules():
+    p = kb.extract_time_periods([
+        'Steve Jobs (Start: 1997-09-16T00:00:00Z) (End: 2011-08-24T00:00:00Z)',
+        'Steve Jobs (Start: 1976-04-01T00:00:00Z) (End: 1985-09-17T00:00:00Z)',
+        'Tim Cook (Start: http://www.wikidata.org/.well-known/genid/abc)',
+        'Plain Name',
+        'Weird (End: not a date)',
+    ])
+    assert list(p) == ['Steve Jobs', 'Tim Cook', 'Plain Name', 'Weird']
+    assert p['Steve Jobs'][0].year == 1976 and p['Steve Jobs'][1].year == 1985   # last wins, first position
+    assert p['Tim Cook'] == (None, None)
+    assert p['Plain Name'] == (None, None)
+    assert kb.extract_time_periods('Solo') == {'Solo': (None, None)}
+
+
+def test_is_within_period():
+    d = parser.parse
+    assert not kb.is_within_period(None, None, None)
+    assert kb.is_within_period(d('2000-01-01'), None, None)
+    assert kb.is_within_period(d('2000-01-01'), d('2000-01-01'), d('2000-01-01'))
+    assert not kb.is_within_period(d('1999-12-31'), d('2000-01-01'), None)
+    assert kb.is_within_period(d('2000-01-01T05:00:00+05:00'), d('2000-01-01'), None)
+    assert not kb.is_within_period(d('2000-01-01T05:00:00+05:01'), d('2000-01-01'), None)
+
+
+def test_classes_of_the_golden_kb(golden):
+    from collections import Counter
+    names = {}
+    for _t, attrs in golden.kb_processed().items():
+        for _a, ns in attrs.items():
+            for n in ns:
+                names[n] = kb.classify_name(n)
+    c = Counter(names.values())
+    assert c == Counter({'F': 2209, 'U': 253, 'S': 127, 'X': 4})
+    ckb = compile_kb(golden.kb_processed())
+    assert ckb.n_patterns == 2462
+    assert ckb.classes[:253] == ['U'] * 253
+    lens = [len(n) for n in ckb.names[253:]]
+    assert lens == sorted(lens, reverse=True)
+    assert max(lens) <= 64
+
+
+# ------------------------------------------------------------------ regex atoms
+def _atoms_finditer(atoms, s):
+    """Python mirror of the device matcher (kwmatch_kernels.hpp rx_match + rx_positions)."""
+    def match_at(st):
+        stack = []
+        a, pos = 0, st
+        while True:
+            fail = False
+            if a == len(atoms):
+                return pos
+            op, val, lo, hi = atoms[a]
+            ok = lambda c: (c == chr(val)) if op == 0 else (c != '\n')
+            if lo == 1 and hi == 1:
+                if pos < len(s) and ok(s[pos]):
+                    pos += 1
+                    a += 1
+                    continue
+                fail = True
+            else:
+                k = 0
+                while (hi < 0 or k < hi) and pos + k < len(s) and ok(s[pos + k]):
+                    k += 1
+                if k < lo:
+                    fail = True
+                else:
+                    stack.append([a, pos, k])
+                    pos += k
+                    a += 1
+                    continue
+            if fail:
+                while stack:
+                    t = stack[-1]
+                    if t[2] > atoms[t[0]][2]:
+                        t[2] -= 1
+                        pos = t[1] + t[2]
+                        a = t[0] + 1
+                        break
+                    stack.pop()
+                else:
+                    return -1
+    out, last = [], 0
+    for st in range(len(s)):
+        e = match_at(st)
+        if e >= 0 and st >= last:
+            out.append(st)
+            last = e if e > st else st + 1
+    return out
+
+
+def test_regex_atoms_match_python_re(golden):
+    rng = random.Random(3)
+    names = [n for n in compile_kb(golden.kb_processed()).names if kb.regex_atoms(n) not in (None, 'invalid')]
+    extra = ['ab+c', 'a.?b', 'x*yz', 'E*Trade', 'Guess?', 'a{2,3}b', '(foo)bar', 'C.+D']
+    for name in names + extra:
+        atoms = kb.regex_atoms(name)
+        alphabet = list(set(name.replace('\\', ''))) + ['\n', 'y', 'Z']
+        for _ in range(40):
+            s = ''.join(rng.choice(alphabet) for _ in range(rng.randint(0, 30)))
+            if rng.random() < 0.5:
+                s = s[:5] + name.replace('(', '').replace(')', '') + s[5:]
+            want = [m.start() for m in re.finditer(name, s)]
+            assert _atoms_finditer(atoms, s) == want, (name, s)
+
+
+def test_regex_atoms_classification():
+    assert kb.regex_atoms('Apple Inc') is None
+    assert kb.regex_atoms('C++') == 'invalid'
+    assert kb.regex_atoms('Disney+ Hotstar')[5] == (0, ord('y'), 1, -1)
+    with pytest.raises(kb.UnsupportedPattern):
+        kb.regex_atoms('[24]7.ai')
+    with pytest.raises(kb.UnsupportedPattern):
+        kb.regex_atoms('A|B')
+
+
+# ------------------------------------------------------------------ assembly (a10) from oracle field results
+def test_assembly_reproduces_reference_dicts(golden):
+    """Host expansion of per-(field, name) results == the reference's ticker_matches."""
+    from advanced_scrapper_amd.matcher import assemble_ticker_matches
+    from tests import oracle_pool
+    processed = golden.kb_processed()
+    ckb = compile_kb(processed)
+    pid = {n: i for i, n in enumerate(ckb.names)}
+    frame = golden.articles_frame()
+    texts = [str(v) if v else "" for v in frame['article_text'].tolist()]
+    titles = [str(v) if v else "" for v in frame['title'].tolist()]
+    dates = [parser.parse(str(v)) if pd.notna(v) else None for v in frame['date_time'].tolist()]
+    ft = oracle_pool.field_results(processed, texts, procs=8)
+    fi = oracle_pool.field_results(processed, titles, procs=8)
+    want = golden.matches()
+    for d in range(len(texts)):
+        fields = {0: {pid[n]: v for n, v in ft[d].items()}, 1: {pid[n]: v for n, v in fi[d].items()}}
+        got = assemble_ticker_matches(ckb, fields, dates[d])
+        assert got == want[d], d
+        assert list(got) == list(want[d])
+        for t in got:
+            assert list(got[t]['text']) == list(want[d][t]['text'])
+            assert list(got[t]['title']) == list(want[d][t]['title'])
+
+
+# ------------------------------------------------------------------ CSV egress (a11, a12)
+def test_csv_egress_bytes(golden, tmp_path, monkeypatch):
+    """Rows built from the golden matches and written/sorted by the drop-in == reference files."""
+    from advanced_scrapper_amd import match_keywords as mk
+    monkeypatch.chdir(tmp_path)
+    os.makedirs('yahoo_ticker_matched_articles')
+    want_m = golden.matches()
+    start = 0
+    for chunk in pd.read_csv(io.BytesIO(golden.articles_csv_bytes()), chunksize=golden.chunksize()):
+        by_ticker = {}
+        for i in range(len(chunk)):
+            for ticker, matched in want_m[start + i].items():
+                by_ticker.setdefault(ticker, []).append(mk._csv_row(matched, chunk.iloc[i]))
+        for ticker, rows in by_ticker.items():
+            mk._append_rows('yahoo', ticker, rows)
+        start += len(chunk)
+    for fn in os.listdir('yahoo_ticker_matched_articles'):
+        mk.sort_matched_csv(f'yahoo_ticker_matched_articles/{fn}')
+    want = golden.outputs()
+    got = sorted(os.listdir('yahoo_ticker_matched_articles'))
+    assert got == sorted(want)
+    for fn in want:
+        with open(os.path.join('yahoo_ticker_matched_articles', fn), 'rb') as fh:
+            assert fh.read() == want[fn], fn
+
+
+def test_append_to_csv_single_row(tmp_path, monkeypatch):
+    from advanced_scrapper_amd import match_keywords as mk
+    monkeypatch.chdir(tmp_path)
+    os.makedirs('src_ticker_matched_articles')
+    art = pd.Series({'date_time': '2020-01-02 03:04:05', 'title': float('nan'), 'url': 'u,1', 'source': 's',
+                     'source_url': 'su', 'article_text': 'He said "hi"\nand left é'})
+    mk.append_to_csv('src', 'AAPL', {'text': {'Apple': [0]}, 'title': {}}, art)
+    mk.append_to_csv('src', 'AAPL', {'text': {'Andrés': []}, 'title': {'X': [1, 2]}}, art)
+    data = open('src_ticker_matched_articles/AAPL_match.csv', encoding='utf-8').read()
+    assert data.count('time_unix') == 1
+    assert '"{""Andr\\u00e9s"": []}"' in data
+    assert '1577934245' in data
+
+
+# ------------------------------------------------------------------ C-ABI boundary
+def _header_functions():
+    hdr = open(os.path.join(os.path.dirname(__file__), '..', 'include', 'kwmatch.h')).read()
+    return sorted(set(re.findall(r'^\s*(?:int|const char \*)\s*\*?(kw_\w+)\s*\(', hdr, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from advanced_scrapper_amd import _native
+    L = _native.lib()
+    funcs = _header_functions()
+    assert funcs, 'no functions parsed from the header'
+    assert sorted(_native.EXPORTS) == funcs
+    for f in funcs:
+        assert hasattr(L, f), f
+    out = subprocess.run(['nm', '-D', '--defined-only', _native.LIB_PATH], capture_output=True, text=True).stdout
+    for f in funcs:
+        assert re.search(rf'\bT {f}\b', out), f
+
+
+def test_compile_rejects_unsupported_without_gpu():
+    """kw_compile validates before touching the device."""
+    import ctypes
+    from advanced_scrapper_amd import _native
+    L = _native.lib()
+    names = ['X' * 70]
+    b = np.frombuffer(names[0].encode(), dtype=np.uint8).copy()
+    off = np.array([0, len(b)], dtype=np.int64)
+    cls = np.array([ord('F')], dtype=np.uint8)
+    h = ctypes.c_void_p()
+    rc = L.kw_compile(_native.ptr(b), _native.ptr(off), _native.ptr(cls), 1, None, None,
+                      _native.ptr(kb.word_bitmap()), 0, ctypes.byref(h))
+    assert rc == _native.KW_EUNSUPPORTED
+    assert b'64' in L.kw_last_error(h)
+    L.kw_destroy(h)
+
+
+# ------------------------------------------------------------------ synthetic corpus
+def test_synth_is_shard_invariant(golden):
+    from advanced_scrapper_amd import synth
+    ckb = compile_kb(golden.kb_processed())
+    names, kinds = synth.injectable_names(ckb)
+    a = synth.generate(300, names, kinds, seed=5)
+    b = synth.generate(100, names, kinds, seed=5, doc_base=200)
+    for i in range(100):
+        assert a.text(200 + i) == b.text(i)
+        assert a.title(200 + i) == b.title(i)
+    c = synth.generate(300, names, kinds, seed=5)
+    assert np.array_equal(a.arena, c.arena) and np.array_equal(a.off, c.off)
+    assert 1500 < a.n_bytes / a.n_docs < 3500
