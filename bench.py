@@ -1,0 +1,177 @@
+"""Benchmark: article GB/s keyword-matched (S&P500 KB) on MI355X — BASELINE.json's metric.
+
+One step = one kw_scan pass (scan + resolve + result compaction) over the
+rank's whole shard of synthetic articles, already resident in HBM, followed
+by the all-gather of the per-rank hit counts (N > 1).  Weak scaling: every
+rank owns ``--docs-per-gpu`` documents (default 1M = config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints one JSON line.  ``roofline`` prices the scan kernel against
+HBM (8.0 TB/s) with the algorithmic bytes = sum of UTF-8 bytes of every
+article's text and title; the kernel time is the HIP-event
+time of the scan kernel on the stream it runs on.  ``cpu_baseline`` times the
+oracle's CPU port (oracle/cpu_port.py) on a bounded sample of the same
+corpus, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0
+METRIC = "article GB/s keyword-matched (S&P500 set) at 1 & 8 GPUs; % of HBM peak"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--docs-per-gpu', type=int, default=1_000_000)
+    ap.add_argument('--seed', type=int, default=20250905)
+    ap.add_argument('--cpu-sample', type=int, default=256, help='docs timed on the CPU port (0 = skip)')
+    ap.add_argument('--cpu-procs', type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument('--gather-hits', action='store_true', help='also time the RCCL all-gather of hit records')
+    args = ap.parse_args()
+
+    import torch
+    from advanced_scrapper_amd import dist, synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    from tests import golden_data
+
+    rank, world, local = dist.init('nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+
+    processed = golden_data.kb_processed()          # info/ticker KB (S&P500 subset), 216 tickers
+    ckb = compile_kb(processed)
+    names, kinds = synth.injectable_names(ckb)
+    n_local = args.docs_per_gpu
+    doc_base = rank * n_local
+    t_gen = time.perf_counter()
+    corpus = synth.generate(n_local, names, kinds, seed=args.seed, doc_base=doc_base)
+    t_gen = time.perf_counter() - t_gen
+    m = GpuMatcher(ckb, local)
+    t_up = time.perf_counter()
+    d_arena, d_off = m.upload(corpus.arena, corpus.off)
+    torch.cuda.synchronize()
+    t_up = time.perf_counter() - t_up
+    local_bytes = corpus.n_bytes
+
+    def step():
+        m.scan(d_arena, d_off, n_local)
+        n = m.n_hits()                                   # waits for the scan, reads the count
+        return dist.allgather_counts(n, dev)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    scan_ms, total_ms = [], []
+    t0 = time.perf_counter()
+    counts = None
+    for _ in range(args.steps):
+        counts = step()
+        s, t = m.kernel_ms()
+        scan_ms.append(s)
+        total_ms.append(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    nb = torch.tensor([float(local_bytes)], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(nb, op=torch.distributed.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_bytes = float(nb.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_bytes / (elapsed / args.steps) / 1e9
+
+    gather_ms = None
+    if args.gather_hits:
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        allh = dist.gather_hits(m.hits_device(), doc_base, dev)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - t) * 1e3
+
+    st = m.stats()
+    if rank != 0:
+        return
+    scan_avg = float(np.mean(scan_ms))
+    achieved = local_bytes / (scan_avg * 1e-3) / 1e9
+    cpu = None
+    if world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(processed, corpus, args.cpu_sample, args.cpu_procs)
+    out = {
+        'metric': METRIC,
+        'value': round(value, 2),
+        'unit': 'GB/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms_per_step, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'u8',
+        'data': 'synthetic (seeded generator, csrc/synth.c; KB = reference info/ticker via tests/golden)',
+        'config': {
+            'workload': 'config 2: S&P500 KB (216 tickers, 2462 active names) vs synthetic ~2 KB articles, '
+                        f'{n_local} docs per GPU',
+            'docs_per_gpu': n_local, 'total_docs': n_local * world, 'bytes_per_gpu': local_bytes,
+            'total_bytes': int(total_bytes), 'hits_total': int(sum(counts)) if counts else None,
+            'parallelism': f'dp{world} (document shards, RCCL all-gather of counts)',
+        },
+        'roofline': {
+            'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+            'kernel': 'kw::kw_scan_kernel', 'kernel_ms_avg': round(scan_avg, 4),
+            'step_kernels_ms_avg': round(float(np.mean(total_ms)), 4),
+        },
+        'cpu_baseline': cpu,
+        'scan_stats': st,
+        'host': {'generate_s': round(t_gen, 2), 'h2d_s': round(t_up, 3),
+                 'h2d_GBps_pcie_inclusive': round(local_bytes / t_up / 1e9, 2) if t_up > 0 else None},
+        'hits_allgather_ms': None if gather_ms is None else round(gather_ms, 3),
+    }
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(processed, corpus, n_sample: int, procs: int):
+    """Time the oracle's CPU port on the first n_sample documents of the same corpus."""
+    from dateutil import parser
+    from oracle import cpu_port
+    n = min(n_sample, corpus.n_docs)
+    rows = []
+    nbytes = 0
+    base = np.datetime64('1980-01-01T00:00:00')
+    for i in range(n):
+        t, ti = corpus.text(i), corpus.title(i)
+        nbytes += len(t.encode('utf-8', 'surrogatepass')) + len(ti.encode('utf-8', 'surrogatepass'))
+        rows.append((t, ti, parser.parse(str(base + np.timedelta64(1420 * (corpus.doc_base + i), 's')))))
+    secs, done = cpu_port.time_port(processed, rows, procs)
+    return {'value': round(nbytes / secs / 1e9, 6), 'unit': 'GB/s', 'cores': procs, 'kind': 'port',
+            'sample': f'first {done} docs of the same corpus ({nbytes} bytes), oracle CPU port '
+                      f'(Python loop + CPython re + C partial_ratio), {procs} processes, {secs:.2f} s wall',
+            'docs_per_s': round(done / secs, 2), 'docs_per_s_per_core': round(done / secs / procs, 3)}
+
+
+if __name__ == '__main__':
+    main()
