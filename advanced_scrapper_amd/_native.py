@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib')
-LIB_PATH = os.path.join(LIB_DIR, 'libkwmatch.so')
+LIB_PATH = os.environ.get('KW_LIB') or os.path.join(LIB_DIR, 'libkwmatch.so')   # KW_LIB: profiling variants
 
 KW_OK = 0
 KW_EINVAL = -1
@@ -48,7 +48,7 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
-    L.kw_compile.argtypes = [vp, vp, vp, i32, vp, vp, vp, i32, ctypes.POINTER(vp)]
+    L.kw_compile.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.POINTER(vp)]
     L.kw_compile.restype = ctypes.c_int
     L.kw_scan.argtypes = [vp, vp, vp, i64, vp]
     L.kw_scan.restype = ctypes.c_int
@@ -56,9 +56,10 @@ def lib() -> ctypes.CDLL:
     L.kw_hits.restype = ctypes.c_int
     L.kw_hits_copy.argtypes = [vp, vp, i64, ctypes.POINTER(i64), vp]
     L.kw_hits_copy.restype = ctypes.c_int
-    L.kw_stats.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.kw_stats.argtypes = [vp, vp, i32]
     L.kw_stats.restype = ctypes.c_int
-    L.kw_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    L.kw_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                    ctypes.POINTER(ctypes.c_float)]
     L.kw_last_kernel_ms.restype = ctypes.c_int
     L.kw_last_error.argtypes = [vp]
     L.kw_last_error.restype = ctypes.c_char_p

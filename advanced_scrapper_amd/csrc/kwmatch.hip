@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "kwmatch_kernels.hpp"
+#include "kwmatch_fast_kernel.hpp"
 
 using namespace kw;
 
@@ -43,13 +44,21 @@ struct kw_handle {
     bool scanned = false;
     bool fetched = false;
     int64_t n_hits = 0;
-    unsigned long long stats[3] = {0, 0, 0};
+    unsigned long long stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     int cus = 256;
     int blocks_per_cu = 2;
     std::string err;
     int n_pat = 0;
     int launched_waves = 0;
+    // fast path
+    FastTables FT{};
+    FastScratch FS{};
+    int nf = 0, ng = 0;
+    uint32_t defer_cap = 0;
+    int fast_blocks_per_cu = 1;
+    int n_anchor_fast = 0;
+    hipEvent_t evg = nullptr;
 };
 
 static thread_local std::string g_err;
@@ -113,6 +122,248 @@ uint32_t dmax_h(uint32_t m)
     return a > b ? a : b;
 }
 
+// ------------------------------------------------------------------ fast-path tables
+// 4-byte q-gram counts of the background sample (the corpus statistics every
+// anchor choice is priced with).  Without a sample every count is 0 and a
+// character-class heuristic breaks the ties.
+struct QStats {
+    std::unordered_map<uint32_t, uint32_t> c4;
+    bool have = false;
+    uint32_t count(const uint8_t *p) const
+    {
+        const uint32_t k = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+        auto it = c4.find(k);
+        uint32_t c = it == c4.end() ? 0u : it->second;
+        // class heuristic: starting inside a lowercase word or on a space is common in prose
+        const uint8_t b = p[0];
+        const uint32_t h = (b >= 'a' && b <= 'z') ? 4u : (b == ' ' ? 2u : 0u);
+        return have ? 4 * c + h : h;
+    }
+};
+
+struct FastBuild {
+    std::vector<uint32_t> filt, b2;
+    uint32_t gate_lo[4] = {0, 0, 0, 0}, gate_hi[4] = {0, 0, 0, 0};
+    int n_gate = 0;
+    std::vector<uint64_t> ht_key, as_head, sig;
+    std::vector<uint32_t> ht_begin, ht_cnt, kl, as_len, as_use_begin, as_use_cnt, use_pat, use_info0, use_info1,
+        rxk, boff;
+    uint32_t ht_mask = 0;
+};
+
+// rarest 4-byte window inside bytes [lo, hi) (hi - lo >= 4); returns its start
+size_t rarest4(const QStats &Q, const uint8_t *s, size_t lo, size_t hi, size_t max_start)
+{
+    size_t best = lo;
+    uint32_t bc = 0xFFFFFFFFu;
+    for (size_t a = lo; a + 4 <= hi && a <= max_start; ++a) {
+        uint32_t c = Q.count(s + a);
+        if (c < bc) { bc = c; best = a; }
+    }
+    return best;
+}
+
+int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_bytes, const int64_t *pat_off,
+               const std::vector<std::vector<uint32_t>> &cps, const std::vector<uint32_t> &pat_info,
+               const std::vector<int4> &atoms, const std::vector<uint32_t> &rxo, std::string &err)
+{
+    struct Use { uint32_t pat, i0, i1; };
+    std::unordered_map<std::string, uint32_t> aid;
+    std::vector<std::string> astr;
+    std::vector<std::vector<Use>> auses;
+    auto add = [&](const std::string &a, Use u) {
+        auto it = aid.find(a);
+        uint32_t id;
+        if (it == aid.end()) { id = (uint32_t)astr.size(); aid.emplace(a, id); astr.push_back(a); auses.emplace_back(); }
+        else id = it->second;
+        auses[id].push_back(u);
+    };
+    B.rxk.assign(std::max(n_pat, 1), RXK_LITERAL);
+    B.boff.assign(std::max(n_pat, 1), 0);
+    B.sig.assign(std::max(n_pat, 1), 0);
+    for (int i = 0; i < n_pat; ++i) {
+        const uint8_t *s = pat_bytes + pat_off[i];
+        const size_t bl = (size_t)(pat_off[i + 1] - pat_off[i]);
+        B.boff[i] = (uint32_t)pat_off[i];
+        const uint32_t m = (uint32_t)cps[i].size();
+        const bool fuzzy = pat_info[i] & PI_FUZZY;
+        for (uint32_t c : cps[i]) B.sig[i] |= 1ull << (c & 63);
+        // whole-name use (U or FULL): anchor at the rarest 4-byte window (offset <= 255)
+        auto span_use = [&](uint32_t kind, size_t sb, size_t se, uint32_t pcp, uint32_t pcl) {
+            const size_t len = se - sb;
+            size_t a = 0, al = len;
+            if (len >= 4) {
+                a = rarest4(Q, s + sb, 0, len, 255) ;
+                al = std::min<size_t>(8, len - a);
+            }
+            Use u;
+            u.pat = (uint32_t)i;
+            u.i0 = kind | ((uint32_t)a << 8) | ((uint32_t)sb << 16);
+            u.i1 = (uint32_t)len | (pcp << 16) | (pcl << 24);
+            add(std::string((const char *)s + sb + a, al), u);
+        };
+        if (!fuzzy) { span_use(FU_UPPER, 0, bl, 0, 0); continue; }
+        if (m == 0) continue;
+        span_use(FU_FULL, 0, bl, 0, 0);
+        // regex kind and the wildcard-match anchor (first literal run)
+        if (rxo[i + 1] > rxo[i]) {
+            bool quant = false;
+            for (uint32_t k = rxo[i]; k < rxo[i + 1]; ++k) quant |= !(atoms[k].z == 1 && atoms[k].w == 1);
+            if (quant) {
+                B.rxk[i] = RXK_GENERIC;
+            } else {
+                std::string run;
+                for (uint32_t k = rxo[i]; k < rxo[i + 1] && atoms[k].x == KW_RX_LIT; ++k) {
+                    uint32_t c = (uint32_t)atoms[k].y;
+                    if (c < 0x80) run.push_back((char)c);
+                    else if (c < 0x800) { run.push_back((char)(0xC0 | (c >> 6))); run.push_back((char)(0x80 | (c & 0x3F))); }
+                    else if (c < 0x10000) { run.push_back((char)(0xE0 | (c >> 12))); run.push_back((char)(0x80 | ((c >> 6) & 0x3F))); run.push_back((char)(0x80 | (c & 0x3F))); }
+                    else { run.push_back((char)(0xF0 | (c >> 18))); run.push_back((char)(0x80 | ((c >> 12) & 0x3F))); run.push_back((char)(0x80 | ((c >> 6) & 0x3F))); run.push_back((char)(0x80 | (c & 0x3F))); }
+                }
+                if (run.size() < 2) {
+                    B.rxk[i] = RXK_GENERIC;
+                } else {
+                    B.rxk[i] = RXK_WILD;
+                    size_t a = 0, al = run.size();
+                    if (run.size() >= 4) {
+                        a = rarest4(Q, (const uint8_t *)run.data(), 0, run.size(), 255);
+                        al = std::min<size_t>(8, run.size() - a);
+                    }
+                    Use u;
+                    u.pat = (uint32_t)i;
+                    u.i0 = FU_RXW | ((uint32_t)a << 8);
+                    u.i1 = (uint32_t)bl;
+                    add(run.substr(a, al), u);
+                }
+            }
+        }
+        // pigeonhole pieces: K = dmax+1 pieces, cuts chosen to minimise the
+        // largest "rarest 4-gram" count over the pieces (each piece is anchored
+        // at its own rarest 4-gram)
+        const uint32_t dm = dmax_h(m);
+        if (dm == 0) continue;
+        const uint32_t K = dm + 1;
+        std::vector<size_t> boffs(m + 1);
+        for (uint32_t c = 0; c <= m; ++c) boffs[c] = utf8_offset(cps[i], c);
+        const uint32_t minlen = 4;
+        if (m < K * minlen) { err = "kw_compile: name too short for its pieces"; return KW_EUNSUPPORTED; }
+        // cost[a][b] for piece cps [a, b)
+        std::vector<uint32_t> cost((size_t)(m + 1) * (m + 1), 0xFFFFFFFFu);
+        for (uint32_t a = 0; a < m; ++a) {
+            uint32_t best = 0xFFFFFFFFu;
+            for (uint32_t b = a + 1; b <= m; ++b) {
+                // add the 4-byte windows that end inside cp b-1
+                size_t lo_b = boffs[a];
+                for (size_t w = (boffs[b - 1] >= 3 ? boffs[b - 1] - 3 : 0); w + 4 <= boffs[b]; ++w)
+                    if (w >= lo_b) best = std::min(best, Q.count(s + w));
+                if (boffs[b] - boffs[a] >= 4) cost[(size_t)a * (m + 1) + b] = best;
+            }
+        }
+        const uint32_t INF = 0xFFFFFFFFu;
+        // dp[k][a]: best (max cost) splitting cps [a, m) into k pieces
+        std::vector<uint32_t> dp((size_t)(K + 1) * (m + 1), INF), nxt((size_t)(K + 1) * (m + 1), 0);
+        for (uint32_t a = 0; a + minlen <= m; ++a) dp[(size_t)1 * (m + 1) + a] = cost[(size_t)a * (m + 1) + m];
+        for (uint32_t k = 2; k <= K; ++k)
+            for (uint32_t a = 0; a + k * minlen <= m; ++a)
+                for (uint32_t b = a + minlen; b + (k - 1) * minlen <= m; ++b) {
+                    const uint32_t c1 = cost[(size_t)a * (m + 1) + b], c2 = dp[(size_t)(k - 1) * (m + 1) + b];
+                    if (c1 == INF || c2 == INF) continue;
+                    const uint32_t v = std::max(c1, c2);
+                    if (v < dp[(size_t)k * (m + 1) + a]) { dp[(size_t)k * (m + 1) + a] = v; nxt[(size_t)k * (m + 1) + a] = b; }
+                }
+        if (dp[(size_t)K * (m + 1)] == INF) { err = "kw_compile: no piece split"; return KW_EUNSUPPORTED; }
+        uint32_t a = 0;
+        for (uint32_t k = K; k >= 1; --k) {
+            const uint32_t b = (k == 1) ? m : nxt[(size_t)k * (m + 1) + a];
+            span_use(FU_PIECE, boffs[a], boffs[b], a, b - a);
+            a = b;
+        }
+    }
+    // ---- anchors, uses
+    const uint32_t na = (uint32_t)astr.size();
+    for (uint32_t a = 0; a < na; ++a) {
+        const std::string &st = astr[a];
+        uint64_t hd = 0;
+        for (size_t k = 0; k < st.size() && k < 8; ++k) hd |= (uint64_t)(uint8_t)st[k] << (8 * k);
+        B.as_head.push_back(hd);
+        B.as_len.push_back((uint32_t)st.size());
+        B.as_use_begin.push_back((uint32_t)B.use_pat.size());
+        B.as_use_cnt.push_back((uint32_t)auses[a].size());
+        for (auto &u : auses[a]) { B.use_pat.push_back(u.pat); B.use_info0.push_back(u.i0); B.use_info1.push_back(u.i1); }
+    }
+    if (B.use_pat.size() > IT_USE_MASK) { err = "kw_compile: more than 2^19 anchor uses"; return KW_EUNSUPPORTED; }
+    // ---- LDS filter, bigram table, gate, global hash table
+    B.filt.assign(FK_FILT_WORDS, 0);
+    B.b2.assign(FK_B2_WORDS, 0);
+    std::unordered_map<uint64_t, std::vector<uint32_t>> keys;
+    std::vector<uint8_t> gate_bytes;
+    bool gate_high = false;
+    for (uint32_t a = 0; a < na; ++a) {
+        const std::string &st = astr[a];
+        const uint8_t *p = (const uint8_t *)st.data();
+        if (st.size() >= 4) {
+            const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+            B.filt[fk_word(k4)] |= 1u << fk_bit(k4);
+            keys[(4ull << 32) | k4].push_back(a);
+        } else if (st.size() == 3) {
+            const uint32_t k3 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+            B.filt[fk_word(k3)] = 0xFFFFFFFFu;
+            keys[(3ull << 32) | k3].push_back(a);
+        } else if (st.size() == 2) {
+            const uint32_t k2 = (uint32_t)p[0] | ((uint32_t)p[1] << 8);
+            const uint32_t x = fk_b2_index(k2);
+            B.b2[x >> 5] |= 1u << (x & 31);
+            keys[(2ull << 32) | k2].push_back(a);
+            gate_bytes.push_back(p[0]);
+            gate_high |= p[0] >= 0x80;
+        } else {
+            err = "kw_compile: one-byte anchor";
+            return KW_EUNSUPPORTED;
+        }
+    }
+    if (!gate_bytes.empty()) {
+        if (gate_high) {
+            B.n_gate = -1;
+        } else {
+            std::sort(gate_bytes.begin(), gate_bytes.end());
+            gate_bytes.erase(std::unique(gate_bytes.begin(), gate_bytes.end()), gate_bytes.end());
+            std::vector<std::pair<uint32_t, uint32_t>> rg;
+            for (uint8_t g : gate_bytes) {
+                if (!rg.empty() && rg.back().second + 1 >= g) rg.back().second = g;
+                else rg.emplace_back(g, g);
+            }
+            while (rg.size() > 4) {   // merge the two closest ranges (a superset gate is still exact)
+                size_t bi = 0;
+                uint32_t bg = 0xFFFFFFFFu;
+                for (size_t r = 0; r + 1 < rg.size(); ++r)
+                    if (rg[r + 1].first - rg[r].second < bg) { bg = rg[r + 1].first - rg[r].second; bi = r; }
+                rg[bi].second = rg[bi + 1].second;
+                rg.erase(rg.begin() + bi + 1);
+            }
+            B.n_gate = (int)rg.size();
+            for (size_t r = 0; r < rg.size(); ++r) { B.gate_lo[r] = rg[r].first; B.gate_hi[r] = rg[r].second; }
+        }
+    }
+    uint32_t hs = 1024;
+    while (hs < 2 * keys.size()) hs <<= 1;
+    B.ht_mask = hs - 1;
+    B.ht_key.assign(hs, ~0ull);
+    B.ht_begin.assign(hs, 0);
+    B.ht_cnt.assign(hs, 0);
+    for (auto &kv : keys) {
+        uint32_t slot = fk_ht_slot(kv.first, B.ht_mask);
+        while (B.ht_key[slot] != ~0ull) slot = (slot + 1) & B.ht_mask;
+        B.ht_key[slot] = kv.first;
+        B.ht_begin[slot] = (uint32_t)B.kl.size();
+        B.ht_cnt[slot] = (uint32_t)kv.second.size();
+        B.kl.insert(B.kl.end(), kv.second.begin(), kv.second.end());
+    }
+    if (B.kl.empty()) B.kl.push_back(0);
+    if (B.as_head.empty()) { B.as_head.push_back(0); B.as_len.push_back(0); B.as_use_begin.push_back(0); B.as_use_cnt.push_back(0); }
+    if (B.use_pat.empty()) { B.use_pat.push_back(0); B.use_info0.push_back(0); B.use_info1.push_back(0); }
+    return KW_OK;
+}
+
 bool is_word_h(const uint32_t *bits, uint32_t c)
 {
     if (c >= 0x110000u) return false;
@@ -131,8 +382,8 @@ size_t push_array(std::vector<uint8_t> &blob, const std::vector<T> &v)
 }  // namespace
 
 extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, const uint8_t *pat_class, int32_t n_pat,
-                          const int32_t *rx_atoms, const int64_t *rx_off, const uint32_t *word_bitmap, int32_t device,
-                          kw_handle **out)
+                          const int32_t *rx_atoms, const int64_t *rx_off, const uint32_t *word_bitmap,
+                          const uint8_t *bg, int64_t bg_len, int32_t device, kw_handle **out)
 {
     if (!out) return KW_EINVAL;
     *out = nullptr;
@@ -359,6 +610,26 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     if (as_head.empty()) { as_head.push_back(0); as_off.push_back(0); as_len.push_back(0); as_use_begin.push_back(0); as_use_cnt.push_back(0); }
     if (as_bytes.empty()) as_bytes.push_back(0);
 
+    // ---- fast-path tables (anchors priced with the background sample's q-grams)
+    QStats Q;
+    if (bg && bg_len >= 4) {
+        Q.have = true;
+        Q.c4.reserve((size_t)std::min<int64_t>(bg_len, 1 << 22));
+        for (int64_t i = 0; i + 4 <= bg_len; ++i) {
+            const uint32_t k = (uint32_t)bg[i] | ((uint32_t)bg[i + 1] << 8) | ((uint32_t)bg[i + 2] << 16) |
+                               ((uint32_t)bg[i + 3] << 24);
+            ++Q.c4[k];
+        }
+    }
+    FastBuild FB;
+    {
+        std::string ferr;
+        int frc = build_fast(FB, Q, n_pat, pat_bytes, pat_off, cps, pat_info, atoms, rxo, ferr);
+        if (frc) return fail(frc, ferr);
+    }
+    std::vector<uint8_t> all_bytes(pat_bytes, pat_bytes + (n_pat ? pat_off[n_pat] : 0));
+    all_bytes.resize(all_bytes.size() + 16, 0);
+
     // ---- one device blob
     std::vector<uint8_t> blob;
     size_t o_filt = push_array(blob, filt), o_htk = push_array(blob, ht_key), o_htb = push_array(blob, ht_begin),
@@ -371,6 +642,13 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            o_rxa = push_array(blob, atoms), o_wb = push_array(blob, wb), o_fc = push_array(blob, f_count_ge),
            o_sk = push_array(blob, sub_key), o_sb = push_array(blob, sub_begin), o_sc = push_array(blob, sub_cnt),
            o_sp = push_array(blob, sub_pat);
+    size_t f_filt = push_array(blob, FB.filt), f_b2 = push_array(blob, FB.b2), f_htk = push_array(blob, FB.ht_key),
+           f_htb = push_array(blob, FB.ht_begin), f_htc = push_array(blob, FB.ht_cnt), f_kl = push_array(blob, FB.kl),
+           f_ash = push_array(blob, FB.as_head), f_asl = push_array(blob, FB.as_len),
+           f_asub = push_array(blob, FB.as_use_begin), f_asuc = push_array(blob, FB.as_use_cnt),
+           f_up = push_array(blob, FB.use_pat), f_ui0 = push_array(blob, FB.use_info0),
+           f_ui1 = push_array(blob, FB.use_info1), f_rxk = push_array(blob, FB.rxk), f_boff = push_array(blob, FB.boff),
+           f_pb = push_array(blob, all_bytes), f_sig = push_array(blob, FB.sig);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -413,51 +691,109 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     T.f_first = f_first;
     T.empty_pat = empty_pat;
 
+    FastTables &F = h->FT;
+    F.filt = (const uint32_t *)(B + f_filt);
+    F.b2 = (const uint32_t *)(B + f_b2);
+    for (int r = 0; r < 4; ++r) { F.gate_lo[r] = FB.gate_lo[r]; F.gate_hi[r] = FB.gate_hi[r]; }
+    F.n_gate = FB.n_gate;
+    F.ht_key = (const uint64_t *)(B + f_htk);
+    F.ht_begin = (const uint32_t *)(B + f_htb);
+    F.ht_cnt = (const uint32_t *)(B + f_htc);
+    F.ht_mask = FB.ht_mask;
+    F.kl = (const uint32_t *)(B + f_kl);
+    F.as_head = (const uint64_t *)(B + f_ash);
+    F.as_len = (const uint32_t *)(B + f_asl);
+    F.as_use_begin = (const uint32_t *)(B + f_asub);
+    F.as_use_cnt = (const uint32_t *)(B + f_asuc);
+    F.use_pat = (const uint32_t *)(B + f_up);
+    F.use_info0 = (const uint32_t *)(B + f_ui0);
+    F.use_info1 = (const uint32_t *)(B + f_ui1);
+    F.pat_info = T.pat_info;
+    F.pat_rxk = (const uint32_t *)(B + f_rxk);
+    F.pat_boff = (const uint32_t *)(B + f_boff);
+    F.pat_bytes = (const uint8_t *)(B + f_pb);
+    F.pat_cp_off = T.pat_cp_off;
+    F.pat_cps = T.pat_cps;
+    F.pat_sig = (const uint64_t *)(B + f_sig);
+    F.f_count_ge = T.f_count_ge;
+    F.sub_key = T.sub_key;
+    F.sub_begin = T.sub_begin;
+    F.sub_cnt = T.sub_cnt;
+    F.sub_pat = T.sub_pat;
+    F.sub_mask = T.sub_mask;
+    F.word_bits = T.word_bits;
+    F.f_first = f_first;
+    F.empty_pat = empty_pat;
+    h->n_anchor_fast = (int)FB.as_len.size();
+
     hipDeviceProp_t prop;
     HIPCHK(h, hipGetDeviceProperties(&prop, device));
     h->cus = prop.multiProcessorCount;
     int bpc = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_scan_kernel, BLOCK, kScanLds));
     h->blocks_per_cu = bpc > 0 ? bpc : 1;
+    bpc = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_fast_kernel, FK_BLOCK, kFastLds));
+    h->fast_blocks_per_cu = bpc > 0 ? bpc : 1;
     HIPCHK(h, hipEventCreate(&h->ev0));
     HIPCHK(h, hipEventCreate(&h->ev1));
+    HIPCHK(h, hipEventCreate(&h->evg));
     HIPCHK(h, hipEventCreate(&h->ev2));
     *out = h;
     return KW_OK;
 }
 
-// (re)allocate scratch for n_waves waves with out_cap records per wave
-static int ensure_scratch(kw_handle *h, int n_waves, uint32_t out_cap)
+// (re)allocate scratch: nf fast waves + ng generic waves, out_cap records per wave, defer list of dcap docs
+static int ensure_scratch(kw_handle *h, int nf, int ng, uint32_t out_cap, uint32_t dcap)
 {
-    if (h->d_scratch && n_waves <= h->n_waves && out_cap <= h->out_cap) return KW_OK;
-    n_waves = std::max(n_waves, h->n_waves);
+    if (h->d_scratch && nf <= h->nf && ng <= h->ng && out_cap <= h->out_cap && dcap <= h->defer_cap) return KW_OK;
+    nf = std::max(nf, h->nf);
+    ng = std::max(ng, h->ng);
     out_cap = std::max(out_cap, h->out_cap);
+    dcap = std::max(dcap, h->defer_cap);
     if (h->d_scratch) { (void)hipFree(h->d_scratch); h->d_scratch = nullptr; }
     if (h->d_small) { (void)hipFree(h->d_small); h->d_small = nullptr; }
     if (h->d_hits) { (void)hipFree(h->d_hits); h->d_hits = nullptr; }
     const size_t per_items = (size_t)2 * ITEM_CAP * sizeof(uint64_t);
     const size_t per_cps = (size_t)CP_CAP * sizeof(uint32_t);
     const size_t per_blk = (size_t)(CP_CAP / 16 + 2) * sizeof(uint32_t);
+    const size_t per_fcps = (size_t)FK_CP_CAP * sizeof(uint32_t);
     const size_t per_out = (size_t)out_cap * sizeof(kw_hit);
-    size_t total = (size_t)n_waves * (per_items + per_cps + per_blk + per_out) + 4096;
+    const int nw = nf + ng;
+    size_t total = (size_t)ng * (per_items + per_cps + per_blk) + (size_t)nf * (per_fcps + per_blk) +
+                   (size_t)nw * per_out + (size_t)dcap * 4 + 8192;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
     uint8_t *p = (uint8_t *)h->d_scratch;
-    h->S.items = (uint64_t *)p; p += (size_t)n_waves * per_items;
-    h->S.cps = (uint32_t *)p; p += (size_t)n_waves * per_cps;
-    h->S.blkcnt = (uint32_t *)p; p += (size_t)n_waves * per_blk;
-    p = (uint8_t *)(((uintptr_t)p + 255) & ~(uintptr_t)255);
-    h->S.out = (kw_hit *)p;
-    size_t small = 256 + (size_t)n_waves * 4 + 256 + (size_t)(n_waves + 1) * 8 + 256;
+    auto carve = [&](size_t bytes) { uint8_t *r = p; p += (bytes + 255) & ~(size_t)255; return r; };
+    h->S.items = (uint64_t *)carve((size_t)ng * per_items);
+    h->S.cps = (uint32_t *)carve((size_t)ng * per_cps);
+    h->S.blkcnt = (uint32_t *)carve((size_t)ng * per_blk);
+    h->FS.cps = (uint32_t *)carve((size_t)nf * per_fcps);
+    h->FS.cpbase = (uint32_t *)carve((size_t)nf * per_blk);
+    kw_hit *outs = (kw_hit *)carve((size_t)nw * per_out);
+    h->FS.defer_list = (uint32_t *)carve((size_t)dcap * 4);
+    size_t small = 1024 + (size_t)nw * 4 + 256 + (size_t)(nw + 1) * 8 + 256;
     HIPCHK(h, hipMalloc(&h->d_small, small));
     uint8_t *q = (uint8_t *)h->d_small;
-    h->S.status = (uint32_t *)q;                       // 4 x u32
-    h->S.stats = (unsigned long long *)(q + 64);       // 3 x u64
-    h->S.out_cnt = (uint32_t *)(q + 256);
-    h->d_offs = (unsigned long long *)(q + 256 + (((size_t)n_waves * 4 + 255) & ~(size_t)255));
+    h->S.status = (uint32_t *)q;                        // 4 x u32
+    h->FS.status = h->S.status;
+    h->FS.defer_cnt = (uint32_t *)(q + 16);
+    h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
+    h->FS.stats = (unsigned long long *)(q + 128);      // 5 x u64 (fast)
+    uint32_t *cnts = (uint32_t *)(q + 1024);
+    h->FS.out_cnt = cnts;
+    h->S.out_cnt = cnts + nf;
+    h->d_offs = (unsigned long long *)(q + 1024 + (((size_t)nw * 4 + 255) & ~(size_t)255));
+    h->FS.out = outs;
+    h->S.out = outs + (size_t)nf * out_cap;
     h->S.out_cap = out_cap;
-    h->n_waves = n_waves;
+    h->FS.out_cap = out_cap;
+    h->FS.defer_cap = dcap;
+    h->nf = nf;
+    h->ng = ng;
     h->out_cap = out_cap;
-    h->hits_cap = (size_t)n_waves * out_cap;
+    h->defer_cap = dcap;
+    h->hits_cap = (size_t)nw * out_cap;
     HIPCHK(h, hipMalloc(&h->d_hits, h->hits_cap * sizeof(kw_hit) + 16));
     h->scratch_bytes = total;
     return KW_OK;
@@ -466,33 +802,41 @@ static int ensure_scratch(kw_handle *h, int n_waves, uint32_t out_cap)
 static int launch_scan(kw_handle *h)
 {
     hipStream_t st = h->stream;
-    int64_t n_docs = h->n_docs;
-    int n_blocks = (int)std::min<int64_t>((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK,
-                                          (int64_t)h->cus * h->blocks_per_cu);
-    if (n_blocks < 1) n_blocks = 1;
-    const int n_waves = n_blocks * WAVES_PER_BLOCK;
-    int64_t docs_per_wave = (n_docs + n_waves - 1) / n_waves;
-    uint32_t want_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_wave * 48), (int64_t)1 << 26);
-    int rc = ensure_scratch(h, n_waves, std::max(want_cap, h->out_cap));
+    const int64_t n_docs = h->n_docs;
+    int nfb = (int)std::min<int64_t>((n_docs + FK_WAVES - 1) / FK_WAVES, (int64_t)h->cus * h->fast_blocks_per_cu);
+    if (nfb < 1) nfb = 1;
+    const int ngb = std::max(1, std::min(h->cus, (int)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)));
+    const int nf = nfb * FK_WAVES, ng = ngb * WAVES_PER_BLOCK;
+    const int64_t docs_per_wave = (n_docs + nf - 1) / nf;
+    const uint32_t want_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_wave * 48), (int64_t)1 << 26);
+    int rc = ensure_scratch(h, nf, ng, std::max(want_cap, h->out_cap), (uint32_t)std::max<int64_t>(n_docs, 1));
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
+    HIPCHK(h, hipMemsetAsync(h->S.out_cnt, 0, (size_t)ng * 4, st));
     HIPCHK(h, hipEventRecord(h->ev0, st));
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_scan_kernel, dim3(n_blocks), dim3(BLOCK), kScanLds, st, h->T, h->arena, h->doc_off,
-                           n_docs, h->S);
+        hipLaunchKernelGGL(kw_fast_kernel, dim3(nfb), dim3(FK_BLOCK), kFastLds, st, h->FT, h->T, h->arena, h->doc_off,
+                           n_docs, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->ev1, st));
-    // compaction of the per-wave regions
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->S.out_cnt, n_waves, h->S.out_cap,
-                           h->d_offs);
-        hipLaunchKernelGGL(kw_gather_kernel, dim3(n_waves), dim3(256), 0, st, h->S.out, h->S.out_cap, h->S.out_cnt,
+        // the generic kernel redoes every document the fast kernel deferred
+        hipLaunchKernelGGL(kw_scan_kernel, dim3(ngb), dim3(BLOCK), kScanLds, st, h->T, h->arena, h->doc_off, n_docs,
+                           h->S, (const uint32_t *)h->FS.defer_list, (const uint32_t *)h->FS.defer_cnt,
+                           h->FS.defer_cap);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->evg, st));
+    const int nw = nf + ng;
+    if (n_docs > 0) {
+        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->FS.out_cnt, nw, h->out_cap, h->d_offs);
+        hipLaunchKernelGGL(kw_gather_kernel, dim3(nw), dim3(256), 0, st, h->FS.out, h->out_cap, h->FS.out_cnt,
                            h->d_offs, h->d_hits);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->ev2, st));
-    h->launched_waves = n_waves;
+    h->launched_waves = nw;
     return KW_OK;
 }
 
@@ -532,10 +876,10 @@ static int finish(kw_handle *h)
         if (status[0] & ST_OUT_OVERFLOW) {
             // grow the per-wave result regions to the largest count seen and rescan
             std::vector<uint32_t> cnt(h->launched_waves);
-            HIPCHK(h, hipMemcpy(cnt.data(), h->S.out_cnt, cnt.size() * 4, hipMemcpyDeviceToHost));
+            HIPCHK(h, hipMemcpy(cnt.data(), h->FS.out_cnt, cnt.size() * 4, hipMemcpyDeviceToHost));
             uint32_t mx = 0;
             for (uint32_t c : cnt) mx = std::max(mx, c);
-            int rc = ensure_scratch(h, h->n_waves, mx + 1024);
+            int rc = ensure_scratch(h, h->nf, h->ng, mx + 1024, h->defer_cap);
             if (rc) return rc;
             rc = launch_scan(h);
             if (rc) return rc;
@@ -543,7 +887,17 @@ static int finish(kw_handle *h)
         }
         unsigned long long tot = 0;
         HIPCHK(h, hipMemcpy(&tot, h->d_offs + h->launched_waves, sizeof(tot), hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy(h->stats, h->S.stats, sizeof(h->stats), hipMemcpyDeviceToHost));
+        unsigned long long gst[3], fst[8];
+        HIPCHK(h, hipMemcpy(gst, h->S.stats, sizeof(gst), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(fst, h->FS.stats, sizeof(fst), hipMemcpyDeviceToHost));
+        h->stats[0] = fst[0] + gst[0];
+        h->stats[1] = fst[1] + gst[1];
+        h->stats[2] = fst[3] + gst[2];
+        h->stats[3] = fst[2];
+        h->stats[4] = fst[4];
+        h->stats[5] = fst[5];
+        h->stats[6] = fst[6];
+        h->stats[7] = fst[7];
         h->n_hits = (int64_t)tot;
         h->fetched = true;
         return KW_OK;
@@ -577,23 +931,22 @@ extern "C" int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n
     return KW_OK;
 }
 
-extern "C" int kw_stats(kw_handle *h, int64_t *candidates, int64_t *anchor_hits, int64_t *windows)
+extern "C" int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats)
 {
-    if (!h) return KW_EINVAL;
+    if (!h || !stats) return KW_EINVAL;
     int rc = finish(h);
     if (rc) return rc;
-    if (candidates) *candidates = (int64_t)h->stats[0];
-    if (anchor_hits) *anchor_hits = (int64_t)h->stats[1];
-    if (windows) *windows = (int64_t)h->stats[2];
+    for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = (int64_t)h->stats[i];
     return KW_OK;
 }
 
-extern "C" int kw_last_kernel_ms(kw_handle *h, float *scan_ms, float *total_ms)
+extern "C" int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *total_ms)
 {
     if (!h) return KW_EINVAL;
     int rc = finish(h);
     if (rc) return rc;
-    if (scan_ms) HIPCHK(h, hipEventElapsedTime(scan_ms, h->ev0, h->ev1));
+    if (fast_ms) HIPCHK(h, hipEventElapsedTime(fast_ms, h->ev0, h->ev1));
+    if (generic_ms) HIPCHK(h, hipEventElapsedTime(generic_ms, h->ev1, h->evg));
     if (total_ms) HIPCHK(h, hipEventElapsedTime(total_ms, h->ev0, h->ev2));
     return KW_OK;
 }
@@ -615,6 +968,7 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->ev2) (void)hipEventDestroy(h->ev2);
+    if (h->evg) (void)hipEventDestroy(h->evg);
     delete h;
     return KW_OK;
 }

@@ -1,0 +1,708 @@
+// Fast-path kernel (see kwmatch_fast.hpp).  Included after kwmatch_kernels.hpp
+// (shares its wave/text helpers).  One wave owns one document at a time; every
+// rare case (more than 64 anchor uses in a field, a quantified regex name that
+// matched, ...) sends the whole document to the generic kernel instead.
+#pragma once
+#include "kwmatch_fast.hpp"
+#include "kwmatch_kernels.hpp"
+
+// profiling builds: 0 = filter only, 1 = + anchor probe, 2 = + resolve w/o LCS, 3 = full
+#ifndef FK_STAGE
+#define FK_STAGE 3
+#endif
+
+namespace kw {
+
+// ---------------------------------------------------------------- hashing (host + device)
+__host__ __device__ __forceinline__ uint32_t fk_word(uint32_t key4)
+{
+    return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;    // depends on bytes 0..2
+}
+__host__ __device__ __forceinline__ uint32_t fk_bit(uint32_t key4)
+{
+    const uint32_t b3 = key4 >> 24;
+    return (b3 ^ (b3 >> 5)) & 31u;
+}
+__host__ __device__ __forceinline__ uint32_t fk_b2_index(uint32_t key2)
+{
+    return ((key2 & 0xFFFFu) * 40503u) & 0xFFFFu;     // bijection on 16 bits (odd multiplier)
+}
+__host__ __device__ __forceinline__ uint32_t fk_ht_slot(uint64_t k, uint32_t mask)
+{
+    uint64_t x = k * 0x9E3779B97F4A7C15ull;
+    return (uint32_t)(x >> 40) & mask;
+}
+
+// ---------------------------------------------------------------- per-doc state
+struct FastDoc {
+    const uint8_t *arena;
+    int64_t t0, t1, t2;
+    uint32_t doc;
+};
+
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *__restrict__ a, int64_t p)
+{
+    const int64_t a0 = p & ~(int64_t)3;
+    const uint32_t s = (uint32_t)(p & 3);
+    const uint32_t x0 = *(const uint32_t *)(a + a0);
+    const uint32_t x1 = *(const uint32_t *)(a + a0 + 4);
+    return __builtin_amdgcn_alignbyte(x1, x0, s);
+}
+
+// byte-exact compare of text[p, p+len) with pat[0, len)
+__device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_t p, const uint8_t *__restrict__ pat,
+                                           uint32_t len)
+{
+    uint32_t i = 0;
+    for (; i + 4 <= len; i += 4) {
+        const uint32_t t = ld_u32_unaligned(a, p + i);
+        const uint32_t q = (uint32_t)pat[i] | ((uint32_t)pat[i + 1] << 8) | ((uint32_t)pat[i + 2] << 16) |
+                           ((uint32_t)pat[i + 3] << 24);
+        if (t != q) return false;
+    }
+    for (; i < len; ++i)
+        if (a[p + i] != pat[i]) return false;
+    return true;
+}
+
+// '.'-wildcard regex (atoms LIT/ANY, no quantifiers) anchored at byte p; returns end byte or -1
+__device__ int64_t wild_match(const DevTables &T, const uint8_t *__restrict__ a, int64_t p, int64_t fe, uint32_t pat)
+{
+    const uint32_t ab = T.rx_off[pat], ae = T.rx_off[pat + 1];
+    int64_t b = p;
+    for (uint32_t k = ab; k < ae; ++k) {
+        if (b >= fe) return -1;
+        const int4 at = T.rx_atoms[k];
+        uint32_t cp;
+        const uint32_t len = decode_at(a, b, fe, &cp);
+        if (at.x == KW_RX_LIT) {
+            if (cp != (uint32_t)at.y) return -1;
+        } else if (cp == '\n') {
+            return -1;
+        }
+        b += len;
+    }
+    return b;
+}
+
+// ---------------------------------------------------------------- probe one candidate (this lane)
+__device__ void fast_probe(const FastTables &FT, const DevTables &T, const FastScratch &S, const FastDoc &D, int64_t p,
+                           uint32_t klen, uint64_t *items, uint32_t *icnt, uint32_t *dflag,
+                           unsigned long long &nanchor)
+{
+    const uint8_t *__restrict__ arena = D.arena;
+    const int f = p < D.t1 ? 0 : 1;
+    const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+    if (p + (klen == 2 ? 2 : 3) > fe) return;   // shortest anchor this candidate can start
+    const uint32_t lo = ld_u32_unaligned(arena, p), hi = ld_u32_unaligned(arena, p + 4);
+    const uint64_t h8 = (uint64_t)lo | ((uint64_t)hi << 32);
+    // probe the lengths this candidate can start: 4 (and 3) from the 4-byte filter, 2 from the gate
+    for (uint32_t L = klen; L >= (klen == 2 ? 2u : 3u); --L) {
+        if (p + (int64_t)L > fe) continue;
+        const uint64_t key = ((uint64_t)L << 32) | (h8 & ((1ull << (8 * L)) - 1));
+        uint32_t slot = fk_ht_slot(key, FT.ht_mask);
+        uint32_t kb = 0, kc = 0;
+        for (;;) {
+            const uint64_t kk = FT.ht_key[slot];
+            if (kk == key) { kb = FT.ht_begin[slot]; kc = FT.ht_cnt[slot]; break; }
+            if (kk == ~0ull) break;
+            slot = (slot + 1) & FT.ht_mask;
+        }
+        for (uint32_t t = 0; t < kc; ++t) {
+            const uint32_t a = FT.kl[kb + t];
+            const uint32_t alen = FT.as_len[a];
+            if (p + (int64_t)alen > fe) continue;
+            const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
+            if ((h8 ^ FT.as_head[a]) & m8) continue;
+            ++nanchor;
+            const uint32_t ub = FT.as_use_begin[a], uc = FT.as_use_cnt[a];
+            for (uint32_t u = ub; u < ub + uc; ++u) {
+                const uint32_t i0 = FT.use_info0[u], i1 = FT.use_info1[u];
+                const uint32_t kind = i0 & 0xFF, aoff = (i0 >> 8) & 0xFF, sboff = i0 >> 16;
+                const uint32_t sblen = i1 & 0xFFFF;
+                const uint32_t pat = FT.use_pat[u];
+                const int64_t s0 = p - (int64_t)aoff;
+                if (s0 < fb) continue;
+                if (kind == FU_RXW) {
+                    if (wild_match(T, arena, s0, fe, pat) < 0) continue;
+                } else {
+                    if (s0 + (int64_t)sblen > fe) continue;
+                    const uint32_t pi = FT.pat_info[pat];
+                    if (kind == FU_PIECE) {
+                        // pieces of names that only allow exact interior windows matter near the edges only
+                        const uint32_t m = pi_m(pi);
+                        if (20u * 1u >= m) {   // kfull(m) == 0  <=>  m <= 20
+                            const int64_t near = 4 * (int64_t)m + 4;
+                            if (s0 - fb >= near && fe - (s0 + (int64_t)sblen) >= near) continue;
+                        }
+                    }
+                    if (!span_equal(arena, s0, FT.pat_bytes + FT.pat_boff[pat] + sboff, sblen)) continue;
+                    if (kind == FU_UPPER) {
+                        const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
+                        const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
+                        if (wp == wf) continue;
+                        bool wn = false;
+                        if (s0 + (int64_t)sblen < fe) {
+                            uint32_t c;
+                            decode_at(arena, s0 + sblen, fe, &c);
+                            wn = is_word_cp(T, c);
+                        }
+                        if (wn == wl) continue;
+                    }
+                }
+                const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(s0 - fb) << IT_POS_SHIFT) |
+                                      ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
+                const uint32_t idx = atomicAdd(&icnt[f], 1u);
+                if (idx < (uint32_t)FK_ITEMS) items[f * FK_ITEMS + idx] = item;
+                else atomicOr(dflag, 1u);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- field helpers
+// code points of a field: ASCII fields are their byte length; others are counted
+__device__ uint32_t field_cp_count(const uint8_t *__restrict__ arena, int64_t fb, int64_t fe, bool ascii)
+{
+    const int64_t L = fe - fb;
+    if (ascii) return (uint32_t)L;
+    const int lane = lane_id();
+    uint32_t cnt = 0;
+    for (int64_t b0 = 0; b0 < L; b0 += WAVE) {
+        const int64_t i = b0 + lane;
+        const bool lead = i < L && ((arena[fb + i] & 0xC0) != 0x80);
+        cnt += (uint32_t)__popcll(__ballot(lead));
+    }
+    return cnt;
+}
+
+__device__ bool field_is_ascii(const uint8_t *__restrict__ arena, int64_t fb, int64_t fe)
+{
+    const int lane = lane_id();
+    bool hi = false;
+    for (int64_t i = fb + lane; i < fe; i += WAVE) hi |= arena[i] >= 0x80;
+    return __ballot(hi) == 0;
+}
+
+// text code point i of the field (ASCII: byte; else decoded scratch)
+__device__ __forceinline__ uint32_t fk_cp(const FieldCtx &F, int64_t i)
+{
+    if (i < 0 || i >= (int64_t)F.n) return 0xFFFFFFFFu;
+    return F.ascii ? (uint32_t)F.arena[F.fb + i] : F.cps[i];
+}
+
+// ---------------------------------------------------------------- wave-cooperative LCS (ballot)
+// V-update with needle bit-vector from a ballot over lanes holding the needle
+__device__ __forceinline__ uint64_t lcs_ballot_step(uint64_t V, uint32_t lanechar, uint32_t c, uint64_t needle_mask)
+{
+    const uint64_t M = __ballot(lanechar == c) & needle_mask;
+    const uint64_t U = V & M;
+    return (V + U) | (V - U);
+}
+
+// Verify one PIECE item of pattern P (needle = name, m < n).  All lanes call.
+// nm: lane i holds name[i] (i < m).  Returns true if some window of the
+// partial_ratio family containing the piece passes.
+__device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint32_t q, uint32_t o, uint32_t pl,
+                                unsigned long long &nwin)
+{
+    if (FK_STAGE < 3) return false;
+    const int lane = lane_id();
+    const uint32_t n = F.n;
+    const uint64_t needle = low_mask(m);
+    const uint32_t k = kfull(m);
+    if (k > 0) {
+        // band test: every name char matched by a passing full window lies within +-2k of base+i
+        const int64_t base = (int64_t)q - (int64_t)o;
+        bool hit = false;
+        if (lane < (int)m) {
+            for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) hit |= (fk_cp(F, base + lane + t) == nm);
+        }
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(hit));
+        if (cnt + k >= m) {
+            int64_t pmin = base - k, pmax = base + k;
+            if (pmin < 0) pmin = 0;
+            if (pmax > (int64_t)(n - m)) pmax = (int64_t)(n - m);
+            for (int64_t p = pmin; p <= pmax; ++p) {
+                // text chars of the window, one per lane (lane j < m)
+                const uint32_t tc = (lane < (int)m) ? fk_cp(F, p + lane) : 0xFFFFFFFEu;
+                uint64_t V = ~0ull;
+                for (uint32_t j = 0; j < m; ++j) {
+                    const uint32_t c = __builtin_amdgcn_readlane(tc, j);
+                    V = lcs_ballot_step(V, nm, c, needle);
+                }
+                ++nwin;
+                const uint32_t L = (uint32_t)__popcll(~V & needle);
+                if (20u * (m - L) < m) return true;
+            }
+        }
+    }
+    if (q + pl + 1 <= m) {   // prefixes text[:w], w in [1, m)
+        const uint32_t tc = (lane < (int)m) ? fk_cp(F, lane) : 0xFFFFFFFEu;
+        uint64_t V = ~0ull;
+        ++nwin;
+        for (uint32_t w = 1; w < m; ++w) {
+            V = lcs_ballot_step(V, nm, __builtin_amdgcn_readlane(tc, w - 1), needle);
+            if (passes((uint32_t)__popcll(~V & needle), m, w)) return true;
+        }
+    }
+    if (q + m > n) {         // suffixes text[i:], i in (n-m, n): reversed needle and text
+        const uint32_t nr = __shfl(nm, (int)m - 1 - lane, WAVE);
+        const uint32_t tc = (lane < (int)m) ? fk_cp(F, (int64_t)n - 1 - lane) : 0xFFFFFFFEu;
+        uint64_t V = ~0ull;
+        ++nwin;
+        for (uint32_t kk = 1; kk < m; ++kk) {
+            V = lcs_ballot_step(V, nr, __builtin_amdgcn_readlane(tc, kk - 1), needle);
+            if (passes((uint32_t)__popcll(~V & needle), m, kk)) return true;
+        }
+    }
+    return false;
+}
+
+// Short field (n <= 64 code points) vs a longer-or-equal name: needle = field.
+// fc: lane i holds field[i] (i < n).  nm_ptr: the name's code points (m >= n).
+__device__ bool fk_short_decide(uint32_t fc, uint32_t n, const uint32_t *__restrict__ nm_ptr, uint32_t m, bool *exact,
+                                unsigned long long &nwin)
+{
+    *exact = false;
+    if (FK_STAGE < 3) return false;
+    const int lane = lane_id();
+    const uint64_t needle = low_mask(n);
+    uint64_t Vf = ~0ull;
+    for (uint32_t p = 0; p + n <= m; ++p) {        // full windows of the name
+        uint64_t V = ~0ull;
+        for (uint32_t j = 0; j < n; ++j) V = lcs_ballot_step(V, fc, nm_ptr[p + j], needle);
+        ++nwin;
+        if (p == 0) Vf = V;
+        const uint32_t L = (uint32_t)__popcll(~V & needle);
+        if (L == n && m == n) *exact = true;
+        if (20u * (n - L) < n) return true;
+    }
+    {   // prefixes of the name
+        uint64_t V = ~0ull;
+        for (uint32_t i = 1; i < n; ++i) {
+            V = lcs_ballot_step(V, fc, nm_ptr[i - 1], needle);
+            if (passes((uint32_t)__popcll(~V & needle), n, i)) return true;
+        }
+    }
+    const uint32_t fr = __shfl(fc, (int)n - 1 - lane, WAVE);
+    uint64_t Vr = ~0ull;
+    {   // suffixes of the name (reversed needle)
+        uint64_t V = ~0ull;
+        for (uint32_t kk = 1; kk < n; ++kk) {
+            V = lcs_ballot_step(V, fr, nm_ptr[m - kk], needle);
+            if (passes((uint32_t)__popcll(~V & needle), n, kk)) return true;
+        }
+    }
+    if (m == n) {   // swapped run: needle = name, windows = prefixes / suffixes of the field
+        for (uint32_t j = 0; j < m; ++j) Vr = lcs_ballot_step(Vr, fr, nm_ptr[m - 1 - j], needle);
+        for (uint32_t i = 1; i < n; ++i) {
+            if (passes((uint32_t)__popcll(~Vf & low_mask(i)), m, i)) return true;
+            if (passes((uint32_t)__popcll(~Vr & low_mask(n - i)), m, n - i)) return true;
+        }
+    }
+    (void)lane;
+    return false;
+}
+
+}  // namespace kw
+
+namespace kw {
+
+// ---------------------------------------------------------------- fast resolve of one field
+// Returns false if the document must go to the generic kernel.
+__device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const FastScratch &S, const DevScratch &GS,
+                                 FieldCtx &F, OutCtx &O, const uint64_t *items_lds, uint32_t N, uint32_t *cps,
+                                 uint32_t *blkcnt, bool maybe_nonascii, unsigned long long &nver,
+                                 unsigned long long &nwin)
+{
+    const int lane = lane_id();
+    // ---- field facts (code points, ASCII) on demand
+    const int64_t flen = F.fe - F.fb;
+    F.ascii = maybe_nonascii ? field_is_ascii(F.arena, F.fb, F.fe) : true;
+    const bool maybe_short = flen <= 4 * MAXM;
+    F.n = (F.ascii || (N == 0 && !maybe_short)) ? (uint32_t)flen : field_cp_count(F.arena, F.fb, F.fe, false);
+    const bool is_short = F.n <= (uint32_t)MAXM;
+    if (N == 0 && !is_short) return 0;
+    if (!F.ascii) {
+        if (flen > (int64_t)FK_CP_CAP) return 1;
+        decode_field(GS, F.arena, F.fb, F.fe, cps, blkcnt);
+        F.cps = cps;
+        F.blkcnt = blkcnt;
+    }
+    if (N > 0) {
+        uint64_t it = (lane < (int)N) ? items_lds[lane] : ~0ull;
+        it = wave_sort_reg(it);
+        const bool valid = lane < (int)N;
+        const uint32_t pat = valid ? it_pat(it) : 0xFFFFFu;
+        const uint32_t kind = it_kind(it);
+        const uint32_t bpos = it_pos(it);
+        const uint32_t use = it_use(it);
+        const uint32_t pi = valid ? FT.pat_info[pat] : 0u;
+        const uint32_t rxk = valid ? FT.pat_rxk[pat] : 0u;
+        const uint32_t m = pi_m(pi);
+        const bool fuzzy = (pi & PI_FUZZY) != 0;
+        const uint32_t prev_pat = (uint32_t)__shfl_up((int)pat, 1, WAVE);
+        const bool head = valid && (lane == 0 || prev_pat != pat);
+        const uint64_t heads = __ballot(head);
+        const uint64_t below = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+        const int gs = 63 - __builtin_clzll(heads & below | 1ull);
+        const uint64_t after = heads & ~below;
+        const int ge = after ? __builtin_ctzll(after) : (int)N;
+        const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
+        // the short path owns fuzzy names at least as long as the field
+        const bool live = valid && !(fuzzy && m >= F.n);
+        const uint64_t fullm = __ballot(live && kind == FU_FULL);
+        const bool decided_full = (fullm & gmask) != 0;
+        // ---- verification of pieces of undecided fuzzy names (wave-serial over such items)
+        uint64_t vneed = __ballot(live && fuzzy && !decided_full && kind == FU_PIECE);
+        uint64_t decided_v = 0;   // bit per lane: its group got decided by a window
+        while (vneed) {
+            const int l = __builtin_ctzll(vneed);
+            vneed &= vneed - 1;
+            const uint64_t lg = __shfl(gmask, l, WAVE);
+            if (decided_v & lg) continue;                       // group already decided
+            const uint32_t P = (uint32_t)__shfl((int)pat, l, WAVE);
+            const uint32_t mm = (uint32_t)__shfl((int)m, l, WAVE);
+            const uint32_t uu = (uint32_t)__shfl((int)use, l, WAVE);
+            const uint32_t bp = (uint32_t)__shfl((int)bpos, l, WAVE);
+            const uint32_t info1 = FT.use_info1[uu];
+            const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
+            const uint32_t nm = (lane < (int)mm) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+            ++nver;
+            if (fk_verify_piece(F, nm, mm, to_cp(F, bp), o, pl, nwin)) decided_v |= lg;
+        }
+        const bool decided = decided_full || ((decided_v >> lane) & 1ull);
+        // ---- positions: items that report re.finditer positions
+        const bool relevant = live && ((!fuzzy && kind == FU_UPPER) ||
+                                       (fuzzy && decided && rxk == RXK_LITERAL && kind == FU_FULL) ||
+                                       (fuzzy && decided && rxk == RXK_WILD && kind == FU_RXW));
+        // a decided fuzzy name whose regex needs the generic engine
+        if (__ballot(live && fuzzy && decided && rxk == RXK_GENERIC)) return 2;
+        const uint32_t cpos = relevant ? to_cp(F, bpos) : 0u;
+        const uint64_t relm = __ballot(relevant);
+        // leftmost non-overlapping selection per group (match length m code points)
+        const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
+        const int pr = prevrel ? 63 - __builtin_clzll(prevrel) : -1;
+        const uint32_t pcpos = (uint32_t)__shfl((int)cpos, pr < 0 ? lane : pr, WAVE);
+        const bool overlap = relevant && pr >= 0 && cpos < pcpos + m;
+        uint64_t keep = relm;
+        if (__ballot(overlap)) {
+            // rare: resolve the greedy chain serially
+            keep = 0;
+            uint64_t mm2 = relm;
+            int cur_head = -1;
+            uint32_t last_end = 0;
+            while (mm2) {
+                const int l = __builtin_ctzll(mm2);
+                mm2 &= mm2 - 1;
+                const int h = __shfl(gs, l, WAVE);
+                const uint32_t s = (uint32_t)__shfl((int)cpos, l, WAVE);
+                const uint32_t len = (uint32_t)__shfl((int)m, l, WAVE);
+                if (h != cur_head) { cur_head = h; last_end = 0; keep |= 1ull << l; last_end = s + len; continue; }
+                if (s >= last_end) { keep |= 1ull << l; last_end = s + len; }
+            }
+        }
+        const bool k_me = (keep >> lane) & 1ull;
+        emit_hits(O, GS, k_me, F.doc, pat, cpos, F.field);
+        // decided fuzzy groups without any reported position: `name: []`
+        const uint64_t keptg = keep;   // per group: any kept?
+        const bool none_kept = (keptg & gmask) == 0;
+        emit_hits(O, GS, head && live && fuzzy && decided && none_kept, F.doc, pat, KW_NOPOS, F.field);
+    }
+    // ---- short field: the field is the needle, the longer names are the haystacks
+    if (is_short) {
+        const uint32_t n = F.n;
+        if (n == 0) {
+            if (FT.empty_pat >= 0) emit_hits(O, GS, lane == 0, F.doc, (uint32_t)FT.empty_pat, 0u, F.field);
+            return 0;
+        }
+        const uint32_t fc = (lane < (int)n) ? fk_cp(F, lane) : 0xFFFFFFFCu;
+        if (n <= (uint32_t)SHORT_EXACT_MAX) {
+            uint64_t h = 0;
+            for (uint32_t i = 0; i < n; ++i) h = h * SUB_B + (uint32_t)__builtin_amdgcn_readlane(fc, i);
+            const uint64_t key = (h + (uint64_t)n * 0x9E3779B97F4A7C15ull) | 1ull;
+            uint32_t slot = (uint32_t)(key >> 32) & FT.sub_mask;
+            uint32_t b = 0, cnt = 0;
+            for (;;) {
+                const uint64_t kk = FT.sub_key[slot];
+                if (kk == key) { b = FT.sub_begin[slot]; cnt = FT.sub_cnt[slot]; break; }
+                if (kk == 0) break;
+                slot = (slot + 1) & FT.sub_mask;
+            }
+            b = __builtin_amdgcn_readfirstlane(b);
+            cnt = __builtin_amdgcn_readfirstlane(cnt);
+            uint32_t fch[SHORT_EXACT_MAX];
+#pragma unroll
+            for (int j = 0; j < SHORT_EXACT_MAX; ++j) fch[j] = __builtin_amdgcn_readlane(fc, j);
+            for (uint32_t c0 = 0; c0 < cnt; c0 += WAVE) {
+                const uint32_t idx = c0 + lane;
+                bool hit = false, exact = false;
+                uint32_t P = 0, rk = 0;
+                if (idx < cnt) {
+                    P = FT.sub_pat[b + idx];
+                    const uint32_t m = pi_m(FT.pat_info[P]);
+                    rk = FT.pat_rxk[P];
+                    const uint32_t *nmp = FT.pat_cps + FT.pat_cp_off[P];
+                    for (uint32_t p = 0; p + n <= m && !hit; ++p) {
+                        bool eq = true;
+#pragma unroll
+                        for (int j = 0; j < SHORT_EXACT_MAX; ++j)
+                            if ((uint32_t)j < n) eq = eq && nmp[p + j] == fch[j];
+                        hit = eq;
+                    }
+                    exact = hit && m == n;
+                }
+                if (__ballot(hit && rk == RXK_GENERIC)) return 2;
+                // literal: position 0 iff the name equals the field; wildcard: iff it matches at 0
+                bool at0 = false;
+                if (hit && rk == RXK_WILD) at0 = wild_match(T, F.arena, F.fb, F.fe, P) == F.fe;
+                if (hit && rk == RXK_LITERAL) at0 = exact;
+                emit_hits(O, GS, hit, F.doc, P, at0 ? 0u : KW_NOPOS, F.field);
+            }
+            return 0;
+        }
+        // signature of the field's characters
+        uint64_t fsig = 0;
+        {
+            uint64_t bit = (lane < (int)n) ? (1ull << (fc & 63)) : 0ull;
+            for (int d = 1; d < WAVE; d <<= 1) bit |= __shfl_xor(bit, d, WAVE);
+            fsig = bit;
+        }
+        const uint32_t allow = (2 * n - 1) / 20;   // unmatched field chars any passing window allows
+        const uint32_t count = (uint32_t)FT.f_count_ge[n];
+        for (uint32_t c0 = 0; c0 < count; c0 += WAVE) {
+            const uint32_t idx = c0 + lane;
+            bool cand = false;
+            if (idx < count) {
+                const uint64_t ns = FT.pat_sig[FT.f_first + idx];
+                cand = (uint32_t)__popcll(fsig & ~ns) <= allow;
+            }
+            uint64_t cm = __ballot(cand);
+            while (cm) {
+                const int l = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                const uint32_t P = (uint32_t)FT.f_first + c0 + (uint32_t)l;
+                const uint32_t m = pi_m(FT.pat_info[P]);
+                bool exact = false;
+                ++nver;
+                if (!fk_short_decide(fc, n, FT.pat_cps + FT.pat_cp_off[P], m, &exact, nwin)) continue;
+                const uint32_t rk = FT.pat_rxk[P];
+                if (rk == RXK_GENERIC) return 2;
+                bool at0 = false;
+                if (rk == RXK_WILD) at0 = wild_match(T, F.arena, F.fb, F.fe, P) == F.fe;
+                else at0 = exact;
+                emit_hits(O, GS, lane == 0, F.doc, P, at0 ? 0u : KW_NOPOS, F.field);
+            }
+        }
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------- the fast kernel
+__global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                           const int64_t *__restrict__ off, int64_t n_docs,
+                                                           FastScratch S, DevScratch GS)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    uint32_t *filt = (uint32_t *)smem_raw;
+    uint32_t *b2 = filt + FK_FILT_WORDS;
+    uint64_t *items_all = (uint64_t *)(b2 + FK_B2_WORDS);                 // FK_WAVES * 2 * FK_ITEMS
+    uint32_t *cand_all = (uint32_t *)(items_all + FK_WAVES * 2 * FK_ITEMS); // FK_WAVES * FK_CAND
+    uint32_t *cnt_all = cand_all + FK_WAVES * FK_CAND;                      // FK_WAVES * 4
+
+    for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FK_BLOCK) filt[i] = FT.filt[i];
+    for (int i = threadIdx.x; i < FK_B2_WORDS; i += FK_BLOCK) b2[i] = FT.b2[i];
+    __syncthreads();
+
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t wave = (int64_t)blockIdx.x * FK_WAVES + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * FK_WAVES;
+    uint64_t *items = items_all + wib * 2 * FK_ITEMS;
+    uint32_t *cand = cand_all + wib * FK_CAND;
+    uint32_t *icnt = cnt_all + wib * 4;       // [0],[1] item counts, [2] defer flag
+    uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
+    uint32_t *blkcnt = S.cpbase + (size_t)wave * (CP_CAP / 16 + 2);
+
+    OutCtx O;
+    O.out = S.out + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    unsigned long long ncand = 0, nanchor = 0, nver = 0, nwin = 0, ndefer = 0;
+    unsigned long long ndef_items = 0, ndef_cp = 0, ndef_rx = 0;
+
+    for (int64_t d = wave; d < n_docs; d += n_waves) {
+        FastDoc D;
+        D.arena = arena;
+        D.t0 = off[2 * d];
+        D.t1 = off[2 * d + 1];
+        D.t2 = off[2 * d + 2];
+        D.doc = (uint32_t)d;
+        if (lane < 4) icnt[lane] = 0;
+        wave_sync();
+        const uint32_t out_mark = O.n;
+        bool defer = (D.t1 - D.t0 > MAX_FIELD_BYTES) || (D.t2 - D.t1 > MAX_FIELD_BYTES);
+        bool na0 = false, na1 = false;
+        const int64_t base = D.t0 & ~(int64_t)15;
+        for (int64_t blk = base; blk < D.t2 && !defer; blk += SCAN_TILE) {
+            const int64_t lp = blk + lane * 16;
+            uint32_t W[5];
+            if (lp < D.t2) {
+                const uint4 v = *(const uint4 *)(arena + lp);
+                W[0] = v.x; W[1] = v.y; W[2] = v.z; W[3] = v.w;
+            } else {
+                W[0] = W[1] = W[2] = W[3] = 0;
+            }
+            W[4] = (uint32_t)__shfl_down((int)W[0], 1, WAVE);
+            if (lane == WAVE - 1) {
+                const int64_t q = blk + SCAN_TILE;
+                W[4] = (q < D.t2) ? *(const uint32_t *)(arena + q) : 0u;
+            }
+            // lane-local position masks
+            const int64_t rel0 = D.t0 - lp, rel2 = D.t2 - lp, rel1 = D.t1 - lp;
+            const int jlo = rel0 <= 0 ? 0 : (rel0 >= 16 ? 16 : (int)rel0);
+            const int jhi = rel2 <= 0 ? 0 : (rel2 >= 16 ? 16 : (int)rel2);
+            uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
+            // a 2-byte match cannot start on the last byte of a field
+            if (rel1 - 1 >= 0 && rel1 - 1 < 16) valid &= ~(1u << (rel1 - 1));
+            if (rel2 - 1 >= 0 && rel2 - 1 < 16) valid &= ~(1u << (rel2 - 1));
+            // non-ASCII bytes: attribute to the field(s) this lane's chunk covers
+            if (((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) && valid) {
+                if (rel1 > 0) na0 = true;
+                if (rel1 < 16) na1 = true;
+            }
+            uint32_t hit = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
+                const uint32_t w = filt[fk_word(key)];
+                hit |= ((w >> fk_bit(key)) & 1u) << j;
+            }
+            hit &= valid;
+            // 2-byte anchors: byte-class gate, then the exact bigram table
+            uint32_t gate = 0;
+            if (FT.n_gate != 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t w = W[k];
+                    uint32_t in80 = 0;
+                    if (FT.n_gate < 0) {
+                        in80 = 0x80808080u;
+                    } else {
+                        const uint32_t t = w & 0x7F7F7F7Fu;
+                        for (int r = 0; r < FT.n_gate; ++r) {
+                            const uint32_t a = t + (0x80u - FT.gate_lo[r]) * 0x01010101u;
+                            const uint32_t bb = t + (0x7Fu - FT.gate_hi[r]) * 0x01010101u;
+                            in80 |= a & ~bb & ~w & 0x80808080u;
+                        }
+                    }
+                    while (in80) {
+                        const int bi = __builtin_ctz(in80) >> 3;
+                        in80 &= in80 - 1;
+                        const int j = 4 * k + bi;
+                        const uint32_t key = __builtin_amdgcn_alignbyte(W[k + 1], W[k], bi) & 0xFFFFu;
+                        const uint32_t x = fk_b2_index(key);
+                        if ((b2[x >> 5] >> (x & 31)) & 1u) gate |= 1u << j;
+                    }
+                }
+                gate &= valid;
+            }
+            // compaction of candidates: entry = (rel pos << 1) | (2-byte gate)
+            const int c = __popc(hit) + __popc(gate);
+            int total;
+            const int ex = wave_excl_scan(c, &total);
+            if (total == 0) continue;
+            ncand += (lane == 0) ? (unsigned long long)total : 0ull;
+            for (int rb = 0; rb < total; rb += FK_CAND) {
+                int k = ex;
+                uint32_t hm = hit, gm = gate;
+                while (hm) {
+                    const int j = __ffs(hm) - 1;
+                    hm &= hm - 1;
+                    if (k >= rb && k < rb + FK_CAND) cand[k - rb] = ((uint32_t)(lp + j - D.t0) << 1);
+                    ++k;
+                }
+                while (gm) {
+                    const int j = __ffs(gm) - 1;
+                    gm &= gm - 1;
+                    if (k >= rb && k < rb + FK_CAND) cand[k - rb] = ((uint32_t)(lp + j - D.t0) << 1) | 1u;
+                    ++k;
+                }
+                wave_sync();
+                const int lim = (total - rb) < FK_CAND ? (total - rb) : FK_CAND;
+                for (int i0 = 0; i0 < lim; i0 += WAVE) {
+                    const int i = i0 + lane;
+                    if (i < lim) {
+                        const uint32_t e = cand[i];
+                        if (FK_STAGE >= 1)
+                            fast_probe(FT, T, S, D, D.t0 + (e >> 1), (e & 1u) ? 2u : 4u, items, icnt, &icnt[2],
+                                       nanchor);
+                    }
+                }
+                wave_sync();
+            }
+            defer = icnt[2] != 0;
+            defer = __builtin_amdgcn_readfirstlane((int)defer) != 0;
+            if (defer) ++ndef_items;
+        }
+        wave_sync();
+        if (!defer) {
+            const uint32_t N0 = __builtin_amdgcn_readfirstlane(icnt[0]);
+            const uint32_t N1 = __builtin_amdgcn_readfirstlane(icnt[1]);
+            const bool mna[2] = {__ballot(na0) != 0, __ballot(na1) != 0};
+            for (int f = 0; f < 2 && !defer; ++f) {
+                FieldCtx F;
+                F.arena = arena;
+                F.fb = f ? D.t1 : D.t0;
+                F.fe = f ? D.t2 : D.t1;
+                F.cps = cps;
+                F.blkcnt = blkcnt;
+                F.doc = D.doc;
+                F.field = (uint32_t)f;
+                F.ascii = true;
+                F.n = 0;
+                const uint32_t N = f ? N1 : N0;
+                const int rs = FK_STAGE < 2 ? 0 : fk_resolve_field(FT, T, S, GS, F, O, items + f * FK_ITEMS, N,
+                                                                   cps, blkcnt, mna[f], nver, nwin);
+                if (rs) {
+                    defer = true;
+                    if (rs == 1) ++ndef_cp;
+                    else ++ndef_rx;
+                }
+            }
+        }
+        if (defer) {
+            O.n = out_mark;   // drop this doc's partial records; the generic kernel redoes it
+            ++ndefer;
+            if (lane == 0) {
+                const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
+                else atomicOr(&GS.status[0], ST_ITEM_OVERFLOW);
+            }
+        }
+    }
+    if (lane == 0) S.out_cnt[wave] = O.n;
+    unsigned long long a = nanchor, v = nver, w = nwin;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        a += __shfl_xor(a, dd, WAVE);
+        v += __shfl_xor(v, dd, WAVE);
+        w += __shfl_xor(w, dd, WAVE);
+    }
+    if (lane == 0) {
+        atomicAdd(&S.stats[0], ncand);
+        atomicAdd(&S.stats[1], a);
+        atomicAdd(&S.stats[2], v / WAVE);
+        atomicAdd(&S.stats[3], w / WAVE);
+        atomicAdd(&S.stats[4], ndefer);
+        atomicAdd(&S.stats[5], ndef_items);
+        atomicAdd(&S.stats[6], ndef_cp);
+        atomicAdd(&S.stats[7], ndef_rx);
+    }
+}
+
+constexpr size_t kFastLds = (size_t)FK_FILT_WORDS * 4 + (size_t)FK_B2_WORDS * 4 +
+                            (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_CAND * 4 + 4 * 4);
+
+}  // namespace kw

@@ -25,6 +25,11 @@
 #pragma once
 #include "kwmatch_device.hpp"
 
+// profiling builds: 0 = filter only, 1 = + anchor probe, 2 = + resolve w/o LCS, 3 = full
+#ifndef KW_STAGE
+#define KW_STAGE 3
+#endif
+
 namespace kw {
 
 // ------------------------------------------------------------------ wave utils
@@ -378,6 +383,7 @@ namespace kw {
 __device__ bool verify_piece(const DevTables &T, const FieldCtx &F, uint32_t P, uint32_t m, uint32_t q, uint32_t o,
                              uint32_t plen, unsigned long long &nwin)
 {
+    if (KW_STAGE < 3) return false;
     const uint32_t n = F.n;
     const uint64_t mask = low_mask(m);
     const uint32_t k = kfull(m);
@@ -752,8 +758,15 @@ __device__ void process_candidate(const DevTables &T, const DevScratch &S, const
 }
 
 __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8_t *__restrict__ arena,
-                                                        const int64_t *__restrict__ off, int64_t n_docs, DevScratch S)
+                                                        const int64_t *__restrict__ off, int64_t n_docs, DevScratch S,
+                                                        const uint32_t *__restrict__ doc_list,
+                                                        const uint32_t *__restrict__ list_cnt, uint32_t list_cap)
 {
+    // doc_list != nullptr: process only the listed documents (the fast kernel's deferrals)
+    if (doc_list) {
+        uint32_t c = *list_cnt;
+        n_docs = c < list_cap ? c : list_cap;
+    }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     uint32_t *filt = (uint32_t *)smem_raw;
     uint64_t *pm_all = (uint64_t *)(filt + FILT_WORDS);                 // WAVES*128
@@ -785,7 +798,8 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
     O.n = 0;
     unsigned long long ncand = 0, nanchor = 0, nwin = 0;
 
-    for (int64_t d = wave; d < n_docs; d += n_waves) {
+    for (int64_t di = wave; di < n_docs; di += n_waves) {
+        const int64_t d = doc_list ? (int64_t)doc_list[di] : di;
         const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
         if (t1 - t0 > MAX_FIELD_BYTES || t2 - t1 > MAX_FIELD_BYTES) {
             if (lane == 0) atomicOr(&S.status[0], ST_FIELD_TOO_LONG);
@@ -842,7 +856,7 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
             wave_sync();
             for (int i0 = 0; i0 < total; i0 += WAVE) {
                 const int i = i0 + lane;
-                if (i < total) process_candidate(T, S, arena, t0, t1, t2, cand[i], items0, items1, icnt, nanchor);
+                if (KW_STAGE >= 1 && i < total) process_candidate(T, S, arena, t0, t1, t2, cand[i], items0, items1, icnt, nanchor);
             }
             wave_sync();
         }
@@ -868,7 +882,7 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
             const uint32_t N = f ? N1 : N0;
             if (N == 0 && F.n > (uint32_t)MAXM) continue;
             if (!F.ascii) decode_field(S, arena, F.fb, F.fe, cps, blkcnt);
-            resolve_field(T, S, F, O, f ? items1 : items0, N, lpm, lext_cp, lext_mask, nwin);
+            if (KW_STAGE >= 2) resolve_field(T, S, F, O, f ? items1 : items0, N, lpm, lext_cp, lext_mask, nwin);
         }
     }
     if (lane == 0) {

@@ -32,7 +32,7 @@ from dateutil import parser
 
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
-from .matcher import GpuMatcher, assemble_ticker_matches, field_str, group_hits, pack_fields
+from .matcher import GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits, pack_fields
 
 OUTPUT_COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source',
                   'source_url', 'article_text')
@@ -84,12 +84,17 @@ def _kb_fingerprint(processed_data) -> str:
     return h.hexdigest()
 
 
-def get_matcher(processed_data, device: Optional[int] = None) -> GpuMatcher:
-    """Compile (once) the knowledge base into a libkwmatch handle."""
+def get_matcher(processed_data, device: Optional[int] = None, sample_texts=None) -> GpuMatcher:
+    """Compile (once) the knowledge base into a libkwmatch handle.
+
+    ``sample_texts`` (the first chunk's articles) tunes the anchor choice to
+    the corpus; results do not depend on it.
+    """
     key = (id(processed_data), _kb_fingerprint(processed_data), device)
     m = _MATCHERS.get(key)
     if m is None:
-        m = GpuMatcher(compile_kb(processed_data), device)
+        bg = background_sample(sample_texts) if sample_texts else None
+        m = GpuMatcher(compile_kb(processed_data), device, bg)
         _MATCHERS.clear()
         _MATCHERS[key] = m
     return m
@@ -117,7 +122,7 @@ def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
             error = exc
             break
     n_ok = len(dates)
-    matcher = matcher or get_matcher(processed_data)
+    matcher = matcher or get_matcher(processed_data, sample_texts=texts[:n_ok])
     results: List[dict] = [{} for _ in range(n_ok)]
     if n_ok:
         hits = matcher.match_strings(texts[:n_ok], titles[:n_ok])
@@ -172,8 +177,10 @@ def main(argv=None):
     processed = read_and_process_json_files(args.info_dir)
     out_dir = f'{args.source}_ticker_matched_articles'
     os.makedirs(out_dir, exist_ok=True)
-    matcher = get_matcher(processed, args.device)
+    matcher = None
     for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
+        if matcher is None:
+            matcher = get_matcher(processed, args.device, [field_str(v) for v in chunk['article_text'].tolist()])
         results, error = match_chunk(chunk, processed, matcher)
         rows_by_ticker: Dict[str, list] = {}
         for i, tm in enumerate(results):

@@ -30,6 +30,18 @@ def field_str(value) -> str:
     return str(value) if value else ""
 
 
+def background_sample(texts: Sequence[str], limit: int = 4 << 20) -> bytes:
+    """UTF-8 sample of article text for the anchor statistics (first `limit` bytes)."""
+    out, n = [], 0
+    for t in texts:
+        b = t.encode('utf-8', 'surrogatepass')
+        out.append(b)
+        n += len(b) + 1
+        if n >= limit:
+            break
+    return b'\n'.join(out)[:limit]
+
+
 def pack_fields(texts: Sequence[str], titles: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
     """Interleave text/title UTF-8 into one arena; offsets have 2n+1 entries."""
     n = len(texts)
@@ -52,7 +64,9 @@ def pack_fields(texts: Sequence[str], titles: Sequence[str]) -> Tuple[np.ndarray
 class GpuMatcher:
     """One compiled knowledge base on one GPU (libkwmatch handle)."""
 
-    def __init__(self, ckb: CompiledKB, device: Optional[int] = None):
+    def __init__(self, ckb: CompiledKB, device: Optional[int] = None, background: Optional[bytes] = None):
+        """``background``: a sample of the article text whose 4-byte statistics
+        price the anchor choice (speed only; results never depend on it)."""
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("GpuMatcher needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -63,9 +77,11 @@ class GpuMatcher:
         h = ctypes.c_void_p()
         rx = np.ascontiguousarray(ckb.rx_atoms, dtype=np.int32)
         wb = word_bitmap()
+        bg = np.frombuffer(background, dtype=np.uint8) if background else np.zeros(0, np.uint8)
         rc = L.kw_compile(_native.ptr(ckb.pat_bytes), _native.ptr(ckb.pat_off), _native.ptr(ckb.pat_class),
                           ckb.n_patterns, _native.ptr(rx) if rx.size else None, _native.ptr(ckb.rx_off),
-                          _native.ptr(wb), self.device, ctypes.byref(h))
+                          _native.ptr(wb), _native.ptr(bg) if bg.size else None, int(bg.size), self.device,
+                          ctypes.byref(h))
         if rc != _native.KW_OK:
             msg = L.kw_last_error(h)
             if h.value:
@@ -75,8 +91,8 @@ class GpuMatcher:
         self._keep = None
 
     @classmethod
-    def from_processed_data(cls, processed_data, device=None) -> "GpuMatcher":
-        return cls(compile_kb(processed_data), device)
+    def from_processed_data(cls, processed_data, device=None, background=None) -> "GpuMatcher":
+        return cls(compile_kb(processed_data), device, background)
 
     def close(self):
         if getattr(self, 'h', None) is not None and self.h.value:
@@ -127,14 +143,18 @@ class GpuMatcher:
         return host.view(np.uint32).reshape(-1, 4).copy().view(_native.HIT_DTYPE).reshape(-1)
 
     def stats(self) -> Dict[str, int]:
-        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        _native.check(_native.lib().kw_stats(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self.h)
-        return {'candidates': a.value, 'anchor_hits': b.value, 'windows': c.value}
+        v = np.zeros(8, dtype=np.int64)
+        _native.check(_native.lib().kw_stats(self.h, _native.ptr(v), 8), self.h)
+        return {'candidates': int(v[0]), 'anchor_hits': int(v[1]), 'lcs_windows': int(v[2]),
+                'verifications': int(v[3]), 'deferred_docs': int(v[4]), 'deferred_items': int(v[5]),
+                'deferred_long_nonascii': int(v[6]), 'deferred_regex': int(v[7])}
 
-    def kernel_ms(self) -> Tuple[float, float]:
-        s, t = ctypes.c_float(), ctypes.c_float()
-        _native.check(_native.lib().kw_last_kernel_ms(self.h, ctypes.byref(s), ctypes.byref(t)), self.h)
-        return float(s.value), float(t.value)
+    def kernel_ms(self) -> Tuple[float, float, float]:
+        """(fast kernel, generic kernel, all kernels incl. compaction) in ms for the last scan."""
+        a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        _native.check(_native.lib().kw_last_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                      self.h)
+        return float(a.value), float(b.value), float(c.value)
 
     def match_strings(self, texts: Sequence[str], titles: Sequence[str]) -> np.ndarray:
         """Convenience: pack, upload, scan and fetch."""

@@ -77,11 +77,15 @@ typedef struct {
  *                       may be NULL (all names literal).
  *   word_bitmap       : 0x110000 bits, bit c set iff chr(c).isalnum() or c == '_'
  *                       (CPython's \b word class, Unicode database of the host).
+ *   bg/bg_len         : optional background sample of the article text (UTF-8).  Its
+ *                       4-byte q-gram counts price the anchor substrings and the
+ *                       pigeonhole piece cuts; any sample (or none) gives the same
+ *                       results, only the speed changes.
  * Fuzzy names longer than 64 code points or one byte long are KW_EUNSUPPORTED
  * (rapidfuzz switches algorithm above 64). */
 int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, const uint8_t *pat_class, int32_t n_pat,
-               const int32_t *rx_atoms, const int64_t *rx_off, const uint32_t *word_bitmap, int32_t device,
-               kw_handle **out);
+               const int32_t *rx_atoms, const int64_t *rx_off, const uint32_t *word_bitmap, const uint8_t *bg,
+               int64_t bg_len, int32_t device, kw_handle **out);
 
 /* Scan n_docs documents.  d_arena: UTF-8 bytes; d_doc_off: 2*n_docs+1 int64
  * byte offsets, text of doc d = [off[2d], off[2d+1]), title = [off[2d+1],
@@ -99,13 +103,18 @@ int kw_hits(kw_handle *h, int64_t *n_hits, const kw_hit **d_hits);
  * `cap` records (asynchronous on `stream`); *n_hits receives the count. */
 int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void *stream);
 
-/* Scan statistics of the last kw_scan (after kw_hits): candidate positions that
- * passed the LDS filter, anchor occurrences, verified windows. */
-int kw_stats(kw_handle *h, int64_t *candidates, int64_t *anchor_hits, int64_t *windows);
+/* Scan statistics of the last kw_scan (after kw_hits), up to 8 values:
+ * [0] candidate positions that passed the LDS filter, [1] anchor occurrences,
+ * [2] LCS windows evaluated, [3] fuzzy verifications, [4] documents the fast
+ * kernel handed to the generic kernel, of which [5] had more anchor uses than
+ * the fast path holds, [6] had a long non-ASCII field, [7] matched a name whose
+ * regex needs the generic engine. */
+int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
-/* Device time (ms) of the scan kernel of the last kw_scan, measured with HIP
- * events on the scan's stream (valid after kw_hits). */
-int kw_last_kernel_ms(kw_handle *h, float *scan_ms, float *total_ms);
+/* Device times (ms) of the last kw_scan, from HIP events on the scan's stream
+ * (valid after kw_hits): the fast scan kernel, the generic kernel that redoes
+ * deferred documents, and everything including result compaction. */
+int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *total_ms);
 
 const char *kw_last_error(kw_handle *h);
 int kw_destroy(kw_handle *h);

@@ -249,7 +249,7 @@ def test_compile_rejects_unsupported_without_gpu():
     cls = np.array([ord('F')], dtype=np.uint8)
     h = ctypes.c_void_p()
     rc = L.kw_compile(_native.ptr(b), _native.ptr(off), _native.ptr(cls), 1, None, None,
-                      _native.ptr(kb.word_bitmap()), 0, ctypes.byref(h))
+                      _native.ptr(kb.word_bitmap()), None, 0, 0, ctypes.byref(h))
     assert rc == _native.KW_EUNSUPPORTED
     assert b'64' in L.kw_last_error(h)
     L.kw_destroy(h)
