@@ -33,13 +33,29 @@ def _stale(target, sources):
 def build_kwmatch(force: bool = False) -> str:
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, 'libkwmatch.so')
-    srcs = [os.path.join(CSRC, f) for f in ('kwmatch.hip', 'kwmatch_kernels.hpp', 'kwmatch_device.hpp',
-                                             'dedup.hip')]
-    srcs.append(os.path.join(HERE, '..', 'include', 'kwmatch.h'))
-    srcs = [s for s in srcs if os.path.exists(s)]
+    srcs = _kw_sources()
     if force or _stale(out, srcs):
         units = [s for s in srcs if s.endswith('.hip')]
         _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',
+              '-o', out] + units)
+    return out
+
+
+def _kw_sources():
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(('.hip', '.hpp')))
+    srcs.append(os.path.join(HERE, '..', 'include', 'kwmatch.h'))
+    return srcs
+
+
+def build_kwmatch_stage(stage: int, force: bool = False) -> str:
+    """Profiling variant of the fast kernel truncated after stage `stage`
+    (0 = filter, 1 = + anchor probe, 2 = + resolve without LCS); bench only."""
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, f'libkwmatch_stage{stage}.so')
+    srcs = _kw_sources()
+    if force or _stale(out, srcs):
+        units = [s for s in srcs if s.endswith('.hip')]
+        _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC', f'-DFK_STAGE={stage}',
               '-o', out] + units)
     return out
 
@@ -59,3 +75,6 @@ def build_all(force: bool = False):
 
 if __name__ == '__main__':
     build_all(force='--force' in sys.argv)
+    if '--stages' in sys.argv:
+        for st in (0, 1, 2):
+            build_kwmatch_stage(st, force='--force' in sys.argv)

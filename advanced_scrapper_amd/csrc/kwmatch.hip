@@ -212,28 +212,36 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
             if (quant) {
                 B.rxk[i] = RXK_GENERIC;
             } else {
-                std::string run;
-                for (uint32_t k = rxo[i]; k < rxo[i + 1] && atoms[k].x == KW_RX_LIT; ++k) {
-                    uint32_t c = (uint32_t)atoms[k].y;
-                    if (c < 0x80) run.push_back((char)c);
-                    else if (c < 0x800) { run.push_back((char)(0xC0 | (c >> 6))); run.push_back((char)(0x80 | (c & 0x3F))); }
-                    else if (c < 0x10000) { run.push_back((char)(0xE0 | (c >> 12))); run.push_back((char)(0x80 | ((c >> 6) & 0x3F))); run.push_back((char)(0x80 | (c & 0x3F))); }
-                    else { run.push_back((char)(0xF0 | (c >> 18))); run.push_back((char)(0x80 | ((c >> 12) & 0x3F))); run.push_back((char)(0x80 | ((c >> 6) & 0x3F))); run.push_back((char)(0x80 | (c & 0x3F))); }
+                // anchor inside any literal run, at a code-point (= atom) boundary; the
+                // device walks back `k` atoms from the anchor to the match start
+                auto enc = [](uint32_t c, std::string &o) {
+                    if (c < 0x80) o.push_back((char)c);
+                    else if (c < 0x800) { o.push_back((char)(0xC0 | (c >> 6))); o.push_back((char)(0x80 | (c & 0x3F))); }
+                    else if (c < 0x10000) { o.push_back((char)(0xE0 | (c >> 12))); o.push_back((char)(0x80 | ((c >> 6) & 0x3F))); o.push_back((char)(0x80 | (c & 0x3F))); }
+                    else { o.push_back((char)(0xF0 | (c >> 18))); o.push_back((char)(0x80 | ((c >> 12) & 0x3F))); o.push_back((char)(0x80 | ((c >> 6) & 0x3F))); o.push_back((char)(0x80 | (c & 0x3F))); }
+                };
+                const uint32_t na_i = rxo[i + 1] - rxo[i];
+                bool found = false;
+                uint32_t best_k = 0, best_c = 0xFFFFFFFFu;
+                std::string best_s;
+                for (uint32_t k = 0; k < na_i && k <= 255; ++k) {
+                    if (atoms[rxo[i] + k].x != KW_RX_LIT) continue;
+                    std::string run;   // literal bytes from atom k to the end of its run
+                    for (uint32_t j = k; j < na_i && atoms[rxo[i] + j].x == KW_RX_LIT && run.size() < 8; ++j)
+                        enc((uint32_t)atoms[rxo[i] + j].y, run);
+                    if (run.size() < 3) continue;
+                    uint32_t c = run.size() >= 4 ? Q.count((const uint8_t *)run.data()) : 0x7FFFFFFFu;
+                    if (!found || c < best_c) { found = true; best_c = c; best_k = k; best_s = run; }
                 }
-                if (run.size() < 2) {
+                if (!found) {
                     B.rxk[i] = RXK_GENERIC;
                 } else {
                     B.rxk[i] = RXK_WILD;
-                    size_t a = 0, al = run.size();
-                    if (run.size() >= 4) {
-                        a = rarest4(Q, (const uint8_t *)run.data(), 0, run.size(), 255);
-                        al = std::min<size_t>(8, run.size() - a);
-                    }
                     Use u;
                     u.pat = (uint32_t)i;
-                    u.i0 = FU_RXW | ((uint32_t)a << 8);
+                    u.i0 = FU_RXW | (best_k << 8);
                     u.i1 = (uint32_t)bl;
-                    add(run.substr(a, al), u);
+                    add(best_s.substr(0, std::min<size_t>(8, best_s.size())), u);
                 }
             }
         }
@@ -812,7 +820,8 @@ static int launch_scan(kw_handle *h)
     int rc = ensure_scratch(h, nf, ng, std::max(want_cap, h->out_cap), (uint32_t)std::max<int64_t>(n_docs, 1));
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
-    HIPCHK(h, hipMemsetAsync(h->S.out_cnt, 0, (size_t)ng * 4, st));
+    // every region's count (regions of waves this launch does not start stay empty)
+    HIPCHK(h, hipMemsetAsync(h->FS.out_cnt, 0, (size_t)(h->nf + h->ng) * 4, st));
     HIPCHK(h, hipEventRecord(h->ev0, st));
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_fast_kernel, dim3(nfb), dim3(FK_BLOCK), kFastLds, st, h->FT, h->T, h->arena, h->doc_off,
@@ -828,7 +837,7 @@ static int launch_scan(kw_handle *h)
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->evg, st));
-    const int nw = nf + ng;
+    const int nw = h->nf + h->ng;   // all regions: fast [0, h->nf), generic [h->nf, h->nf + h->ng)
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->FS.out_cnt, nw, h->out_cap, h->d_offs);
         hipLaunchKernelGGL(kw_gather_kernel, dim3(nw), dim3(256), 0, st, h->FS.out, h->out_cap, h->FS.out_cnt,

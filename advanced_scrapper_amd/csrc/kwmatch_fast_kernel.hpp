@@ -121,11 +121,19 @@ __device__ void fast_probe(const FastTables &FT, const DevTables &T, const FastS
                 const uint32_t kind = i0 & 0xFF, aoff = (i0 >> 8) & 0xFF, sboff = i0 >> 16;
                 const uint32_t sblen = i1 & 0xFFFF;
                 const uint32_t pat = FT.use_pat[u];
-                const int64_t s0 = p - (int64_t)aoff;
-                if (s0 < fb) continue;
+                int64_t s0 = p - (int64_t)aoff;
                 if (kind == FU_RXW) {
+                    // aoff = atoms before the anchor: walk back that many code points
+                    s0 = p;
+                    uint32_t j = 0;
+                    for (; j < aoff && s0 > fb; ++j) {
+                        --s0;
+                        while (s0 > fb && (arena[s0] & 0xC0) == 0x80) --s0;
+                    }
+                    if (j < aoff) continue;
                     if (wild_match(T, arena, s0, fe, pat) < 0) continue;
                 } else {
+                    if (s0 < fb) continue;
                     if (s0 + (int64_t)sblen > fe) continue;
                     const uint32_t pi = FT.pat_info[pat];
                     if (kind == FU_PIECE) {
@@ -346,7 +354,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         const bool head = valid && (lane == 0 || prev_pat != pat);
         const uint64_t heads = __ballot(head);
         const uint64_t below = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
-        const int gs = 63 - __builtin_clzll(heads & below | 1ull);
+        const int gs = 63 - __builtin_clzll((heads & below) | 1ull);
         const uint64_t after = heads & ~below;
         const int ge = after ? __builtin_ctzll(after) : (int)N;
         const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
@@ -381,11 +389,13 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         if (__ballot(live && fuzzy && decided && rxk == RXK_GENERIC)) return 2;
         const uint32_t cpos = relevant ? to_cp(F, bpos) : 0u;
         const uint64_t relm = __ballot(relevant);
-        // leftmost non-overlapping selection per group (match length m code points)
+        // leftmost non-overlapping selection per group; a match spans m code points
+        // (literal) or one code point per atom ('.'-wildcard regex)
+        const uint32_t mlen = (relevant && rxk == RXK_WILD && kind == FU_RXW) ? T.rx_off[pat + 1] - T.rx_off[pat] : m;
         const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
         const int pr = prevrel ? 63 - __builtin_clzll(prevrel) : -1;
         const uint32_t pcpos = (uint32_t)__shfl((int)cpos, pr < 0 ? lane : pr, WAVE);
-        const bool overlap = relevant && pr >= 0 && cpos < pcpos + m;
+        const bool overlap = relevant && pr >= 0 && cpos < pcpos + mlen;
         uint64_t keep = relm;
         if (__ballot(overlap)) {
             // rare: resolve the greedy chain serially
@@ -398,7 +408,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                 mm2 &= mm2 - 1;
                 const int h = __shfl(gs, l, WAVE);
                 const uint32_t s = (uint32_t)__shfl((int)cpos, l, WAVE);
-                const uint32_t len = (uint32_t)__shfl((int)m, l, WAVE);
+                const uint32_t len = (uint32_t)__shfl((int)mlen, l, WAVE);
                 if (h != cur_head) { cur_head = h; last_end = 0; keep |= 1ull << l; last_end = s + len; continue; }
                 if (s >= last_end) { keep |= 1ull << l; last_end = s + len; }
             }

@@ -176,3 +176,32 @@ def test_batch_invariance_and_determinism(env):
     tail['doc'] += half
     tail = np.sort(tail, order=['doc', 'field', 'pattern', 'pos'])
     assert np.array_equal(full[full['doc'] >= half], tail)
+
+
+_WILD_NAMES = ['x.yz.free', 'C.H. Robinson Worldwide', 'U.S. Smokeless Tobacco', '.zappos', 'ab.ab.ab',
+               'é.éé.Zürich', 'E. I. du Pont de Nemours', 'Disney+ Hotstar', 'q..q..q..qq', 'Ab.c']
+
+
+def test_wildcard_regex_names_vs_oracle():
+    """'.'-wildcard names anchored in any literal run: positions, overlaps, edges, non-ASCII."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    processed = {'TK': {'name': {n: (None, None) for n in _WILD_NAMES}}}
+    m = GpuMatcher(compile_kb(processed))
+    rng = random.Random(17)
+    subs = ['.', 'X', ' ', 'é', '中', '-', '\n']
+    texts, titles = [], []
+    for n in _WILD_NAMES:
+        for _ in range(6):
+            w = ''.join(rng.choice(subs) if ch == '.' else ch for ch in n)
+            k = rng.randrange(len(n))
+            texts.append(rng.choice(['', 'é', 'lorem ']) + w + w + ' ' + w[1:] + n[:k] + n[k + 1:] + w)
+            titles.append(w + rng.choice(['', ' tail', 'é']))
+    texts += ['ab.ab.ab.ab.ab', 'abXabXabXabXabXab', 'ab\nab.ab', 'q..q..q..qqq..q..q..qq', '.zappos' * 5]
+    titles += ['ab.ab.ab', 'ab.ab.a', '', 'q..q..q..qq', 'zappos']
+    got = _gpu_maps(m, texts, titles)
+    bad = _compare(processed, texts, titles, got)
+    assert not bad, f"GPU differs from the oracle on wildcard docs {bad[:20]}"
