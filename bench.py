@@ -39,9 +39,11 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--docs-per-gpu', type=int, default=1_000_000)
     ap.add_argument('--seed', type=int, default=20250905)
-    ap.add_argument('--cpu-sample', type=int, default=256, help='docs timed on the CPU port (0 = skip)')
+    ap.add_argument('--cpu-sample', type=int, default=4096, help='docs timed on the CPU port (0 = skip)')
     ap.add_argument('--cpu-procs', type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument('--gather-hits', action='store_true', help='also time the RCCL all-gather of hit records')
+    ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'traffic_r01.json'),
+                    help='per-launch HBM bytes from the rocprofv3 PMC passes (profiles/pmc_traffic.py)')
     args = ap.parse_args()
 
     import torch
@@ -144,7 +146,9 @@ def main():
         },
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+            'frac': round(achieved / HBM_PEAK_GBS, 4),
+            'traffic': pmc_traffic(args.traffic_json, 'kw_fast_kernel', n_local, args.seed),
+            'algorithmic_bytes_per_launch': local_bytes,
             'kernel': 'kw::kw_fast_kernel', 'kernel_ms_avg': round(scan_avg, 4),
             'generic_kernel_ms_avg': round(float(np.mean(gen_ms)), 4),
             'step_kernels_ms_avg': round(float(np.mean(total_ms)), 4),
@@ -156,6 +160,22 @@ def main():
         'hits_allgather_ms': None if gather_ms is None else round(gather_ms, 3),
     }
     print(json.dumps(out), flush=True)
+
+
+def pmc_traffic(path: str, kernel: str, docs: int, seed: int):
+    """HBM bytes per launch of `kernel` measured by the PMC passes of the same
+    workload (FETCH_SIZE x2 + WRITE_SIZE, see profiles/pmc_traffic.py), or None."""
+    try:
+        j = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    w = j.get('workload', {})
+    if str(w.get('docs_per_gpu')) != str(docs) or str(w.get('seed')) != str(seed):
+        return None
+    for k, v in j.get('kernels', {}).items():
+        if kernel in k:
+            return int(v['hbm_bytes_per_launch'])
+    return None
 
 
 def cpu_baseline(processed, corpus, n_sample: int, procs: int):
