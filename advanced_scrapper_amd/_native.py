@@ -27,7 +27,8 @@ HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('fiel
 
 # every symbol include/kwmatch.h declares
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
-           'kw_last_error', 'kw_destroy')
+           'kw_last_kernel_times', 'kw_last_error', 'kw_destroy')
+KW_N_STATS = 10
 
 
 class KwError(RuntimeError):
@@ -61,6 +62,8 @@ def lib() -> ctypes.CDLL:
     L.kw_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                     ctypes.POINTER(ctypes.c_float)]
     L.kw_last_kernel_ms.restype = ctypes.c_int
+    L.kw_last_kernel_times.argtypes = [vp, vp, i32]
+    L.kw_last_kernel_times.restype = ctypes.c_int
     L.kw_last_error.argtypes = [vp]
     L.kw_last_error.restype = ctypes.c_char_p
     L.kw_destroy.argtypes = [vp]

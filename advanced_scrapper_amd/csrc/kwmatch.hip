@@ -44,21 +44,23 @@ struct kw_handle {
     bool scanned = false;
     bool fetched = false;
     int64_t n_hits = 0;
-    unsigned long long stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long stats[KW_N_STATS] = {0};
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     int cus = 256;
     int blocks_per_cu = 2;
     std::string err;
     int n_pat = 0;
     int launched_waves = 0;
-    // fast path
+    // fast path: scan waves (nk), resolve waves (nr), generic waves (ng)
     FastTables FT{};
     FastScratch FS{};
-    int nf = 0, ng = 0;
-    uint32_t defer_cap = 0;
-    int fast_blocks_per_cu = 1;
+    int nk = 0, nr = 0, ng = 0;
+    uint32_t defer_cap = 0, item_cap = 0;
+    int64_t hdr_cap = 0;
+    int items_blocks_per_cu = 1, resolve_blocks_per_cu = 1;
     int n_anchor_fast = 0;
-    hipEvent_t evg = nullptr;
+    unsigned long long fstats[16] = {0};
+    hipEvent_t evr = nullptr, evg = nullptr;
 };
 
 static thread_local std::string g_err;
@@ -142,13 +144,18 @@ struct QStats {
 };
 
 struct FastBuild {
-    std::vector<uint32_t> filt, b2;
+    std::vector<uint32_t> filt, l2, t3, b2, edge_pre, edge_suf;
     uint32_t gate_lo[4] = {0, 0, 0, 0}, gate_hi[4] = {0, 0, 0, 0};
     int n_gate = 0;
+    int has_t3 = 0;
     std::vector<uint64_t> ht_key, as_head, sig;
     std::vector<uint32_t> ht_begin, ht_cnt, kl, as_len, as_use_begin, as_use_cnt, use_pat, use_info0, use_info1,
         rxk, boff;
     uint32_t ht_mask = 0;
+    std::unordered_map<uint64_t, std::vector<uint32_t>> edge;   // one-deletion variants
+    std::vector<uint64_t> edge_key;
+    std::vector<uint32_t> edge_begin, edge_cnt, edge_ent;
+    uint32_t edge_mask = 0;
 };
 
 // rarest 4-byte window inside bytes [lo, hi) (hi - lo >= 4); returns its start
@@ -179,6 +186,8 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         auses[id].push_back(u);
     };
     B.rxk.assign(std::max(n_pat, 1), RXK_LITERAL);
+    B.edge_pre.assign(FK_EDGE_WORDS, 0);
+    B.edge_suf.assign(FK_EDGE_WORDS, 0);
     B.boff.assign(std::max(n_pat, 1), 0);
     B.sig.assign(std::max(n_pat, 1), 0);
     for (int i = 0; i < n_pat; ++i) {
@@ -205,45 +214,32 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         if (!fuzzy) { span_use(FU_UPPER, 0, bl, 0, 0); continue; }
         if (m == 0) continue;
         span_use(FU_FULL, 0, bl, 0, 0);
-        // regex kind and the wildcard-match anchor (first literal run)
-        if (rxo[i + 1] > rxo[i]) {
-            bool quant = false;
-            for (uint32_t k = rxo[i]; k < rxo[i + 1]; ++k) quant |= !(atoms[k].z == 1 && atoms[k].w == 1);
-            if (quant) {
-                B.rxk[i] = RXK_GENERIC;
-            } else {
-                // anchor inside any literal run, at a code-point (= atom) boundary; the
-                // device walks back `k` atoms from the anchor to the match start
-                auto enc = [](uint32_t c, std::string &o) {
-                    if (c < 0x80) o.push_back((char)c);
-                    else if (c < 0x800) { o.push_back((char)(0xC0 | (c >> 6))); o.push_back((char)(0x80 | (c & 0x3F))); }
-                    else if (c < 0x10000) { o.push_back((char)(0xE0 | (c >> 12))); o.push_back((char)(0x80 | ((c >> 6) & 0x3F))); o.push_back((char)(0x80 | (c & 0x3F))); }
-                    else { o.push_back((char)(0xF0 | (c >> 18))); o.push_back((char)(0x80 | ((c >> 12) & 0x3F))); o.push_back((char)(0x80 | ((c >> 6) & 0x3F))); o.push_back((char)(0x80 | (c & 0x3F))); }
-                };
-                const uint32_t na_i = rxo[i + 1] - rxo[i];
-                bool found = false;
-                uint32_t best_k = 0, best_c = 0xFFFFFFFFu;
-                std::string best_s;
-                for (uint32_t k = 0; k < na_i && k <= 255; ++k) {
-                    if (atoms[rxo[i] + k].x != KW_RX_LIT) continue;
-                    std::string run;   // literal bytes from atom k to the end of its run
-                    for (uint32_t j = k; j < na_i && atoms[rxo[i] + j].x == KW_RX_LIT && run.size() < 8; ++j)
-                        enc((uint32_t)atoms[rxo[i] + j].y, run);
-                    if (run.size() < 3) continue;
-                    uint32_t c = run.size() >= 4 ? Q.count((const uint8_t *)run.data()) : 0x7FFFFFFFu;
-                    if (!found || c < best_c) { found = true; best_c = c; best_k = k; best_s = run; }
-                }
-                if (!found) {
-                    B.rxk[i] = RXK_GENERIC;
-                } else {
-                    B.rxk[i] = RXK_WILD;
-                    Use u;
-                    u.pat = (uint32_t)i;
-                    u.i0 = FU_RXW | (best_k << 8);
-                    u.i1 = (uint32_t)bl;
-                    add(best_s.substr(0, std::min<size_t>(8, best_s.size())), u);
+        // positions: literal search, or the regex engine after the decision
+        if (rxo[i + 1] > rxo[i]) B.rxk[i] = RXK_REGEX;
+        // m <= 20: interior windows must be exact (FULL); the one-deletion edge
+        // windows (11 <= m <= 20) go to the edge table instead of pieces
+        if (kfull_h(m) == 0) {
+            if (m >= EDGE_MIN_M && m <= EDGE_MAX_M) {
+                for (uint32_t del = 0; del < m; ++del) {
+                    if (del > 0 && cps[i][del] == cps[i][del - 1]) continue;   // same variant as del-1
+                    uint64_t hh = 0;
+                    for (uint32_t j = 0; j < m; ++j)
+                        if (j != del) hh = hh * SUB_B + cps[i][j];
+                    const uint64_t key = (hh + (uint64_t)(m - 1) * 0x9E3779B97F4A7C15ull) | 1ull;
+                    B.edge[key].push_back(((uint32_t)i << 5) | del);
+                    // prefilter keys: first / last four UTF-8 bytes of the variant
+                    std::string v;
+                    v.append((const char *)s, utf8_offset(cps[i], del));
+                    v.append((const char *)s + utf8_offset(cps[i], del + 1), bl - utf8_offset(cps[i], del + 1));
+                    const uint8_t *vp = (const uint8_t *)v.data();
+                    const uint32_t kp = (uint32_t)vp[0] | ((uint32_t)vp[1] << 8) | ((uint32_t)vp[2] << 16) | ((uint32_t)vp[3] << 24);
+                    const uint8_t *ve = vp + v.size() - 4;
+                    const uint32_t ks = (uint32_t)ve[0] | ((uint32_t)ve[1] << 8) | ((uint32_t)ve[2] << 16) | ((uint32_t)ve[3] << 24);
+                    B.edge_pre[fk_edge_index(kp) >> 5] |= 1u << (fk_edge_index(kp) & 31);
+                    B.edge_suf[fk_edge_index(ks) >> 5] |= 1u << (fk_edge_index(ks) & 31);
                 }
             }
+            continue;
         }
         // pigeonhole pieces: K = dmax+1 pieces, cuts chosen to minimise the
         // largest "rarest 4-gram" count over the pieces (each piece is anchored
@@ -302,6 +298,8 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     if (B.use_pat.size() > IT_USE_MASK) { err = "kw_compile: more than 2^19 anchor uses"; return KW_EUNSUPPORTED; }
     // ---- LDS filter, bigram table, gate, global hash table
     B.filt.assign(FK_FILT_WORDS, 0);
+    B.l2.assign(FK_L2_WORDS, 0);
+    B.t3.assign(FK_T3_WORDS, 0);
     B.b2.assign(FK_B2_WORDS, 0);
     std::unordered_map<uint64_t, std::vector<uint32_t>> keys;
     std::vector<uint8_t> gate_bytes;
@@ -312,10 +310,13 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         if (st.size() >= 4) {
             const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
             B.filt[fk_word(k4)] |= 1u << fk_bit(k4);
+            B.l2[fk_l2_index(k4) >> 5] |= 1u << (fk_l2_index(k4) & 31);
             keys[(4ull << 32) | k4].push_back(a);
         } else if (st.size() == 3) {
             const uint32_t k3 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
             B.filt[fk_word(k3)] = 0xFFFFFFFFu;
+            B.t3[fk_t3_index(k3) >> 5] |= 1u << (fk_t3_index(k3) & 31);
+            B.has_t3 = 1;
             keys[(3ull << 32) | k3].push_back(a);
         } else if (st.size() == 2) {
             const uint32_t k2 = (uint32_t)p[0] | ((uint32_t)p[1] << 8);
@@ -367,6 +368,23 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         B.kl.insert(B.kl.end(), kv.second.begin(), kv.second.end());
     }
     if (B.kl.empty()) B.kl.push_back(0);
+    {
+        uint32_t es = 256;
+        while (es < 2 * B.edge.size()) es <<= 1;
+        B.edge_mask = es - 1;
+        B.edge_key.assign(es, 0);
+        B.edge_begin.assign(es, 0);
+        B.edge_cnt.assign(es, 0);
+        for (auto &kv : B.edge) {
+            uint32_t slot = (uint32_t)(kv.first >> 32) & B.edge_mask;
+            while (B.edge_key[slot] != 0) slot = (slot + 1) & B.edge_mask;
+            B.edge_key[slot] = kv.first;
+            B.edge_begin[slot] = (uint32_t)B.edge_ent.size();
+            B.edge_cnt[slot] = (uint32_t)kv.second.size();
+            B.edge_ent.insert(B.edge_ent.end(), kv.second.begin(), kv.second.end());
+        }
+        if (B.edge_ent.empty()) B.edge_ent.push_back(0);
+    }
     if (B.as_head.empty()) { B.as_head.push_back(0); B.as_len.push_back(0); B.as_use_begin.push_back(0); B.as_use_cnt.push_back(0); }
     if (B.use_pat.empty()) { B.use_pat.push_back(0); B.use_info0.push_back(0); B.use_info1.push_back(0); }
     return KW_OK;
@@ -635,6 +653,18 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
         int frc = build_fast(FB, Q, n_pat, pat_bytes, pat_off, cps, pat_info, atoms, rxo, ferr);
         if (frc) return fail(frc, ferr);
     }
+    if (const char *dump = getenv("KW_DUMP_ANCHORS")) {
+        // developer aid: one line per anchor use "hex(anchor) pattern kind" (anchor tuning)
+        if (FILE *f = fopen(dump, "w")) {
+            for (size_t a = 0; a < FB.as_len.size(); ++a)
+                for (uint32_t u = FB.as_use_begin[a]; u < FB.as_use_begin[a] + FB.as_use_cnt[a]; ++u) {
+                    for (uint32_t k = 0; k < std::min<uint32_t>(FB.as_len[a], 8); ++k)
+                        fprintf(f, "%02x", (unsigned)((FB.as_head[a] >> (8 * k)) & 0xFF));
+                    fprintf(f, " %u %u\n", FB.use_pat[u], FB.use_info0[u] & 0xFF);
+                }
+            fclose(f);
+        }
+    }
     std::vector<uint8_t> all_bytes(pat_bytes, pat_bytes + (n_pat ? pat_off[n_pat] : 0));
     all_bytes.resize(all_bytes.size() + 16, 0);
 
@@ -650,13 +680,16 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            o_rxa = push_array(blob, atoms), o_wb = push_array(blob, wb), o_fc = push_array(blob, f_count_ge),
            o_sk = push_array(blob, sub_key), o_sb = push_array(blob, sub_begin), o_sc = push_array(blob, sub_cnt),
            o_sp = push_array(blob, sub_pat);
-    size_t f_filt = push_array(blob, FB.filt), f_b2 = push_array(blob, FB.b2), f_htk = push_array(blob, FB.ht_key),
+    size_t f_filt = push_array(blob, FB.filt), f_b2 = push_array(blob, FB.b2), f_l2 = push_array(blob, FB.l2),
+           f_t3 = push_array(blob, FB.t3), f_epre = push_array(blob, FB.edge_pre), f_esuf = push_array(blob, FB.edge_suf), f_htk = push_array(blob, FB.ht_key),
            f_htb = push_array(blob, FB.ht_begin), f_htc = push_array(blob, FB.ht_cnt), f_kl = push_array(blob, FB.kl),
            f_ash = push_array(blob, FB.as_head), f_asl = push_array(blob, FB.as_len),
            f_asub = push_array(blob, FB.as_use_begin), f_asuc = push_array(blob, FB.as_use_cnt),
            f_up = push_array(blob, FB.use_pat), f_ui0 = push_array(blob, FB.use_info0),
            f_ui1 = push_array(blob, FB.use_info1), f_rxk = push_array(blob, FB.rxk), f_boff = push_array(blob, FB.boff),
-           f_pb = push_array(blob, all_bytes), f_sig = push_array(blob, FB.sig);
+           f_pb = push_array(blob, all_bytes), f_sig = push_array(blob, FB.sig),
+           f_ek = push_array(blob, FB.edge_key), f_eb = push_array(blob, FB.edge_begin),
+           f_ec = push_array(blob, FB.edge_cnt), f_ee = push_array(blob, FB.edge_ent);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -702,6 +735,11 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     FastTables &F = h->FT;
     F.filt = (const uint32_t *)(B + f_filt);
     F.b2 = (const uint32_t *)(B + f_b2);
+    F.l2 = (const uint32_t *)(B + f_l2);
+    F.t3 = (const uint32_t *)(B + f_t3);
+    F.edge_pre = (const uint32_t *)(B + f_epre);
+    F.edge_suf = (const uint32_t *)(B + f_esuf);
+    F.has_t3 = FB.has_t3;
     for (int r = 0; r < 4; ++r) { F.gate_lo[r] = FB.gate_lo[r]; F.gate_hi[r] = FB.gate_hi[r]; }
     F.n_gate = FB.n_gate;
     F.ht_key = (const uint64_t *)(B + f_htk);
@@ -729,6 +767,11 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.sub_cnt = T.sub_cnt;
     F.sub_pat = T.sub_pat;
     F.sub_mask = T.sub_mask;
+    F.edge_key = (const uint64_t *)(B + f_ek);
+    F.edge_begin = (const uint32_t *)(B + f_eb);
+    F.edge_cnt = (const uint32_t *)(B + f_ec);
+    F.edge_ent = (const uint32_t *)(B + f_ee);
+    F.edge_mask = FB.edge_mask;
     F.word_bits = T.word_bits;
     F.f_first = f_first;
     F.empty_pat = empty_pat;
@@ -741,23 +784,34 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_scan_kernel, BLOCK, kScanLds));
     h->blocks_per_cu = bpc > 0 ? bpc : 1;
     bpc = 0;
-    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_fast_kernel, FK_BLOCK, kFastLds));
-    h->fast_blocks_per_cu = bpc > 0 ? bpc : 1;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_items_kernel, FK_BLOCK, kItemsLds));
+    h->items_blocks_per_cu = bpc > 0 ? bpc : 1;
+    bpc = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_resolve_kernel, RK_BLOCK, 0));
+    h->resolve_blocks_per_cu = bpc > 0 ? bpc : 1;
     HIPCHK(h, hipEventCreate(&h->ev0));
     HIPCHK(h, hipEventCreate(&h->ev1));
     HIPCHK(h, hipEventCreate(&h->evg));
+    HIPCHK(h, hipEventCreate(&h->evr));
     HIPCHK(h, hipEventCreate(&h->ev2));
     *out = h;
     return KW_OK;
 }
 
-// (re)allocate scratch: nf fast waves + ng generic waves, out_cap records per wave, defer list of dcap docs
-static int ensure_scratch(kw_handle *h, int nf, int ng, uint32_t out_cap, uint32_t dcap)
+// (re)allocate scratch for nk scan waves (item_cap items each), nr resolve waves, ng generic
+// waves (out_cap records per resolve/generic wave), n_docs headers and a defer list of dcap docs
+static int ensure_scratch(kw_handle *h, int nk, int nr, int ng, uint32_t item_cap, uint32_t out_cap, int64_t n_docs,
+                          uint32_t dcap)
 {
-    if (h->d_scratch && nf <= h->nf && ng <= h->ng && out_cap <= h->out_cap && dcap <= h->defer_cap) return KW_OK;
-    nf = std::max(nf, h->nf);
+    if (h->d_scratch && nk <= h->nk && nr <= h->nr && ng <= h->ng && item_cap <= h->item_cap &&
+        out_cap <= h->out_cap && n_docs <= h->hdr_cap && dcap <= h->defer_cap)
+        return KW_OK;
+    nk = std::max(nk, h->nk);
+    nr = std::max(nr, h->nr);
     ng = std::max(ng, h->ng);
+    item_cap = std::max(item_cap, h->item_cap);
     out_cap = std::max(out_cap, h->out_cap);
+    n_docs = std::max(n_docs, h->hdr_cap);
     dcap = std::max(dcap, h->defer_cap);
     if (h->d_scratch) { (void)hipFree(h->d_scratch); h->d_scratch = nullptr; }
     if (h->d_small) { (void)hipFree(h->d_small); h->d_small = nullptr; }
@@ -767,18 +821,21 @@ static int ensure_scratch(kw_handle *h, int nf, int ng, uint32_t out_cap, uint32
     const size_t per_blk = (size_t)(CP_CAP / 16 + 2) * sizeof(uint32_t);
     const size_t per_fcps = (size_t)FK_CP_CAP * sizeof(uint32_t);
     const size_t per_out = (size_t)out_cap * sizeof(kw_hit);
-    const int nw = nf + ng;
-    size_t total = (size_t)ng * (per_items + per_cps + per_blk) + (size_t)nf * (per_fcps + per_blk) +
-                   (size_t)nw * per_out + (size_t)dcap * 4 + 8192;
+    const int nw = nr + ng;   // result regions: resolve [0, nr), generic [nr, nr + ng)
+    size_t total = (size_t)ng * (per_items + per_cps + per_blk) + (size_t)nr * (per_fcps + per_blk) +
+                   (size_t)nw * per_out + (size_t)nk * item_cap * 8 + (size_t)n_docs * 8 + (size_t)dcap * 4 +
+                   16 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
     uint8_t *p = (uint8_t *)h->d_scratch;
     auto carve = [&](size_t bytes) { uint8_t *r = p; p += (bytes + 255) & ~(size_t)255; return r; };
     h->S.items = (uint64_t *)carve((size_t)ng * per_items);
     h->S.cps = (uint32_t *)carve((size_t)ng * per_cps);
     h->S.blkcnt = (uint32_t *)carve((size_t)ng * per_blk);
-    h->FS.cps = (uint32_t *)carve((size_t)nf * per_fcps);
-    h->FS.cpbase = (uint32_t *)carve((size_t)nf * per_blk);
+    h->FS.cps = (uint32_t *)carve((size_t)nr * per_fcps);
+    h->FS.cpbase = (uint32_t *)carve((size_t)nr * per_blk);
     kw_hit *outs = (kw_hit *)carve((size_t)nw * per_out);
+    h->FS.items = (uint64_t *)carve((size_t)nk * item_cap * 8);
+    h->FS.hdr = (uint2 *)carve((size_t)n_docs * 8);
     h->FS.defer_list = (uint32_t *)carve((size_t)dcap * 4);
     size_t small = 1024 + (size_t)nw * 4 + 256 + (size_t)(nw + 1) * 8 + 256;
     HIPCHK(h, hipMalloc(&h->d_small, small));
@@ -787,19 +844,23 @@ static int ensure_scratch(kw_handle *h, int nf, int ng, uint32_t out_cap, uint32
     h->FS.status = h->S.status;
     h->FS.defer_cnt = (uint32_t *)(q + 16);
     h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
-    h->FS.stats = (unsigned long long *)(q + 128);      // 5 x u64 (fast)
+    h->FS.stats = (unsigned long long *)(q + 128);      // 16 x u64 (fast path)
     uint32_t *cnts = (uint32_t *)(q + 1024);
     h->FS.out_cnt = cnts;
-    h->S.out_cnt = cnts + nf;
+    h->S.out_cnt = cnts + nr;
     h->d_offs = (unsigned long long *)(q + 1024 + (((size_t)nw * 4 + 255) & ~(size_t)255));
     h->FS.out = outs;
-    h->S.out = outs + (size_t)nf * out_cap;
+    h->S.out = outs + (size_t)nr * out_cap;
     h->S.out_cap = out_cap;
     h->FS.out_cap = out_cap;
+    h->FS.item_cap = item_cap;
     h->FS.defer_cap = dcap;
-    h->nf = nf;
+    h->nk = nk;
+    h->nr = nr;
     h->ng = ng;
+    h->item_cap = item_cap;
     h->out_cap = out_cap;
+    h->hdr_cap = n_docs;
     h->defer_cap = dcap;
     h->hits_cap = (size_t)nw * out_cap;
     HIPCHK(h, hipMalloc(&h->d_hits, h->hits_cap * sizeof(kw_hit) + 16));
@@ -811,33 +872,45 @@ static int launch_scan(kw_handle *h)
 {
     hipStream_t st = h->stream;
     const int64_t n_docs = h->n_docs;
-    int nfb = (int)std::min<int64_t>((n_docs + FK_WAVES - 1) / FK_WAVES, (int64_t)h->cus * h->fast_blocks_per_cu);
-    if (nfb < 1) nfb = 1;
+    int nkb = (int)std::min<int64_t>((n_docs + FK_WAVES - 1) / FK_WAVES, (int64_t)h->cus * h->items_blocks_per_cu);
+    if (nkb < 1) nkb = 1;
+    int nrb = (int)std::min<int64_t>((n_docs + (int64_t)RK_WAVES * WAVE - 1) / ((int64_t)RK_WAVES * WAVE),
+                                     (int64_t)h->cus * h->resolve_blocks_per_cu);
+    if (nrb < 1) nrb = 1;
     const int ngb = std::max(1, std::min(h->cus, (int)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)));
-    const int nf = nfb * FK_WAVES, ng = ngb * WAVES_PER_BLOCK;
-    const int64_t docs_per_wave = (n_docs + nf - 1) / nf;
-    const uint32_t want_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_wave * 48), (int64_t)1 << 26);
-    int rc = ensure_scratch(h, nf, ng, std::max(want_cap, h->out_cap), (uint32_t)std::max<int64_t>(n_docs, 1));
+    const int nk = nkb * FK_WAVES, nr = nrb * RK_WAVES, ng = ngb * WAVES_PER_BLOCK;
+    const int64_t docs_per_k = (n_docs + nk - 1) / nk;
+    const uint32_t want_items = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_k * 40), (int64_t)1 << 24);
+    const int64_t docs_per_r = (n_docs + nr - 1) / nr;
+    const uint32_t want_out = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_r * 48), (int64_t)1 << 26);
+    int rc = ensure_scratch(h, nk, nr, ng, std::max(want_items, h->item_cap), std::max(want_out, h->out_cap),
+                            std::max<int64_t>(n_docs, 1), (uint32_t)std::max<int64_t>(n_docs, 1));
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
     // every region's count (regions of waves this launch does not start stay empty)
-    HIPCHK(h, hipMemsetAsync(h->FS.out_cnt, 0, (size_t)(h->nf + h->ng) * 4, st));
+    HIPCHK(h, hipMemsetAsync(h->FS.out_cnt, 0, (size_t)(h->nr + h->ng) * 4, st));
     HIPCHK(h, hipEventRecord(h->ev0, st));
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_fast_kernel, dim3(nfb), dim3(FK_BLOCK), kFastLds, st, h->FT, h->T, h->arena, h->doc_off,
-                           n_docs, h->FS, h->S);
+        hipLaunchKernelGGL(kw_items_kernel, dim3(nkb), dim3(FK_BLOCK), kItemsLds, st, h->FT, h->T, h->arena,
+                           h->doc_off, n_docs, h->FS);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
-        // the generic kernel redoes every document the fast kernel deferred
+        hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+                           n_docs, h->FS, h->S);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->evr, st));
+    if (n_docs > 0) {
+        // the generic kernel redoes every document the fast path deferred
         hipLaunchKernelGGL(kw_scan_kernel, dim3(ngb), dim3(BLOCK), kScanLds, st, h->T, h->arena, h->doc_off, n_docs,
                            h->S, (const uint32_t *)h->FS.defer_list, (const uint32_t *)h->FS.defer_cnt,
                            h->FS.defer_cap);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->evg, st));
-    const int nw = h->nf + h->ng;   // all regions: fast [0, h->nf), generic [h->nf, h->nf + h->ng)
+    const int nw = h->nr + h->ng;   // all regions: resolve [0, h->nr), generic [h->nr, h->nr + h->ng)
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->FS.out_cnt, nw, h->out_cap, h->d_offs);
         hipLaunchKernelGGL(kw_gather_kernel, dim3(nw), dim3(256), 0, st, h->FS.out, h->out_cap, h->FS.out_cnt,
@@ -888,7 +961,7 @@ static int finish(kw_handle *h)
             HIPCHK(h, hipMemcpy(cnt.data(), h->FS.out_cnt, cnt.size() * 4, hipMemcpyDeviceToHost));
             uint32_t mx = 0;
             for (uint32_t c : cnt) mx = std::max(mx, c);
-            int rc = ensure_scratch(h, h->nf, h->ng, mx + 1024, h->defer_cap);
+            int rc = ensure_scratch(h, h->nk, h->nr, h->ng, h->item_cap, mx + 1024, h->hdr_cap, h->defer_cap);
             if (rc) return rc;
             rc = launch_scan(h);
             if (rc) return rc;
@@ -896,17 +969,14 @@ static int finish(kw_handle *h)
         }
         unsigned long long tot = 0;
         HIPCHK(h, hipMemcpy(&tot, h->d_offs + h->launched_waves, sizeof(tot), hipMemcpyDeviceToHost));
-        unsigned long long gst[3], fst[8];
+        unsigned long long gst[3], fst[16];
         HIPCHK(h, hipMemcpy(gst, h->S.stats, sizeof(gst), hipMemcpyDeviceToHost));
         HIPCHK(h, hipMemcpy(fst, h->FS.stats, sizeof(fst), hipMemcpyDeviceToHost));
         h->stats[0] = fst[0] + gst[0];
         h->stats[1] = fst[1] + gst[1];
-        h->stats[2] = fst[3] + gst[2];
-        h->stats[3] = fst[2];
-        h->stats[4] = fst[4];
-        h->stats[5] = fst[5];
-        h->stats[6] = fst[6];
-        h->stats[7] = fst[7];
+        h->stats[2] = fst[2] + gst[2];
+        h->stats[3] = fst[3];
+        for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
         h->n_hits = (int64_t)tot;
         h->fetched = true;
         return KW_OK;
@@ -945,7 +1015,7 @@ extern "C" int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats)
     if (!h || !stats) return KW_EINVAL;
     int rc = finish(h);
     if (rc) return rc;
-    for (int i = 0; i < n_stats && i < 8; ++i) stats[i] = (int64_t)h->stats[i];
+    for (int i = 0; i < n_stats && i < KW_N_STATS; ++i) stats[i] = (int64_t)h->stats[i];
     return KW_OK;
 }
 
@@ -954,9 +1024,20 @@ extern "C" int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms
     if (!h) return KW_EINVAL;
     int rc = finish(h);
     if (rc) return rc;
-    if (fast_ms) HIPCHK(h, hipEventElapsedTime(fast_ms, h->ev0, h->ev1));
-    if (generic_ms) HIPCHK(h, hipEventElapsedTime(generic_ms, h->ev1, h->evg));
+    if (fast_ms) HIPCHK(h, hipEventElapsedTime(fast_ms, h->ev0, h->evr));
+    if (generic_ms) HIPCHK(h, hipEventElapsedTime(generic_ms, h->evr, h->evg));
     if (total_ms) HIPCHK(h, hipEventElapsedTime(total_ms, h->ev0, h->ev2));
+    return KW_OK;
+}
+
+extern "C" int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n)
+{
+    if (!h || !ms) return KW_EINVAL;
+    int rc = finish(h);
+    if (rc) return rc;
+    hipEvent_t ev[6] = {h->ev0, h->ev1, h->evr, h->evg, h->ev2, h->ev2};
+    for (int i = 0; i < n && i < 4; ++i) HIPCHK(h, hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+    if (n > 4) HIPCHK(h, hipEventElapsedTime(&ms[4], h->ev0, h->ev2));
     return KW_OK;
 }
 
@@ -978,6 +1059,7 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->ev2) (void)hipEventDestroy(h->ev2);
     if (h->evg) (void)hipEventDestroy(h->evg);
+    if (h->evr) (void)hipEventDestroy(h->evr);
     delete h;
     return KW_OK;
 }

@@ -1,4 +1,6 @@
-// Fast path of libkwmatch (gfx950): lean scan + register-resident resolve.
+// Fast path of libkwmatch (gfx950): a lean byte scan (kw_items_kernel) that
+// turns every anchor occurrence into an item, and a resolve kernel
+// (kw_resolve_kernel) that decides the names of each field from its items.
 //
 // Anchors.  Every use of a name is found through a short "anchor" substring
 // (4..8 bytes, or the whole name when it is only 2-3 bytes) chosen at the
@@ -7,38 +9,76 @@
 // anchor hit:
 //   U      whole uppercase name + the two \b conditions  (match_keywords.py:167)
 //   FULL   whole fuzzy name, byte-exact  (an exact substring = score 100)
-//   PIECE  one pigeonhole piece of a fuzzy name (seeds the LCS verification)
-//   RXW    whole name as a '.'-wildcard regex (positions of re.finditer)
+//   PIECE  one pigeonhole piece of a fuzzy name with m >= 21 (seeds the LCS
+//          verification; shorter names only allow exact interior windows)
+// Fuzzy names with 11 <= m <= 20 can also pass on an edge window: the first or
+// last m-1 code points of the field equal the name with one code point
+// deleted.  Those are found per field through the "edge" hash table of all
+// one-deletion variants and enter the item list as EDGE items.  A decided
+// name whose re.finditer needs the regex engine is searched wave-parallel
+// over its field after the decision (rx_positions).
 // Any anchor choice is correct; only the speed depends on the statistics.
 //
-// Filter.  4-byte keys in a 2^18-bit LDS table: word = hash(b0,b1,b2),
-// bit = mix(b3); 3-byte anchors fill their whole word.  2-byte anchors are
-// found through a cheap byte-class gate + an exact 64K-bit bigram table.
+// Filters (all in LDS).  Stage 1, every byte position: 4-byte key -> one bit
+// of a 2^18-bit table, word = hash(b0,b1,b2), bit = mix(b3); a 3-byte anchor
+// fills its whole word.  2-byte anchors: a byte-class gate + an exact 64K-bit
+// bigram table.  Stage 2, compacted survivors only: an independent hash of
+// the 4-byte key (2^17 bits) or of the 3-byte key (2^16 bits) must hit before
+// the global anchor hash table is probed.  Field edges: the first / last four
+// bytes of a field are tested against the prefix / suffix keys of the
+// one-deletion variants (2 x 2^15 bits); only flagged fields run the edge check.
 #pragma once
 #include "kwmatch_device.hpp"
 
 namespace kw {
 
-constexpr int FK_WAVES = 16;                    // waves per workgroup (1024 threads)
+constexpr int FK_WAVES = 16;                    // waves per scan workgroup (1024 threads)
 constexpr int FK_BLOCK = FK_WAVES * WAVE;
-constexpr int FK_FILT_WORDS = 8192;             // 32 KB
-constexpr int FK_B2_WORDS = 2048;               // 8 KB (64K bits)
+constexpr int FK_FILT_WORDS = 8192;             // stage 1: 2^18 bits = 32 KB
+constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
+constexpr int FK_T3_BITS = 16;                  // stage 2, 3-byte keys: 8 KB
+constexpr int FK_B2_WORDS = 2048;               // exact bigram table: 8 KB
+constexpr int FK_EDGE_BITS = 15;                // edge prefix / suffix keys: 2 x 4 KB
 constexpr int FK_CAND = 256;                    // candidates per compaction round
 constexpr int FK_ITEMS = 64;                    // items per field on the fast path
 constexpr int FK_CP_CAP = 16384;                // bytes of a non-ASCII field the fast path decodes
-constexpr uint32_t FK_MUL1 = 0x9E3779u;         // 24-bit multipliers (v_mul_u32_u24)
-constexpr uint32_t FK_MUL2 = 0xC2B2AEu;
+constexpr int RK_WAVES = 4;                     // waves per resolve workgroup
+constexpr int RK_BLOCK = RK_WAVES * WAVE;
+constexpr uint32_t FK_MUL1 = 0x9E3779u;         // 24-bit multiplier (v_mul_u32_u24)
+constexpr uint32_t FK_MUL2 = 0x85EBCA6Bu;
+constexpr uint32_t FK_MUL3 = 0xC2B2AE35u;
+constexpr uint32_t FK_MUL4 = 0x27D4EB2Fu;
 
-enum FastUseKind : uint32_t { FU_UPPER = 0, FU_FULL = 1, FU_PIECE = 2, FU_RXW = 3 };
+constexpr int FK_L2_WORDS = 1 << (FK_L2_BITS - 5);
+constexpr int FK_T3_WORDS = 1 << (FK_T3_BITS - 5);
+constexpr int FK_EDGE_WORDS = 1 << (FK_EDGE_BITS - 5);
 
-// pattern regex kind (bits [25:24] of fpat_info... kept in a separate array)
-enum RxKind : uint32_t { RXK_LITERAL = 0, RXK_WILD = 1, RXK_GENERIC = 2 };
+enum FastUseKind : uint32_t { FU_UPPER = 0, FU_FULL = 1, FU_PIECE = 2, FU_EDGE = 3 };
+
+// how re.finditer(name) finds positions: literal search or the regex engine
+enum RxKind : uint32_t { RXK_LITERAL = 0, RXK_REGEX = 1 };
+constexpr uint32_t EDGE_MIN_M = 11, EDGE_MAX_M = 20;   // names with edge-only fuzzy windows
+
+// per-document header written by the scan kernel (uint2):
+//   x = index of the document's first item in FastScratch::items
+//   y = n0 [6:0] | n1 [13:7] | flags
+constexpr uint32_t DH_NEED = 1u << 16;          // the resolve kernel has work on this document
+constexpr uint32_t DH_EDGE0 = 1u << 17;         // field 0: edge prefilter hit (prefix or suffix)
+constexpr uint32_t DH_EDGE1 = 1u << 18;
+constexpr uint32_t DH_NA0 = 1u << 19;           // field 0 has non-ASCII bytes
+constexpr uint32_t DH_NA1 = 1u << 20;
+constexpr uint32_t DH_DEFER = 1u << 21;         // sent to the generic kernel by the scan
 
 struct FastTables {
     const uint32_t *filt;       // FK_FILT_WORDS
+    const uint32_t *l2;         // FK_L2_WORDS
+    const uint32_t *t3;         // FK_T3_WORDS
     const uint32_t *b2;         // FK_B2_WORDS
+    const uint32_t *edge_pre;   // FK_EDGE_WORDS
+    const uint32_t *edge_suf;   // FK_EDGE_WORDS
     uint32_t gate_lo[4], gate_hi[4];   // byte ranges gating the 2-byte path
     int n_gate;                 // 0 = no 2-byte anchors, -1 = test every position
+    int has_t3;                 // any 3-byte anchor
     const uint64_t *ht_key;     // (len << 32) | key bytes; ~0 = empty
     const uint32_t *ht_begin;
     const uint32_t *ht_cnt;
@@ -64,22 +104,59 @@ struct FastTables {
     const uint32_t *sub_cnt;
     const uint32_t *sub_pat;
     uint32_t sub_mask;
+    const uint64_t *edge_key;   // (hash of L code points + L * golden) | 1; 0 = empty
+    const uint32_t *edge_begin;
+    const uint32_t *edge_cnt;
+    const uint32_t *edge_ent;   // pattern << 5 | deleted code-point index
+    uint32_t edge_mask;
     const uint32_t *word_bits;
     int f_first;
     int empty_pat;
 };
 
 struct FastScratch {
-    kw_hit *out;                // per wave: out_cap records
-    uint32_t *out_cnt;          // per wave
+    uint64_t *items;            // per scan wave: item_cap items
+    uint32_t item_cap;
+    uint2 *hdr;                 // per document
+    kw_hit *out;                // per resolve wave: out_cap records
+    uint32_t *out_cnt;          // per resolve wave
     uint32_t out_cap;
-    uint32_t *cps;              // per wave: CP_CAP decoded code points (non-ASCII fields)
-    uint32_t *cpbase;           // per wave: CP_CAP/4 cumulative lead counts per 16-byte chunk
+    uint32_t *cps;              // per resolve wave: FK_CP_CAP decoded code points (non-ASCII fields)
+    uint32_t *cpbase;           // per resolve wave: cumulative lead counts per 64-byte block
     uint32_t *defer_list;       // docs sent to the generic kernel
     uint32_t *defer_cnt;
     uint32_t defer_cap;
     uint32_t *status;
-    unsigned long long *stats;  // [0] candidates [1] anchor hits [2] verify items [3] LCS windows [4] deferred
+    unsigned long long *stats;  // see kw_stats
 };
+
+// host + device hashes of the LDS tables
+__host__ __device__ __forceinline__ uint32_t fk_word(uint32_t key4)
+{
+    return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;    // depends on bytes 0..2
+}
+__host__ __device__ __forceinline__ uint32_t fk_bit(uint32_t key4)
+{
+    const uint32_t b3 = key4 >> 24;
+    return (b3 ^ (b3 >> 5)) & 31u;
+}
+__host__ __device__ __forceinline__ uint32_t fk_l2_index(uint32_t key4) { return (key4 * FK_MUL2) >> (32 - FK_L2_BITS); }
+__host__ __device__ __forceinline__ uint32_t fk_t3_index(uint32_t key4)
+{
+    return ((key4 & 0xFFFFFFu) * FK_MUL3) >> (32 - FK_T3_BITS);
+}
+__host__ __device__ __forceinline__ uint32_t fk_edge_index(uint32_t key4)
+{
+    return (key4 * FK_MUL4) >> (32 - FK_EDGE_BITS);
+}
+__host__ __device__ __forceinline__ uint32_t fk_b2_index(uint32_t key2)
+{
+    return ((key2 & 0xFFFFu) * 40503u) & 0xFFFFu;     // bijection on 16 bits (odd multiplier)
+}
+__host__ __device__ __forceinline__ uint32_t fk_ht_slot(uint64_t k, uint32_t mask)
+{
+    uint64_t x = k * 0x9E3779B97F4A7C15ull;
+    return (uint32_t)(x >> 40) & mask;
+}
 
 }  // namespace kw

@@ -1,7 +1,14 @@
-// Fast-path kernel (see kwmatch_fast.hpp).  Included after kwmatch_kernels.hpp
-// (shares its wave/text helpers).  One wave owns one document at a time; every
-// rare case (more than 64 anchor uses in a field, a quantified regex name that
-// matched, ...) sends the whole document to the generic kernel instead.
+// Fast path kernels (see kwmatch_fast.hpp).  Included after kwmatch_kernels.hpp
+// (shares its wave/text helpers).
+//
+//   kw_items_kernel    one wave per document: LDS filters over every byte,
+//                      anchor probes, items -> HBM, per-document header
+//   kw_resolve_kernel  one wave per document with work: sort the items of a
+//                      field, decide fuzzy names (exact / edge / LCS-verified
+//                      pieces), report re.finditer positions
+//
+// Rare documents (more than FK_ITEMS items in a field, non-ASCII fields longer
+// than FK_CP_CAP bytes) are handed to the generic kernel (kw_scan_kernel).
 #pragma once
 #include "kwmatch_fast.hpp"
 #include "kwmatch_kernels.hpp"
@@ -12,26 +19,6 @@
 #endif
 
 namespace kw {
-
-// ---------------------------------------------------------------- hashing (host + device)
-__host__ __device__ __forceinline__ uint32_t fk_word(uint32_t key4)
-{
-    return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;    // depends on bytes 0..2
-}
-__host__ __device__ __forceinline__ uint32_t fk_bit(uint32_t key4)
-{
-    const uint32_t b3 = key4 >> 24;
-    return (b3 ^ (b3 >> 5)) & 31u;
-}
-__host__ __device__ __forceinline__ uint32_t fk_b2_index(uint32_t key2)
-{
-    return ((key2 & 0xFFFFu) * 40503u) & 0xFFFFu;     // bijection on 16 bits (odd multiplier)
-}
-__host__ __device__ __forceinline__ uint32_t fk_ht_slot(uint64_t k, uint32_t mask)
-{
-    uint64_t x = k * 0x9E3779B97F4A7C15ull;
-    return (uint32_t)(x >> 40) & mask;
-}
 
 // ---------------------------------------------------------------- per-doc state
 struct FastDoc {
@@ -49,6 +36,18 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *__restrict__
     return __builtin_amdgcn_alignbyte(x1, x0, s);
 }
 
+// the 4-byte key at position j (0..15) of a lane's 16-byte chunk W[0..4]
+__device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], int j)
+{
+    uint32_t a = W[0], b = W[1];
+    if (j >= 4) { a = W[1]; b = W[2]; }
+    if (j >= 8) { a = W[2]; b = W[3]; }
+    if (j >= 12) { a = W[3]; b = W[4]; }
+    return __builtin_amdgcn_alignbyte(b, a, j & 3);
+}
+
+__device__ __forceinline__ bool lds_bit(const uint32_t *t, uint32_t idx) { return (t[idx >> 5] >> (idx & 31)) & 1u; }
+
 // byte-exact compare of text[p, p+len) with pat[0, len)
 __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_t p, const uint8_t *__restrict__ pat,
                                            uint32_t len)
@@ -65,39 +64,28 @@ __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_
     return true;
 }
 
-// '.'-wildcard regex (atoms LIT/ANY, no quantifiers) anchored at byte p; returns end byte or -1
-__device__ int64_t wild_match(const DevTables &T, const uint8_t *__restrict__ a, int64_t p, int64_t fe, uint32_t pat)
-{
-    const uint32_t ab = T.rx_off[pat], ae = T.rx_off[pat + 1];
-    int64_t b = p;
-    for (uint32_t k = ab; k < ae; ++k) {
-        if (b >= fe) return -1;
-        const int4 at = T.rx_atoms[k];
-        uint32_t cp;
-        const uint32_t len = decode_at(a, b, fe, &cp);
-        if (at.x == KW_RX_LIT) {
-            if (cp != (uint32_t)at.y) return -1;
-        } else if (cp == '\n') {
-            return -1;
-        }
-        b += len;
-    }
-    return b;
-}
-
 // ---------------------------------------------------------------- probe one candidate (this lane)
-__device__ void fast_probe(const FastTables &FT, const DevTables &T, const FastScratch &S, const FastDoc &D, int64_t p,
-                           uint32_t klen, uint64_t *items, uint32_t *icnt, uint32_t *dflag,
-                           unsigned long long &nanchor)
+// klen 4: a stage-1 filter hit (4- and 3-byte anchors); klen 2: a bigram-table hit.
+// Returns the number of stage-2 survivors (0 or 1) for the statistics.
+__device__ uint32_t fast_probe(const FastTables &FT, const DevTables &T, const FastDoc &D, int64_t p, uint32_t klen,
+                               uint32_t lo, const uint32_t *l2, const uint32_t *t3, uint64_t *items, uint32_t *icnt,
+                               uint32_t *dflag, unsigned long long &nanchor)
 {
     const uint8_t *__restrict__ arena = D.arena;
     const int f = p < D.t1 ? 0 : 1;
     const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
-    if (p + (klen == 2 ? 2 : 3) > fe) return;   // shortest anchor this candidate can start
-    const uint32_t lo = ld_u32_unaligned(arena, p), hi = ld_u32_unaligned(arena, p + 4);
-    const uint64_t h8 = (uint64_t)lo | ((uint64_t)hi << 32);
-    // probe the lengths this candidate can start: 4 (and 3) from the 4-byte filter, 2 from the gate
-    for (uint32_t L = klen; L >= (klen == 2 ? 2u : 3u); --L) {
+    if (p + (klen == 2 ? 2 : 3) > fe) return 0;   // shortest anchor this candidate can start
+    // stage 2: independent hashes of the 4- and 3-byte keys
+    bool try4 = false, try3 = false, try2 = klen == 2;
+    if (klen == 4) {
+        try4 = p + 4 <= fe && lds_bit(l2, fk_l2_index(lo));
+        try3 = FT.has_t3 && lds_bit(t3, fk_t3_index(lo));
+        if (!try4 && !try3) return 0;
+    }
+    const uint32_t hi = ld_u32_unaligned(arena, p + 4);
+    const uint64_t h8 = (uint64_t)lo | ((uint64_t)hi << 32);   // lo: the key from the scan registers
+    for (uint32_t L = 4; L >= 2; --L) {
+        if (!(L == 4 ? try4 : (L == 3 ? try3 : try2))) continue;
         if (p + (int64_t)L > fe) continue;
         const uint64_t key = ((uint64_t)L << 32) | (h8 & ((1ull << (8 * L)) - 1));
         uint32_t slot = fk_ht_slot(key, FT.ht_mask);
@@ -121,42 +109,21 @@ __device__ void fast_probe(const FastTables &FT, const DevTables &T, const FastS
                 const uint32_t kind = i0 & 0xFF, aoff = (i0 >> 8) & 0xFF, sboff = i0 >> 16;
                 const uint32_t sblen = i1 & 0xFFFF;
                 const uint32_t pat = FT.use_pat[u];
-                int64_t s0 = p - (int64_t)aoff;
-                if (kind == FU_RXW) {
-                    // aoff = atoms before the anchor: walk back that many code points
-                    s0 = p;
-                    uint32_t j = 0;
-                    for (; j < aoff && s0 > fb; ++j) {
-                        --s0;
-                        while (s0 > fb && (arena[s0] & 0xC0) == 0x80) --s0;
-                    }
-                    if (j < aoff) continue;
-                    if (wild_match(T, arena, s0, fe, pat) < 0) continue;
-                } else {
-                    if (s0 < fb) continue;
-                    if (s0 + (int64_t)sblen > fe) continue;
+                const int64_t s0 = p - (int64_t)aoff;
+                if (s0 < fb || s0 + (int64_t)sblen > fe) continue;
+                if (!span_equal(arena, s0, FT.pat_bytes + FT.pat_boff[pat] + sboff, sblen)) continue;
+                if (kind == FU_UPPER) {
                     const uint32_t pi = FT.pat_info[pat];
-                    if (kind == FU_PIECE) {
-                        // pieces of names that only allow exact interior windows matter near the edges only
-                        const uint32_t m = pi_m(pi);
-                        if (20u * 1u >= m) {   // kfull(m) == 0  <=>  m <= 20
-                            const int64_t near = 4 * (int64_t)m + 4;
-                            if (s0 - fb >= near && fe - (s0 + (int64_t)sblen) >= near) continue;
-                        }
+                    const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
+                    const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
+                    if (wp == wf) continue;
+                    bool wn = false;
+                    if (s0 + (int64_t)sblen < fe) {
+                        uint32_t c;
+                        decode_at(arena, s0 + sblen, fe, &c);
+                        wn = is_word_cp(T, c);
                     }
-                    if (!span_equal(arena, s0, FT.pat_bytes + FT.pat_boff[pat] + sboff, sblen)) continue;
-                    if (kind == FU_UPPER) {
-                        const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
-                        const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
-                        if (wp == wf) continue;
-                        bool wn = false;
-                        if (s0 + (int64_t)sblen < fe) {
-                            uint32_t c;
-                            decode_at(arena, s0 + sblen, fe, &c);
-                            wn = is_word_cp(T, c);
-                        }
-                        if (wn == wl) continue;
-                    }
+                    if (wn == wl) continue;
                 }
                 const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(s0 - fb) << IT_POS_SHIFT) |
                                       ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
@@ -166,6 +133,7 @@ __device__ void fast_probe(const FastTables &FT, const DevTables &T, const FastS
             }
         }
     }
+    return 1;
 }
 
 // ---------------------------------------------------------------- field helpers
@@ -313,24 +281,122 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, const uint32_t *__restr
     return false;
 }
 
-}  // namespace kw
 
-namespace kw {
+// ---------------------------------------------------------------- edge windows (11 <= m <= 20)
+// A fuzzy name with 11 <= m <= 20 and m < n passes partial_ratio on an edge
+// window iff the first or the last m-1 code points of the field equal the
+// name with one code point deleted (20*1 < 2m-1; every other window of such a
+// name needs an exact occurrence, which the FULL use finds).  Lanes 0..19 take
+// (side, L = m-1): hash the window, look it up among the one-deletion variants,
+// verify exactly and append an EDGE item.  Returns the number of items added.
+__device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint64_t *items, uint32_t *icnt_f,
+                                  uint32_t *dflag)
+{
+    const int lane = lane_id();
+    const uint32_t L = (EDGE_MIN_M - 1) + (uint32_t)(lane % 10);
+    const bool act = lane < 20 && L + 2 <= F.n;
+    const uint8_t *__restrict__ a = F.arena;
+    uint64_t hh = 0;
+    int64_t b0 = F.fb;
+    if (F.ascii) {
+        // bytes are code points: the wave holds the first and the last 20 bytes
+        const int64_t flen = F.fe - F.fb;
+        const int t20 = flen < 20 ? (int)flen : 20;
+        const uint32_t head = (lane < t20) ? a[F.fb + lane] : 0u;
+        const uint32_t tail = (lane < t20) ? a[F.fe - t20 + lane] : 0u;
+        if (lane >= 10) b0 = F.fe - (int64_t)L;
+        const int tbase = t20 - (int)L;   // suffix window = tail[t20-L, t20)
+#pragma unroll
+        for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j) {
+            const uint32_t ch = (uint32_t)__shfl((int)head, j, WAVE);
+            const uint32_t ct = (uint32_t)__shfl((int)tail, (tbase + j) & 63, WAVE);
+            const uint32_t c = lane >= 10 ? ct : ch;
+            if ((uint32_t)j < L) hh = hh * SUB_B + c;
+        }
+    } else if (act) {
+        if (lane >= 10) {   // suffix: walk back L code points from the field end
+            b0 = F.fe;
+            for (uint32_t j = 0; j < L; ++j) {
+                --b0;
+                while ((a[b0] & 0xC0) == 0x80) --b0;
+            }
+        }
+        int64_t b = b0;
+        for (uint32_t j = 0; j < L; ++j) {
+            uint32_t c;
+            b += decode_at(a, b, F.fe, &c);
+            hh = hh * SUB_B + c;
+        }
+    }
+    uint32_t added = 0;
+    if (act) {
+        const uint64_t key = (hh + (uint64_t)L * 0x9E3779B97F4A7C15ull) | 1ull;
+        uint32_t slot = (uint32_t)(key >> 32) & FT.edge_mask;
+        uint32_t eb = 0, ec = 0;
+        for (;;) {
+            const uint64_t kk = FT.edge_key[slot];
+            if (kk == key) { eb = FT.edge_begin[slot]; ec = FT.edge_cnt[slot]; break; }
+            if (kk == 0) break;
+            slot = (slot + 1) & FT.edge_mask;
+        }
+        for (uint32_t e = 0; e < ec; ++e) {
+            const uint32_t ent = FT.edge_ent[eb + e];
+            const uint32_t P = ent >> 5, del = ent & 31u;
+            if (pi_m(FT.pat_info[P]) != L + 1) continue;
+            const uint32_t *nm = FT.pat_cps + FT.pat_cp_off[P];
+            bool eq = true;
+            int64_t bb = b0;
+            for (uint32_t j = 0; j < L && eq; ++j) {
+                uint32_t c;
+                bb += decode_at(a, bb, F.fe, &c);
+                eq = c == nm[j < del ? j : j + 1];
+            }
+            if (!eq) continue;
+            const uint32_t idx = atomicAdd(icnt_f, 1u);
+            if (idx < (uint32_t)FK_ITEMS)
+                items[idx] = ((uint64_t)P << IT_PAT_SHIFT) | ((uint64_t)FU_EDGE << IT_KIND_SHIFT);
+            else
+                atomicOr(dflag, 1u);
+            ++added;
+        }
+    }
+    return added;
+}
+
+// every match position of a decided regex-class name (re.finditer, :177-180),
+// or `name: []` when there is none
+__device__ __noinline__ void fk_regex_positions(const DevTables &T, const DevScratch &GS, const FieldCtx &F, OutCtx &O, uint32_t P)
+{
+    const uint32_t cnt = rx_positions(T, GS, F, O, P);
+    if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
+}
 
 // ---------------------------------------------------------------- fast resolve of one field
-// Returns false if the document must go to the generic kernel.
-__device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const FastScratch &S, const DevScratch &GS,
-                                 FieldCtx &F, OutCtx &O, const uint64_t *items_lds, uint32_t N, uint32_t *cps,
-                                 uint32_t *blkcnt, bool maybe_nonascii, unsigned long long &nver,
-                                 unsigned long long &nwin)
+// Returns 0 when done, 1 if the field is a long non-ASCII field and 3 if the
+// items overflowed: the document then goes to the generic kernel.
+__device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const DevScratch &GS, FieldCtx &F, OutCtx &O,
+                                 uint64_t *items_lds, uint32_t *icnt_f, uint32_t *dflag, uint32_t *cps,
+                                 uint32_t *blkcnt, bool maybe_nonascii, bool edge, unsigned long long &nver,
+                                 unsigned long long &nwin, unsigned long long &nedge)
 {
     const int lane = lane_id();
     // ---- field facts (code points, ASCII) on demand
     const int64_t flen = F.fe - F.fb;
     F.ascii = maybe_nonascii ? field_is_ascii(F.arena, F.fb, F.fe) : true;
-    const bool maybe_short = flen <= 4 * MAXM;
-    F.n = (F.ascii || (N == 0 && !maybe_short)) ? (uint32_t)flen : field_cp_count(F.arena, F.fb, F.fe, false);
+    F.n = F.ascii ? (uint32_t)flen : field_cp_count(F.arena, F.fb, F.fe, false);
     const bool is_short = F.n <= (uint32_t)MAXM;
+    // ---- one-deletion edge windows of the 11..20-code-point names (prefiltered by the scan)
+    if (edge && F.n >= EDGE_MIN_M + 1) {
+        uint32_t added = fk_edge_items(FT, F, items_lds, icnt_f, dflag);
+        added = (uint32_t)wave_sum((int)added);
+        if (added) {
+            nedge += added;
+            wave_sync();
+            if (__builtin_amdgcn_readfirstlane(*dflag)) return 3;
+        }
+    }
+    wave_sync();
+    const uint32_t N = __builtin_amdgcn_readfirstlane(*icnt_f);
     if (N == 0 && !is_short) return 0;
     if (!F.ascii) {
         if (flen > (int64_t)FK_CP_CAP) return 1;
@@ -360,7 +426,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
         // the short path owns fuzzy names at least as long as the field
         const bool live = valid && !(fuzzy && m >= F.n);
-        const uint64_t fullm = __ballot(live && kind == FU_FULL);
+        const uint64_t fullm = __ballot(live && (kind == FU_FULL || kind == FU_EDGE));
         const bool decided_full = (fullm & gmask) != 0;
         // ---- verification of pieces of undecided fuzzy names (wave-serial over such items)
         uint64_t vneed = __ballot(live && fuzzy && !decided_full && kind == FU_PIECE);
@@ -381,21 +447,16 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
             if (fk_verify_piece(F, nm, mm, to_cp(F, bp), o, pl, nwin)) decided_v |= lg;
         }
         const bool decided = decided_full || ((decided_v >> lane) & 1ull);
-        // ---- positions: items that report re.finditer positions
+        // ---- positions: U names and literal fuzzy names report their exact occurrences
         const bool relevant = live && ((!fuzzy && kind == FU_UPPER) ||
-                                       (fuzzy && decided && rxk == RXK_LITERAL && kind == FU_FULL) ||
-                                       (fuzzy && decided && rxk == RXK_WILD && kind == FU_RXW));
-        // a decided fuzzy name whose regex needs the generic engine
-        if (__ballot(live && fuzzy && decided && rxk == RXK_GENERIC)) return 2;
+                                       (fuzzy && decided && rxk == RXK_LITERAL && kind == FU_FULL));
         const uint32_t cpos = relevant ? to_cp(F, bpos) : 0u;
         const uint64_t relm = __ballot(relevant);
-        // leftmost non-overlapping selection per group; a match spans m code points
-        // (literal) or one code point per atom ('.'-wildcard regex)
-        const uint32_t mlen = (relevant && rxk == RXK_WILD && kind == FU_RXW) ? T.rx_off[pat + 1] - T.rx_off[pat] : m;
+        // leftmost non-overlapping selection per group (a match spans m code points)
         const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
         const int pr = prevrel ? 63 - __builtin_clzll(prevrel) : -1;
         const uint32_t pcpos = (uint32_t)__shfl((int)cpos, pr < 0 ? lane : pr, WAVE);
-        const bool overlap = relevant && pr >= 0 && cpos < pcpos + mlen;
+        const bool overlap = relevant && pr >= 0 && cpos < pcpos + m;
         uint64_t keep = relm;
         if (__ballot(overlap)) {
             // rare: resolve the greedy chain serially
@@ -408,17 +469,24 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                 mm2 &= mm2 - 1;
                 const int h = __shfl(gs, l, WAVE);
                 const uint32_t s = (uint32_t)__shfl((int)cpos, l, WAVE);
-                const uint32_t len = (uint32_t)__shfl((int)mlen, l, WAVE);
+                const uint32_t len = (uint32_t)__shfl((int)m, l, WAVE);
                 if (h != cur_head) { cur_head = h; last_end = 0; keep |= 1ull << l; last_end = s + len; continue; }
                 if (s >= last_end) { keep |= 1ull << l; last_end = s + len; }
             }
         }
         const bool k_me = (keep >> lane) & 1ull;
         emit_hits(O, GS, k_me, F.doc, pat, cpos, F.field);
-        // decided fuzzy groups without any reported position: `name: []`
-        const uint64_t keptg = keep;   // per group: any kept?
-        const bool none_kept = (keptg & gmask) == 0;
-        emit_hits(O, GS, head && live && fuzzy && decided && none_kept, F.doc, pat, KW_NOPOS, F.field);
+        // decided literal fuzzy groups without any occurrence: `name: []`
+        const bool none_kept = (keep & gmask) == 0;
+        emit_hits(O, GS, head && live && fuzzy && decided && rxk == RXK_LITERAL && none_kept, F.doc, pat, KW_NOPOS,
+                  F.field);
+        // decided regex-class names: re.finditer over the field
+        uint64_t rxm = __ballot(head && live && fuzzy && decided && rxk == RXK_REGEX);
+        while (rxm) {
+            const int l = __builtin_ctzll(rxm);
+            rxm &= rxm - 1;
+            fk_regex_positions(T, GS, F, O, (uint32_t)__shfl((int)pat, l, WAVE));
+        }
     }
     // ---- short field: the field is the needle, the longer names are the haystacks
     if (is_short) {
@@ -463,12 +531,15 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                     }
                     exact = hit && m == n;
                 }
-                if (__ballot(hit && rk == RXK_GENERIC)) return 2;
-                // literal: position 0 iff the name equals the field; wildcard: iff it matches at 0
-                bool at0 = false;
-                if (hit && rk == RXK_WILD) at0 = wild_match(T, F.arena, F.fb, F.fe, P) == F.fe;
-                if (hit && rk == RXK_LITERAL) at0 = exact;
-                emit_hits(O, GS, hit, F.doc, P, at0 ? 0u : KW_NOPOS, F.field);
+                // literal: position 0 iff the name equals the field
+                const bool lit = hit && rk == RXK_LITERAL;
+                emit_hits(O, GS, lit, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
+                uint64_t rxm = __ballot(hit && rk == RXK_REGEX);
+                while (rxm) {
+                    const int l = __builtin_ctzll(rxm);
+                    rxm &= rxm - 1;
+                    fk_regex_positions(T, GS, F, O, (uint32_t)__shfl((int)P, l, WAVE));
+                }
             }
             return 0;
         }
@@ -497,32 +568,36 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                 bool exact = false;
                 ++nver;
                 if (!fk_short_decide(fc, n, FT.pat_cps + FT.pat_cp_off[P], m, &exact, nwin)) continue;
-                const uint32_t rk = FT.pat_rxk[P];
-                if (rk == RXK_GENERIC) return 2;
-                bool at0 = false;
-                if (rk == RXK_WILD) at0 = wild_match(T, F.arena, F.fb, F.fe, P) == F.fe;
-                else at0 = exact;
-                emit_hits(O, GS, lane == 0, F.doc, P, at0 ? 0u : KW_NOPOS, F.field);
+                if (FT.pat_rxk[P] == RXK_REGEX) fk_regex_positions(T, GS, F, O, P);
+                else emit_hits(O, GS, lane == 0, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
             }
         }
     }
     return 0;
 }
 
-// ---------------------------------------------------------------- the fast kernel
-__global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                           const int64_t *__restrict__ off, int64_t n_docs,
-                                                           FastScratch S, DevScratch GS)
+
+// ---------------------------------------------------------------- kernel 1: the scan
+__global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                            const int64_t *__restrict__ off, int64_t n_docs,
+                                                            FastScratch S)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     uint32_t *filt = (uint32_t *)smem_raw;
-    uint32_t *b2 = filt + FK_FILT_WORDS;
-    uint64_t *items_all = (uint64_t *)(b2 + FK_B2_WORDS);                 // FK_WAVES * 2 * FK_ITEMS
-    uint32_t *cand_all = (uint32_t *)(items_all + FK_WAVES * 2 * FK_ITEMS); // FK_WAVES * FK_CAND
-    uint32_t *cnt_all = cand_all + FK_WAVES * FK_CAND;                      // FK_WAVES * 4
+    uint32_t *l2 = filt + FK_FILT_WORDS;
+    uint32_t *t3 = l2 + FK_L2_WORDS;
+    uint32_t *b2 = t3 + FK_T3_WORDS;
+    uint32_t *epre = b2 + FK_B2_WORDS;
+    uint32_t *esuf = epre + FK_EDGE_WORDS;
+    uint64_t *items_all = (uint64_t *)(esuf + FK_EDGE_WORDS);               // FK_WAVES * 2 * FK_ITEMS
+    uint2 *cand_all = (uint2 *)(items_all + FK_WAVES * 2 * FK_ITEMS);       // FK_WAVES * FK_CAND
+    uint32_t *cnt_all = (uint32_t *)(cand_all + FK_WAVES * FK_CAND);         // FK_WAVES * 4
 
     for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FK_BLOCK) filt[i] = FT.filt[i];
+    for (int i = threadIdx.x; i < FK_L2_WORDS; i += FK_BLOCK) l2[i] = FT.l2[i];
+    for (int i = threadIdx.x; i < FK_T3_WORDS; i += FK_BLOCK) t3[i] = FT.t3[i];
     for (int i = threadIdx.x; i < FK_B2_WORDS; i += FK_BLOCK) b2[i] = FT.b2[i];
+    for (int i = threadIdx.x; i < FK_EDGE_WORDS; i += FK_BLOCK) { epre[i] = FT.edge_pre[i]; esuf[i] = FT.edge_suf[i]; }
     __syncthreads();
 
     const int lane = lane_id();
@@ -530,17 +605,11 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTab
     const int64_t wave = (int64_t)blockIdx.x * FK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * FK_WAVES;
     uint64_t *items = items_all + wib * 2 * FK_ITEMS;
-    uint32_t *cand = cand_all + wib * FK_CAND;
+    uint2 *cand = cand_all + wib * FK_CAND;   // (rel pos << 1 | 2-byte gate, 4-byte key)
     uint32_t *icnt = cnt_all + wib * 4;       // [0],[1] item counts, [2] defer flag
-    uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
-    uint32_t *blkcnt = S.cpbase + (size_t)wave * (CP_CAP / 16 + 2);
-
-    OutCtx O;
-    O.out = S.out + (size_t)wave * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = 0;
-    unsigned long long ncand = 0, nanchor = 0, nver = 0, nwin = 0, ndefer = 0;
-    unsigned long long ndef_items = 0, ndef_cp = 0, ndef_rx = 0;
+    uint64_t *gitems = S.items + (size_t)wave * S.item_cap;
+    uint32_t cursor = 0;                      // items this wave wrote to HBM
+    unsigned long long ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;
 
     for (int64_t d = wave; d < n_docs; d += n_waves) {
         FastDoc D;
@@ -551,8 +620,21 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTab
         D.doc = (uint32_t)d;
         if (lane < 4) icnt[lane] = 0;
         wave_sync();
-        const uint32_t out_mark = O.n;
         bool defer = (D.t1 - D.t0 > MAX_FIELD_BYTES) || (D.t2 - D.t1 > MAX_FIELD_BYTES);
+        // edge prefilter: first / last four bytes of each field (lanes 0..3)
+        uint32_t flags = 0;
+        {
+            const int f = lane >> 1;
+            const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+            bool e = false;
+            if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+                const uint32_t k = ld_u32_unaligned(arena, (lane & 1) ? fe - 4 : fb);
+                e = lds_bit((lane & 1) ? esuf : epre, fk_edge_index(k));
+            }
+            const uint64_t em = __ballot(e);
+            if (em & 3ull) flags |= DH_EDGE0;
+            if (em & 12ull) flags |= DH_EDGE1;
+        }
         bool na0 = false, na1 = false;
         const int64_t base = D.t0 & ~(int64_t)15;
         for (int64_t blk = base; blk < D.t2 && !defer; blk += SCAN_TILE) {
@@ -630,13 +712,15 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTab
                 while (hm) {
                     const int j = __ffs(hm) - 1;
                     hm &= hm - 1;
-                    if (k >= rb && k < rb + FK_CAND) cand[k - rb] = ((uint32_t)(lp + j - D.t0) << 1);
+                    if (k >= rb && k < rb + FK_CAND)
+                        cand[k - rb] = make_uint2((uint32_t)(lp + j - D.t0) << 1, fk_key_at(W, j));
                     ++k;
                 }
                 while (gm) {
                     const int j = __ffs(gm) - 1;
                     gm &= gm - 1;
-                    if (k >= rb && k < rb + FK_CAND) cand[k - rb] = ((uint32_t)(lp + j - D.t0) << 1) | 1u;
+                    if (k >= rb && k < rb + FK_CAND)
+                        cand[k - rb] = make_uint2(((uint32_t)(lp + j - D.t0) << 1) | 1u, fk_key_at(W, j));
                     ++k;
                 }
                 wave_sync();
@@ -644,10 +728,10 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTab
                 for (int i0 = 0; i0 < lim; i0 += WAVE) {
                     const int i = i0 + lane;
                     if (i < lim) {
-                        const uint32_t e = cand[i];
+                        const uint2 e = cand[i];
                         if (FK_STAGE >= 1)
-                            fast_probe(FT, T, S, D, D.t0 + (e >> 1), (e & 1u) ? 2u : 4u, items, icnt, &icnt[2],
-                                       nanchor);
+                            ncand2 += fast_probe(FT, T, D, D.t0 + (e.x >> 1), (e.x & 1u) ? 2u : 4u, e.y, l2, t3, items,
+                                                 icnt, &icnt[2], nanchor);
                     }
                 }
                 wave_sync();
@@ -657,62 +741,145 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_fast_kernel(FastTables FT, DevTab
             if (defer) ++ndef_items;
         }
         wave_sync();
-        if (!defer) {
-            const uint32_t N0 = __builtin_amdgcn_readfirstlane(icnt[0]);
-            const uint32_t N1 = __builtin_amdgcn_readfirstlane(icnt[1]);
-            const bool mna[2] = {__ballot(na0) != 0, __ballot(na1) != 0};
-            for (int f = 0; f < 2 && !defer; ++f) {
-                FieldCtx F;
-                F.arena = arena;
-                F.fb = f ? D.t1 : D.t0;
-                F.fe = f ? D.t2 : D.t1;
-                F.cps = cps;
-                F.blkcnt = blkcnt;
-                F.doc = D.doc;
-                F.field = (uint32_t)f;
-                F.ascii = true;
-                F.n = 0;
-                const uint32_t N = f ? N1 : N0;
-                const int rs = FK_STAGE < 2 ? 0 : fk_resolve_field(FT, T, S, GS, F, O, items + f * FK_ITEMS, N,
-                                                                   cps, blkcnt, mna[f], nver, nwin);
-                if (rs) {
-                    defer = true;
-                    if (rs == 1) ++ndef_cp;
-                    else ++ndef_rx;
-                }
-            }
-        }
+        const uint32_t n0 = __builtin_amdgcn_readfirstlane(icnt[0]);
+        const uint32_t n1 = __builtin_amdgcn_readfirstlane(icnt[1]);
+        if (!defer && cursor + n0 + n1 > S.item_cap) { defer = true; ++ndef_items; }
+        if (__ballot(na0)) flags |= DH_NA0;
+        if (__ballot(na1)) flags |= DH_NA1;
+        uint2 h;
+        h.x = (uint32_t)(wave * S.item_cap + cursor);
         if (defer) {
-            O.n = out_mark;   // drop this doc's partial records; the generic kernel redoes it
             ++ndefer;
+            h.y = DH_DEFER;
             if (lane == 0) {
                 const uint32_t i = atomicAdd(S.defer_cnt, 1u);
                 if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
-                else atomicOr(&GS.status[0], ST_ITEM_OVERFLOW);
+                else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
             }
+        } else {
+            // items -> HBM (field 0 then field 1)
+            if (lane < (int)n0) gitems[cursor + lane] = items[lane];
+            if (lane < (int)n1) gitems[cursor + n0 + lane] = items[FK_ITEMS + lane];
+            cursor += n0 + n1;
+            // the resolve kernel has work: items, an edge candidate, or a field that may be short
+            const int64_t l0 = D.t1 - D.t0, l1 = D.t2 - D.t1;
+            const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
+            const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
+            const bool need = (n0 + n1) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
+            h.y = n0 | (n1 << 7) | flags | (need ? DH_NEED : 0u);
         }
+        if (lane == 0) S.hdr[d] = h;
     }
-    if (lane == 0) S.out_cnt[wave] = O.n;
-    unsigned long long a = nanchor, v = nver, w = nwin;
+    unsigned long long a = nanchor, c2 = ncand2;
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) {
         a += __shfl_xor(a, dd, WAVE);
-        v += __shfl_xor(v, dd, WAVE);
-        w += __shfl_xor(w, dd, WAVE);
+        c2 += __shfl_xor(c2, dd, WAVE);
     }
     if (lane == 0) {
         atomicAdd(&S.stats[0], ncand);
         atomicAdd(&S.stats[1], a);
-        atomicAdd(&S.stats[2], v / WAVE);
-        atomicAdd(&S.stats[3], w / WAVE);
         atomicAdd(&S.stats[4], ndefer);
         atomicAdd(&S.stats[5], ndef_items);
-        atomicAdd(&S.stats[6], ndef_cp);
-        atomicAdd(&S.stats[7], ndef_rx);
+        atomicAdd(&S.stats[8], c2);
     }
 }
 
-constexpr size_t kFastLds = (size_t)FK_FILT_WORDS * 4 + (size_t)FK_B2_WORDS * 4 +
-                            (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_CAND * 4 + 4 * 4);
+constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS + FK_B2_WORDS + 2 * FK_EDGE_WORDS) * 4 +
+                             (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_CAND * 8 + 4 * 4);
+
+// ---------------------------------------------------------------- kernel 2: resolve
+__global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, DevTables T,
+                                                              const uint8_t *__restrict__ arena,
+                                                              const int64_t *__restrict__ off, int64_t n_docs,
+                                                              FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
+    __shared__ uint32_t cnt_all[RK_WAVES * 4];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t wave = (int64_t)blockIdx.x * RK_WAVES + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * RK_WAVES;
+    uint64_t *items = items_all + wib * FK_ITEMS;
+    uint32_t *icnt = cnt_all + wib * 4;
+    uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
+    uint32_t *blkcnt = S.cpbase + (size_t)wave * (CP_CAP / 16 + 2);
+    OutCtx O;
+    O.out = S.out + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    unsigned long long nver = 0, nwin = 0, nedge = 0, ndefer = 0, ndef_cp = 0, ndef_items = 0, nres = 0;
+
+    for (int64_t c0 = wave * WAVE; c0 < n_docs; c0 += n_waves * WAVE) {
+        const int64_t dl = c0 + lane;
+        uint2 hl = make_uint2(0u, 0u);
+        if (dl < n_docs) hl = S.hdr[dl];
+        uint64_t todo = __ballot((hl.y & DH_NEED) != 0 && (hl.y & DH_DEFER) == 0);
+        while (todo) {
+            const int l = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t d = c0 + l;
+            const uint32_t hx = (uint32_t)__shfl((int)hl.x, l, WAVE);
+            const uint32_t hy = (uint32_t)__shfl((int)hl.y, l, WAVE);
+            const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
+            const uint32_t nf[2] = {hy & 127u, (hy >> 7) & 127u};
+            const uint32_t out_mark = O.n;
+            bool defer = false;
+            ++nres;
+            for (int f = 0; f < 2 && !defer; ++f) {
+                const uint32_t N = nf[f];
+                const uint64_t *src = S.items + hx + (f ? nf[0] : 0u);
+                if (lane < (int)N) items[lane] = src[lane];
+                if (lane == 0) { icnt[0] = N; icnt[1] = 0; }
+                wave_sync();
+                FieldCtx F;
+                F.arena = arena;
+                F.fb = f ? t1 : t0;
+                F.fe = f ? t2 : t1;
+                F.cps = cps;
+                F.blkcnt = blkcnt;
+                F.doc = (uint32_t)d;
+                F.field = (uint32_t)f;
+                F.ascii = true;
+                F.n = 0;
+                const bool na = (hy & (f ? DH_NA1 : DH_NA0)) != 0;
+                const bool edge = (hy & (f ? DH_EDGE1 : DH_EDGE0)) != 0;
+                const int rs = FK_STAGE < 2 ? 0 : fk_resolve_field(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps,
+                                                                   blkcnt, na, edge, nver, nwin, nedge);
+                if (rs) {
+                    defer = true;
+                    if (rs == 1) ++ndef_cp;
+                    else ++ndef_items;
+                }
+                wave_sync();
+            }
+            if (defer) {
+                O.n = out_mark;   // drop this doc's partial records; the generic kernel redoes it
+                ++ndefer;
+                if (lane == 0) {
+                    const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                    if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
+                    else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+                }
+            }
+        }
+    }
+    if (lane == 0) S.out_cnt[wave] = O.n;
+    unsigned long long v = nver, w = nwin;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        v += __shfl_xor(v, dd, WAVE);
+        w += __shfl_xor(w, dd, WAVE);
+    }
+    if (lane == 0) {
+        atomicAdd(&S.stats[2], w / WAVE);
+        atomicAdd(&S.stats[3], v / WAVE);
+        atomicAdd(&S.stats[4], ndefer);
+        atomicAdd(&S.stats[5], ndef_items);
+        atomicAdd(&S.stats[6], ndef_cp);
+        atomicAdd(&S.stats[7], nedge);
+        atomicAdd(&S.stats[9], nres);
+    }
+}
 
 }  // namespace kw

@@ -142,12 +142,19 @@ class GpuMatcher:
         host = d.cpu().numpy()
         return host.view(np.uint32).reshape(-1, 4).copy().view(_native.HIT_DTYPE).reshape(-1)
 
+    STAT_KEYS = ('candidates', 'anchor_hits', 'lcs_windows', 'verifications', 'deferred_docs', 'deferred_items',
+                 'deferred_long_nonascii', 'edge_items', 'candidates_stage2', 'resolved_docs')
+
     def stats(self) -> Dict[str, int]:
-        v = np.zeros(8, dtype=np.int64)
-        _native.check(_native.lib().kw_stats(self.h, _native.ptr(v), 8), self.h)
-        return {'candidates': int(v[0]), 'anchor_hits': int(v[1]), 'lcs_windows': int(v[2]),
-                'verifications': int(v[3]), 'deferred_docs': int(v[4]), 'deferred_items': int(v[5]),
-                'deferred_long_nonascii': int(v[6]), 'deferred_regex': int(v[7])}
+        v = np.zeros(_native.KW_N_STATS, dtype=np.int64)
+        _native.check(_native.lib().kw_stats(self.h, _native.ptr(v), _native.KW_N_STATS), self.h)
+        return {k: int(x) for k, x in zip(self.STAT_KEYS, v)}
+
+    def kernel_times(self) -> Dict[str, float]:
+        """Per-kernel device times (ms) of the last scan."""
+        v = np.zeros(5, dtype=np.float32)
+        _native.check(_native.lib().kw_last_kernel_times(self.h, _native.ptr(v), 5), self.h)
+        return dict(zip(('scan', 'resolve', 'generic', 'compact', 'total'), (float(x) for x in v)))
 
     def kernel_ms(self) -> Tuple[float, float, float]:
         """(fast kernel, generic kernel, all kernels incl. compaction) in ms for the last scan."""

@@ -84,15 +84,12 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    scan_ms, gen_ms, total_ms = [], [], []
+    ktimes = []
     t0 = time.perf_counter()
     counts = None
     for _ in range(args.steps):
         counts = step()
-        fk, gk, t = m.kernel_ms()
-        scan_ms.append(fk)
-        gen_ms.append(gk)
-        total_ms.append(t)
+        ktimes.append(m.kernel_times())
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -119,7 +116,8 @@ def main():
     st = m.stats()
     if rank != 0:
         return
-    scan_avg = float(np.mean(scan_ms))
+    kavg = {k: float(np.mean([t[k] for t in ktimes])) for k in ktimes[0]}
+    scan_avg = kavg['scan']
     achieved = local_bytes / (scan_avg * 1e-3) / 1e9
     cpu = None
     if world == 1 and args.cpu_sample > 0:
@@ -147,11 +145,11 @@ def main():
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
-            'traffic': pmc_traffic(args.traffic_json, 'kw_fast_kernel', n_local, args.seed),
+            'traffic': pmc_traffic(args.traffic_json, 'kw_items_kernel', n_local, args.seed),
             'algorithmic_bytes_per_launch': local_bytes,
-            'kernel': 'kw::kw_fast_kernel', 'kernel_ms_avg': round(scan_avg, 4),
-            'generic_kernel_ms_avg': round(float(np.mean(gen_ms)), 4),
-            'step_kernels_ms_avg': round(float(np.mean(total_ms)), 4),
+            'kernel': 'kw::kw_items_kernel', 'kernel_ms_avg': round(scan_avg, 4),
+            'kernels_ms_avg': {k: round(v, 4) for k, v in kavg.items()},
+            'all_kernels_GBps': round(local_bytes / (kavg['total'] * 1e-3) / 1e9, 2),
         },
         'cpu_baseline': cpu,
         'scan_stats': st,

@@ -103,18 +103,25 @@ int kw_hits(kw_handle *h, int64_t *n_hits, const kw_hit **d_hits);
  * `cap` records (asynchronous on `stream`); *n_hits receives the count. */
 int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void *stream);
 
-/* Scan statistics of the last kw_scan (after kw_hits), up to 8 values:
- * [0] candidate positions that passed the LDS filter, [1] anchor occurrences,
- * [2] LCS windows evaluated, [3] fuzzy verifications, [4] documents the fast
- * kernel handed to the generic kernel, of which [5] had more anchor uses than
- * the fast path holds, [6] had a long non-ASCII field, [7] matched a name whose
- * regex needs the generic engine. */
+/* Scan statistics of the last kw_scan (after kw_hits), up to KW_N_STATS values:
+ * [0] byte positions that passed the stage-1 LDS filter, [1] anchor
+ * occurrences, [2] LCS windows evaluated, [3] fuzzy verifications, [4]
+ * documents handed to the generic kernel, of which [5] had more anchor items
+ * than the fast path holds and [6] had a long non-ASCII field, [7] one-deletion
+ * edge windows found (fuzzy names of 11..20 code points), [8] candidates that
+ * passed the stage-2 filter, [9] documents the resolve kernel worked on. */
+#define KW_N_STATS 10
 int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
 /* Device times (ms) of the last kw_scan, from HIP events on the scan's stream
- * (valid after kw_hits): the fast scan kernel, the generic kernel that redoes
- * deferred documents, and everything including result compaction. */
+ * (valid after kw_hits): the fast path (scan + resolve kernels), the generic
+ * kernel that redoes deferred documents, and everything including result
+ * compaction. */
 int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *total_ms);
+
+/* Per-kernel device times (ms) of the last kw_scan, up to 5 values: [0] scan
+ * (kw_items_kernel), [1] resolve, [2] generic, [3] result compaction, [4] total. */
+int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 
 const char *kw_last_error(kw_handle *h);
 int kw_destroy(kw_handle *h);

@@ -9,8 +9,7 @@ for fn in sorted(glob.glob('gpurun_out/*.log')):
     if js:
         j = json.loads(js[-1])
         r = j.get('roofline') or {}
-        print(os.path.basename(fn), j['value'], j['unit'], 'fast', r.get('kernel_ms_avg'), 'generic',
-              r.get('generic_kernel_ms_avg'), 'frac', r.get('frac'))
+        print(os.path.basename(fn), j['value'], j['unit'], 'frac', r.get('frac'), r.get('kernels_ms_avg'))
         print('   ', j.get('scan_stats'))
         if j.get('cpu_baseline'):
             print('   cpu', j['cpu_baseline'])
