@@ -1,8 +1,8 @@
 #!/bin/bash
-# Stage breakdown of the fast kernel (profiling variants built with -DFK_STAGE) + parity tests.
+# Parity tests + stage breakdown of the fast path (profiling variants built with -DFK_STAGE) + full bench.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -x -q > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest_rc=$rc" >> gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for st in 0 1 2; do

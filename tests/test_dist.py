@@ -1,0 +1,108 @@
+"""Multi-process (world_size 2, gloo on CPU) coverage of the sharded path.
+
+The GPU run uses the same functions over RCCL (backend "nccl"); here the
+collectives run over gloo so the N > 1 logic is exercised without a GPU:
+contiguous byte-balanced shards, the hit-count all-gather and the padded
+all-gather of packed hit records, whose rank-order concatenation must equal
+the single-process result in document order.
+"""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _fake_hits(lo: int, hi: int) -> np.ndarray:
+    """Deterministic [n, 4] int32 records for documents [lo, hi) (doc ids local to the shard)."""
+    rows = []
+    for d in range(lo, hi):
+        for k in range(d % 3):                 # 0, 1 or 2 hits per document: ragged ranks
+            rows.append((d - lo, 7 * d + k, k, d & 1))
+    return np.asarray(rows, dtype=np.int32).reshape(-1, 4)
+
+
+def _worker(rank, world, port, off, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from advanced_scrapper_amd import dist
+    r, w, _ = dist.init('gloo')
+    assert (r, w) == (rank, world)
+    lo, hi = dist.byte_balanced_ranges(off, world)[rank]
+    local = torch.from_numpy(_fake_hits(lo, hi))
+    counts = dist.allgather_counts(local.shape[0], torch.device('cpu'))
+    allh = dist.gather_hits(local, lo, torch.device('cpu'))
+    q.put((rank, counts, allh.numpy().tolist()))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def _run(world, off):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, off, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_gloo_sharded_gather_equals_single_process():
+    from advanced_scrapper_amd import dist
+    world = 2
+    rng = np.random.default_rng(3)
+    n_docs = 97
+    lens = rng.integers(0, 5000, size=2 * n_docs)
+    off = np.zeros(2 * n_docs + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    ranges = dist.byte_balanced_ranges(off, world)
+    res = _run(world, off)
+    want_counts = [len(_fake_hits(lo, hi)) for lo, hi in ranges]
+    exp = []
+    for lo, hi in ranges:
+        h = _fake_hits(lo, hi)
+        h[:, 0] += lo
+        exp.append(h)
+    exp = np.concatenate(exp)
+    single = _fake_hits(0, n_docs)          # one process over every document (global doc ids)
+    assert np.array_equal(exp, single)
+    for rank, counts, allh in res:
+        assert counts == want_counts, rank
+        got = np.asarray(allh, dtype=np.int32).reshape(-1, 4)
+        assert np.array_equal(got, single), rank
+
+
+def test_byte_balanced_ranges_cover_and_balance():
+    from advanced_scrapper_amd import dist
+    rng = np.random.default_rng(5)
+    for world in (1, 2, 4, 8):
+        n = 1000
+        lens = rng.lognormal(7.6, 0.6, size=2 * n).astype(np.int64)
+        off = np.zeros(2 * n + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        rr = dist.byte_balanced_ranges(off, world)
+        assert rr[0][0] == 0 and rr[-1][1] == n
+        assert all(rr[i][1] == rr[i + 1][0] for i in range(world - 1))
+        sizes = [off[2 * hi] - off[2 * lo] for lo, hi in rr]
+        assert max(sizes) - min(sizes) <= 2 * lens.reshape(-1, 2).sum(1).max()
+
+
+def test_shard_range_partitions():
+    from advanced_scrapper_amd import dist
+    for n in (0, 1, 7, 1000):
+        for world in (1, 2, 3, 8):
+            rr = [dist.shard_range(n, r, world) for r in range(world)]
+            assert rr[0][0] == 0 and rr[-1][1] == n
+            assert all(rr[i][1] == rr[i + 1][0] for i in range(world - 1))
+            assert max(h - l for l, h in rr) - min(h - l for l, h in rr) <= 1
