@@ -28,7 +28,7 @@ HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('fiel
 # every symbol include/kwmatch.h declares
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
            'kw_last_kernel_times', 'kw_last_error', 'kw_destroy')
-KW_N_STATS = 10
+KW_N_STATS = 13
 
 
 class KwError(RuntimeError):

@@ -55,7 +55,7 @@ struct kw_handle {
     FastTables FT{};
     FastScratch FS{};
     int nk = 0, nr = 0, ng = 0;
-    uint32_t defer_cap = 0, item_cap = 0;
+    uint32_t defer_cap = 0, item_cap = 0, rx_cap = 0;
     int64_t hdr_cap = 0;
     int items_blocks_per_cu = 1, resolve_blocks_per_cu = 1;
     int n_anchor_fast = 0;
@@ -156,6 +156,9 @@ struct FastBuild {
     std::vector<uint64_t> edge_key;
     std::vector<uint32_t> edge_begin, edge_cnt, edge_ent;
     uint32_t edge_mask = 0;
+    std::vector<int32_t> rxf_idx;
+    std::vector<uint64_t> rxf_pm, rxf_any, rxf_ext_mask;
+    std::vector<uint32_t> rxf_len, rxf_ext_off, rxf_ext_cp;
 };
 
 // rarest 4-byte window inside bytes [lo, hi) (hi - lo >= 4); returns its start
@@ -186,6 +189,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         auses[id].push_back(u);
     };
     B.rxk.assign(std::max(n_pat, 1), RXK_LITERAL);
+    B.rxf_idx.assign(std::max(n_pat, 1), -1);
     B.edge_pre.assign(FK_EDGE_WORDS, 0);
     B.edge_suf.assign(FK_EDGE_WORDS, 0);
     B.boff.assign(std::max(n_pat, 1), 0);
@@ -215,7 +219,35 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         if (m == 0) continue;
         span_use(FU_FULL, 0, bl, 0, 0);
         // positions: literal search, or the regex engine after the decision
-        if (rxo[i + 1] > rxo[i]) B.rxk[i] = RXK_REGEX;
+        if (rxo[i + 1] > rxo[i]) {
+            B.rxk[i] = RXK_REGEX;
+            // quantifier-free programs of <= 64 atoms take the shift-and search
+            bool fixed = rxo[i + 1] - rxo[i] <= 64;
+            for (uint32_t a = rxo[i]; a < rxo[i + 1] && fixed; ++a) fixed = atoms[a].z == 1 && atoms[a].w == 1;
+            if (fixed) {
+                const uint32_t r = (uint32_t)B.rxf_len.size();
+                B.rxf_idx[i] = (int32_t)r;
+                B.rxf_len.push_back(rxo[i + 1] - rxo[i]);
+                uint64_t any = 0;
+                std::vector<std::pair<uint32_t, uint64_t>> ext;
+                B.rxf_pm.resize((size_t)(r + 1) * 128, 0);
+                for (uint32_t a = rxo[i]; a < rxo[i + 1]; ++a) {
+                    const uint64_t bit = 1ull << (a - rxo[i]);
+                    if (atoms[a].x == KW_RX_ANY) { any |= bit; continue; }
+                    const uint32_t c = (uint32_t)atoms[a].y;
+                    if (c < 128) { B.rxf_pm[(size_t)r * 128 + c] |= bit; continue; }
+                    size_t k = 0;
+                    while (k < ext.size() && ext[k].first != c) ++k;
+                    if (k == ext.size()) ext.emplace_back(c, 0);
+                    ext[k].second |= bit;
+                }
+                for (uint32_t c = 0; c < 128; ++c)
+                    if (c != '\n') B.rxf_pm[(size_t)r * 128 + c] |= any;   // '.' matches anything but '\n'
+                B.rxf_any.push_back(any);
+                B.rxf_ext_off.push_back((uint32_t)B.rxf_ext_cp.size());
+                for (auto &e : ext) { B.rxf_ext_cp.push_back(e.first); B.rxf_ext_mask.push_back(e.second); }
+            }
+        }
         // m <= 20: interior windows must be exact (FULL); the one-deletion edge
         // windows (11 <= m <= 20) go to the edge table instead of pieces
         if (kfull_h(m) == 0) {
@@ -385,6 +417,9 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         }
         if (B.edge_ent.empty()) B.edge_ent.push_back(0);
     }
+    B.rxf_ext_off.push_back((uint32_t)B.rxf_ext_cp.size());
+    if (B.rxf_len.empty()) { B.rxf_len.push_back(1); B.rxf_any.push_back(0); B.rxf_pm.resize(128, 0); }
+    if (B.rxf_ext_cp.empty()) { B.rxf_ext_cp.push_back(0); B.rxf_ext_mask.push_back(0); }
     if (B.as_head.empty()) { B.as_head.push_back(0); B.as_len.push_back(0); B.as_use_begin.push_back(0); B.as_use_cnt.push_back(0); }
     if (B.use_pat.empty()) { B.use_pat.push_back(0); B.use_info0.push_back(0); B.use_info1.push_back(0); }
     return KW_OK;
@@ -689,7 +724,10 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_ui1 = push_array(blob, FB.use_info1), f_rxk = push_array(blob, FB.rxk), f_boff = push_array(blob, FB.boff),
            f_pb = push_array(blob, all_bytes), f_sig = push_array(blob, FB.sig),
            f_ek = push_array(blob, FB.edge_key), f_eb = push_array(blob, FB.edge_begin),
-           f_ec = push_array(blob, FB.edge_cnt), f_ee = push_array(blob, FB.edge_ent);
+           f_ec = push_array(blob, FB.edge_cnt), f_ee = push_array(blob, FB.edge_ent),
+           f_rxi = push_array(blob, FB.rxf_idx), f_rxp = push_array(blob, FB.rxf_pm), f_rxa = push_array(blob, FB.rxf_any),
+           f_rxl = push_array(blob, FB.rxf_len), f_rxeo = push_array(blob, FB.rxf_ext_off),
+           f_rxec = push_array(blob, FB.rxf_ext_cp), f_rxem = push_array(blob, FB.rxf_ext_mask);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -773,6 +811,13 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.edge_ent = (const uint32_t *)(B + f_ee);
     F.edge_mask = FB.edge_mask;
     F.word_bits = T.word_bits;
+    F.rxf_idx = (const int32_t *)(B + f_rxi);
+    F.rxf_pm = (const uint64_t *)(B + f_rxp);
+    F.rxf_any = (const uint64_t *)(B + f_rxa);
+    F.rxf_len = (const uint32_t *)(B + f_rxl);
+    F.rxf_ext_off = (const uint32_t *)(B + f_rxeo);
+    F.rxf_ext_cp = (const uint32_t *)(B + f_rxec);
+    F.rxf_ext_mask = (const uint64_t *)(B + f_rxem);
     F.f_first = f_first;
     F.empty_pat = empty_pat;
     h->n_anchor_fast = (int)FB.as_len.size();
@@ -801,11 +846,12 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
 // (re)allocate scratch for nk scan waves (item_cap items each), nr resolve waves, ng generic
 // waves (out_cap records per resolve/generic wave), n_docs headers and a defer list of dcap docs
 static int ensure_scratch(kw_handle *h, int nk, int nr, int ng, uint32_t item_cap, uint32_t out_cap, int64_t n_docs,
-                          uint32_t dcap)
+                          uint32_t dcap, uint32_t rx_cap)
 {
     if (h->d_scratch && nk <= h->nk && nr <= h->nr && ng <= h->ng && item_cap <= h->item_cap &&
-        out_cap <= h->out_cap && n_docs <= h->hdr_cap && dcap <= h->defer_cap)
+        out_cap <= h->out_cap && n_docs <= h->hdr_cap && dcap <= h->defer_cap && rx_cap <= h->rx_cap)
         return KW_OK;
+    rx_cap = std::max(rx_cap, h->rx_cap);
     nk = std::max(nk, h->nk);
     nr = std::max(nr, h->nr);
     ng = std::max(ng, h->ng);
@@ -824,7 +870,7 @@ static int ensure_scratch(kw_handle *h, int nk, int nr, int ng, uint32_t item_ca
     const int nw = nr + ng;   // result regions: resolve [0, nr), generic [nr, nr + ng)
     size_t total = (size_t)ng * (per_items + per_cps + per_blk) + (size_t)nr * (per_fcps + per_blk) +
                    (size_t)nw * per_out + (size_t)nk * item_cap * 8 + (size_t)n_docs * 8 + (size_t)dcap * 4 +
-                   16 * 256;
+                   (size_t)nr * rx_cap * 16 + 16 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
     uint8_t *p = (uint8_t *)h->d_scratch;
     auto carve = [&](size_t bytes) { uint8_t *r = p; p += (bytes + 255) & ~(size_t)255; return r; };
@@ -837,6 +883,9 @@ static int ensure_scratch(kw_handle *h, int nk, int nr, int ng, uint32_t item_ca
     h->FS.items = (uint64_t *)carve((size_t)nk * item_cap * 8);
     h->FS.hdr = (uint2 *)carve((size_t)n_docs * 8);
     h->FS.defer_list = (uint32_t *)carve((size_t)dcap * 4);
+    h->FS.rx_tasks = (uint4 *)carve((size_t)nr * rx_cap * 16);
+    h->FS.rx_cap = rx_cap;
+    h->rx_cap = rx_cap;
     size_t small = 1024 + (size_t)nw * 4 + 256 + (size_t)(nw + 1) * 8 + 256;
     HIPCHK(h, hipMalloc(&h->d_small, small));
     uint8_t *q = (uint8_t *)h->d_small;
@@ -883,8 +932,9 @@ static int launch_scan(kw_handle *h)
     const uint32_t want_items = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_k * 40), (int64_t)1 << 24);
     const int64_t docs_per_r = (n_docs + nr - 1) / nr;
     const uint32_t want_out = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_r * 48), (int64_t)1 << 26);
+    const uint32_t want_rx = (uint32_t)std::min<int64_t>(docs_per_r * 2 + 64, (int64_t)1 << 20);
     int rc = ensure_scratch(h, nk, nr, ng, std::max(want_items, h->item_cap), std::max(want_out, h->out_cap),
-                            std::max<int64_t>(n_docs, 1), (uint32_t)std::max<int64_t>(n_docs, 1));
+                            std::max<int64_t>(n_docs, 1), (uint32_t)std::max<int64_t>(n_docs, 1), want_rx);
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
     // every region's count (regions of waves this launch does not start stay empty)
@@ -955,13 +1005,15 @@ static int finish(kw_handle *h)
             h->err = buf;
             return KW_EOVERFLOW;
         }
-        if (status[0] & ST_OUT_OVERFLOW) {
-            // grow the per-wave result regions to the largest count seen and rescan
+        if (status[0] & (ST_OUT_OVERFLOW | ST_RX_OVERFLOW)) {
+            // grow the per-wave result regions to the largest count seen (and the regex queues) and rescan
             std::vector<uint32_t> cnt(h->launched_waves);
             HIPCHK(h, hipMemcpy(cnt.data(), h->FS.out_cnt, cnt.size() * 4, hipMemcpyDeviceToHost));
             uint32_t mx = 0;
             for (uint32_t c : cnt) mx = std::max(mx, c);
-            int rc = ensure_scratch(h, h->nk, h->nr, h->ng, h->item_cap, mx + 1024, h->hdr_cap, h->defer_cap);
+            const uint32_t out_cap = (status[0] & ST_OUT_OVERFLOW) ? mx + 1024 : h->out_cap;
+            const uint32_t rx_cap = (status[0] & ST_RX_OVERFLOW) ? h->rx_cap * 4 : h->rx_cap;
+            int rc = ensure_scratch(h, h->nk, h->nr, h->ng, h->item_cap, out_cap, h->hdr_cap, h->defer_cap, rx_cap);
             if (rc) return rc;
             rc = launch_scan(h);
             if (rc) return rc;

@@ -100,5 +100,6 @@ constexpr uint32_t ST_ITEM_OVERFLOW = 1u;
 constexpr uint32_t ST_OUT_OVERFLOW = 2u;
 constexpr uint32_t ST_CP_OVERFLOW = 4u;
 constexpr uint32_t ST_FIELD_TOO_LONG = 8u;
+constexpr uint32_t ST_RX_OVERFLOW = 16u;     // a resolve wave queued more regex searches than rx_cap
 
 }  // namespace kw

@@ -112,6 +112,14 @@ struct FastTables {
     const uint32_t *word_bits;
     int f_first;
     int empty_pat;
+    // quantifier-free regex names (literals and '.', <= 64 atoms): shift-and tables
+    const int32_t *rxf_idx;     // per pattern: row r, or -1 (quantified: the backtracking engine)
+    const uint64_t *rxf_pm;     // [r][128] ASCII masks ('.' bits except for '\n')
+    const uint64_t *rxf_any;    // [r] '.' bits (masks of non-ASCII code points)
+    const uint32_t *rxf_len;    // [r] atoms = match length in code points
+    const uint32_t *rxf_ext_off;   // [r + 1] non-ASCII literal atoms
+    const uint32_t *rxf_ext_cp;
+    const uint64_t *rxf_ext_mask;
 };
 
 struct FastScratch {
@@ -128,6 +136,8 @@ struct FastScratch {
     uint32_t defer_cap;
     uint32_t *status;
     unsigned long long *stats;  // see kw_stats
+    uint4 *rx_tasks;            // per resolve wave: rx_cap regex-position tasks (doc, field|ascii, pattern, n)
+    uint32_t rx_cap;
 };
 
 // host + device hashes of the LDS tables

@@ -17,6 +17,15 @@
 #ifndef FK_STAGE
 #define FK_STAGE 3
 #endif
+// waves per SIMD the resolve kernel is compiled for (register budget)
+#ifndef RK_OCC
+#define RK_OCC 4
+#endif
+// profiling builds: bit 0 skips the short-field path, bit 1 the edge windows, bit 2 the items,
+// bit 3 the regex positions
+#ifndef RK_SKIP
+#define RK_SKIP 0
+#endif
 
 namespace kw {
 
@@ -176,8 +185,32 @@ __device__ __forceinline__ uint64_t lcs_ballot_step(uint64_t V, uint32_t lanecha
     return (V + U) | (V - U);
 }
 
+// Text code points [lo, lo + 128) of a field staged one per lane in two
+// registers (out-of-range positions read as 0xFFFFFFFF, which no name holds).
+__device__ __forceinline__ void fk_stage_text(const FieldCtx &F, int64_t lo, uint32_t &ta, uint32_t &tb)
+{
+    const int lane = lane_id();
+    ta = fk_cp(F, lo + lane);
+    tb = fk_cp(F, lo + 64 + lane);
+}
+
+// staged code point at a wave-uniform index (0..127)
+__device__ __forceinline__ uint32_t fk_staged_u(uint32_t ta, uint32_t tb, int idx)
+{
+    return idx < 64 ? __builtin_amdgcn_readlane(ta, idx) : __builtin_amdgcn_readlane(tb, idx - 64);
+}
+
+// staged code point at a per-lane index (0..127); every lane must execute it
+__device__ __forceinline__ uint32_t fk_staged_v(uint32_t ta, uint32_t tb, int idx)
+{
+    const uint32_t a = (uint32_t)__shfl((int)ta, idx & 63, WAVE);
+    const uint32_t b = (uint32_t)__shfl((int)tb, idx & 63, WAVE);
+    return idx < 64 ? a : b;
+}
+
 // Verify one PIECE item of pattern P (needle = name, m < n).  All lanes call.
-// nm: lane i holds name[i] (i < m).  Returns true if some window of the
+// nm: lane i holds name[i] (i < m).  base = q - o is the text code point the
+// name's first code point aligns with.  Returns true if some window of the
 // partial_ratio family containing the piece passes.
 __device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint32_t q, uint32_t o, uint32_t pl,
                                 unsigned long long &nwin)
@@ -188,11 +221,16 @@ __device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint
     const uint64_t needle = low_mask(m);
     const uint32_t k = kfull(m);
     if (k > 0) {
-        // band test: every name char matched by a passing full window lies within +-2k of base+i
+        // band test: every name char matched by a passing full window lies within +-2k of base+i.
+        // The text [base-2k, base+m+2k) (<= 76 code points) is staged in registers.
         const int64_t base = (int64_t)q - (int64_t)o;
+        const int64_t lo = base - 2 * (int64_t)k;
+        uint32_t ta, tb;
+        fk_stage_text(F, lo, ta, tb);
         bool hit = false;
-        if (lane < (int)m) {
-            for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) hit |= (fk_cp(F, base + lane + t) == nm);
+        for (int t = 0; t <= 4 * (int)k; ++t) {
+            const uint32_t c = fk_staged_v(ta, tb, lane + t);
+            hit |= (lane < (int)m) && c == nm;
         }
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hit));
         if (cnt + k >= m) {
@@ -200,13 +238,9 @@ __device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint
             if (pmin < 0) pmin = 0;
             if (pmax > (int64_t)(n - m)) pmax = (int64_t)(n - m);
             for (int64_t p = pmin; p <= pmax; ++p) {
-                // text chars of the window, one per lane (lane j < m)
-                const uint32_t tc = (lane < (int)m) ? fk_cp(F, p + lane) : 0xFFFFFFFEu;
+                const int i0 = (int)(p - lo);
                 uint64_t V = ~0ull;
-                for (uint32_t j = 0; j < m; ++j) {
-                    const uint32_t c = __builtin_amdgcn_readlane(tc, j);
-                    V = lcs_ballot_step(V, nm, c, needle);
-                }
+                for (uint32_t j = 0; j < m; ++j) V = lcs_ballot_step(V, nm, fk_staged_u(ta, tb, i0 + (int)j), needle);
                 ++nwin;
                 const uint32_t L = (uint32_t)__popcll(~V & needle);
                 if (20u * (m - L) < m) return true;
@@ -236,8 +270,8 @@ __device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint
 }
 
 // Short field (n <= 64 code points) vs a longer-or-equal name: needle = field.
-// fc: lane i holds field[i] (i < n).  nm_ptr: the name's code points (m >= n).
-__device__ bool fk_short_decide(uint32_t fc, uint32_t n, const uint32_t *__restrict__ nm_ptr, uint32_t m, bool *exact,
+// fc: lane i holds field[i] (i < n); nmr: lane i holds name[i] (i < m, m >= n).
+__device__ bool fk_short_decide(uint32_t fc, uint32_t n, uint32_t nmr, uint32_t m, bool *exact,
                                 unsigned long long &nwin)
 {
     *exact = false;
@@ -247,7 +281,7 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, const uint32_t *__restr
     uint64_t Vf = ~0ull;
     for (uint32_t p = 0; p + n <= m; ++p) {        // full windows of the name
         uint64_t V = ~0ull;
-        for (uint32_t j = 0; j < n; ++j) V = lcs_ballot_step(V, fc, nm_ptr[p + j], needle);
+        for (uint32_t j = 0; j < n; ++j) V = lcs_ballot_step(V, fc, __builtin_amdgcn_readlane(nmr, p + j), needle);
         ++nwin;
         if (p == 0) Vf = V;
         const uint32_t L = (uint32_t)__popcll(~V & needle);
@@ -257,7 +291,7 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, const uint32_t *__restr
     {   // prefixes of the name
         uint64_t V = ~0ull;
         for (uint32_t i = 1; i < n; ++i) {
-            V = lcs_ballot_step(V, fc, nm_ptr[i - 1], needle);
+            V = lcs_ballot_step(V, fc, __builtin_amdgcn_readlane(nmr, i - 1), needle);
             if (passes((uint32_t)__popcll(~V & needle), n, i)) return true;
         }
     }
@@ -266,12 +300,12 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, const uint32_t *__restr
     {   // suffixes of the name (reversed needle)
         uint64_t V = ~0ull;
         for (uint32_t kk = 1; kk < n; ++kk) {
-            V = lcs_ballot_step(V, fr, nm_ptr[m - kk], needle);
+            V = lcs_ballot_step(V, fr, __builtin_amdgcn_readlane(nmr, m - kk), needle);
             if (passes((uint32_t)__popcll(~V & needle), n, kk)) return true;
         }
     }
     if (m == n) {   // swapped run: needle = name, windows = prefixes / suffixes of the field
-        for (uint32_t j = 0; j < m; ++j) Vr = lcs_ballot_step(Vr, fr, nm_ptr[m - 1 - j], needle);
+        for (uint32_t j = 0; j < m; ++j) Vr = lcs_ballot_step(Vr, fr, __builtin_amdgcn_readlane(nmr, m - 1 - j), needle);
         for (uint32_t i = 1; i < n; ++i) {
             if (passes((uint32_t)__popcll(~Vf & low_mask(i)), m, i)) return true;
             if (passes((uint32_t)__popcll(~Vr & low_mask(n - i)), m, n - i)) return true;
@@ -363,12 +397,117 @@ __device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint6
     return added;
 }
 
-// every match position of a decided regex-class name (re.finditer, :177-180),
-// or `name: []` when there is none
-__device__ __noinline__ void fk_regex_positions(const DevTables &T, const DevScratch &GS, const FieldCtx &F, OutCtx &O, uint32_t P)
+// re.finditer positions of a quantifier-free regex name (literals and '.'):
+// shift-and over the field, lane l owning the 32 start positions
+// [r0 + 32 l, r0 + 32 l + 32) of each 2048-position round.  tab = this wave's
+// LDS copy of the row's 128 ASCII masks; txt = this wave's LDS staging buffer
+// (RX_TXT bytes) for the round's text of an ASCII field.  Leftmost
+// non-overlapping selection (every match is L code points long).  Returns the
+// number of positions emitted.
+constexpr int RX_TXT = 2048 + 64 + 16 + 16;   // 2048 starts + L - 1 <= 63 tail bytes + alignment slack
+
+__device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O,
+                                          uint32_t P, uint32_t r, uint64_t *tab, uint8_t *txt)
 {
-    const uint32_t cnt = rx_positions(T, GS, F, O, P);
-    if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
+    const int lane = lane_id();
+    const uint32_t L = FT.rxf_len[r];
+    const uint64_t anym = FT.rxf_any[r];
+    wave_sync();
+    tab[lane] = FT.rxf_pm[(size_t)r * 128 + lane];
+    tab[lane + 64] = FT.rxf_pm[(size_t)r * 128 + 64 + lane];
+    const int64_t n = F.n;
+    if (n < (int64_t)L) return 0;
+    const int64_t nstarts = n - L + 1;
+    const uint64_t fin = 1ull << (L - 1);
+    const uint32_t eb = FT.rxf_ext_off[r], ee = FT.rxf_ext_off[r + 1];
+    uint32_t last_end = 0, emitted = 0;
+    for (int64_t r0 = 0; r0 < nstarts; r0 += 64 * 32) {
+        int64_t tb = 0;   // txt[k] = field byte tb + k
+        if (F.ascii) {
+            // stage field bytes [r0, r0 + 2048 + L - 1) with coalesced 16-byte loads (the arena is padded)
+            const int64_t a0 = (F.fb + r0) & ~(int64_t)15;
+            const int64_t a1 = F.fb + r0 + 2048 + L - 1 < F.fe ? F.fb + r0 + 2048 + L - 1 : F.fe;
+            tb = a0 - F.fb;
+            wave_sync();
+            for (int c = lane; c < RX_TXT / 16; c += WAVE) {
+                const int64_t a = a0 + 16 * (int64_t)c;
+                if (a < a1) ((uint4 *)txt)[c] = *(const uint4 *)(F.arena + a);
+            }
+            wave_sync();
+        } else {
+            wave_sync();
+        }
+        const int64_t s_lo = r0 + (int64_t)lane * 32;
+        uint32_t mask = 0;
+        if (s_lo < nstarts) {
+            const int64_t s_hi = s_lo + 32 < nstarts ? s_lo + 32 : nstarts;
+            const int c_cnt = (int)(s_hi + L - 1 - s_lo);
+            uint64_t D = 0;
+            if (F.ascii) {
+                const uint8_t *t = txt + (s_lo - tb);
+#pragma unroll 8
+                for (int k = 0; k < c_cnt; ++k) {
+                    D = ((D << 1) | 1ull) & tab[t[k] & 0x7Fu];
+                    if (D & fin) mask |= 1u << (uint32_t)(k - (int)(L - 1));
+                }
+            } else {
+                for (int k = 0; k < c_cnt; ++k) {
+                    const uint32_t c = F.cps[s_lo + k];
+                    uint64_t B;
+                    if (c < 128) {
+                        B = tab[c];
+                    } else {
+                        B = anym;
+                        for (uint32_t e = eb; e < ee; ++e)
+                            if (FT.rxf_ext_cp[e] == c) B |= FT.rxf_ext_mask[e];
+                    }
+                    D = ((D << 1) | 1ull) & B;
+                    if (D & fin) mask |= 1u << (uint32_t)(k - (int)(L - 1));
+                }
+            }
+        }
+        // greedy selection in position order (lanes in order, bits in order)
+        uint64_t lanes = __ballot(mask != 0);
+        uint32_t keep = 0;
+        while (lanes) {
+            const int l = __builtin_ctzll(lanes);
+            lanes &= lanes - 1;
+            uint32_t mk = (uint32_t)__builtin_amdgcn_readlane((int)mask, l), kp = 0;
+            while (mk) {
+                const int b = __builtin_ctz(mk);
+                mk &= mk - 1;
+                const uint32_t st = (uint32_t)(r0 + (int64_t)l * 32 + b);
+                if (st >= last_end) { kp |= 1u << b; last_end = st + L; }
+            }
+            if (lane == l) keep = kp;
+        }
+        while (__ballot(keep != 0)) {
+            const int b = keep ? __builtin_ctz(keep) : 0;
+            emit_hits(O, GS, keep != 0, F.doc, P, (uint32_t)(s_lo + b), F.field);
+            emitted += (uint32_t)__popcll(__ballot(keep != 0));
+            keep &= keep - 1;
+        }
+    }
+    return emitted;
+}
+
+// Regex-position tasks are queued per wave and run after the wave's last
+// document, where few registers are live (a call from inside the resolve
+// would spill the caller's state on every decided regex name).
+struct RxQueue {
+    uint4 *q;
+    uint32_t n, cap;
+    uint8_t *txt;   // the wave's LDS text staging buffer (RX_TXT bytes)
+};
+
+__device__ __forceinline__ void fk_regex_enqueue(const DevScratch &GS, const FieldCtx &F, uint32_t P, RxQueue &Q)
+{
+    if (Q.n < Q.cap) {
+        if (lane_id() == 0) Q.q[Q.n] = make_uint4(F.doc, F.field | (F.ascii ? 2u : 0u), P, F.n);
+    } else if (lane_id() == 0) {
+        atomicOr(&GS.status[0], ST_RX_OVERFLOW);   // the host grows the queues and scans again
+    }
+    ++Q.n;
 }
 
 // ---------------------------------------------------------------- fast resolve of one field
@@ -376,7 +515,8 @@ __device__ __noinline__ void fk_regex_positions(const DevTables &T, const DevScr
 // items overflowed: the document then goes to the generic kernel.
 __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const DevScratch &GS, FieldCtx &F, OutCtx &O,
                                  uint64_t *items_lds, uint32_t *icnt_f, uint32_t *dflag, uint32_t *cps,
-                                 uint32_t *blkcnt, bool maybe_nonascii, bool edge, unsigned long long &nver,
+                                 uint32_t *blkcnt, uint64_t *rxtab, RxQueue &RQ, bool maybe_nonascii, bool edge,
+                                 unsigned long long &nver,
                                  unsigned long long &nwin, unsigned long long &nedge)
 {
     const int lane = lane_id();
@@ -384,9 +524,9 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     const int64_t flen = F.fe - F.fb;
     F.ascii = maybe_nonascii ? field_is_ascii(F.arena, F.fb, F.fe) : true;
     F.n = F.ascii ? (uint32_t)flen : field_cp_count(F.arena, F.fb, F.fe, false);
-    const bool is_short = F.n <= (uint32_t)MAXM;
+    const bool is_short = !(RK_SKIP & 1) && F.n <= (uint32_t)MAXM;
     // ---- one-deletion edge windows of the 11..20-code-point names (prefiltered by the scan)
-    if (edge && F.n >= EDGE_MIN_M + 1) {
+    if (!(RK_SKIP & 2) && edge && F.n >= EDGE_MIN_M + 1) {
         uint32_t added = fk_edge_items(FT, F, items_lds, icnt_f, dflag);
         added = (uint32_t)wave_sum((int)added);
         if (added) {
@@ -404,7 +544,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         F.cps = cps;
         F.blkcnt = blkcnt;
     }
-    if (N > 0) {
+    if (!(RK_SKIP & 4) && N > 0) {
         uint64_t it = (lane < (int)N) ? items_lds[lane] : ~0ull;
         it = wave_sort_reg(it);
         const bool valid = lane < (int)N;
@@ -431,20 +571,28 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         // ---- verification of pieces of undecided fuzzy names (wave-serial over such items)
         uint64_t vneed = __ballot(live && fuzzy && !decided_full && kind == FU_PIECE);
         uint64_t decided_v = 0;   // bit per lane: its group got decided by a window
+        uint32_t last_P = 0xFFFFFFFFu, nm = 0xFFFFFFFDu;
+        int64_t last_base = -1;
         while (vneed) {
             const int l = __builtin_ctzll(vneed);
             vneed &= vneed - 1;
             const uint64_t lg = __shfl(gmask, l, WAVE);
             if (decided_v & lg) continue;                       // group already decided
-            const uint32_t P = (uint32_t)__shfl((int)pat, l, WAVE);
-            const uint32_t mm = (uint32_t)__shfl((int)m, l, WAVE);
-            const uint32_t uu = (uint32_t)__shfl((int)use, l, WAVE);
-            const uint32_t bp = (uint32_t)__shfl((int)bpos, l, WAVE);
+            const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pat, l);
+            const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
+            const uint32_t uu = (uint32_t)__builtin_amdgcn_readlane((int)use, l);
+            const uint32_t bp = (uint32_t)__builtin_amdgcn_readlane((int)bpos, l);
             const uint32_t info1 = FT.use_info1[uu];
             const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
-            const uint32_t nm = (lane < (int)mm) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+            const uint32_t q = to_cp(F, bp);
+            // pieces of one occurrence share the alignment base = q - o: verify it once
+            const int64_t base = (int64_t)q - (int64_t)o;
+            if (P == last_P && base == last_base) continue;
+            if (P != last_P) nm = (lane < (int)mm) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+            last_P = P;
+            last_base = base;
             ++nver;
-            if (fk_verify_piece(F, nm, mm, to_cp(F, bp), o, pl, nwin)) decided_v |= lg;
+            if (fk_verify_piece(F, nm, mm, q, o, pl, nwin)) decided_v |= lg;
         }
         const bool decided = decided_full || ((decided_v >> lane) & 1ull);
         // ---- positions: U names and literal fuzzy names report their exact occurrences
@@ -485,7 +633,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         while (rxm) {
             const int l = __builtin_ctzll(rxm);
             rxm &= rxm - 1;
-            fk_regex_positions(T, GS, F, O, (uint32_t)__shfl((int)pat, l, WAVE));
+            fk_regex_enqueue(GS, F, (uint32_t)__shfl((int)pat, l, WAVE), RQ);
         }
     }
     // ---- short field: the field is the needle, the longer names are the haystacks
@@ -538,7 +686,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                 while (rxm) {
                     const int l = __builtin_ctzll(rxm);
                     rxm &= rxm - 1;
-                    fk_regex_positions(T, GS, F, O, (uint32_t)__shfl((int)P, l, WAVE));
+                    fk_regex_enqueue(GS, F, (uint32_t)__shfl((int)P, l, WAVE), RQ);
                 }
             }
             return 0;
@@ -567,8 +715,9 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                 const uint32_t m = pi_m(FT.pat_info[P]);
                 bool exact = false;
                 ++nver;
-                if (!fk_short_decide(fc, n, FT.pat_cps + FT.pat_cp_off[P], m, &exact, nwin)) continue;
-                if (FT.pat_rxk[P] == RXK_REGEX) fk_regex_positions(T, GS, F, O, P);
+                const uint32_t nmr = (lane < (int)m) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+                if (!fk_short_decide(fc, n, nmr, m, &exact, nwin)) continue;
+                if (FT.pat_rxk[P] == RXK_REGEX) fk_regex_enqueue(GS, F, P, RQ);
                 else emit_hits(O, GS, lane == 0, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
             }
         }
@@ -789,18 +938,21 @@ constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS 
                              (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_CAND * 8 + 4 * 4);
 
 // ---------------------------------------------------------------- kernel 2: resolve
-__global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, DevTables T,
+__global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables FT, DevTables T,
                                                               const uint8_t *__restrict__ arena,
                                                               const int64_t *__restrict__ off, int64_t n_docs,
                                                               FastScratch S, DevScratch GS)
 {
     __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
+    __shared__ uint64_t rxtab_all[RK_WAVES * 128];
+    __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
     __shared__ uint32_t cnt_all[RK_WAVES * 4];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t wave = (int64_t)blockIdx.x * RK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * RK_WAVES;
     uint64_t *items = items_all + wib * FK_ITEMS;
+    uint64_t *rxtab = rxtab_all + wib * 128;
     uint32_t *icnt = cnt_all + wib * 4;
     uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
     uint32_t *blkcnt = S.cpbase + (size_t)wave * (CP_CAP / 16 + 2);
@@ -808,7 +960,13 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, Dev
     O.out = S.out + (size_t)wave * S.out_cap;
     O.cap = S.out_cap;
     O.n = 0;
+    RxQueue RQ;
+    RQ.q = S.rx_tasks + (size_t)wave * S.rx_cap;
+    RQ.cap = S.rx_cap;
+    RQ.n = 0;
+    RQ.txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
     unsigned long long nver = 0, nwin = 0, nedge = 0, ndefer = 0, ndef_cp = 0, ndef_items = 0, nres = 0;
+    unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
 
     for (int64_t c0 = wave * WAVE; c0 < n_docs; c0 += n_waves * WAVE) {
         const int64_t dl = c0 + lane;
@@ -823,7 +981,7 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, Dev
             const uint32_t hy = (uint32_t)__shfl((int)hl.y, l, WAVE);
             const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
             const uint32_t nf[2] = {hy & 127u, (hy >> 7) & 127u};
-            const uint32_t out_mark = O.n;
+            const uint32_t out_mark = O.n, rq_mark = RQ.n;
             bool defer = false;
             ++nres;
             for (int f = 0; f < 2 && !defer; ++f) {
@@ -845,7 +1003,7 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, Dev
                 const bool na = (hy & (f ? DH_NA1 : DH_NA0)) != 0;
                 const bool edge = (hy & (f ? DH_EDGE1 : DH_EDGE0)) != 0;
                 const int rs = FK_STAGE < 2 ? 0 : fk_resolve_field(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps,
-                                                                   blkcnt, na, edge, nver, nwin, nedge);
+                                                                   blkcnt, rxtab, RQ, na, edge, nver, nwin, nedge);
                 if (rs) {
                     defer = true;
                     if (rs == 1) ++ndef_cp;
@@ -855,6 +1013,7 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, Dev
             }
             if (defer) {
                 O.n = out_mark;   // drop this doc's partial records; the generic kernel redoes it
+                RQ.n = rq_mark;
                 ++ndefer;
                 if (lane == 0) {
                     const uint32_t i = atomicAdd(S.defer_cnt, 1u);
@@ -863,6 +1022,33 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, Dev
                 }
             }
         }
+    }
+    // the queued regex-position tasks of this wave's documents
+    wave_sync_global();
+    const uint32_t n_rx = RQ.n < RQ.cap ? RQ.n : RQ.cap;
+    for (uint32_t t = 0; t < n_rx; ++t) {
+        const uint4 tk = RQ.q[t];
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x);
+        const uint32_t fy = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.z);
+        FieldCtx F;
+        F.arena = arena;
+        F.field = fy & 1u;
+        F.fb = off[2 * (int64_t)d + F.field];
+        F.fe = off[2 * (int64_t)d + F.field + 1];
+        F.ascii = (fy & 2u) != 0;
+        F.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.w);
+        F.cps = cps;
+        F.blkcnt = blkcnt;
+        F.doc = d;
+        if (!F.ascii) decode_field(GS, arena, F.fb, F.fe, cps, blkcnt);
+        const int32_t r = FT.rxf_idx[P];
+        ++nrx;
+        nrx_bt += r < 0;
+        nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
+        const uint32_t cnt = (RK_SKIP & 8) ? 1u : (r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, RQ.txt)
+                                                         : ((RK_SKIP & 16) ? 1u : rx_positions(T, GS, F, O, P)));
+        if (cnt == 0) emit_hits(O, GS, lane == 0, d, P, KW_NOPOS, F.field);
     }
     if (lane == 0) S.out_cnt[wave] = O.n;
     unsigned long long v = nver, w = nwin;
@@ -879,6 +1065,9 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_resolve_kernel(FastTables FT, Dev
         atomicAdd(&S.stats[6], ndef_cp);
         atomicAdd(&S.stats[7], nedge);
         atomicAdd(&S.stats[9], nres);
+        atomicAdd(&S.stats[10], nrx);
+        atomicAdd(&S.stats[11], nrx_bt);
+        atomicAdd(&S.stats[12], nrx_rounds);
     }
 }
 

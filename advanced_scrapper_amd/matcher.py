@@ -143,7 +143,8 @@ class GpuMatcher:
         return host.view(np.uint32).reshape(-1, 4).copy().view(_native.HIT_DTYPE).reshape(-1)
 
     STAT_KEYS = ('candidates', 'anchor_hits', 'lcs_windows', 'verifications', 'deferred_docs', 'deferred_items',
-                 'deferred_long_nonascii', 'edge_items', 'candidates_stage2', 'resolved_docs')
+                 'deferred_long_nonascii', 'edge_items', 'candidates_stage2', 'resolved_docs', 'regex_searches',
+                 'regex_backtracking', 'regex_rounds')
 
     def stats(self) -> Dict[str, int]:
         v = np.zeros(_native.KW_N_STATS, dtype=np.int64)

@@ -109,8 +109,11 @@ int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void
  * documents handed to the generic kernel, of which [5] had more anchor items
  * than the fast path holds and [6] had a long non-ASCII field, [7] one-deletion
  * edge windows found (fuzzy names of 11..20 code points), [8] candidates that
- * passed the stage-2 filter, [9] documents the resolve kernel worked on. */
-#define KW_N_STATS 10
+ * passed the stage-2 filter, [9] documents the resolve kernel worked on,
+ * [10] regex-position searches of decided regex-class names, of which [11]
+ * ran the backtracking engine (quantified atoms), [12] 2048-position rounds of
+ * the shift-and search. */
+#define KW_N_STATS 13
 int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
 /* Device times (ms) of the last kw_scan, from HIP events on the scan's stream
