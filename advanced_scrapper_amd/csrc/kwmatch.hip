@@ -156,6 +156,7 @@ struct FastBuild {
     std::vector<uint64_t> edge_key;
     std::vector<uint32_t> edge_begin, edge_cnt, edge_ent;
     uint32_t edge_mask = 0;
+    std::vector<uint32_t> ht4, arec, urec, urec2;   // merged probe records (4 x u32 each)
     std::vector<int32_t> rxf_idx;
     std::vector<uint64_t> rxf_pm, rxf_any, rxf_ext_mask;
     std::vector<uint32_t> rxf_len, rxf_ext_off, rxf_ext_cp;
@@ -400,6 +401,42 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         B.kl.insert(B.kl.end(), kv.second.begin(), kv.second.end());
     }
     if (B.kl.empty()) B.kl.push_back(0);
+    // merged records for the scan's probe: slot {key lo, key hi, first anchor record, count} ->
+    // anchor record {head lo, head hi, first use, uses << 8 | len} -> use {info0, info1, pattern, byte offset of the span}
+    B.ht4.assign((size_t)hs * 4, 0);
+    for (uint32_t sl = 0; sl < hs; ++sl) {
+        B.ht4[4 * sl] = (uint32_t)B.ht_key[sl];
+        B.ht4[4 * sl + 1] = (uint32_t)(B.ht_key[sl] >> 32);
+        B.ht4[4 * sl + 2] = B.ht_begin[sl];
+        B.ht4[4 * sl + 3] = B.ht_cnt[sl];
+    }
+    for (uint32_t a : B.kl) {
+        if (B.as_len.empty()) break;
+        if (B.as_use_cnt[a] >= (1u << 24)) { err = "kw_compile: anchor with more than 2^24 uses"; return KW_EUNSUPPORTED; }
+        B.arec.push_back((uint32_t)B.as_head[a]);
+        B.arec.push_back((uint32_t)(B.as_head[a] >> 32));
+        B.arec.push_back(B.as_use_begin[a]);
+        B.arec.push_back((B.as_use_cnt[a] << 8) | B.as_len[a]);
+    }
+    for (size_t u = 0; u < B.use_pat.size(); ++u) {
+        const uint32_t sb = B.boff[B.use_pat[u]] + (B.use_info0[u] >> 16), sl = B.use_info1[u] & 0xFFFF;
+        B.urec.push_back(B.use_info0[u]);
+        B.urec.push_back(B.use_info1[u]);
+        B.urec.push_back(B.use_pat[u]);
+        B.urec.push_back(sb);
+        // first and last (up to) 8 bytes of the span: spans of <= 16 bytes need no other compare
+        uint64_t hd = 0, tl = 0;
+        const uint32_t hl = sl < 8 ? sl : 8;
+        for (uint32_t k = 0; k < hl; ++k) hd |= (uint64_t)pat_bytes[sb + k] << (8 * k);
+        for (uint32_t k = 0; k < hl; ++k) tl |= (uint64_t)pat_bytes[sb + sl - hl + k] << (8 * k);
+        B.urec2.push_back((uint32_t)hd);
+        B.urec2.push_back((uint32_t)(hd >> 32));
+        B.urec2.push_back((uint32_t)tl);
+        B.urec2.push_back((uint32_t)(tl >> 32));
+    }
+    if (B.urec2.empty()) B.urec2.assign(4, 0);
+    if (B.arec.empty()) B.arec.assign(4, 0);
+    if (B.urec.empty()) B.urec.assign(4, 0);
     {
         uint32_t es = 256;
         while (es < 2 * B.edge.size()) es <<= 1;
@@ -727,7 +764,9 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_ec = push_array(blob, FB.edge_cnt), f_ee = push_array(blob, FB.edge_ent),
            f_rxi = push_array(blob, FB.rxf_idx), f_rxp = push_array(blob, FB.rxf_pm), f_rxa = push_array(blob, FB.rxf_any),
            f_rxl = push_array(blob, FB.rxf_len), f_rxeo = push_array(blob, FB.rxf_ext_off),
-           f_rxec = push_array(blob, FB.rxf_ext_cp), f_rxem = push_array(blob, FB.rxf_ext_mask);
+           f_rxec = push_array(blob, FB.rxf_ext_cp), f_rxem = push_array(blob, FB.rxf_ext_mask),
+           f_ht4 = push_array(blob, FB.ht4), f_arec = push_array(blob, FB.arec), f_urec = push_array(blob, FB.urec),
+           f_urec2 = push_array(blob, FB.urec2);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -811,6 +850,10 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.edge_ent = (const uint32_t *)(B + f_ee);
     F.edge_mask = FB.edge_mask;
     F.word_bits = T.word_bits;
+    F.ht4 = (const uint4 *)(B + f_ht4);
+    F.arec = (const uint4 *)(B + f_arec);
+    F.urec = (const uint4 *)(B + f_urec);
+    F.urec2 = (const uint4 *)(B + f_urec2);
     F.rxf_idx = (const int32_t *)(B + f_rxi);
     F.rxf_pm = (const uint64_t *)(B + f_rxp);
     F.rxf_any = (const uint64_t *)(B + f_rxa);
@@ -932,7 +975,8 @@ static int launch_scan(kw_handle *h)
     const uint32_t want_items = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_k * 40), (int64_t)1 << 24);
     const int64_t docs_per_r = (n_docs + nr - 1) / nr;
     const uint32_t want_out = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_r * 48), (int64_t)1 << 26);
-    const uint32_t want_rx = (uint32_t)std::min<int64_t>(docs_per_r * 2 + 64, (int64_t)1 << 20);
+    uint32_t want_rx = (uint32_t)std::min<int64_t>(docs_per_r * 2 + 64, (int64_t)1 << 20);
+    if (const char *e = getenv("KW_TEST_RX_CAP")) want_rx = (uint32_t)std::max(1, atoi(e));   // tests: force the rescan
     int rc = ensure_scratch(h, nk, nr, ng, std::max(want_items, h->item_cap), std::max(want_out, h->out_cap),
                             std::max<int64_t>(n_docs, 1), (uint32_t)std::max<int64_t>(n_docs, 1), want_rx);
     if (rc) return rc;
@@ -1012,7 +1056,7 @@ static int finish(kw_handle *h)
             uint32_t mx = 0;
             for (uint32_t c : cnt) mx = std::max(mx, c);
             const uint32_t out_cap = (status[0] & ST_OUT_OVERFLOW) ? mx + 1024 : h->out_cap;
-            const uint32_t rx_cap = (status[0] & ST_RX_OVERFLOW) ? h->rx_cap * 4 : h->rx_cap;
+            const uint32_t rx_cap = (status[0] & ST_RX_OVERFLOW) ? std::max(status[2], h->rx_cap * 2) : h->rx_cap;
             int rc = ensure_scratch(h, h->nk, h->nr, h->ng, h->item_cap, out_cap, h->hdr_cap, h->defer_cap, rx_cap);
             if (rc) return rc;
             rc = launch_scan(h);

@@ -39,8 +39,8 @@ constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
 constexpr int FK_T3_BITS = 16;                  // stage 2, 3-byte keys: 8 KB
 constexpr int FK_B2_WORDS = 2048;               // exact bigram table: 8 KB
 constexpr int FK_EDGE_BITS = 15;                // edge prefix / suffix keys: 2 x 4 KB
-constexpr int FK_CAND = 256;                    // candidates per compaction round
-constexpr int FK_ITEMS = 64;                    // items per field on the fast path
+constexpr int FK_Q = 256;                       // per-wave ring of stage-2 survivors (power of 2)
+constexpr int FK_ITEMS = 128;                   // items per field on the fast path
 constexpr int FK_CP_CAP = 16384;                // bytes of a non-ASCII field the fast path decodes
 constexpr int RK_WAVES = 4;                     // waves per resolve workgroup
 constexpr int RK_BLOCK = RK_WAVES * WAVE;
@@ -61,7 +61,7 @@ constexpr uint32_t EDGE_MIN_M = 11, EDGE_MAX_M = 20;   // names with edge-only f
 
 // per-document header written by the scan kernel (uint2):
 //   x = index of the document's first item in FastScratch::items
-//   y = n0 [6:0] | n1 [13:7] | flags
+//   y = n0 [7:0] | n1 [15:8] | flags
 constexpr uint32_t DH_NEED = 1u << 16;          // the resolve kernel has work on this document
 constexpr uint32_t DH_EDGE0 = 1u << 17;         // field 0: edge prefilter hit (prefix or suffix)
 constexpr uint32_t DH_EDGE1 = 1u << 18;
@@ -112,6 +112,10 @@ struct FastTables {
     const uint32_t *word_bits;
     int f_first;
     int empty_pat;
+    const uint4 *ht4;           // probe records: {key lo, key hi, first arec, count} per slot
+    const uint4 *arec;          // {head lo, head hi, first use, uses << 8 | len} (grouped by key)
+    const uint4 *urec;          // {use_info0, use_info1, pattern, byte offset of the span in pat_bytes}
+    const uint4 *urec2;         // {first 8 bytes of the span, last 8 bytes} (little endian, <= 8 when shorter)
     // quantifier-free regex names (literals and '.', <= 64 atoms): shift-and tables
     const int32_t *rxf_idx;     // per pattern: row r, or -1 (quantified: the backtracking engine)
     const uint64_t *rxf_pm;     // [r][128] ASCII masks ('.' bits except for '\n')

@@ -17,6 +17,10 @@
 #ifndef FK_STAGE
 #define FK_STAGE 3
 #endif
+// profiling builds: stage-2 filter and ring without the anchor-table probe
+#ifndef FK_NOPROBE
+#define FK_NOPROBE 0
+#endif
 // waves per SIMD the resolve kernel is compiled for (register budget)
 #ifndef RK_OCC
 #define RK_OCC 4
@@ -73,76 +77,112 @@ __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_
     return true;
 }
 
-// ---------------------------------------------------------------- probe one candidate (this lane)
-// klen 4: a stage-1 filter hit (4- and 3-byte anchors); klen 2: a bigram-table hit.
-// Returns the number of stage-2 survivors (0 or 1) for the statistics.
-__device__ uint32_t fast_probe(const FastTables &FT, const DevTables &T, const FastDoc &D, int64_t p, uint32_t klen,
-                               uint32_t lo, const uint32_t *l2, const uint32_t *t3, uint64_t *items, uint32_t *icnt,
-                               uint32_t *dflag, unsigned long long &nanchor)
+// ---------------------------------------------------------------- probe a batch of candidates
+// Candidate entry (stage-2 survivor): x = position relative to the document << 3 | try2 << 2 | try3 << 1 |
+// try4 (which anchor lengths to look up), y = the 4 bytes at the position.
+//
+// Stage A (lane = candidate): hash-probe the anchor table and step to the
+// lane's next anchor whose <= 8 head bytes match the text.  Stage B (lane =
+// (candidate, use) pair): the matched anchors' uses are spread over the lanes
+// by a wave prefix sum, so a popular anchor with many uses does not serialise
+// one lane; each use compares the first / last 8 bytes of its span (and the
+// middle when the span is longer than 16 bytes), then \b for uppercase names.
+__device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const DevTables &T, const FastDoc &D,
+                                                 const uint2 *ring, uint32_t head, uint32_t cnt, uint64_t *items,
+                                                 uint32_t *icnt, unsigned long long &nanchor)
 {
+    if (FK_STAGE < 1 || FK_NOPROBE) return;
+    const int lane = lane_id();
     const uint8_t *__restrict__ arena = D.arena;
-    const int f = p < D.t1 ? 0 : 1;
-    const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
-    if (p + (klen == 2 ? 2 : 3) > fe) return 0;   // shortest anchor this candidate can start
-    // stage 2: independent hashes of the 4- and 3-byte keys
-    bool try4 = false, try3 = false, try2 = klen == 2;
-    if (klen == 4) {
-        try4 = p + 4 <= fe && lds_bit(l2, fk_l2_index(lo));
-        try3 = FT.has_t3 && lds_bit(t3, fk_t3_index(lo));
-        if (!try4 && !try3) return 0;
-    }
-    const uint32_t hi = ld_u32_unaligned(arena, p + 4);
-    const uint64_t h8 = (uint64_t)lo | ((uint64_t)hi << 32);   // lo: the key from the scan registers
-    for (uint32_t L = 4; L >= 2; --L) {
-        if (!(L == 4 ? try4 : (L == 3 ? try3 : try2))) continue;
-        if (p + (int64_t)L > fe) continue;
-        const uint64_t key = ((uint64_t)L << 32) | (h8 & ((1ull << (8 * L)) - 1));
-        uint32_t slot = fk_ht_slot(key, FT.ht_mask);
-        uint32_t kb = 0, kc = 0;
-        for (;;) {
-            const uint64_t kk = FT.ht_key[slot];
-            if (kk == key) { kb = FT.ht_begin[slot]; kc = FT.ht_cnt[slot]; break; }
-            if (kk == ~0ull) break;
-            slot = (slot + 1) & FT.ht_mask;
-        }
-        for (uint32_t t = 0; t < kc; ++t) {
-            const uint32_t a = FT.kl[kb + t];
-            const uint32_t alen = FT.as_len[a];
-            if (p + (int64_t)alen > fe) continue;
-            const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
-            if ((h8 ^ FT.as_head[a]) & m8) continue;
-            ++nanchor;
-            const uint32_t ub = FT.as_use_begin[a], uc = FT.as_use_cnt[a];
-            for (uint32_t u = ub; u < ub + uc; ++u) {
-                const uint32_t i0 = FT.use_info0[u], i1 = FT.use_info1[u];
-                const uint32_t kind = i0 & 0xFF, aoff = (i0 >> 8) & 0xFF, sboff = i0 >> 16;
-                const uint32_t sblen = i1 & 0xFFFF;
-                const uint32_t pat = FT.use_pat[u];
-                const int64_t s0 = p - (int64_t)aoff;
-                if (s0 < fb || s0 + (int64_t)sblen > fe) continue;
-                if (!span_equal(arena, s0, FT.pat_bytes + FT.pat_boff[pat] + sboff, sblen)) continue;
-                if (kind == FU_UPPER) {
-                    const uint32_t pi = FT.pat_info[pat];
-                    const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
-                    const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
-                    if (wp == wf) continue;
-                    bool wn = false;
-                    if (s0 + (int64_t)sblen < fe) {
-                        uint32_t c;
-                        decode_at(arena, s0 + sblen, fe, &c);
-                        wn = is_word_cp(T, c);
-                    }
-                    if (wn == wl) continue;
-                }
-                const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(s0 - fb) << IT_POS_SHIFT) |
-                                      ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
-                const uint32_t idx = atomicAdd(&icnt[f], 1u);
-                if (idx < (uint32_t)FK_ITEMS) items[f * FK_ITEMS + idx] = item;
-                else atomicOr(dflag, 1u);
+    const bool valid = lane < (int)cnt;
+    const uint2 e = valid ? ring[(head + (uint32_t)lane) & (FK_Q - 1)] : make_uint2(0u, 0u);
+    const int64_t p = D.t0 + (int64_t)(e.x >> 3);
+    const int64_t fe = p < D.t1 ? D.t1 : D.t2;
+    const uint32_t hi = valid ? ld_u32_unaligned(arena, p + 4) : 0u;
+    const uint64_t h8 = (uint64_t)e.y | ((uint64_t)hi << 32);
+    int L = 5;                       // next key length to look up is L - 1
+    uint32_t tcur = 0, tend = 0;     // anchor records of the current key
+    bool more = valid;
+    while (__ballot(more)) {
+        // stage A: this lane's next matching anchor
+        uint32_t ub = 0, uc = 0;
+        while (more) {
+            if (tcur < tend) {
+                const uint4 ar = FT.arec[tcur++];
+                const uint32_t alen = ar.w & 0xFFu;
+                if (p + (int64_t)alen > fe) continue;
+                const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
+                if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) continue;
+                ++nanchor;
+                ub = ar.z;
+                uc = ar.w >> 8;
+                break;
+            }
+            --L;
+            if (L < 2) { more = false; break; }
+            if (!((e.x >> (4 - L)) & 1u) || p + L > fe) continue;   // try4 = bit 0, try3 = bit 1, try2 = bit 2
+            const uint64_t key = ((uint64_t)L << 32) | (h8 & ((1ull << (8 * L)) - 1));
+            uint32_t slot = fk_ht_slot(key, FT.ht_mask);
+            for (;;) {
+                const uint4 hs = FT.ht4[slot];
+                const uint64_t kk = (uint64_t)hs.x | ((uint64_t)hs.y << 32);
+                if (kk == key) { tcur = hs.z; tend = hs.z + hs.w; break; }
+                if (kk == ~0ull) break;
+                slot = (slot + 1) & FT.ht_mask;
             }
         }
+        // stage B: (candidate, use) pairs over the lanes
+        int total;
+        const int ex = wave_excl_scan((int)uc, &total);
+        for (int c0 = 0; c0 < total; c0 += WAVE) {
+            const int g = c0 + lane;
+            int owner = 0;   // the last lane whose prefix <= g
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int cand = owner + step;
+                const int exc = __shfl(ex, cand & 63, WAVE);
+                if (cand < WAVE && exc <= g) owner = cand;
+            }
+            const int exo = __shfl(ex, owner, WAVE);
+            const uint32_t u = (uint32_t)__shfl((int)ub, owner, WAVE) + (uint32_t)(g - exo);
+            const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)p, owner, WAVE);
+            const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)p >> 32), owner, WAVE);
+            if (g >= total) continue;
+            const int64_t pp = (int64_t)(((uint64_t)phi << 32) | plo);
+            const int f = pp < D.t1 ? 0 : 1;
+            const int64_t fb = f ? D.t1 : D.t0, fe2 = f ? D.t2 : D.t1;
+            const uint4 ur = FT.urec[u];
+            const uint32_t kind = ur.x & 0xFF, aoff = (ur.x >> 8) & 0xFF;
+            const uint32_t sblen = ur.y & 0xFFFF;
+            const uint32_t pat = ur.z;
+            const int64_t s0 = pp - (int64_t)aoff;
+            if (s0 < fb || s0 + (int64_t)sblen > fe2) continue;
+            const uint4 u2 = FT.urec2[u];
+            const uint32_t hl = sblen < 8 ? sblen : 8;
+            const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
+            if ((load8(arena, s0) ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
+            if (sblen > 8 && load8(arena, s0 + sblen - 8) != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) continue;
+            if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) continue;
+            if (kind == FU_UPPER) {
+                const uint32_t pi = FT.pat_info[pat];
+                const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
+                const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
+                if (wp == wf) continue;
+                bool wn = false;
+                if (s0 + (int64_t)sblen < fe2) {
+                    uint32_t ch;
+                    decode_at(arena, s0 + sblen, fe2, &ch);
+                    wn = is_word_cp(T, ch);
+                }
+                if (wn == wl) continue;
+            }
+            const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(s0 - fb) << IT_POS_SHIFT) |
+                                  ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
+            const uint32_t idx = atomicAdd(&icnt[f], 1u);
+            if (idx < (uint32_t)FK_ITEMS) items[f * FK_ITEMS + idx] = item;
+            else atomicOr(&icnt[2], 1u);
+        }
     }
-    return 1;
 }
 
 // ---------------------------------------------------------------- field helpers
@@ -491,6 +531,28 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
     return emitted;
 }
 
+// sort n <= FK_ITEMS u64 keys in this wave's LDS buffer (bitonic over the next power of two; pads with ~0)
+__device__ void wave_sort_lds(uint64_t *a, uint32_t n)
+{
+    const int lane = lane_id();
+    uint32_t n2 = WAVE;
+    while (n2 < n) n2 <<= 1;
+    for (uint32_t i = n + (uint32_t)lane; i < n2; i += WAVE) a[i] = ~0ull;
+    wave_sync();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = (uint32_t)lane; i < n2; i += WAVE) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = a[i], y = a[l];
+                    if ((x > y) == ((i & k) == 0)) { a[i] = y; a[l] = x; }
+                }
+            }
+            wave_sync();
+        }
+    }
+}
+
 // Regex-position tasks are queued per wave and run after the wave's last
 // document, where few registers are live (a call from inside the resolve
 // would spill the caller's state on every decided regex name).
@@ -544,10 +606,24 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         F.cps = cps;
         F.blkcnt = blkcnt;
     }
-    if (!(RK_SKIP & 4) && N > 0) {
-        uint64_t it = (lane < (int)N) ? items_lds[lane] : ~0ull;
+    if (N > (uint32_t)WAVE) {
+        // more than one register tile: sort in LDS, then take pattern-aligned batches of <= 64 items
+        wave_sort_lds(items_lds, N);
+    }
+    for (uint32_t bs = 0; !(RK_SKIP & 4) && bs < N;) {
+        uint32_t be = N;
+        if (N > (uint32_t)WAVE) {
+            be = bs + WAVE < N ? bs + WAVE : N;
+            if (be < N) {
+                while (be > bs && it_pat(items_lds[be]) == it_pat(items_lds[be - 1])) --be;
+                if (be == bs) return 3;   // one name with more than 64 items: the generic kernel
+            }
+        }
+        const uint32_t NB = be - bs;
+        uint64_t it = (lane < (int)NB) ? items_lds[bs + lane] : ~0ull;
+        bs = be;
         it = wave_sort_reg(it);
-        const bool valid = lane < (int)N;
+        const bool valid = lane < (int)NB;
         const uint32_t pat = valid ? it_pat(it) : 0xFFFFFu;
         const uint32_t kind = it_kind(it);
         const uint32_t bpos = it_pos(it);
@@ -562,7 +638,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         const uint64_t below = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
         const int gs = 63 - __builtin_clzll((heads & below) | 1ull);
         const uint64_t after = heads & ~below;
-        const int ge = after ? __builtin_ctzll(after) : (int)N;
+        const int ge = after ? __builtin_ctzll(after) : (int)NB;
         const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
         // the short path owns fuzzy names at least as long as the field
         const bool live = valid && !(fuzzy && m >= F.n);
@@ -739,8 +815,8 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     uint32_t *epre = b2 + FK_B2_WORDS;
     uint32_t *esuf = epre + FK_EDGE_WORDS;
     uint64_t *items_all = (uint64_t *)(esuf + FK_EDGE_WORDS);               // FK_WAVES * 2 * FK_ITEMS
-    uint2 *cand_all = (uint2 *)(items_all + FK_WAVES * 2 * FK_ITEMS);       // FK_WAVES * FK_CAND
-    uint32_t *cnt_all = (uint32_t *)(cand_all + FK_WAVES * FK_CAND);         // FK_WAVES * 4
+    uint2 *ring_all = (uint2 *)(items_all + FK_WAVES * 2 * FK_ITEMS);        // FK_WAVES * FK_Q
+    uint32_t *cnt_all = (uint32_t *)(ring_all + FK_WAVES * FK_Q);            // FK_WAVES * 4
 
     for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FK_BLOCK) filt[i] = FT.filt[i];
     for (int i = threadIdx.x; i < FK_L2_WORDS; i += FK_BLOCK) l2[i] = FT.l2[i];
@@ -754,11 +830,12 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     const int64_t wave = (int64_t)blockIdx.x * FK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * FK_WAVES;
     uint64_t *items = items_all + wib * 2 * FK_ITEMS;
-    uint2 *cand = cand_all + wib * FK_CAND;   // (rel pos << 1 | 2-byte gate, 4-byte key)
+    uint2 *ring = ring_all + wib * FK_Q;
     uint32_t *icnt = cnt_all + wib * 4;       // [0],[1] item counts, [2] defer flag
     uint64_t *gitems = S.items + (size_t)wave * S.item_cap;
     uint32_t cursor = 0;                      // items this wave wrote to HBM
     unsigned long long ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;
+    const bool has_t3 = FT.has_t3 != 0;
 
     for (int64_t d = wave; d < n_docs; d += n_waves) {
         FastDoc D;
@@ -785,6 +862,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             if (em & 12ull) flags |= DH_EDGE1;
         }
         bool na0 = false, na1 = false;
+        uint32_t qh = 0, qt = 0;                 // ring head / tail (wave-uniform)
         const int64_t base = D.t0 & ~(int64_t)15;
         for (int64_t blk = base; blk < D.t2 && !defer; blk += SCAN_TILE) {
             const int64_t lp = blk + lane * 16;
@@ -849,47 +927,71 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 }
                 gate &= valid;
             }
-            // compaction of candidates: entry = (rel pos << 1) | (2-byte gate)
-            const int c = __popc(hit) + __popc(gate);
-            int total;
-            const int ex = wave_excl_scan(c, &total);
-            if (total == 0) continue;
-            ncand += (lane == 0) ? (unsigned long long)total : 0ull;
-            for (int rb = 0; rb < total; rb += FK_CAND) {
-                int k = ex;
-                uint32_t hm = hit, gm = gate;
+            ncand += (unsigned long long)__popc(hit);
+            // stage 2 on the stage-1 hits: independent hashes of the 4- and 3-byte keys
+            uint32_t m4 = 0, m3 = 0;
+            {
+                uint32_t hm = FK_STAGE >= 1 ? hit : 0u;
                 while (hm) {
                     const int j = __ffs(hm) - 1;
                     hm &= hm - 1;
-                    if (k >= rb && k < rb + FK_CAND)
-                        cand[k - rb] = make_uint2((uint32_t)(lp + j - D.t0) << 1, fk_key_at(W, j));
-                    ++k;
+                    const uint32_t key = fk_key_at(W, j);
+                    const int64_t p = lp + j;
+                    const int64_t fe = p < D.t1 ? D.t1 : D.t2;
+                    if (p + 4 <= fe && lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
+                    if (has_t3 && lds_bit(t3, fk_t3_index(key))) m3 |= 1u << j;
                 }
-                while (gm) {
-                    const int j = __ffs(gm) - 1;
-                    gm &= gm - 1;
-                    if (k >= rb && k < rb + FK_CAND)
-                        cand[k - rb] = make_uint2(((uint32_t)(lp + j - D.t0) << 1) | 1u, fk_key_at(W, j));
-                    ++k;
-                }
-                wave_sync();
-                const int lim = (total - rb) < FK_CAND ? (total - rb) : FK_CAND;
-                for (int i0 = 0; i0 < lim; i0 += WAVE) {
-                    const int i = i0 + lane;
-                    if (i < lim) {
-                        const uint2 e = cand[i];
-                        if (FK_STAGE >= 1)
-                            ncand2 += fast_probe(FT, T, D, D.t0 + (e.x >> 1), (e.x & 1u) ? 2u : 4u, e.y, l2, t3, items,
-                                                 icnt, &icnt[2], nanchor);
-                    }
+            }
+            const uint32_t cm = m4 | m3 | gate;
+            int total;
+            const int ex = wave_excl_scan(__popc(cm), &total);
+            if (total == 0) continue;
+            ncand2 += (lane == 0) ? (unsigned long long)total : 0ull;
+            // survivors -> the ring; full batches of 64 are probed as they fill
+            if (qt - qh + (uint32_t)total > (uint32_t)FK_Q) {
+                while (qh != qt) {
+                    const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
+                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+                    qh += c;
                 }
                 wave_sync();
             }
-            defer = icnt[2] != 0;
-            defer = __builtin_amdgcn_readfirstlane((int)defer) != 0;
+            for (int rb = 0; rb < total; rb += FK_Q) {
+                int k = ex;
+                uint32_t mm = cm;
+                while (mm) {
+                    const int j = __ffs(mm) - 1;
+                    mm &= mm - 1;
+                    if (k >= rb && k < rb + FK_Q) {
+                        const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
+                        ring[(qt + (uint32_t)(k - rb)) & (FK_Q - 1)] =
+                            make_uint2(((uint32_t)(lp + j - D.t0) << 3) | fl, fk_key_at(W, j));
+                    }
+                    ++k;
+                }
+                qt += (uint32_t)((total - rb) < FK_Q ? (total - rb) : FK_Q);
+                wave_sync();
+                const bool more = rb + FK_Q < total;
+                while (qt - qh >= 64u || (more && qh != qt)) {
+                    const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
+                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+                    qh += c;
+                }
+                if (more) wave_sync();
+            }
+            wave_sync();
+            defer = __builtin_amdgcn_readfirstlane((int)icnt[2]) != 0;
             if (defer) ++ndef_items;
         }
+        // the rest of the ring
+        while (!defer && qh != qt) {
+            const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
+            fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+            qh += c;
+        }
         wave_sync();
+        if (!defer && icnt[2] != 0) { defer = true; ++ndef_items; }
+        defer = __builtin_amdgcn_readfirstlane((int)defer) != 0;
         const uint32_t n0 = __builtin_amdgcn_readfirstlane(icnt[0]);
         const uint32_t n1 = __builtin_amdgcn_readfirstlane(icnt[1]);
         if (!defer && cursor + n0 + n1 > S.item_cap) { defer = true; ++ndef_items; }
@@ -907,35 +1009,36 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             }
         } else {
             // items -> HBM (field 0 then field 1)
-            if (lane < (int)n0) gitems[cursor + lane] = items[lane];
-            if (lane < (int)n1) gitems[cursor + n0 + lane] = items[FK_ITEMS + lane];
+            for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) gitems[cursor + i] = items[i];
+            for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) gitems[cursor + n0 + i] = items[FK_ITEMS + i];
             cursor += n0 + n1;
             // the resolve kernel has work: items, an edge candidate, or a field that may be short
             const int64_t l0 = D.t1 - D.t0, l1 = D.t2 - D.t1;
             const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
             const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
             const bool need = (n0 + n1) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
-            h.y = n0 | (n1 << 7) | flags | (need ? DH_NEED : 0u);
+            h.y = n0 | (n1 << 8) | flags | (need ? DH_NEED : 0u);
         }
         if (lane == 0) S.hdr[d] = h;
+        wave_sync();
     }
-    unsigned long long a = nanchor, c2 = ncand2;
+    unsigned long long a = nanchor, c1 = ncand;
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) {
         a += __shfl_xor(a, dd, WAVE);
-        c2 += __shfl_xor(c2, dd, WAVE);
+        c1 += __shfl_xor(c1, dd, WAVE);
     }
     if (lane == 0) {
-        atomicAdd(&S.stats[0], ncand);
+        atomicAdd(&S.stats[0], c1);
         atomicAdd(&S.stats[1], a);
         atomicAdd(&S.stats[4], ndefer);
         atomicAdd(&S.stats[5], ndef_items);
-        atomicAdd(&S.stats[8], c2);
+        atomicAdd(&S.stats[8], ncand2);
     }
 }
 
 constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS + FK_B2_WORDS + 2 * FK_EDGE_WORDS) * 4 +
-                             (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_CAND * 8 + 4 * 4);
+                             (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_Q * 8 + 4 * 4);
 
 // ---------------------------------------------------------------- kernel 2: resolve
 __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables FT, DevTables T,
@@ -980,14 +1083,14 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
             const uint32_t hx = (uint32_t)__shfl((int)hl.x, l, WAVE);
             const uint32_t hy = (uint32_t)__shfl((int)hl.y, l, WAVE);
             const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
-            const uint32_t nf[2] = {hy & 127u, (hy >> 7) & 127u};
+            const uint32_t nf[2] = {hy & 255u, (hy >> 8) & 255u};
             const uint32_t out_mark = O.n, rq_mark = RQ.n;
             bool defer = false;
             ++nres;
             for (int f = 0; f < 2 && !defer; ++f) {
                 const uint32_t N = nf[f];
                 const uint64_t *src = S.items + hx + (f ? nf[0] : 0u);
-                if (lane < (int)N) items[lane] = src[lane];
+                for (uint32_t i = (uint32_t)lane; i < N; i += WAVE) items[i] = src[i];
                 if (lane == 0) { icnt[0] = N; icnt[1] = 0; }
                 wave_sync();
                 FieldCtx F;
@@ -1025,6 +1128,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     }
     // the queued regex-position tasks of this wave's documents
     wave_sync_global();
+    if (RQ.n > RQ.cap && lane == 0) atomicMax(&GS.status[2], RQ.n);   // the queue size a rescan needs
     const uint32_t n_rx = RQ.n < RQ.cap ? RQ.n : RQ.cap;
     for (uint32_t t = 0; t < n_rx; ++t) {
         const uint4 tk = RQ.q[t];

@@ -205,3 +205,21 @@ def test_wildcard_regex_names_vs_oracle():
     got = _gpu_maps(m, texts, titles)
     bad = _compare(processed, texts, titles, got)
     assert not bad, f"GPU differs from the oracle on wildcard docs {bad[:20]}"
+
+
+def test_regex_queue_overflow_rescans(monkeypatch):
+    """A resolve wave whose regex-position queue overflows makes the host grow it and scan again."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    monkeypatch.setenv('KW_TEST_RX_CAP', '1')
+    processed = {'TK': {'name': {n: (None, None) for n in _WILD_NAMES}}}
+    m = GpuMatcher(compile_kb(processed))
+    texts = [' '.join(_WILD_NAMES) + ' x' * k for k in range(40)]
+    titles = [_WILD_NAMES[k % len(_WILD_NAMES)] for k in range(40)]
+    got = _gpu_maps(m, texts, titles)
+    bad = _compare(processed, texts, titles, got)
+    assert not bad, f"GPU differs from the oracle after the regex-queue rescan on docs {bad[:20]}"
+    assert m.stats()['regex_searches'] > 40
