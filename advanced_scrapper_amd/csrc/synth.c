@@ -315,3 +315,88 @@ void synth_fill(const synth_ctx *c, uint64_t seed, int64_t doc_base, int64_t n_d
 }
 
 int synth_ctx_size(void) { return (int)sizeof(synth_ctx); }
+
+/* ------------------------------------------------------------------------
+ * Synthetic CDX link rows (config 5): the `original` URL
+ * column of an Internet-Archive CDX listing of finance.yahoo.com/news/ URLs.
+ * Row r is a pure function of (seed, r).  About 30 % of rows repeat an earlier
+ * article (uniform article ids over 1.31 n), and the spellings exercise every
+ * rule of yahoo_links_selenium.py:63-79: http vs https, ':80' ports, query
+ * strings / fragments after '.html', 'www.' hosts, rows without '.html',
+ * 'news/%' and "news/'" paths, '<x>html' regex matches, non-ASCII slugs.
+ * ------------------------------------------------------------------------ */
+static const char *URL_WORDS[] = {
+    "stocks", "market", "rally", "fed", "rates", "earnings", "beat", "miss", "oil", "gold", "bitcoin", "tesla",
+    "apple", "nvidia", "amazon", "google", "microsoft", "bank", "jobs", "report", "inflation", "cpi", "dollar",
+    "yields", "bonds", "tech", "shares", "surge", "drop", "record", "high", "low", "week", "ahead", "what",
+    "know", "why", "how", "analyst", "upgrade", "downgrade", "deal", "merger", "ipo", "crypto", "china", "trade",
+    "tariffs", "retail", "sales", "housing", "consumer", "outlook", "guidance", "q1", "q2", "q3", "q4"};
+#define N_URL_WORDS ((int)(sizeof(URL_WORDS) / sizeof(URL_WORDS[0])))
+
+static int64_t gen_url(uint8_t *out, uint64_t seed, int64_t row, int64_t n_articles, int64_t *ts)
+{
+    rng_t r = {seed * 0x9E3779B97F4A7C15ull ^ (uint64_t)row * 0xD1B54A32D192ED03ull};
+    rnext(&r);
+    const uint64_t art = (uint64_t)((rnext(&r) >> 11) % (uint64_t)(n_articles > 0 ? n_articles : 1));
+    rng_t a = {seed ^ art * 0x94D049BB133111EBull};
+    rnext(&a);
+    wr_t w = {out, 0, 0};
+    const uint32_t v = rint_(&r, 1000);
+    /* scheme and host */
+    const char *scheme = (v < 200) ? "http://" : "https://";
+    put(&w, (const uint8_t *)scheme, (int64_t)strlen(scheme));
+    if (v >= 950 && v < 1000) put(&w, (const uint8_t *)"www.", 4);
+    put(&w, (const uint8_t *)"finance.yahoo.com", 17);
+    if (rint_(&r, 20) == 0) put(&w, (const uint8_t *)":80", 3);
+    put(&w, (const uint8_t *)"/news/", 6);
+    const uint32_t odd = rint_(&r, 200);
+    if (odd == 0) put(&w, (const uint8_t *)"%20", 3);
+    else if (odd == 1) put(&w, (const uint8_t *)"'", 1);
+    /* slug of the article */
+    const int nw = 3 + (int)rint_(&a, 8);
+    for (int i = 0; i < nw; ++i) {
+        const char *s = URL_WORDS[rint_(&a, N_URL_WORDS)];
+        if (i) putc_(&w, '-');
+        put(&w, (const uint8_t *)s, (int64_t)strlen(s));
+    }
+    if (rint_(&a, 100) == 0) put(&w, (const uint8_t *)"-caf\xc3\xa9", 6);
+    char id[24];
+    int nd = 0;
+    uint64_t x = 100000000ull + (art % 900000000ull);
+    while (x) { id[nd++] = (char)('0' + x % 10); x /= 10; }
+    putc_(&w, '-');
+    while (nd) putc_(&w, (uint8_t)id[--nd]);
+    /* ending */
+    const uint32_t e = rint_(&r, 100);
+    if (e < 5) {
+        put(&w, (const uint8_t *)".htm", 4);                   /* no '.html': dropped */
+    } else if (e < 6) {
+        put(&w, (const uint8_t *)"xhtml", 5);                  /* regex '.html' matches 'xhtml' */
+    } else {
+        put(&w, (const uint8_t *)".html", 5);
+        if (e >= 80 && e < 95) put(&w, (const uint8_t *)"?.tsrc=rss", 10);
+        else if (e >= 95 && e < 98) put(&w, (const uint8_t *)"#comments", 9);
+        else if (e >= 98) put(&w, (const uint8_t *)".html", 5);
+    }
+    if (ts) {
+        /* 14-digit CDX timestamp YYYYMMDDhhmmss (2017..2025) */
+        const uint64_t t = rnext(&r);
+        const int64_t Y = 2017 + (int64_t)(t % 9), M = 1 + (int64_t)((t >> 8) % 12), D = 1 + (int64_t)((t >> 16) % 28);
+        const int64_t h = (int64_t)((t >> 24) % 24), mi = (int64_t)((t >> 32) % 60), s = (int64_t)((t >> 40) % 60);
+        *ts = ((((Y * 100 + M) * 100 + D) * 100 + h) * 100 + mi) * 100 + s;
+    }
+    return w.n;
+}
+
+void synth_url_lengths(uint64_t seed, int64_t row_base, int64_t n_rows, int64_t n_articles, int64_t *lens)
+{
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t i = 0; i < n_rows; ++i) lens[i] = gen_url(NULL, seed, row_base + i, n_articles, NULL);
+}
+
+void synth_url_fill(uint64_t seed, int64_t row_base, int64_t n_rows, int64_t n_articles, const int64_t *off,
+                    uint8_t *arena, int64_t *ts)
+{
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t i = 0; i < n_rows; ++i) gen_url(arena + off[i], seed, row_base + i, n_articles, ts ? ts + i : NULL);
+}

@@ -188,3 +188,55 @@ def to_dataframe(corpus: Corpus, source: str = 'yahoo'):
         'article_text': texts, 'title': titles, 'date_time': dates, 'url': urls,
         'source': [source] * n, 'source_url': ['https://finance.yahoo.com'] * n,
     })
+
+
+# --------------------------------------------------------------------- CDX link rows (config 5)
+class UrlRows:
+    """Synthetic CDX rows: URL arena (uint8, padded), offsets (n+1), CDX timestamps (int64)."""
+
+    def __init__(self, arena: np.ndarray, off: np.ndarray, ts: np.ndarray, row_base: int, seed: int):
+        self.arena, self.off, self.ts, self.row_base, self.seed = arena, off, ts, row_base, seed
+
+    @property
+    def n(self) -> int:
+        return len(self.ts)
+
+    @property
+    def n_bytes(self) -> int:
+        return int(self.off[-1] - self.off[0])
+
+    def url(self, i: int) -> str:
+        return bytes(self.arena[self.off[i]:self.off[i + 1]]).decode('utf-8', 'surrogatepass')
+
+    def urls(self) -> List[str]:
+        return [self.url(i) for i in range(self.n)]
+
+    def cdx_text(self, lo: int = 0, hi: int = None) -> str:
+        """The rows as CDX listing lines (urlkey timestamp original mimetype statuscode digest length)."""
+        hi = self.n if hi is None else hi
+        lines = []
+        for i in range(lo, hi):
+            u = self.url(i)
+            key = 'com,yahoo,finance)/' + u.split('/', 3)[-1].lower()
+            lines.append(f"{key} {int(self.ts[i])} {u} text/html 200 SYNTH{(self.row_base + i) % 99991:05d} {len(u) + 900}")
+        return '\n'.join(lines) + '\n'
+
+
+def generate_urls(n_rows: int, seed: int = DEFAULT_SEED, row_base: int = 0, n_articles: int = None) -> UrlRows:
+    """Rows [row_base, row_base + n_rows) of the seeded CDX corpus (~30 % repeated articles)."""
+    L = _lib()
+    if not hasattr(L, '_url_types'):
+        L.synth_url_lengths.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        L.synth_url_fill.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+        L._url_types = True
+    if n_articles is None:
+        n_articles = max(1, int(1.31 * (row_base + n_rows)))
+    lens = np.zeros(n_rows, dtype=np.int64)
+    L.synth_url_lengths(seed, row_base, n_rows, n_articles, lens.ctypes.data)
+    off = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    arena = np.zeros(int(off[-1]) + ARENA_PAD, dtype=np.uint8)
+    ts = np.zeros(n_rows, dtype=np.int64)
+    L.synth_url_fill(seed, row_base, n_rows, n_articles, off.ctypes.data, arena.ctypes.data, ts.ctypes.data)
+    return UrlRows(arena, off, ts, row_base, seed)
