@@ -25,9 +25,15 @@ KW_NOPOS = 0xFFFFFFFF
 
 HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('field', '<u4')])
 
-# every symbol include/kwmatch.h declares
+# every symbol include/kwmatch.h and include/kwdedup.h declare
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
-           'kw_last_kernel_times', 'kw_last_error', 'kw_destroy')
+           'kw_last_kernel_times', 'kw_last_error', 'kw_destroy',
+           'kw_dedup_create', 'kw_dedup_run', 'kw_dedup_counts', 'kw_dedup_kept_size', 'kw_dedup_kept_copy',
+           'kw_dedup_last_ms', 'kw_dedup_last_error', 'kw_dedup_destroy', 'dedup_urls')
+
+# KW_URL_* row codes (include/kwdedup.h)
+KW_URL_NO_HTML, KW_URL_KEPT, KW_URL_FILTERED, KW_URL_DUPLICATE = 0, 1, 2, 3
+KW_DEDUP_NORMALIZE = 1
 KW_N_STATS = 13
 
 
@@ -49,6 +55,19 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.kw_dedup_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.kw_dedup_run.argtypes = [vp, vp, vp, i64, i32, vp, vp]
+    L.kw_dedup_counts.argtypes = [vp, vp]
+    L.kw_dedup_kept_size.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.kw_dedup_kept_copy.argtypes = [vp, vp, vp, vp, vp]
+    L.kw_dedup_last_ms.argtypes = [vp, vp, i32]
+    L.kw_dedup_last_error.argtypes = [vp]
+    L.kw_dedup_last_error.restype = ctypes.c_char_p
+    L.kw_dedup_destroy.argtypes = [vp]
+    L.dedup_urls.argtypes = [vp, vp, i64, vp, vp]
+    for f in ('kw_dedup_create', 'kw_dedup_run', 'kw_dedup_counts', 'kw_dedup_kept_size', 'kw_dedup_kept_copy',
+              'kw_dedup_last_ms', 'kw_dedup_destroy', 'dedup_urls'):
+        getattr(L, f).restype = ctypes.c_int
     L.kw_compile.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, i64, i32, ctypes.POINTER(vp)]
     L.kw_compile.restype = ctypes.c_int
     L.kw_scan.argtypes = [vp, vp, vp, i64, vp]

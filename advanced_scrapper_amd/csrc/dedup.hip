@@ -1,0 +1,772 @@
+// libkwmatch: CDX link-row normalise + keep-first dedup (include/kwdedup.h).
+//
+// Reference: yahoo_links_selenium.py:63-79 (per part) and :160-174 (merge);
+// restated in oracle/dedup_oracle.py.  One pass per row (lane per row):
+//
+//   dd_transform_kernel  find the cut (first "html" after a code point that is
+//                        not '\n'), rewrite the prefix (':80' removed, 'http:'
+//                        -> 'https:'), append ".html", flag 'news/%' / "news/'",
+//                        write the normalised URL into a sparse 8-aligned arena
+//                        and hash it (two independent 64-bit word hashes).
+//                        Rows whose only ':' is the scheme's take a word-wide
+//                        copy; the rest run the byte-serial rewrite.
+//   dd_insert_kernel     open-addressing table of 64-bit slots {tag, row}: the
+//                        first inserter claims a slot by CAS, rows with the same
+//                        tag keep the smallest row by atomicMin (keep='first').
+//   dd_decide_kernel     each row finds its slot; rep == row -> kept, else the
+//                        row is a duplicate iff its normalised bytes equal the
+//                        rep's (length, second hash, then every word).  Rows
+//                        that share a tag with a different URL (a 64-bit hash
+//                        collision) are resolved exactly on the host.
+//   dd_count / dd_scan / dd_place / dd_copy
+//                        dense offsets, source rows and bytes of the kept rows.
+//
+// All byte/integer work: the roofline is HBM bandwidth.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/kwmatch.h"
+#include "../../include/kwdedup.h"
+
+namespace dd {
+
+constexpr int BLOCK = 256;
+constexpr int SCAN_ROWS = 4;                       // rows per thread in the scan kernels
+constexpr int SCAN_TILE = BLOCK * SCAN_ROWS;
+constexpr uint32_t HTML4 = 0x6C6D7468u;            // "html"
+constexpr uint32_t NEWS4 = 0x7377656Eu;            // "news"
+constexpr uint64_t DOTHTML = 0x6C6D74682Eull;      // ".html"
+constexpr uint8_t CODE_COLLIDE = 4;                // internal: tag shared with a different URL
+
+// sparse output arena: row i's normalised URL starts at obase(off[i], i) (8-aligned, room for
+// len + len/5 + 16 bytes: at most one extra 's' per 5 input bytes, ".html", word padding)
+__host__ __device__ __forceinline__ int64_t obase(int64_t off_i, int64_t i)
+{
+    return (off_i + off_i / 5 + 24 * i + 7) & ~(int64_t)7;
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t *__restrict__ a, int64_t p)
+{
+    const int64_t a0 = p & ~(int64_t)3;
+    const uint32_t x0 = *(const uint32_t *)(a + a0);
+    const uint32_t x1 = *(const uint32_t *)(a + a0 + 4);
+    return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)(p & 3));
+}
+
+__device__ __forceinline__ uint64_t ld64(const uint8_t *__restrict__ a, int64_t p)
+{
+    const int64_t a0 = p & ~(int64_t)3;
+    const uint32_t s = (uint32_t)(p & 3);
+    const uint32_t x0 = *(const uint32_t *)(a + a0);
+    const uint32_t x1 = *(const uint32_t *)(a + a0 + 4);
+    const uint32_t x2 = *(const uint32_t *)(a + a0 + 8);
+    return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s) << 32);
+}
+
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v)   // high bit set in (at least) every zero byte
+{
+    return (v - 0x01010101u) & ~v & 0x80808080u;
+}
+
+__host__ __device__ __forceinline__ uint64_t mix1(uint64_t h, uint64_t w)
+{
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 32);
+}
+__host__ __device__ __forceinline__ uint64_t mix2(uint64_t h, uint64_t w)
+{
+    h = (h ^ w) * 0xC2B2AE3D27D4EB4Full;
+    h ^= h >> 29;
+    return h * 0x165667B19E3779F9ull;
+}
+__host__ __device__ __forceinline__ uint64_t fmix(uint64_t h)
+{
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    h *= 0xC4CEB9FE1A85EC53ull;
+    return h ^ (h >> 33);
+}
+
+struct Scratch {
+    uint8_t *out;            // sparse normalised URLs
+    uint64_t *h1, *h2;       // per row
+    uint32_t *len3;          // per row: normalised length
+    unsigned long long *table;
+    uint64_t mask;
+    unsigned long long *cnt;   // [0..4] per code
+    int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
+    int normalize;           // KW_DEDUP_NORMALIZE: apply :63-76; else keep-first over the raw strings
+};
+
+// byte-serial writer of the normalised URL: 8-byte words to the sparse arena + hashes + filter window
+struct Emit {
+    uint64_t w, win, h1, h2;
+    int64_t pos, len;
+    int nb;
+    bool bad;
+    uint8_t *out;
+    __device__ __forceinline__ void put(uint32_t c)
+    {
+        w |= (uint64_t)c << (8 * nb);
+        ++nb;
+        ++len;
+        win = (win << 8) | c;
+        const uint64_t w6 = win & 0xFFFFFFFFFFFFull;
+        // 'news/%' and "news/'" (newest byte lowest)
+        bad |= w6 == 0x6E6577732F25ull || w6 == 0x6E6577732F27ull;
+        if (nb == 8) {
+            *(uint64_t *)(out + pos) = w;
+            h1 = mix1(h1, w);
+            h2 = mix2(h2, w);
+            pos += 8;
+            w = 0;
+            nb = 0;
+        }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if (nb) {
+            *(uint64_t *)(out + pos) = w;
+            h1 = mix1(h1, w);
+            h2 = mix2(h2, w);
+        }
+    }
+};
+
+// the reference's rewrite of the cut prefix u[0, j): ':80' removed (left to right), then 'http:' -> 'https:'
+struct Rewrite {
+    uint32_t P;
+    int np;           // pending bytes of the ':80' window
+    uint64_t Q;
+    int nq;           // pending bytes of the 'http:' window
+    __device__ __forceinline__ void h_push(Emit &E, uint32_t c)
+    {
+        Q |= (uint64_t)c << (8 * nq);
+        if (++nq == 5) {
+            if (Q == 0x3A70747468ull) {    // "http:"
+                E.put('h'); E.put('t'); E.put('t'); E.put('p'); E.put('s'); E.put(':');
+                Q = 0;
+                nq = 0;
+            } else {
+                E.put((uint32_t)(Q & 0xFF));
+                Q >>= 8;
+                nq = 4;
+            }
+        }
+    }
+    __device__ __forceinline__ void r_push(Emit &E, uint32_t c)
+    {
+        P |= c << (8 * np);
+        if (++np == 3) {
+            if (P == 0x30383Au) {          // ":80"
+                P = 0;
+                np = 0;
+            } else {
+                h_push(E, P & 0xFF);
+                P >>= 8;
+                np = 2;
+            }
+        }
+    }
+    __device__ __forceinline__ void flush(Emit &E)
+    {
+        while (np) { h_push(E, P & 0xFF); P >>= 8; --np; }
+        while (nq) { E.put((uint32_t)(Q & 0xFF)); Q >>= 8; --nq; }
+    }
+};
+
+__global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__restrict__ arena,
+                                                             const int64_t *__restrict__ off, int64_t n,
+                                                             uint8_t *__restrict__ code, Scratch S)
+{
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t b = off[i], L = off[i + 1] - b;
+        if (!S.normalize) {
+            // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
+            uint8_t *out = S.out + obase(b, i);
+            uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
+            for (int64_t x0 = 0; x0 < L; x0 += 8) {
+                uint64_t w = ld64(arena, b + x0);
+                if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
+                *(uint64_t *)(out + x0) = w;
+                h1 = mix1(h1, w);
+                h2 = mix2(h2, w);
+            }
+            h1 = fmix(h1 ^ (uint64_t)L);
+            h2 = fmix(h2 ^ ((uint64_t)L * 0x9E3779B97F4A7C15ull));
+            if (S.weak) h1 &= 0xFull;
+            S.h1[i] = h1;
+            S.h2[i] = h2;
+            S.len3[i] = (uint32_t)L;
+            code[i] = KW_URL_KEPT;
+            continue;
+        }
+        // ---- pass 1: the cut j, the first extra ':' and the first 'news/%' | "news/'" end
+        int64_t j = -1, ec = INT64_MAX, kf = INT64_MAX;
+        bool scheme_http = false;
+        for (int64_t t = 0; t < L && j < 0; t += 4) {
+            const uint32_t x = ld32(arena, b + t);
+            uint32_t hm = zero_bytes(x ^ 0x68686868u);   // 'h'
+            uint32_t cm = zero_bytes(x ^ 0x3A3A3A3Au);   // ':'
+            uint32_t nm = zero_bytes(x ^ 0x6E6E6E6Eu);   // 'n'
+            while (cm) {
+                const int64_t q = t + (__builtin_ctz(cm) >> 3);
+                cm &= cm - 1;
+                if (q >= L) break;
+                if (((ld32(arena, b + q) ^ 0x3Au) & 0xFFu) != 0) continue;   // false positive of zero_bytes
+                // the scheme's colon ("http:" / "https:"), unless it starts a ':80'
+                const bool p80 = q + 3 <= L && (ld32(arena, b + q) & 0xFFFFFFu) == 0x30383Au;
+                if (!p80 && q == 4 && ld32(arena, b) == 0x70747468u) { scheme_http = true; continue; }
+                if (!p80 && q == 5 && ld32(arena, b) == 0x70747468u && (ld32(arena, b + 4) & 0xFFFFu) == 0x3A73u) continue;
+                if (q < ec) ec = q;
+            }
+            while (nm) {
+                const int64_t q = t + (__builtin_ctz(nm) >> 3);
+                nm &= nm - 1;
+                if (q + 6 > L || q + 5 >= kf) continue;
+                if (ld32(arena, b + q) != NEWS4) continue;
+                const uint32_t y = ld32(arena, b + q + 4);
+                if ((y & 0xFF) == '/' && (((y >> 8) & 0xFF) == '%' || ((y >> 8) & 0xFF) == '\'')) kf = q + 5;
+            }
+            while (hm) {
+                const int64_t q = t + (__builtin_ctz(hm) >> 3);
+                hm &= hm - 1;
+                if (q < 1 || q + 4 > L) continue;
+                if (ld32(arena, b + q) != HTML4) continue;
+                const uint32_t pv = ld32(arena, b + q - 1) & 0xFFu;
+                if (pv == '\n') continue;
+                // the code point before "html" starts at its lead byte
+                int64_t s = q - 1;
+                if (pv >= 0x80) {
+                    while (s > 0 && (ld32(arena, b + s) & 0xC0u) == 0x80u && q - s < 4) --s;
+                }
+                j = s;
+                break;
+            }
+        }
+        if (j < 0) {
+            code[i] = KW_URL_NO_HTML;
+            S.len3[i] = 0;
+            continue;
+        }
+        uint8_t *out = S.out + obase(b, i);
+        uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
+        int64_t len3;
+        bool bad;
+        if (ec >= j) {
+            // ---- fast path: no ':80' and no 'http:' in the prefix except the scheme's
+            const int ins = (scheme_http && j > 4) ? 1 : 0;
+            const int64_t E = j + ins;
+            len3 = E + 5;
+            bad = kf < j;
+            for (int64_t x0 = 0; x0 < len3; x0 += 8) {
+                uint64_t w = 0;
+                if (x0 < E) {
+                    if (!ins) w = ld64(arena, b + x0);
+                    else if (x0 == 0) w = 0x7370747468ull | (ld64(arena, b + 4) << 40);   // "https" + u[4..7)
+                    else w = ld64(arena, b + x0 - 1);
+                }
+                if (E < x0 + 8) {   // splice ".html" at E, zeros after it
+                    if (E >= x0) {
+                        const int sh = (int)(E - x0) * 8;
+                        w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
+                    } else {
+                        w = DOTHTML >> ((x0 - E) * 8);
+                    }
+                }
+                *(uint64_t *)(out + x0) = w;
+                h1 = mix1(h1, w);
+                h2 = mix2(h2, w);
+            }
+        } else {
+            // ---- general rewrite, byte by byte
+            Emit Em;
+            Em.w = 0; Em.win = 0; Em.h1 = h1; Em.h2 = h2; Em.pos = 0; Em.len = 0; Em.nb = 0; Em.bad = false; Em.out = out;
+            Rewrite R;
+            R.P = 0; R.np = 0; R.Q = 0; R.nq = 0;
+            for (int64_t t = 0; t < j; t += 4) {
+                const uint32_t x = ld32(arena, b + t);
+                const int m = (int)(j - t < 4 ? j - t : 4);
+                for (int k = 0; k < m; ++k) R.r_push(Em, (x >> (8 * k)) & 0xFFu);
+            }
+            R.flush(Em);
+            Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
+            Em.finish();
+            h1 = Em.h1;
+            h2 = Em.h2;
+            len3 = Em.len;
+            bad = Em.bad;
+        }
+        h1 = fmix(h1 ^ (uint64_t)len3);
+        h2 = fmix(h2 ^ ((uint64_t)len3 * 0x9E3779B97F4A7C15ull));
+        if (S.weak) h1 &= 0xFull;
+        S.h1[i] = h1;
+        S.h2[i] = h2;
+        S.len3[i] = (uint32_t)len3;
+        code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
+    }
+}
+
+__device__ __forceinline__ uint64_t slot_key(uint64_t h1, int64_t row)
+{
+    const uint32_t tag = (uint32_t)(h1 >> 32) | 1u;   // never 0 (0 = empty slot)
+    return ((uint64_t)tag << 32) | (uint64_t)(uint32_t)row;
+}
+
+__global__ __launch_bounds__(BLOCK) void dd_insert_kernel(const uint8_t *__restrict__ code, int64_t n, Scratch S)
+{
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        if (code[i] != KW_URL_KEPT) continue;
+        const uint64_t h = S.h1[i];
+        const unsigned long long key = slot_key(h, i);
+        uint64_t slot = (h ^ (h >> 29)) & S.mask;
+        for (;;) {
+            unsigned long long cur = S.table[slot];
+            if (cur == 0ull) {
+                cur = atomicCAS(&S.table[slot], 0ull, key);
+                if (cur == 0ull) break;
+            }
+            if ((cur >> 32) == (key >> 32)) {
+                if ((uint32_t)cur > (uint32_t)key) atomicMin(&S.table[slot], key);
+                break;
+            }
+            slot = (slot + 1) & S.mask;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__restrict__ code, Scratch S,
+                                                          const int64_t *__restrict__ off)
+{
+    unsigned long long c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        uint8_t k = code[i];
+        if (k == KW_URL_KEPT) {
+            const uint64_t h = S.h1[i];
+            const uint32_t tag = (uint32_t)(h >> 32) | 1u;
+            uint64_t slot = (h ^ (h >> 29)) & S.mask;
+            unsigned long long cur;
+            for (;;) {
+                cur = S.table[slot];
+                if ((uint32_t)(cur >> 32) == tag) break;
+                slot = (slot + 1) & S.mask;
+            }
+            const int64_t rep = (int64_t)(uint32_t)cur;
+            if (rep != i) {
+                bool eq = S.len3[rep] == S.len3[i] && S.h2[rep] == S.h2[i];
+                if (eq) {
+                    const uint64_t *a = (const uint64_t *)(S.out + obase(off[i], i));
+                    const uint64_t *r = (const uint64_t *)(S.out + obase(off[rep], rep));
+                    const uint32_t nw = (S.len3[i] + 7) / 8;
+                    for (uint32_t w = 0; w < nw && eq; ++w) eq = a[w] == r[w];
+                }
+                k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
+                code[i] = k;
+            }
+        }
+        c0 += k == 0;
+        c1 += k == 1;
+        c2 += k == 2;
+        c3 += k == 3;
+        c4 += k == CODE_COLLIDE;
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        unsigned long long v = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : c4;
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&S.cnt[q], v);
+    }
+}
+
+// ---- dense kept rows: per-tile counts, one-block scan of the tiles, placement, byte copy
+__device__ __forceinline__ void block_excl_scan2(uint64_t &a, uint64_t &b, uint64_t *sh, uint64_t &ta, uint64_t &tb)
+{
+    // exclusive scan of (a, b) over the block; ta/tb = block totals
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t xa = a, xb = b;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t ya = __shfl_up(xa, d, 64), yb = __shfl_up(xb, d, 64);
+        if (lane >= d) { xa += ya; xb += yb; }
+    }
+    if (lane == 63) { sh[2 * wv] = xa; sh[2 * wv + 1] = xb; }
+    __syncthreads();
+    uint64_t pa = 0, pb = 0;
+    ta = 0;
+    tb = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        if (w < wv) { pa += sh[2 * w]; pb += sh[2 * w + 1]; }
+        ta += sh[2 * w];
+        tb += sh[2 * w + 1];
+    }
+    __syncthreads();
+    a = pa + xa - a;
+    b = pb + xb - b;
+}
+
+__global__ __launch_bounds__(BLOCK) void dd_count_kernel(const uint8_t *__restrict__ code, int64_t n, Scratch S,
+                                                         unsigned long long *__restrict__ tile_cnt,
+                                                         unsigned long long *__restrict__ tile_bytes)
+{
+    __shared__ uint64_t sh[2 * BLOCK / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ROWS;
+    uint64_t c = 0, by = 0;
+    for (int r = 0; r < SCAN_ROWS; ++r) {
+        const int64_t i = base + r;
+        if (i < n && code[i] == KW_URL_KEPT) { ++c; by += S.len3[i]; }
+    }
+    uint64_t ta, tb;
+    block_excl_scan2(c, by, sh, ta, tb);
+    if (threadIdx.x == 0) { tile_cnt[blockIdx.x] = ta; tile_bytes[blockIdx.x] = tb; }
+}
+
+__global__ __launch_bounds__(1024) void dd_scan_tiles_kernel(unsigned long long *__restrict__ tile_cnt,
+                                                             unsigned long long *__restrict__ tile_bytes, int64_t nt,
+                                                             unsigned long long *__restrict__ totals)
+{
+    __shared__ unsigned long long pc[1024], pb[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (nt + 1023) / 1024;
+    unsigned long long sc = 0, sb = 0;
+    for (int64_t k = t * per; k < (t + 1) * per && k < nt; ++k) { sc += tile_cnt[k]; sb += tile_bytes[k]; }
+    pc[t] = sc;
+    pb[t] = sb;
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long ac = 0, ab = 0;
+        for (int k = 0; k < 1024; ++k) {
+            const unsigned long long vc = pc[k], vb = pb[k];
+            pc[k] = ac;
+            pb[k] = ab;
+            ac += vc;
+            ab += vb;
+        }
+        totals[0] = ac;
+        totals[1] = ab;
+    }
+    __syncthreads();
+    unsigned long long ac = pc[t], ab = pb[t];
+    for (int64_t k = t * per; k < (t + 1) * per && k < nt; ++k) {
+        const unsigned long long vc = tile_cnt[k], vb = tile_bytes[k];
+        tile_cnt[k] = ac;
+        tile_bytes[k] = ab;
+        ac += vc;
+        ab += vb;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restrict__ code, int64_t n, Scratch S,
+                                                         const unsigned long long *__restrict__ tile_cnt,
+                                                         const unsigned long long *__restrict__ tile_bytes,
+                                                         int64_t *__restrict__ kept_off, int64_t *__restrict__ kept_row)
+{
+    __shared__ uint64_t sh[2 * BLOCK / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ROWS;
+    uint64_t c = 0, by = 0;
+    for (int r = 0; r < SCAN_ROWS; ++r) {
+        const int64_t i = base + r;
+        if (i < n && code[i] == KW_URL_KEPT) { ++c; by += S.len3[i]; }
+    }
+    uint64_t ta, tb;
+    block_excl_scan2(c, by, sh, ta, tb);
+    c += tile_cnt[blockIdx.x];
+    by += tile_bytes[blockIdx.x];
+    for (int r = 0; r < SCAN_ROWS; ++r) {
+        const int64_t i = base + r;
+        if (i < n && code[i] == KW_URL_KEPT) {
+            kept_off[c] = (int64_t)by;
+            kept_row[c] = i;
+            ++c;
+            by += S.len3[i];
+        }
+    }
+}
+
+// one wave per kept row at a time: lanes copy bytes (coalesced 64-byte stores)
+__global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
+                                                        const int64_t *__restrict__ kept_row,
+                                                        const int64_t *__restrict__ off, Scratch S,
+                                                        uint8_t *__restrict__ dst)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    for (int64_t k0 = wave * 64; k0 < n_kept; k0 += n_waves * 64) {
+        // lane l prefetches row k0 + l's facts, then the wave walks the 64 rows
+        const int64_t kk = k0 + lane;
+        int64_t d0 = 0, src = 0;
+        uint32_t len = 0;
+        if (kk < n_kept) {
+            const int64_t row = kept_row[kk];
+            d0 = kept_off[kk];
+            src = obase(off[row], row);
+            len = S.len3[row];
+        }
+        const int m = (int)(n_kept - k0 < 64 ? n_kept - k0 : 64);
+        for (int r = 0; r < m; ++r) {
+            const int64_t rd = __shfl(d0, r, 64), rs = __shfl(src, r, 64);
+            const uint32_t rl = (uint32_t)__shfl((int)len, r, 64);
+            for (uint32_t x = (uint32_t)lane; x < rl; x += 64) dst[rd + x] = S.out[rs + x];
+        }
+    }
+}
+
+}  // namespace dd
+
+using namespace dd;
+
+struct kw_dedup {
+    int device = 0;
+    int cus = 256;
+    std::string err;
+    void *d_buf = nullptr;
+    size_t buf_bytes = 0;
+    Scratch S{};
+    unsigned long long *tile_cnt = nullptr, *tile_bytes = nullptr, *totals = nullptr;
+    int64_t *kept_off = nullptr, *kept_row = nullptr;
+    uint8_t *kept_bytes = nullptr;
+    size_t kept_bytes_cap = 0;
+    void *d_kept = nullptr;
+    int64_t n = 0, n_kept = 0, n_kept_bytes = 0;
+    int64_t counts[4] = {0, 0, 0, 0};
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool have_run = false;
+};
+
+#define DDCHK(h, x)                                                                    \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            (h)->err = std::string("HIP error ") + hipGetErrorString(e_) + " at " #x; \
+            return KW_EHIP;                                                            \
+        }                                                                              \
+    } while (0)
+
+extern "C" int kw_dedup_create(int32_t device, kw_dedup **out)
+{
+    if (!out) return KW_EINVAL;
+    kw_dedup *h = new kw_dedup();
+    *out = h;
+    h->device = device;
+    DDCHK(h, hipSetDevice(device));
+    hipDeviceProp_t prop;
+    DDCHK(h, hipGetDeviceProperties(&prop, device));
+    h->cus = prop.multiProcessorCount;
+    for (auto &e : h->ev) DDCHK(h, hipEventCreate(&e));
+    return KW_OK;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// exact keep-first over the rows that share a hash tag with a different URL
+static int resolve_collisions(kw_dedup *h, const int64_t *d_off, int64_t n, uint8_t *d_code, hipStream_t st)
+{
+    std::vector<uint8_t> code(n);
+    DDCHK(h, hipMemcpyAsync(code.data(), d_code, n, hipMemcpyDeviceToHost, st));
+    DDCHK(h, hipStreamSynchronize(st));
+    std::unordered_set<std::string> seen;
+    std::vector<int64_t> offs(2);
+    std::vector<uint32_t> len(1);
+    for (int64_t i = 0; i < n; ++i) {
+        if (code[i] != CODE_COLLIDE) continue;
+        DDCHK(h, hipMemcpy(offs.data(), d_off + i, 8, hipMemcpyDeviceToHost));
+        DDCHK(h, hipMemcpy(len.data(), h->S.len3 + i, 4, hipMemcpyDeviceToHost));
+        std::string s(len[0], '\0');
+        if (len[0]) DDCHK(h, hipMemcpy(&s[0], h->S.out + obase(offs[0], i), len[0], hipMemcpyDeviceToHost));
+        const uint8_t k = seen.insert(s).second ? (uint8_t)KW_URL_KEPT : (uint8_t)KW_URL_DUPLICATE;
+        DDCHK(h, hipMemcpy(d_code + i, &k, 1, hipMemcpyHostToDevice));
+        ++h->counts[k];
+    }
+    return KW_OK;
+}
+
+extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *d_off, int64_t n, int32_t flags,
+                            uint8_t *d_code, void *stream)
+{
+    if (!h) return KW_EINVAL;
+    if (n < 0 || (n > 0 && (!d_arena || !d_off || !d_code))) { h->err = "kw_dedup_run: bad arguments"; return KW_EINVAL; }
+    if (((uintptr_t)d_arena & 15) != 0) { h->err = "kw_dedup_run: arena must be 16-byte aligned"; return KW_EINVAL; }
+    if (n >= ((int64_t)1 << 32)) { h->err = "kw_dedup_run: more than 2^32 - 1 rows"; return KW_EUNSUPPORTED; }
+    DDCHK(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    h->n = n;
+    h->have_run = true;
+    for (int k = 0; k < 4; ++k) h->counts[k] = 0;
+    h->n_kept = h->n_kept_bytes = 0;
+    if (n == 0) return KW_OK;
+    int64_t arena_end = 0;
+    DDCHK(h, hipMemcpyAsync(&arena_end, d_off + n, 8, hipMemcpyDeviceToHost, st));
+    DDCHK(h, hipStreamSynchronize(st));
+    // ---- scratch (grown on demand)
+    uint64_t tsize = 1024;
+    while (tsize < 2 * (uint64_t)n) tsize <<= 1;
+    const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
+    const size_t need = out_bytes + align256(8 * (size_t)n) * 2 + align256(4 * (size_t)n) + align256(8 * tsize) +
+                        align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
+                        2 * align256(8 * ((size_t)n + 1));
+    if (need > h->buf_bytes) {
+        if (h->d_buf) (void)hipFree(h->d_buf);
+        h->d_buf = nullptr;
+        h->buf_bytes = 0;
+        DDCHK(h, hipMalloc(&h->d_buf, need));
+        h->buf_bytes = need;
+    }
+    uint8_t *p = (uint8_t *)h->d_buf;
+    auto carve = [&](size_t bytes) { uint8_t *r = p; p += align256(bytes); return r; };
+    Scratch &S = h->S;
+    S.out = carve(out_bytes);
+    S.h1 = (uint64_t *)carve(8 * (size_t)n);
+    S.h2 = (uint64_t *)carve(8 * (size_t)n);
+    S.len3 = (uint32_t *)carve(4 * (size_t)n);
+    S.table = (unsigned long long *)carve(8 * tsize);
+    S.mask = tsize - 1;
+    S.cnt = (unsigned long long *)carve(8 * 8);
+    S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
+    S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
+    h->tile_cnt = (unsigned long long *)carve(8 * (size_t)ntiles);
+    h->tile_bytes = (unsigned long long *)carve(8 * (size_t)ntiles);
+    h->totals = (unsigned long long *)carve(16);
+    h->kept_off = (int64_t *)carve(8 * ((size_t)n + 1));
+    h->kept_row = (int64_t *)carve(8 * ((size_t)n + 1));
+    DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
+    DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
+    const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
+    DDCHK(h, hipEventRecord(h->ev[0], st));
+    hipLaunchKernelGGL(dd_transform_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
+    DDCHK(h, hipGetLastError());
+    DDCHK(h, hipEventRecord(h->ev[1], st));
+    hipLaunchKernelGGL(dd_insert_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S);
+    DDCHK(h, hipGetLastError());
+    DDCHK(h, hipEventRecord(h->ev[2], st));
+    hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, n, d_code, S, d_off);
+    DDCHK(h, hipGetLastError());
+    unsigned long long cnt[5];
+    DDCHK(h, hipMemcpyAsync(cnt, S.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    DDCHK(h, hipStreamSynchronize(st));
+    for (int k = 0; k < 4; ++k) h->counts[k] = (int64_t)cnt[k];
+    if (cnt[CODE_COLLIDE]) {
+        int rc = resolve_collisions(h, d_off, n, d_code, st);
+        if (rc) return rc;
+    }
+    DDCHK(h, hipEventRecord(h->ev[3], st));
+    hipLaunchKernelGGL(dd_count_kernel, dim3((unsigned)ntiles), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S,
+                       h->tile_cnt, h->tile_bytes);
+    hipLaunchKernelGGL(dd_scan_tiles_kernel, dim3(1), dim3(1024), 0, st, h->tile_cnt, h->tile_bytes, ntiles, h->totals);
+    hipLaunchKernelGGL(dd_place_kernel, dim3((unsigned)ntiles), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S,
+                       h->tile_cnt, h->tile_bytes, h->kept_off, h->kept_row);
+    DDCHK(h, hipGetLastError());
+    unsigned long long tot[2];
+    DDCHK(h, hipMemcpyAsync(tot, h->totals, sizeof(tot), hipMemcpyDeviceToHost, st));
+    DDCHK(h, hipStreamSynchronize(st));
+    h->n_kept = (int64_t)tot[0];
+    h->n_kept_bytes = (int64_t)tot[1];
+    DDCHK(h, hipMemcpyAsync(h->kept_off + h->n_kept, &h->n_kept_bytes, 8, hipMemcpyHostToDevice, st));
+    if ((size_t)h->n_kept_bytes + 64 > h->kept_bytes_cap) {
+        if (h->d_kept) (void)hipFree(h->d_kept);
+        h->d_kept = nullptr;
+        h->kept_bytes_cap = 0;
+        DDCHK(h, hipMalloc(&h->d_kept, (size_t)h->n_kept_bytes + 64));
+        h->kept_bytes_cap = (size_t)h->n_kept_bytes + 64;
+    }
+    h->kept_bytes = (uint8_t *)h->d_kept;
+    if (h->n_kept > 0) {
+        const int cgrid = (int)std::min<int64_t>((h->n_kept + 63) / 64 * 64 / BLOCK + 1, (int64_t)h->cus * 8);
+        hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, h->n_kept, (const int64_t *)h->kept_off,
+                           (const int64_t *)h->kept_row, d_off, S, h->kept_bytes);
+        DDCHK(h, hipGetLastError());
+    }
+    DDCHK(h, hipEventRecord(h->ev[4], st));
+    DDCHK(h, hipStreamSynchronize(st));
+    return KW_OK;
+}
+
+extern "C" int kw_dedup_counts(kw_dedup *h, int64_t *counts)
+{
+    if (!h || !counts) return KW_EINVAL;
+    if (!h->have_run) { h->err = "kw_dedup_counts: no run"; return KW_ESTATE; }
+    for (int k = 0; k < 4; ++k) counts[k] = h->counts[k];
+    return KW_OK;
+}
+
+extern "C" int kw_dedup_kept_size(kw_dedup *h, int64_t *n_kept, int64_t *n_bytes)
+{
+    if (!h || !n_kept || !n_bytes) return KW_EINVAL;
+    if (!h->have_run) { h->err = "kw_dedup_kept_size: no run"; return KW_ESTATE; }
+    *n_kept = h->n_kept;
+    *n_bytes = h->n_kept_bytes;
+    return KW_OK;
+}
+
+extern "C" int kw_dedup_kept_copy(kw_dedup *h, uint8_t *d_bytes, int64_t *d_off, int64_t *d_rows, void *stream)
+{
+    if (!h) return KW_EINVAL;
+    if (!h->have_run) { h->err = "kw_dedup_kept_copy: no run"; return KW_ESTATE; }
+    DDCHK(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (h->n == 0 || h->n_kept == 0) {
+        if (d_off) DDCHK(h, hipMemsetAsync(d_off, 0, 8, st));
+        return KW_OK;
+    }
+    if (d_bytes && h->n_kept_bytes)
+        DDCHK(h, hipMemcpyAsync(d_bytes, h->kept_bytes, (size_t)h->n_kept_bytes, hipMemcpyDeviceToDevice, st));
+    if (d_off) DDCHK(h, hipMemcpyAsync(d_off, h->kept_off, 8 * ((size_t)h->n_kept + 1), hipMemcpyDeviceToDevice, st));
+    if (d_rows) DDCHK(h, hipMemcpyAsync(d_rows, h->kept_row, 8 * (size_t)h->n_kept, hipMemcpyDeviceToDevice, st));
+    return KW_OK;
+}
+
+extern "C" int kw_dedup_last_ms(kw_dedup *h, float *ms, int32_t k)
+{
+    if (!h || !ms) return KW_EINVAL;
+    if (!h->have_run || h->n == 0) { for (int i = 0; i < k; ++i) ms[i] = 0.f; return KW_OK; }
+    for (int i = 0; i < k && i < 4; ++i) DDCHK(h, hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]));
+    if (k > 4) DDCHK(h, hipEventElapsedTime(&ms[4], h->ev[0], h->ev[4]));
+    return KW_OK;
+}
+
+extern "C" const char *kw_dedup_last_error(kw_dedup *h) { return h ? h->err.c_str() : "null handle"; }
+
+extern "C" int kw_dedup_destroy(kw_dedup *h)
+{
+    if (!h) return KW_OK;
+    (void)hipSetDevice(h->device);
+    if (h->d_buf) (void)hipFree(h->d_buf);
+    if (h->d_kept) (void)hipFree(h->d_kept);
+    for (auto &e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete h;
+    return KW_OK;
+}
+
+namespace {
+__global__ void dd_keep_mask_kernel(const uint8_t *__restrict__ code, int64_t n, uint8_t *__restrict__ mask)
+{
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK)
+        mask[i] = code[i] == KW_URL_KEPT ? 1 : 0;
+}
+}  // namespace
+
+extern "C" int dedup_urls(const uint8_t *d_arena, const int64_t *d_off, int64_t n, uint8_t *d_keep_mask, void *stream)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return KW_EHIP;
+    kw_dedup *h = nullptr;
+    int rc = kw_dedup_create(dev, &h);
+    if (rc == KW_OK) rc = kw_dedup_run(h, d_arena, d_off, n, KW_DEDUP_NORMALIZE, d_keep_mask, stream);
+    if (rc == KW_OK && n > 0) {
+        const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, 4096);
+        hipLaunchKernelGGL(dd_keep_mask_kernel, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream,
+                           (const uint8_t *)d_keep_mask, n, d_keep_mask);
+        if (hipGetLastError() != hipSuccess) rc = KW_EHIP;
+        else if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = KW_EHIP;
+    }
+    kw_dedup_destroy(h);
+    return rc;
+}

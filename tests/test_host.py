@@ -221,8 +221,9 @@ def test_append_to_csv_single_row(tmp_path, monkeypatch):
 
 # ------------------------------------------------------------------ C-ABI boundary
 def _header_functions():
-    hdr = open(os.path.join(os.path.dirname(__file__), '..', 'include', 'kwmatch.h')).read()
-    return sorted(set(re.findall(r'^\s*(?:int|const char \*)\s*\*?(kw_\w+)\s*\(', hdr, re.M)))
+    inc = os.path.join(os.path.dirname(__file__), '..', 'include')
+    hdr = ''.join(open(os.path.join(inc, f)).read() for f in sorted(os.listdir(inc)) if f.endswith('.h'))
+    return sorted(set(re.findall(r'^\s*(?:int|const char \*)\s*\*?(kw_\w+|dedup_urls)\s*\(', hdr, re.M)))
 
 
 def test_library_exports_every_header_symbol():
