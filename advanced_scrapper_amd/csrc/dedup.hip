@@ -104,6 +104,8 @@ struct Scratch {
     unsigned long long *cnt;   // [0..4] per code
     int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
     int normalize;           // KW_DEDUP_NORMALIZE: apply :63-76; else keep-first over the raw strings
+    uint2 *slow;             // rows (index, cut) for the byte-serial rewrite
+    unsigned long long *nslow;
 };
 
 // byte-serial writer of the normalised URL: 8-byte words to the sparse arena + hashes + filter window
@@ -183,135 +185,228 @@ struct Rewrite {
     }
 };
 
+// row bytes from the arena in global memory, or from the wave's LDS copy of its rows
+struct GlobalSrc {
+    const uint8_t *a;
+    __device__ __forceinline__ uint32_t ld32(int64_t p) const { return dd::ld32(a, p); }
+    __device__ __forceinline__ uint64_t ld64(int64_t p) const { return dd::ld64(a, p); }
+};
+struct LdsSrc {
+    const uint32_t *w;   // staged words; byte p of the arena is byte p - base of the stage
+    int64_t base;
+    __device__ __forceinline__ uint32_t ld32(int64_t p) const
+    {
+        const int64_t q = p - base;
+        const int k = (int)(q >> 2);
+        return __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)(q & 3));
+    }
+    __device__ __forceinline__ uint64_t ld64(int64_t p) const
+    {
+        const int64_t q = p - base;
+        const int k = (int)(q >> 2);
+        const uint32_t s = (uint32_t)(q & 3), x0 = w[k], x1 = w[k + 1], x2 = w[k + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s) << 32);
+    }
+};
+
+// finish a row: hashes, length, code
+__device__ __forceinline__ void finish_row(uint64_t h1, uint64_t h2, int64_t len3, bool bad, int64_t i,
+                                           uint8_t *__restrict__ code, const Scratch &S)
+{
+    h1 = fmix(h1 ^ (uint64_t)len3);
+    h2 = fmix(h2 ^ ((uint64_t)len3 * 0x9E3779B97F4A7C15ull));
+    if (S.weak) h1 &= 0xFull;
+    S.h1[i] = h1;
+    S.h2[i] = h2;
+    S.len3[i] = (uint32_t)len3;
+    code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
+}
+
+// the general rewrite of the cut prefix u[0, j), byte by byte (rows with ':80' or a second 'http:')
+__device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j, int64_t i,
+                         uint8_t *__restrict__ code, const Scratch &S)
+{
+    Emit Em;
+    Em.w = 0; Em.win = 0; Em.h1 = 0x243F6A8885A308D3ull; Em.h2 = 0x13198A2E03707344ull;
+    Em.pos = 0; Em.len = 0; Em.nb = 0; Em.bad = false; Em.out = S.out + obase(b, i);
+    Rewrite R;
+    R.P = 0; R.np = 0; R.Q = 0; R.nq = 0;
+    for (int64_t t = 0; t < j; t += 4) {
+        const uint32_t x = ld32(arena, b + t);
+        const int m = (int)(j - t < 4 ? j - t : 4);
+        for (int k = 0; k < m; ++k) R.r_push(Em, (x >> (8 * k)) & 0xFFu);
+    }
+    R.flush(Em);
+    Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
+    Em.finish();
+    finish_row(Em.h1, Em.h2, Em.len, Em.bad, i, code, S);
+}
+
+// one row: returns -1 when done, or the cut j of a row that needs slow_row
+template <class Src>
+__device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int64_t L, int64_t i,
+                                                 uint8_t *__restrict__ code, const Scratch &S, uint8_t *out)
+{
+    if (!S.normalize) {
+        // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
+        uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
+        for (int64_t x0 = 0; x0 < L; x0 += 8) {
+            uint64_t w = src.ld64(b + x0);
+            if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
+            *(uint64_t *)(out + x0) = w;
+            h1 = mix1(h1, w);
+            h2 = mix2(h2, w);
+        }
+        h1 = fmix(h1 ^ (uint64_t)L);
+        h2 = fmix(h2 ^ ((uint64_t)L * 0x9E3779B97F4A7C15ull));
+        if (S.weak) h1 &= 0xFull;
+        S.h1[i] = h1;
+        S.h2[i] = h2;
+        S.len3[i] = (uint32_t)L;
+        code[i] = KW_URL_KEPT;
+        return -1;
+    }
+    // ---- pass 1: the cut j, the first extra ':' and the first 'news/%' | "news/'" end
+    int64_t j = -1, ec = INT64_MAX, kf = INT64_MAX;
+    bool scheme_http = false;
+    for (int64_t t = 0; t < L && j < 0; t += 4) {
+        const uint32_t x = src.ld32(b + t);
+        uint32_t hm = zero_bytes(x ^ 0x68686868u);   // 'h'
+        uint32_t cm = zero_bytes(x ^ 0x3A3A3A3Au);   // ':'
+        uint32_t nm = zero_bytes(x ^ 0x6E6E6E6Eu);   // 'n'
+        while (cm) {
+            const int64_t q = t + (__builtin_ctz(cm) >> 3);
+            cm &= cm - 1;
+            if (q >= L) break;
+            if (((src.ld32(b + q) ^ 0x3Au) & 0xFFu) != 0) continue;   // false positive of zero_bytes
+            // the scheme's colon ("http:" / "https:"), unless it starts a ':80'
+            const bool p80 = q + 3 <= L && (src.ld32(b + q) & 0xFFFFFFu) == 0x30383Au;
+            if (!p80 && q == 4 && src.ld32(b) == 0x70747468u) { scheme_http = true; continue; }
+            if (!p80 && q == 5 && src.ld32(b) == 0x70747468u && (src.ld32(b + 4) & 0xFFFFu) == 0x3A73u) continue;
+            if (q < ec) ec = q;
+        }
+        while (nm) {
+            const int64_t q = t + (__builtin_ctz(nm) >> 3);
+            nm &= nm - 1;
+            if (q + 6 > L || q + 5 >= kf) continue;
+            if (src.ld32(b + q) != NEWS4) continue;
+            const uint32_t y = src.ld32(b + q + 4);
+            if ((y & 0xFF) == '/' && (((y >> 8) & 0xFF) == '%' || ((y >> 8) & 0xFF) == '\'')) kf = q + 5;
+        }
+        while (hm) {
+            const int64_t q = t + (__builtin_ctz(hm) >> 3);
+            hm &= hm - 1;
+            if (q < 1 || q + 4 > L) continue;
+            if (src.ld32(b + q) != HTML4) continue;
+            const uint32_t pv = src.ld32(b + q - 1) & 0xFFu;
+            if (pv == '\n') continue;
+            // the code point before "html" starts at its lead byte
+            int64_t s = q - 1;
+            if (pv >= 0x80) {
+                while (s > 0 && (src.ld32(b + s) & 0xC0u) == 0x80u && q - s < 4) --s;
+            }
+            j = s;
+            break;
+        }
+    }
+    if (j < 0) {
+        code[i] = KW_URL_NO_HTML;
+        S.len3[i] = 0;
+        return -1;
+    }
+    uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
+    int64_t len3;
+    bool bad;
+    if (ec >= j) {
+        // ---- fast path: no ':80' and no 'http:' in the prefix except the scheme's
+        const int ins = (scheme_http && j > 4) ? 1 : 0;
+        const int64_t E = j + ins;
+        len3 = E + 5;
+        bad = kf < j;
+        for (int64_t x0 = 0; x0 < len3; x0 += 8) {
+            uint64_t w = 0;
+            if (x0 < E) {
+                if (!ins) w = src.ld64(b + x0);
+                else if (x0 == 0) w = 0x7370747468ull | (src.ld64(b + 4) << 40);   // "https" + u[4..7)
+                else w = src.ld64(b + x0 - 1);
+            }
+            if (E < x0 + 8) {   // splice ".html" at E, zeros after it
+                if (E >= x0) {
+                    const int sh = (int)(E - x0) * 8;
+                    w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
+                } else {
+                    w = DOTHTML >> ((x0 - E) * 8);
+                }
+            }
+            *(uint64_t *)(out + x0) = w;
+            h1 = mix1(h1, w);
+            h2 = mix2(h2, w);
+        }
+    } else {
+        return j;   // the byte-serial rewrite runs in dd_slow_kernel, off the divergent path
+    }
+    finish_row(h1, h2, len3, bad, i, code, S);
+    return -1;
+}
+
+constexpr int STAGE_BYTES = 8192;   // per-wave LDS copy of the wave's 64 rows
+
+// lane = row; the wave's 64 rows are staged into LDS with coalesced 16-byte loads when they fit
 __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__restrict__ arena,
                                                              const int64_t *__restrict__ off, int64_t n,
                                                              uint8_t *__restrict__ code, Scratch S)
 {
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
-        const int64_t b = off[i], L = off[i + 1] - b;
-        if (!S.normalize) {
-            // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
-            uint8_t *out = S.out + obase(b, i);
-            uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
-            for (int64_t x0 = 0; x0 < L; x0 += 8) {
-                uint64_t w = ld64(arena, b + x0);
-                if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
-                *(uint64_t *)(out + x0) = w;
-                h1 = mix1(h1, w);
-                h2 = mix2(h2, w);
-            }
-            h1 = fmix(h1 ^ (uint64_t)L);
-            h2 = fmix(h2 ^ ((uint64_t)L * 0x9E3779B97F4A7C15ull));
-            if (S.weak) h1 &= 0xFull;
-            S.h1[i] = h1;
-            S.h2[i] = h2;
-            S.len3[i] = (uint32_t)L;
-            code[i] = KW_URL_KEPT;
-            continue;
-        }
-        // ---- pass 1: the cut j, the first extra ':' and the first 'news/%' | "news/'" end
-        int64_t j = -1, ec = INT64_MAX, kf = INT64_MAX;
-        bool scheme_http = false;
-        for (int64_t t = 0; t < L && j < 0; t += 4) {
-            const uint32_t x = ld32(arena, b + t);
-            uint32_t hm = zero_bytes(x ^ 0x68686868u);   // 'h'
-            uint32_t cm = zero_bytes(x ^ 0x3A3A3A3Au);   // ':'
-            uint32_t nm = zero_bytes(x ^ 0x6E6E6E6Eu);   // 'n'
-            while (cm) {
-                const int64_t q = t + (__builtin_ctz(cm) >> 3);
-                cm &= cm - 1;
-                if (q >= L) break;
-                if (((ld32(arena, b + q) ^ 0x3Au) & 0xFFu) != 0) continue;   // false positive of zero_bytes
-                // the scheme's colon ("http:" / "https:"), unless it starts a ':80'
-                const bool p80 = q + 3 <= L && (ld32(arena, b + q) & 0xFFFFFFu) == 0x30383Au;
-                if (!p80 && q == 4 && ld32(arena, b) == 0x70747468u) { scheme_http = true; continue; }
-                if (!p80 && q == 5 && ld32(arena, b) == 0x70747468u && (ld32(arena, b + 4) & 0xFFFFu) == 0x3A73u) continue;
-                if (q < ec) ec = q;
-            }
-            while (nm) {
-                const int64_t q = t + (__builtin_ctz(nm) >> 3);
-                nm &= nm - 1;
-                if (q + 6 > L || q + 5 >= kf) continue;
-                if (ld32(arena, b + q) != NEWS4) continue;
-                const uint32_t y = ld32(arena, b + q + 4);
-                if ((y & 0xFF) == '/' && (((y >> 8) & 0xFF) == '%' || ((y >> 8) & 0xFF) == '\'')) kf = q + 5;
-            }
-            while (hm) {
-                const int64_t q = t + (__builtin_ctz(hm) >> 3);
-                hm &= hm - 1;
-                if (q < 1 || q + 4 > L) continue;
-                if (ld32(arena, b + q) != HTML4) continue;
-                const uint32_t pv = ld32(arena, b + q - 1) & 0xFFu;
-                if (pv == '\n') continue;
-                // the code point before "html" starts at its lead byte
-                int64_t s = q - 1;
-                if (pv >= 0x80) {
-                    while (s > 0 && (ld32(arena, b + s) & 0xC0u) == 0x80u && q - s < 4) --s;
-                }
-                j = s;
-                break;
-            }
-        }
-        if (j < 0) {
-            code[i] = KW_URL_NO_HTML;
-            S.len3[i] = 0;
-            continue;
-        }
-        uint8_t *out = S.out + obase(b, i);
-        uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
-        int64_t len3;
-        bool bad;
-        if (ec >= j) {
-            // ---- fast path: no ':80' and no 'http:' in the prefix except the scheme's
-            const int ins = (scheme_http && j > 4) ? 1 : 0;
-            const int64_t E = j + ins;
-            len3 = E + 5;
-            bad = kf < j;
-            for (int64_t x0 = 0; x0 < len3; x0 += 8) {
-                uint64_t w = 0;
-                if (x0 < E) {
-                    if (!ins) w = ld64(arena, b + x0);
-                    else if (x0 == 0) w = 0x7370747468ull | (ld64(arena, b + 4) << 40);   // "https" + u[4..7)
-                    else w = ld64(arena, b + x0 - 1);
-                }
-                if (E < x0 + 8) {   // splice ".html" at E, zeros after it
-                    if (E >= x0) {
-                        const int sh = (int)(E - x0) * 8;
-                        w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
-                    } else {
-                        w = DOTHTML >> ((x0 - E) * 8);
-                    }
-                }
-                *(uint64_t *)(out + x0) = w;
-                h1 = mix1(h1, w);
-                h2 = mix2(h2, w);
-            }
+    __shared__ uint4 stage_all[(BLOCK / 64) * (STAGE_BYTES / 16)];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    uint4 *stage = stage_all + wib * (STAGE_BYTES / 16);
+    const int64_t n_groups = (n + 63) / 64;
+    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * (BLOCK / 64);
+    for (int64_t g = wave; g < n_groups; g += n_waves) {
+        const int64_t i0 = g * 64, i1 = i0 + 64 < n ? i0 + 64 : n;
+        const int64_t A0 = off[i0], A1 = off[i1];
+        const int64_t base = A0 & ~(int64_t)15;
+        const int64_t nch = (A1 + 16 - base + 15) >> 4;   // chunks to cover [A0, A1 + 16)
+        const int64_t i = i0 + lane;
+        int64_t b = 0, L = 0;
+        if (i < n) { b = off[i]; L = off[i + 1] - b; }
+        int64_t jslow = -1;
+        if (nch * 16 + 16 <= STAGE_BYTES) {
+            __builtin_amdgcn_wave_barrier();
+            for (int64_t c = lane; c < nch; c += 64) stage[c] = *(const uint4 *)(arena + base + 16 * c);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            LdsSrc src{(const uint32_t *)stage, base};
+            if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
         } else {
-            // ---- general rewrite, byte by byte
-            Emit Em;
-            Em.w = 0; Em.win = 0; Em.h1 = h1; Em.h2 = h2; Em.pos = 0; Em.len = 0; Em.nb = 0; Em.bad = false; Em.out = out;
-            Rewrite R;
-            R.P = 0; R.np = 0; R.Q = 0; R.nq = 0;
-            for (int64_t t = 0; t < j; t += 4) {
-                const uint32_t x = ld32(arena, b + t);
-                const int m = (int)(j - t < 4 ? j - t : 4);
-                for (int k = 0; k < m; ++k) R.r_push(Em, (x >> (8 * k)) & 0xFFu);
-            }
-            R.flush(Em);
-            Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
-            Em.finish();
-            h1 = Em.h1;
-            h2 = Em.h2;
-            len3 = Em.len;
-            bad = Em.bad;
+            GlobalSrc src{arena};
+            if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
         }
-        h1 = fmix(h1 ^ (uint64_t)len3);
-        h2 = fmix(h2 ^ ((uint64_t)len3 * 0x9E3779B97F4A7C15ull));
-        if (S.weak) h1 &= 0xFull;
-        S.h1[i] = h1;
-        S.h2[i] = h2;
-        S.len3[i] = (uint32_t)len3;
-        code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
+        // rows for the byte-serial rewrite -> the slow list (one atomic per wave)
+        const uint64_t sm = __ballot(jslow >= 0);
+        if (sm) {
+            unsigned long long at = 0;
+            if (lane == 0) at = atomicAdd(S.nslow, (unsigned long long)__popcll(sm));
+            at = __shfl(at, 0, 64);
+            if (jslow >= 0) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                S.slow[at + r] = make_uint2((uint32_t)i, (uint32_t)jslow);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void dd_slow_kernel(const uint8_t *__restrict__ arena,
+                                                        const int64_t *__restrict__ off, uint8_t *__restrict__ code,
+                                                        Scratch S)
+{
+    const unsigned long long ns = *S.nslow;
+    for (unsigned long long k = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x; k < ns;
+         k += (unsigned long long)gridDim.x * BLOCK) {
+        const uint2 e = S.slow[k];
+        slow_row(arena, off[e.x], (int64_t)e.y, (int64_t)e.x, code, S);
     }
 }
 
@@ -489,7 +584,12 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
     }
 }
 
-// one wave per kept row at a time: lanes copy bytes (coalesced 64-byte stores)
+// dense kept rows: a wave owns kept rows [k0, k0 + 64) whose dense bytes are one contiguous range
+// [D0, D1).  Lane l handles the 8-aligned destination chunks D0 & ~7 + 8 (l + 64 t): a chunk inside
+// one row is one unaligned 8-byte load from the sparse arena and one aligned 8-byte store; a chunk
+// with a row boundary (or a range edge) is written byte by byte from up to 8 rows, whose offsets all
+// lanes fetch with the same shuffles.  The owner row of a byte is the last of the 64 whose dense
+// offset is <= it (binary search over shuffles).
 __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                         const int64_t *__restrict__ kept_row,
                                                         const int64_t *__restrict__ off, Scratch S,
@@ -499,21 +599,53 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
     const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * BLOCK) >> 6;
     for (int64_t k0 = wave * 64; k0 < n_kept; k0 += n_waves * 64) {
-        // lane l prefetches row k0 + l's facts, then the wave walks the 64 rows
         const int64_t kk = k0 + lane;
-        int64_t d0 = 0, src = 0;
-        uint32_t len = 0;
+        const int64_t kend = k0 + 64 < n_kept ? k0 + 64 : n_kept;
+        const int64_t D1 = kept_off[kend];
+        int64_t d0 = D1, src = 0;   // lanes past the end hold the range end
         if (kk < n_kept) {
             const int64_t row = kept_row[kk];
             d0 = kept_off[kk];
             src = obase(off[row], row);
-            len = S.len3[row];
         }
-        const int m = (int)(n_kept - k0 < 64 ? n_kept - k0 : 64);
-        for (int r = 0; r < m; ++r) {
-            const int64_t rd = __shfl(d0, r, 64), rs = __shfl(src, r, 64);
-            const uint32_t rl = (uint32_t)__shfl((int)len, r, 64);
-            for (uint32_t x = (uint32_t)lane; x < rl; x += 64) dst[rd + x] = S.out[rs + x];
+        const int64_t D0 = __shfl(d0, 0, 64);
+        for (int64_t x0 = (D0 & ~(int64_t)7) + 8 * (int64_t)lane; x0 - 8 * (int64_t)lane < D1; x0 += 64 * 8) {
+            const bool live = x0 < D1;
+            const int64_t xs = x0 > D0 ? x0 : D0, xe = x0 + 8 < D1 ? x0 + 8 : D1;
+            int o = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int c = o + step;
+                const int64_t dc = __shfl(d0, c & 63, 64);
+                if (c < 64 && dc <= xs) o = c;
+            }
+            const int64_t od = __shfl(d0, o, 64), os = __shfl(src, o, 64);
+            int64_t nd = __shfl(d0, (o + 1) & 63, 64);
+            if (o == 63) nd = D1;
+            const bool inner = live && xs == x0 && xe == x0 + 8;   // the whole chunk is this group's
+            const bool full = inner && x0 + 8 <= nd;
+            if (full) *(uint64_t *)(dst + x0) = ld64(S.out, os + (x0 - od));
+            const bool edge = live && !full;
+            if (__ballot(edge)) {
+                uint64_t w = 0;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int idx = o + r;
+                    // every lane runs every shuffle (a lane that skips one would not serve its value)
+                    const int64_t sd = __shfl(d0, idx & 63, 64), rs = __shfl(src, idx & 63, 64);
+                    const int64_t sn = __shfl(d0, (idx + 1) & 63, 64);
+                    const int64_t rd = idx < 64 ? sd : D1, rn = idx + 1 < 64 ? sn : D1;
+                    if (edge) {
+                        const int64_t y0 = xs > rd ? xs : rd, y1 = xe < rn ? xe : rn;
+                        for (int64_t y = y0; y < y1; ++y) {
+                            const uint32_t c = S.out[rs + (y - rd)];
+                            if (inner) w |= (uint64_t)c << (8 * (y - x0));
+                            else dst[y] = (uint8_t)c;   // a chunk shared with the neighbouring group
+                        }
+                    }
+                }
+                if (edge && inner) *(uint64_t *)(dst + x0) = w;   // assembled from several rows: one full store
+            }
         }
     }
 }
@@ -609,7 +741,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     while (tsize < 2 * (uint64_t)n) tsize <<= 1;
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
-    const size_t need = out_bytes + align256(8 * (size_t)n) * 2 + align256(4 * (size_t)n) + align256(8 * tsize) +
+    const size_t need = out_bytes + align256(8 * (size_t)n) * 3 + align256(4 * (size_t)n) + align256(8 * tsize) +
                         align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
                         2 * align256(8 * ((size_t)n + 1));
     if (need > h->buf_bytes) {
@@ -629,6 +761,8 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.table = (unsigned long long *)carve(8 * tsize);
     S.mask = tsize - 1;
     S.cnt = (unsigned long long *)carve(8 * 8);
+    S.nslow = S.cnt + 6;
+    S.slow = (uint2 *)carve(8 * (size_t)n);
     S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
     h->tile_cnt = (unsigned long long *)carve(8 * (size_t)ntiles);
@@ -640,7 +774,9 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
     const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
     DDCHK(h, hipEventRecord(h->ev[0], st));
-    hipLaunchKernelGGL(dd_transform_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
+    const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 8);
+    hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
+    hipLaunchKernelGGL(dd_slow_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
     DDCHK(h, hipGetLastError());
     DDCHK(h, hipEventRecord(h->ev[1], st));
     hipLaunchKernelGGL(dd_insert_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S);

@@ -44,7 +44,12 @@ def main():
     ap.add_argument('--gather-hits', action='store_true', help='also time the RCCL all-gather of hit records')
     ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'traffic_r01.json'),
                     help='per-launch HBM bytes from the rocprofv3 PMC passes (profiles/pmc_traffic.py)')
+    ap.add_argument('--workload', choices=('match', 'dedup'), default='match',
+                    help='match = BASELINE.json metric (config 2/3); dedup = CDX URL dedup (config 5)')
+    ap.add_argument('--rows-per-gpu', type=int, default=200_000_000, help='dedup: CDX rows per GPU')
     args = ap.parse_args()
+    if args.workload == 'dedup':
+        return bench_dedup(args)
 
     import torch
     from advanced_scrapper_amd import dist, synth
@@ -158,6 +163,98 @@ def main():
         'hits_allgather_ms': None if gather_ms is None else round(gather_ms, 3),
     }
     print(json.dumps(out), flush=True)
+
+
+def bench_dedup(args):
+    """Config 5: CDX link-row normalise + keep-first dedup (yahoo_links_selenium.py:59-82,160-179).
+
+    One step = one kw_dedup_run over the rank's rows (resident in HBM): rewrite +
+    hash, table insert, rep compare, dense kept rows.  value = (URL bytes + 8 B
+    per offset) of all ranks / step time."""
+    import torch
+    from advanced_scrapper_amd import dist, synth
+    from advanced_scrapper_amd.cdx_dedup import GpuUrlDedup
+    rank, world, local = dist.init('nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    n = args.rows_per_gpu
+    t_gen = time.perf_counter()
+    rows = synth.generate_urls(n, seed=args.seed, row_base=rank * n, n_articles=int(1.31 * n * world))
+    t_gen = time.perf_counter() - t_gen
+    g = GpuUrlDedup(local)
+    d_a, d_o = g.upload(rows.arena, rows.off)
+    torch.cuda.synchronize()
+    local_bytes = rows.n_bytes + 8 * rows.n
+    for _ in range(args.warmup):
+        g.run(d_a, d_o, rows.n)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    kt = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.run(d_a, d_o, rows.n)
+        kt.append(g.last_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    nb = torch.tensor([float(local_bytes)], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(nb, op=torch.distributed.ReduceOp.SUM)
+    elapsed = float(el.item())
+    counts = g.counts()
+    if rank != 0:
+        return
+    k = np.mean(np.asarray(kt), axis=0)
+    names = ('transform_hash', 'insert', 'decide', 'compact', 'total')
+    kms = {a: round(float(b), 4) for a, b in zip(names, k)}
+    transform_gbs = rows.n_bytes / (kms['transform_hash'] * 1e-3) / 1e9
+    cpu = None
+    if world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline_dedup(rows, min(n, 2_000_000))
+    out = {
+        'metric': 'CDX URL dedup GB/s (URL bytes + 8 B offsets), bit-exact vs pandas drop_duplicates keep-first',
+        'value': round(float(nb.item()) / (elapsed / args.steps) / 1e9, 2), 'unit': 'GB/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
+        'data': 'synthetic CDX rows (csrc/synth.c generate_urls, ~30 % repeated articles)',
+        'config': {'workload': f'config 5: CDX link-row normalise + keep-first dedup, {n} rows per GPU',
+                   'rows_per_gpu': n, 'bytes_per_gpu': local_bytes, 'kept': counts[1],
+                   'dropped_no_html': counts[0], 'dropped_filter': counts[2], 'duplicates': counts[3],
+                   'parallelism': 'replicas only (one independent keep-first per GPU)' if world > 1 else 'single GPU'},
+        'roofline': {'bound': 'hbm', 'achieved': round(transform_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(transform_gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'algorithmic_bytes_per_launch': rows.n_bytes, 'kernel': 'dd::dd_transform_kernel',
+                     'kernel_ms_avg': kms['transform_hash'], 'kernels_ms_avg': kms},
+        'cpu_baseline': cpu,
+        'host': {'generate_s': round(t_gen, 2)},
+    }
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_dedup(rows, n_sample: int):
+    """The reference's pandas steps (:63-79 + the :174 keep-first) on the first n_sample rows, one process."""
+    import pandas as pd
+    urls = [rows.url(i) for i in range(n_sample)]
+    nbytes = int(rows.off[n_sample] - rows.off[0]) + 8 * n_sample
+    df = pd.DataFrame({'date_time': rows.ts[:n_sample], 'url': urls})
+    t = time.perf_counter()
+    df = df[df['url'].str.contains('.html')]
+    df['url'] = df['url'].str.split('.html').str[0] + '.html'
+    df['url'] = df['url'].str.replace(':80', '', regex=False)
+    df['url'] = df['url'].str.replace('http:', 'https:', regex=False)
+    df = df[~df['url'].str.contains('news/%')]
+    df = df[~df['url'].str.contains("news/'")]
+    df = df.drop_duplicates(subset=['url'])
+    secs = time.perf_counter() - t
+    return {'value': round(nbytes / secs / 1e9, 6), 'unit': 'GB/s', 'cores': 1, 'kind': 'port',
+            'sample': f'first {n_sample} rows ({nbytes} bytes incl. offsets), the reference\'s pandas calls '
+                      f'(yahoo_links_selenium.py:63-79), one process, {secs:.2f} s', 'kept': int(len(df))}
 
 
 def pmc_traffic(path: str, kernel: str, docs: int, seed: int):
