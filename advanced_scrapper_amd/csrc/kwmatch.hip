@@ -21,6 +21,30 @@
 
 using namespace kw;
 
+// Scratch sizes of one launch configuration (every field only grows over a handle's life).
+struct ScratchCaps {
+    int nk = 0, nr = 0, ng = 0;            // scan, resolve and generic waves (task waves = nk)
+    uint32_t item_cap = 0, out_cap = 0;    // per scan wave items, per wave result records
+    int64_t hdr_cap = 0;                   // documents
+    uint32_t defer_cap = 0, rx_cap = 0;
+    uint32_t vcap = 0, ecap = 0, scap = 0, xcap = 0;   // per scan wave task regions
+    uint64_t dsize = 0;                    // decided-set slots (power of two)
+    bool covers(const ScratchCaps &o) const
+    {
+        return nk >= o.nk && nr >= o.nr && ng >= o.ng && item_cap >= o.item_cap && out_cap >= o.out_cap &&
+               hdr_cap >= o.hdr_cap && defer_cap >= o.defer_cap && rx_cap >= o.rx_cap && vcap >= o.vcap &&
+               ecap >= o.ecap && scap >= o.scap && xcap >= o.xcap && dsize >= o.dsize;
+    }
+    void grow(const ScratchCaps &o)
+    {
+        nk = std::max(nk, o.nk); nr = std::max(nr, o.nr); ng = std::max(ng, o.ng);
+        item_cap = std::max(item_cap, o.item_cap); out_cap = std::max(out_cap, o.out_cap);
+        hdr_cap = std::max(hdr_cap, o.hdr_cap); defer_cap = std::max(defer_cap, o.defer_cap);
+        rx_cap = std::max(rx_cap, o.rx_cap); vcap = std::max(vcap, o.vcap); ecap = std::max(ecap, o.ecap);
+        scap = std::max(scap, o.scap); xcap = std::max(xcap, o.xcap); dsize = std::max(dsize, o.dsize);
+    }
+};
+
 struct kw_handle {
     int device = 0;
     DevTables T{};
@@ -56,6 +80,9 @@ struct kw_handle {
     FastScratch FS{};
     int nk = 0, nr = 0, ng = 0;
     uint32_t defer_cap = 0, item_cap = 0, rx_cap = 0;
+    ScratchCaps caps;
+    uint32_t *out_cnt_all = nullptr;   // counts of every result region (scan, task, resolve, generic)
+    kw_hit *out_all = nullptr;
     int64_t hdr_cap = 0;
     int items_blocks_per_cu = 1, resolve_blocks_per_cu = 1;
     int n_anchor_fast = 0;
@@ -524,7 +551,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
             if (m > 255) return fail(KW_EUNSUPPORTED, "kw_compile: uppercase name longer than 255 code points");
         }
         if (bl > 65535) return fail(KW_EUNSUPPORTED, "kw_compile: name longer than 65535 bytes");
-        uint32_t pi = (fuzzy ? PI_FUZZY : 0u) | (m << 8) | ((uint32_t)bl << 16);
+        uint32_t pi = (fuzzy ? PI_FUZZY : 0u) | (m << 8) | ((uint32_t)bl << 16) | (bl == m ? PI_ASCII : 0u);
         if (!fuzzy) {
             if (is_word_h(word_bitmap, cps[i].front())) pi |= PI_WORD_FIRST;
             if (is_word_h(word_bitmap, cps[i].back())) pi |= PI_WORD_LAST;
@@ -886,22 +913,13 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     return KW_OK;
 }
 
-// (re)allocate scratch for nk scan waves (item_cap items each), nr resolve waves, ng generic
-// waves (out_cap records per resolve/generic wave), n_docs headers and a defer list of dcap docs
-static int ensure_scratch(kw_handle *h, int nk, int nr, int ng, uint32_t item_cap, uint32_t out_cap, int64_t n_docs,
-                          uint32_t dcap, uint32_t rx_cap)
+// (re)allocate scratch.  Result regions, in order: scan waves [0, nk), task waves [nk, 2 nk),
+// resolve waves [2 nk, 2 nk + nr), generic waves after them (one count array, one gather).
+static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
 {
-    if (h->d_scratch && nk <= h->nk && nr <= h->nr && ng <= h->ng && item_cap <= h->item_cap &&
-        out_cap <= h->out_cap && n_docs <= h->hdr_cap && dcap <= h->defer_cap && rx_cap <= h->rx_cap)
-        return KW_OK;
-    rx_cap = std::max(rx_cap, h->rx_cap);
-    nk = std::max(nk, h->nk);
-    nr = std::max(nr, h->nr);
-    ng = std::max(ng, h->ng);
-    item_cap = std::max(item_cap, h->item_cap);
-    out_cap = std::max(out_cap, h->out_cap);
-    n_docs = std::max(n_docs, h->hdr_cap);
-    dcap = std::max(dcap, h->defer_cap);
+    if (h->d_scratch && h->caps.covers(want)) return KW_OK;
+    ScratchCaps c = h->caps;
+    c.grow(want);
     if (h->d_scratch) { (void)hipFree(h->d_scratch); h->d_scratch = nullptr; }
     if (h->d_small) { (void)hipFree(h->d_small); h->d_small = nullptr; }
     if (h->d_hits) { (void)hipFree(h->d_hits); h->d_hits = nullptr; }
@@ -909,52 +927,77 @@ static int ensure_scratch(kw_handle *h, int nk, int nr, int ng, uint32_t item_ca
     const size_t per_cps = (size_t)CP_CAP * sizeof(uint32_t);
     const size_t per_blk = (size_t)(CP_CAP / 16 + 2) * sizeof(uint32_t);
     const size_t per_fcps = (size_t)FK_CP_CAP * sizeof(uint32_t);
-    const size_t per_out = (size_t)out_cap * sizeof(kw_hit);
-    const int nw = nr + ng;   // result regions: resolve [0, nr), generic [nr, nr + ng)
-    size_t total = (size_t)ng * (per_items + per_cps + per_blk) + (size_t)nr * (per_fcps + per_blk) +
-                   (size_t)nw * per_out + (size_t)nk * item_cap * 8 + (size_t)n_docs * 8 + (size_t)dcap * 4 +
-                   (size_t)nr * rx_cap * 16 + 16 * 256;
+    const size_t per_out = (size_t)c.out_cap * sizeof(kw_hit);
+    const size_t nw = (size_t)2 * c.nk + c.nr + c.ng;
+    const size_t per_tasks = (size_t)(c.vcap + c.ecap + c.scap + c.xcap) * 16;
+    size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_blk) +
+                   nw * per_out + (size_t)c.nk * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 4 +
+                   (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
+                   32 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
     uint8_t *p = (uint8_t *)h->d_scratch;
     auto carve = [&](size_t bytes) { uint8_t *r = p; p += (bytes + 255) & ~(size_t)255; return r; };
-    h->S.items = (uint64_t *)carve((size_t)ng * per_items);
-    h->S.cps = (uint32_t *)carve((size_t)ng * per_cps);
-    h->S.blkcnt = (uint32_t *)carve((size_t)ng * per_blk);
-    h->FS.cps = (uint32_t *)carve((size_t)nr * per_fcps);
-    h->FS.cpbase = (uint32_t *)carve((size_t)nr * per_blk);
-    kw_hit *outs = (kw_hit *)carve((size_t)nw * per_out);
-    h->FS.items = (uint64_t *)carve((size_t)nk * item_cap * 8);
-    h->FS.hdr = (uint2 *)carve((size_t)n_docs * 8);
-    h->FS.defer_list = (uint32_t *)carve((size_t)dcap * 4);
-    h->FS.rx_tasks = (uint4 *)carve((size_t)nr * rx_cap * 16);
-    h->FS.rx_cap = rx_cap;
-    h->rx_cap = rx_cap;
-    size_t small = 1024 + (size_t)nw * 4 + 256 + (size_t)(nw + 1) * 8 + 256;
+    h->S.items = (uint64_t *)carve((size_t)c.ng * per_items);
+    h->S.cps = (uint32_t *)carve((size_t)c.ng * per_cps);
+    h->S.blkcnt = (uint32_t *)carve((size_t)c.ng * per_blk);
+    h->FS.cps = (uint32_t *)carve((size_t)c.nr * per_fcps);
+    h->FS.cpbase = (uint32_t *)carve((size_t)c.nr * per_blk);
+    kw_hit *outs = (kw_hit *)carve(nw * per_out);
+    h->FS.items = (uint64_t *)carve((size_t)c.nk * c.item_cap * 8);
+    h->FS.hdr = (uint2 *)carve((size_t)c.hdr_cap * 8);
+    h->FS.defer_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
+    h->FS.rx_tasks = (uint4 *)carve((size_t)c.nr * c.rx_cap * 16);
+    h->FS.rx_cap = c.rx_cap;
+    h->FS.vq = (uint4 *)carve((size_t)c.nk * c.vcap * 16);
+    h->FS.eq = (uint4 *)carve((size_t)c.nk * c.ecap * 16);
+    h->FS.sq = (uint4 *)carve((size_t)c.nk * c.scap * 16);
+    h->FS.xq = (uint4 *)carve((size_t)c.nk * c.xcap * 16);
+    h->FS.vcap = c.vcap;
+    h->FS.ecap = c.ecap;
+    h->FS.scap = c.scap;
+    h->FS.xcap = c.xcap;
+    uint32_t *tcnt = (uint32_t *)carve((size_t)c.nk * 16);
+    h->FS.vcnt = tcnt;
+    h->FS.ecnt = tcnt + c.nk;
+    h->FS.scnt = tcnt + 2 * (size_t)c.nk;
+    h->FS.xcnt = tcnt + 3 * (size_t)c.nk;
+    h->FS.dset = (unsigned long long *)carve(c.dsize * 8);
+    h->FS.dmask = c.dsize - 1;
+    size_t small = 1024 + nw * 4 + 256 + (nw + 1) * 8 + 256;
     HIPCHK(h, hipMalloc(&h->d_small, small));
     uint8_t *q = (uint8_t *)h->d_small;
     h->S.status = (uint32_t *)q;                        // 4 x u32
     h->FS.status = h->S.status;
     h->FS.defer_cnt = (uint32_t *)(q + 16);
+    h->FS.tmax = (uint32_t *)(q + 32);                  // 4 x u32
     h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
     h->FS.stats = (unsigned long long *)(q + 128);      // 16 x u64 (fast path)
     uint32_t *cnts = (uint32_t *)(q + 1024);
-    h->FS.out_cnt = cnts;
-    h->S.out_cnt = cnts + nr;
-    h->d_offs = (unsigned long long *)(q + 1024 + (((size_t)nw * 4 + 255) & ~(size_t)255));
-    h->FS.out = outs;
-    h->S.out = outs + (size_t)nr * out_cap;
-    h->S.out_cap = out_cap;
-    h->FS.out_cap = out_cap;
-    h->FS.item_cap = item_cap;
-    h->FS.defer_cap = dcap;
-    h->nk = nk;
-    h->nr = nr;
-    h->ng = ng;
-    h->item_cap = item_cap;
-    h->out_cap = out_cap;
-    h->hdr_cap = n_docs;
-    h->defer_cap = dcap;
-    h->hits_cap = (size_t)nw * out_cap;
+    h->out_cnt_all = cnts;
+    h->FS.kout_cnt = cnts;
+    h->FS.tout_cnt = cnts + c.nk;
+    h->FS.out_cnt = cnts + 2 * (size_t)c.nk;
+    h->S.out_cnt = cnts + 2 * (size_t)c.nk + c.nr;
+    h->d_offs = (unsigned long long *)(q + 1024 + ((nw * 4 + 255) & ~(size_t)255));
+    h->out_all = outs;
+    h->FS.kout = outs;
+    h->FS.tout = outs + (size_t)c.nk * c.out_cap;
+    h->FS.out = outs + (size_t)2 * c.nk * c.out_cap;
+    h->S.out = outs + ((size_t)2 * c.nk + c.nr) * c.out_cap;
+    h->S.out_cap = c.out_cap;
+    h->FS.out_cap = c.out_cap;
+    h->FS.item_cap = c.item_cap;
+    h->FS.defer_cap = c.defer_cap;
+    h->caps = c;
+    h->nk = c.nk;
+    h->nr = c.nr;
+    h->ng = c.ng;
+    h->item_cap = c.item_cap;
+    h->out_cap = c.out_cap;
+    h->hdr_cap = c.hdr_cap;
+    h->defer_cap = c.defer_cap;
+    h->rx_cap = c.rx_cap;
+    h->hits_cap = nw * c.out_cap;
     HIPCHK(h, hipMalloc(&h->d_hits, h->hits_cap * sizeof(kw_hit) + 16));
     h->scratch_bytes = total;
     return KW_OK;
@@ -970,27 +1013,46 @@ static int launch_scan(kw_handle *h)
                                      (int64_t)h->cus * h->resolve_blocks_per_cu);
     if (nrb < 1) nrb = 1;
     const int ngb = std::max(1, std::min(h->cus, (int)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)));
-    const int nk = nkb * FK_WAVES, nr = nrb * RK_WAVES, ng = ngb * WAVES_PER_BLOCK;
-    const int64_t docs_per_k = (n_docs + nk - 1) / nk;
-    const uint32_t want_items = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_k * 40), (int64_t)1 << 24);
-    const int64_t docs_per_r = (n_docs + nr - 1) / nr;
-    const uint32_t want_out = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_r * 48), (int64_t)1 << 26);
-    uint32_t want_rx = (uint32_t)std::min<int64_t>(docs_per_r * 2 + 64, (int64_t)1 << 20);
-    if (const char *e = getenv("KW_TEST_RX_CAP")) want_rx = (uint32_t)std::max(1, atoi(e));   // tests: force the rescan
-    int rc = ensure_scratch(h, nk, nr, ng, std::max(want_items, h->item_cap), std::max(want_out, h->out_cap),
-                            std::max<int64_t>(n_docs, 1), (uint32_t)std::max<int64_t>(n_docs, 1), want_rx);
+    ScratchCaps w;
+    w.nk = nkb * FK_WAVES;
+    w.nr = nrb * RK_WAVES;
+    w.ng = ngb * WAVES_PER_BLOCK;
+    const int64_t docs_per_k = (n_docs + w.nk - 1) / w.nk;
+    w.item_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_k * 40), (int64_t)1 << 24);
+    const int64_t docs_per_r = (n_docs + w.nr - 1) / w.nr;
+    w.out_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, std::max(docs_per_r, docs_per_k) * 48),
+                                            (int64_t)1 << 26);
+    w.rx_cap = (uint32_t)std::min<int64_t>(docs_per_r * 2 + 64, (int64_t)1 << 20);
+    if (const char *e = getenv("KW_TEST_RX_CAP")) w.rx_cap = (uint32_t)std::max(1, atoi(e));   // tests: force the rescan
+    w.hdr_cap = std::max<int64_t>(n_docs, 1);
+    w.defer_cap = (uint32_t)std::max<int64_t>(n_docs, 1);
+    w.vcap = (uint32_t)std::min<int64_t>(docs_per_k * 8 + 256, (int64_t)1 << 24);
+    w.ecap = (uint32_t)std::min<int64_t>(docs_per_k * 2 + 16, (int64_t)1 << 24);
+    w.scap = w.ecap;
+    w.xcap = (uint32_t)std::min<int64_t>(docs_per_k * 4 + 64, (int64_t)1 << 24);
+    if (const char *e = getenv("KW_TEST_TASK_CAP")) w.vcap = w.ecap = w.scap = w.xcap = (uint32_t)std::max(1, atoi(e));
+    w.dsize = 4096;
+    while (w.dsize < (uint64_t)std::max<int64_t>(n_docs, 1) * 16) w.dsize <<= 1;
+    if (const char *e = getenv("KW_TEST_DSET_SIZE")) w.dsize = std::max<uint64_t>(2, (uint64_t)atoll(e));
+    int rc = ensure_scratch(h, w);
     if (rc) return rc;
+    const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
     HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
-    // every region's count (regions of waves this launch does not start stay empty)
-    HIPCHK(h, hipMemsetAsync(h->FS.out_cnt, 0, (size_t)(h->nr + h->ng) * 4, st));
+    HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
+    HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
+    HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
     HIPCHK(h, hipEventRecord(h->ev0, st));
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_items_kernel, dim3(nkb), dim3(FK_BLOCK), kItemsLds, st, h->FT, h->T, h->arena,
-                           h->doc_off, n_docs, h->FS);
+                           h->doc_off, n_docs, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
+        const int ntb = (nkb * FK_WAVES + RK_WAVES - 1) / RK_WAVES;
+        hipLaunchKernelGGL(kw_task_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+                           nkb * FK_WAVES, h->FS, h->S);
+        HIPCHK(h, hipGetLastError());
         hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
                            n_docs, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
@@ -1004,10 +1066,10 @@ static int launch_scan(kw_handle *h)
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->evg, st));
-    const int nw = h->nr + h->ng;   // all regions: resolve [0, h->nr), generic [h->nr, h->nr + h->ng)
+    const int nw = 2 * nk + h->nr + h->ng;
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->FS.out_cnt, nw, h->out_cap, h->d_offs);
-        hipLaunchKernelGGL(kw_gather_kernel, dim3(nw), dim3(256), 0, st, h->FS.out, h->out_cap, h->FS.out_cnt,
+        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->out_cnt_all, nw, h->out_cap, h->d_offs);
+        hipLaunchKernelGGL(kw_gather_kernel, dim3(nw), dim3(256), 0, st, h->out_all, h->out_cap, h->out_cnt_all,
                            h->d_offs, h->d_hits);
         HIPCHK(h, hipGetLastError());
     }
@@ -1035,7 +1097,7 @@ static int finish(kw_handle *h)
 {
     if (!h->scanned) { h->err = "kw_hits: no scan"; return KW_ESTATE; }
     if (h->fetched) return KW_OK;
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    for (int attempt = 0; attempt < 6; ++attempt) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
         uint32_t status[4];
         HIPCHK(h, hipMemcpy(status, h->S.status, sizeof(status), hipMemcpyDeviceToHost));
@@ -1049,15 +1111,27 @@ static int finish(kw_handle *h)
             h->err = buf;
             return KW_EOVERFLOW;
         }
-        if (status[0] & (ST_OUT_OVERFLOW | ST_RX_OVERFLOW)) {
-            // grow the per-wave result regions to the largest count seen (and the regex queues) and rescan
-            std::vector<uint32_t> cnt(h->launched_waves);
-            HIPCHK(h, hipMemcpy(cnt.data(), h->FS.out_cnt, cnt.size() * 4, hipMemcpyDeviceToHost));
-            uint32_t mx = 0;
-            for (uint32_t c : cnt) mx = std::max(mx, c);
-            const uint32_t out_cap = (status[0] & ST_OUT_OVERFLOW) ? mx + 1024 : h->out_cap;
-            const uint32_t rx_cap = (status[0] & ST_RX_OVERFLOW) ? std::max(status[2], h->rx_cap * 2) : h->rx_cap;
-            int rc = ensure_scratch(h, h->nk, h->nr, h->ng, h->item_cap, out_cap, h->hdr_cap, h->defer_cap, rx_cap);
+        if (status[0] & (ST_OUT_OVERFLOW | ST_RX_OVERFLOW | ST_TASK_OVERFLOW | ST_DSET_FULL)) {
+            // grow what overflowed (result regions to the largest count seen, queues to the largest need) and rescan
+            ScratchCaps w = h->caps;
+            if (status[0] & ST_OUT_OVERFLOW) {
+                std::vector<uint32_t> cnt(h->launched_waves);
+                HIPCHK(h, hipMemcpy(cnt.data(), h->out_cnt_all, cnt.size() * 4, hipMemcpyDeviceToHost));
+                uint32_t mx = 0;
+                for (uint32_t c : cnt) mx = std::max(mx, c);
+                w.out_cap = std::max(w.out_cap, mx + 1024);
+            }
+            if (status[0] & ST_RX_OVERFLOW) w.rx_cap = std::max(status[2], w.rx_cap * 2);
+            if (status[0] & ST_TASK_OVERFLOW) {
+                uint32_t tm[4];
+                HIPCHK(h, hipMemcpy(tm, h->FS.tmax, sizeof(tm), hipMemcpyDeviceToHost));
+                w.vcap = std::max(w.vcap, tm[0]);
+                w.ecap = std::max(w.ecap, tm[1]);
+                w.scap = std::max(w.scap, tm[2]);
+                w.xcap = std::max(w.xcap, tm[3]);
+            }
+            if (status[0] & ST_DSET_FULL) w.dsize *= 4;
+            int rc = ensure_scratch(h, w);
             if (rc) return rc;
             rc = launch_scan(h);
             if (rc) return rc;

@@ -42,6 +42,7 @@ constexpr uint32_t PI_FUZZY = 1u;        // class F (else U)
 constexpr uint32_t PI_LITERAL = 2u;      // F: re.finditer(name) == literal search
 constexpr uint32_t PI_WORD_FIRST = 4u;   // U: first code point is a \b word char
 constexpr uint32_t PI_WORD_LAST = 8u;    // U: last code point is a \b word char
+constexpr uint32_t PI_ASCII = 16u;       // every code point < 128 (bytes = code points)
 // m (code points) in bits [15:8], byte length in bits [31:16]
 __host__ __device__ inline uint32_t pi_m(uint32_t pi) { return (pi >> 8) & 0xFF; }
 __host__ __device__ inline uint32_t pi_blen(uint32_t pi) { return pi >> 16; }
@@ -101,5 +102,7 @@ constexpr uint32_t ST_OUT_OVERFLOW = 2u;
 constexpr uint32_t ST_CP_OVERFLOW = 4u;
 constexpr uint32_t ST_FIELD_TOO_LONG = 8u;
 constexpr uint32_t ST_RX_OVERFLOW = 16u;     // a resolve wave queued more regex searches than rx_cap
+constexpr uint32_t ST_TASK_OVERFLOW = 32u;   // a scan wave made more tasks than a task region holds
+constexpr uint32_t ST_DSET_FULL = 64u;       // the decided-name set is full
 
 }  // namespace kw

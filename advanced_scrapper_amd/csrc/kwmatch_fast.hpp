@@ -142,6 +142,17 @@ struct FastScratch {
     unsigned long long *stats;  // see kw_stats
     uint4 *rx_tasks;            // per resolve wave: rx_cap regex-position tasks (doc, field|ascii, pattern, n)
     uint32_t rx_cap;
+    // flat resolve of all-ASCII documents (scan epilogue -> task kernel)
+    kw_hit *kout;               // per scan wave: out_cap records (hits the scan epilogue emits)
+    uint32_t *kout_cnt;
+    kw_hit *tout;               // per task wave: out_cap records
+    uint32_t *tout_cnt;
+    uint4 *vq, *eq, *sq, *xq;   // per scan wave: verify / edge / short / regex task regions
+    uint32_t vcap, ecap, scap, xcap;
+    uint32_t *vcnt, *ecnt, *scnt, *xcnt;   // per scan wave
+    uint32_t *tmax;             // [4] largest task count a wave needed (rescan sizing)
+    unsigned long long *dset;   // decided (doc, field, pattern) set: open addressing, 0 = empty
+    unsigned long long dmask;
 };
 
 // host + device hashes of the LDS tables

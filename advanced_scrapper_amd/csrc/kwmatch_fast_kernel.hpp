@@ -17,6 +17,10 @@
 #ifndef FK_STAGE
 #define FK_STAGE 3
 #endif
+// profiling builds: task phases to skip (1 verify, 2 edge, 4 short, 8 regex)
+#ifndef TK_SKIP
+#define TK_SKIP 0
+#endif
 // profiling builds: stage-2 filter and ring without the anchor-table probe
 #ifndef FK_NOPROBE
 #define FK_NOPROBE 0
@@ -207,6 +211,85 @@ __device__ bool field_is_ascii(const uint8_t *__restrict__ arena, int64_t fb, in
     bool hi = false;
     for (int64_t i = fb + lane; i < fe; i += WAVE) hi |= arena[i] >= 0x80;
     return __ballot(hi) == 0;
+}
+
+// Decode a non-ASCII field into code points, 16 bytes per lane per step (coalesced), with the
+// cumulative lead-byte count at every 64-byte block of the arena from base = fb & ~15 (blkcnt[k] =
+// code points of the field before base + 64 k).  Returns the field's code points.
+__device__ uint32_t decode_field_fast(const uint8_t *__restrict__ a, int64_t fb, int64_t fe, uint32_t *cps,
+                                      uint32_t *blkcnt, uint32_t cap)
+{
+    const int lane = lane_id();
+    const int64_t base = fb & ~(int64_t)15;
+    uint32_t count = 0;
+    for (int64_t blk = base; blk < fe; blk += 1024) {
+        const int64_t lp = blk + 16 * (int64_t)lane;
+        uint32_t W[5];
+        if (lp < fe) {
+            const uint4 v = *(const uint4 *)(a + lp);
+            W[0] = v.x; W[1] = v.y; W[2] = v.z; W[3] = v.w;
+        } else {
+            W[0] = W[1] = W[2] = W[3] = 0;
+        }
+        W[4] = (uint32_t)__shfl_down((int)W[0], 1, WAVE);
+        if (lane == WAVE - 1) W[4] = (blk + 1024 < fe) ? *(const uint32_t *)(a + blk + 1024) : 0u;
+        const int64_t r0 = fb - lp, r2 = fe - lp;
+        const int jlo = r0 <= 0 ? 0 : (r0 >= 16 ? 16 : (int)r0);
+        const int jhi = r2 <= 0 ? 0 : (r2 >= 16 ? 16 : (int)r2);
+        const uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
+        uint32_t lead = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t b = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            lead |= (uint32_t)((b & 0xC0u) != 0x80u) << j;
+        }
+        lead &= valid;
+        int total;
+        const int ex = wave_excl_scan(__popc(lead), &total);
+        if ((lane & 3) == 0) blkcnt[(lp - base) >> 6] = count + (uint32_t)ex;
+        uint32_t idx = count + (uint32_t)ex;
+        uint32_t lm = lead;
+        while (lm) {
+            const int j = __ffs(lm) - 1;
+            lm &= lm - 1;
+            // bytes j.. of this chunk, continuing into the next lane's first word
+            const uint32_t b0 = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            uint32_t c = b0;
+            if (b0 >= 0x80u) {
+                const uint32_t n = (b0 >= 0xF0u) ? 4u : (b0 >= 0xE0u) ? 3u : 2u;
+                c = b0 & (0x7Fu >> n);
+                for (uint32_t k = 1; k < n; ++k) {
+                    const int jj = j + (int)k;
+                    const uint32_t bk = (lp + jj < fe) ? ((W[jj >> 2] >> (8 * (jj & 3))) & 0xFFu) : 0x80u;
+                    c = (c << 6) | (bk & 0x3Fu);
+                }
+            }
+            if (idx < cap) cps[idx] = c;
+            ++idx;
+        }
+        count += (uint32_t)total;
+    }
+    wave_sync_global();
+    return count;
+}
+
+// code point offset of field byte bpos (non-ASCII fields decoded by decode_field_fast)
+__device__ __forceinline__ uint32_t to_cp_fast(const FieldCtx &F, uint32_t bpos)
+{
+    if (F.ascii) return bpos;
+    const int64_t base = F.fb & ~(int64_t)15, p = F.fb + bpos;
+    const int64_t b64 = (p - base) & ~(int64_t)63;
+    uint32_t c = F.blkcnt[b64 >> 6];
+    // leads in [max(base + b64, fb), p)
+    for (int64_t q = base + b64; q < p; q += 4) {
+        const uint32_t w = *(const uint32_t *)(F.arena + q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t y = q + k;
+            if (y >= F.fb && y < p) c += (((w >> (8 * k)) & 0xC0u) != 0x80u);
+        }
+    }
+    return c;
 }
 
 // text code point i of the field (ASCII: byte; else decoded scratch)
@@ -572,6 +655,99 @@ __device__ __forceinline__ void fk_regex_enqueue(const DevScratch &GS, const Fie
     ++Q.n;
 }
 
+// Short field (n <= 64 code points): the field is the needle, the fuzzy names at least as long as
+// the field are the haystacks (exact-substring table for n <= 10, signatures + LCS above).
+// on_regex(P) receives the decided regex-class names (their positions need the regex search).
+template <class RxFn>
+__device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O,
+                               unsigned long long &nver, unsigned long long &nwin, RxFn on_regex)
+{
+    const int lane = lane_id();
+    const uint32_t n = F.n;
+    if (n == 0) {
+        if (FT.empty_pat >= 0) emit_hits(O, GS, lane == 0, F.doc, (uint32_t)FT.empty_pat, 0u, F.field);
+        return;
+    }
+    const uint32_t fc = (lane < (int)n) ? fk_cp(F, lane) : 0xFFFFFFFCu;
+    if (n <= (uint32_t)SHORT_EXACT_MAX) {
+        uint64_t h = 0;
+        for (uint32_t i = 0; i < n; ++i) h = h * SUB_B + (uint32_t)__builtin_amdgcn_readlane(fc, i);
+        const uint64_t key = (h + (uint64_t)n * 0x9E3779B97F4A7C15ull) | 1ull;
+        uint32_t slot = (uint32_t)(key >> 32) & FT.sub_mask;
+        uint32_t b = 0, cnt = 0;
+        for (;;) {
+            const uint64_t kk = FT.sub_key[slot];
+            if (kk == key) { b = FT.sub_begin[slot]; cnt = FT.sub_cnt[slot]; break; }
+            if (kk == 0) break;
+            slot = (slot + 1) & FT.sub_mask;
+        }
+        b = __builtin_amdgcn_readfirstlane(b);
+        cnt = __builtin_amdgcn_readfirstlane(cnt);
+        uint32_t fch[SHORT_EXACT_MAX];
+#pragma unroll
+        for (int j = 0; j < SHORT_EXACT_MAX; ++j) fch[j] = __builtin_amdgcn_readlane(fc, j);
+        for (uint32_t c0 = 0; c0 < cnt; c0 += WAVE) {
+            const uint32_t idx = c0 + lane;
+            bool hit = false, exact = false;
+            uint32_t P = 0, rk = 0;
+            if (idx < cnt) {
+                P = FT.sub_pat[b + idx];
+                const uint32_t m = pi_m(FT.pat_info[P]);
+                rk = FT.pat_rxk[P];
+                const uint32_t *nmp = FT.pat_cps + FT.pat_cp_off[P];
+                for (uint32_t p = 0; p + n <= m && !hit; ++p) {
+                    bool eq = true;
+#pragma unroll
+                    for (int j = 0; j < SHORT_EXACT_MAX; ++j)
+                        if ((uint32_t)j < n) eq = eq && nmp[p + j] == fch[j];
+                    hit = eq;
+                }
+                exact = hit && m == n;
+            }
+            // literal: position 0 iff the name equals the field
+            const bool lit = hit && rk == RXK_LITERAL;
+            emit_hits(O, GS, lit, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
+            uint64_t rxm = __ballot(hit && rk == RXK_REGEX);
+            while (rxm) {
+                const int l = __builtin_ctzll(rxm);
+                rxm &= rxm - 1;
+                on_regex((uint32_t)__shfl((int)P, l, WAVE));
+            }
+        }
+        return;
+    }
+    // signature of the field's characters
+    uint64_t fsig = 0;
+    {
+        uint64_t bit = (lane < (int)n) ? (1ull << (fc & 63)) : 0ull;
+        for (int d = 1; d < WAVE; d <<= 1) bit |= __shfl_xor(bit, d, WAVE);
+        fsig = bit;
+    }
+    const uint32_t allow = (2 * n - 1) / 20;   // unmatched field chars any passing window allows
+    const uint32_t count = (uint32_t)FT.f_count_ge[n];
+    for (uint32_t c0 = 0; c0 < count; c0 += WAVE) {
+        const uint32_t idx = c0 + lane;
+        bool cand = false;
+        if (idx < count) {
+            const uint64_t ns = FT.pat_sig[FT.f_first + idx];
+            cand = (uint32_t)__popcll(fsig & ~ns) <= allow;
+        }
+        uint64_t cm = __ballot(cand);
+        while (cm) {
+            const int l = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const uint32_t P = (uint32_t)FT.f_first + c0 + (uint32_t)l;
+            const uint32_t m = pi_m(FT.pat_info[P]);
+            bool exact = false;
+            ++nver;
+            const uint32_t nmr = (lane < (int)m) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+            if (!fk_short_decide(fc, n, nmr, m, &exact, nwin)) continue;
+            if (FT.pat_rxk[P] == RXK_REGEX) on_regex(P);
+            else emit_hits(O, GS, lane == 0, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- fast resolve of one field
 // Returns 0 when done, 1 if the field is a long non-ASCII field and 3 if the
 // items overflowed: the document then goes to the generic kernel.
@@ -584,8 +760,15 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     const int lane = lane_id();
     // ---- field facts (code points, ASCII) on demand
     const int64_t flen = F.fe - F.fb;
-    F.ascii = maybe_nonascii ? field_is_ascii(F.arena, F.fb, F.fe) : true;
-    F.n = F.ascii ? (uint32_t)flen : field_cp_count(F.arena, F.fb, F.fe, false);
+    // the scan's non-ASCII flags are exact per field
+    F.ascii = !maybe_nonascii;
+    F.n = (uint32_t)flen;
+    if (!F.ascii) {
+        if (flen > (int64_t)FK_CP_CAP) return 1;
+        F.n = decode_field_fast(F.arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
+        F.cps = cps;
+        F.blkcnt = blkcnt;
+    }
     const bool is_short = !(RK_SKIP & 1) && F.n <= (uint32_t)MAXM;
     // ---- one-deletion edge windows of the 11..20-code-point names (prefiltered by the scan)
     if (!(RK_SKIP & 2) && edge && F.n >= EDGE_MIN_M + 1) {
@@ -600,12 +783,6 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     wave_sync();
     const uint32_t N = __builtin_amdgcn_readfirstlane(*icnt_f);
     if (N == 0 && !is_short) return 0;
-    if (!F.ascii) {
-        if (flen > (int64_t)FK_CP_CAP) return 1;
-        decode_field(GS, F.arena, F.fb, F.fe, cps, blkcnt);
-        F.cps = cps;
-        F.blkcnt = blkcnt;
-    }
     if (N > (uint32_t)WAVE) {
         // more than one register tile: sort in LDS, then take pattern-aligned batches of <= 64 items
         wave_sort_lds(items_lds, N);
@@ -660,7 +837,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
             const uint32_t bp = (uint32_t)__builtin_amdgcn_readlane((int)bpos, l);
             const uint32_t info1 = FT.use_info1[uu];
             const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
-            const uint32_t q = to_cp(F, bp);
+            const uint32_t q = to_cp_fast(F, bp);
             // pieces of one occurrence share the alignment base = q - o: verify it once
             const int64_t base = (int64_t)q - (int64_t)o;
             if (P == last_P && base == last_base) continue;
@@ -674,7 +851,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         // ---- positions: U names and literal fuzzy names report their exact occurrences
         const bool relevant = live && ((!fuzzy && kind == FU_UPPER) ||
                                        (fuzzy && decided && rxk == RXK_LITERAL && kind == FU_FULL));
-        const uint32_t cpos = relevant ? to_cp(F, bpos) : 0u;
+        const uint32_t cpos = relevant ? to_cp_fast(F, bpos) : 0u;
         const uint64_t relm = __ballot(relevant);
         // leftmost non-overlapping selection per group (a match spans m code points)
         const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
@@ -713,99 +890,500 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         }
     }
     // ---- short field: the field is the needle, the longer names are the haystacks
-    if (is_short) {
-        const uint32_t n = F.n;
-        if (n == 0) {
-            if (FT.empty_pat >= 0) emit_hits(O, GS, lane == 0, F.doc, (uint32_t)FT.empty_pat, 0u, F.field);
-            return 0;
-        }
-        const uint32_t fc = (lane < (int)n) ? fk_cp(F, lane) : 0xFFFFFFFCu;
-        if (n <= (uint32_t)SHORT_EXACT_MAX) {
-            uint64_t h = 0;
-            for (uint32_t i = 0; i < n; ++i) h = h * SUB_B + (uint32_t)__builtin_amdgcn_readlane(fc, i);
-            const uint64_t key = (h + (uint64_t)n * 0x9E3779B97F4A7C15ull) | 1ull;
-            uint32_t slot = (uint32_t)(key >> 32) & FT.sub_mask;
-            uint32_t b = 0, cnt = 0;
-            for (;;) {
-                const uint64_t kk = FT.sub_key[slot];
-                if (kk == key) { b = FT.sub_begin[slot]; cnt = FT.sub_cnt[slot]; break; }
-                if (kk == 0) break;
-                slot = (slot + 1) & FT.sub_mask;
-            }
-            b = __builtin_amdgcn_readfirstlane(b);
-            cnt = __builtin_amdgcn_readfirstlane(cnt);
-            uint32_t fch[SHORT_EXACT_MAX];
-#pragma unroll
-            for (int j = 0; j < SHORT_EXACT_MAX; ++j) fch[j] = __builtin_amdgcn_readlane(fc, j);
-            for (uint32_t c0 = 0; c0 < cnt; c0 += WAVE) {
-                const uint32_t idx = c0 + lane;
-                bool hit = false, exact = false;
-                uint32_t P = 0, rk = 0;
-                if (idx < cnt) {
-                    P = FT.sub_pat[b + idx];
-                    const uint32_t m = pi_m(FT.pat_info[P]);
-                    rk = FT.pat_rxk[P];
-                    const uint32_t *nmp = FT.pat_cps + FT.pat_cp_off[P];
-                    for (uint32_t p = 0; p + n <= m && !hit; ++p) {
-                        bool eq = true;
-#pragma unroll
-                        for (int j = 0; j < SHORT_EXACT_MAX; ++j)
-                            if ((uint32_t)j < n) eq = eq && nmp[p + j] == fch[j];
-                        hit = eq;
-                    }
-                    exact = hit && m == n;
-                }
-                // literal: position 0 iff the name equals the field
-                const bool lit = hit && rk == RXK_LITERAL;
-                emit_hits(O, GS, lit, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
-                uint64_t rxm = __ballot(hit && rk == RXK_REGEX);
-                while (rxm) {
-                    const int l = __builtin_ctzll(rxm);
-                    rxm &= rxm - 1;
-                    fk_regex_enqueue(GS, F, (uint32_t)__shfl((int)P, l, WAVE), RQ);
-                }
-            }
-            return 0;
-        }
-        // signature of the field's characters
-        uint64_t fsig = 0;
-        {
-            uint64_t bit = (lane < (int)n) ? (1ull << (fc & 63)) : 0ull;
-            for (int d = 1; d < WAVE; d <<= 1) bit |= __shfl_xor(bit, d, WAVE);
-            fsig = bit;
-        }
-        const uint32_t allow = (2 * n - 1) / 20;   // unmatched field chars any passing window allows
-        const uint32_t count = (uint32_t)FT.f_count_ge[n];
-        for (uint32_t c0 = 0; c0 < count; c0 += WAVE) {
-            const uint32_t idx = c0 + lane;
-            bool cand = false;
-            if (idx < count) {
-                const uint64_t ns = FT.pat_sig[FT.f_first + idx];
-                cand = (uint32_t)__popcll(fsig & ~ns) <= allow;
-            }
-            uint64_t cm = __ballot(cand);
-            while (cm) {
-                const int l = __builtin_ctzll(cm);
-                cm &= cm - 1;
-                const uint32_t P = (uint32_t)FT.f_first + c0 + (uint32_t)l;
-                const uint32_t m = pi_m(FT.pat_info[P]);
-                bool exact = false;
-                ++nver;
-                const uint32_t nmr = (lane < (int)m) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
-                if (!fk_short_decide(fc, n, nmr, m, &exact, nwin)) continue;
-                if (FT.pat_rxk[P] == RXK_REGEX) fk_regex_enqueue(GS, F, P, RQ);
-                else emit_hits(O, GS, lane == 0, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
-            }
-        }
-    }
+    if (is_short) fk_short_field(FT, GS, F, O, nver, nwin, [&](uint32_t P) { fk_regex_enqueue(GS, F, P, RQ); });
     return 0;
 }
 
 
+// ---------------------------------------------------------------- flat resolve (all-ASCII documents)
+// The scan kernel finishes an all-ASCII document itself (fk_scan_epilogue): it sorts the document's
+// items, emits the positions of uppercase names and of exact occurrences of literal fuzzy names,
+// and leaves the rest as tasks in its wave's task regions for kw_task_kernel:
+//   vq  {doc, P << 1 | field, q, o | pl << 8}   a pigeonhole piece of an undecided fuzzy name
+//   eq  {doc, field, 0, 0}                       a field flagged by the edge prefilter
+//   sq  {doc, field, 0, 0}                       a field of <= 64 code points
+//   xq  {doc, P << 1 | field, 0, 0}              a regex-class name decided by an exact occurrence
+// A name can be decided by more than one source (an exact occurrence and an edge window; several
+// pieces); the decided set makes the first one the only one that emits `name: []` or runs the
+// regex search.
+__device__ __forceinline__ unsigned long long dset_key(uint32_t doc, uint32_t P, uint32_t field)
+{
+    return (((unsigned long long)doc << 21) | ((unsigned long long)P << 1) | field) + 1ull;
+}
+
+__device__ __forceinline__ unsigned long long dset_slot(unsigned long long key, unsigned long long mask)
+{
+    return ((key * 0x9E3779B97F4A7C15ull) >> 20) & mask;
+}
+
+// true iff this call inserted the key (one lane calls)
+__device__ bool dset_insert(const FastScratch &S, unsigned long long key)
+{
+    unsigned long long slot = dset_slot(key, S.dmask);
+    for (unsigned long long probe = 0; probe <= S.dmask; ++probe) {
+        const unsigned long long cur = atomicCAS(&S.dset[slot], 0ull, key);
+        if (cur == 0ull) return true;
+        if (cur == key) return false;
+        slot = (slot + 1) & S.dmask;
+    }
+    atomicOr(&S.status[0], ST_DSET_FULL);
+    return false;
+}
+
+__device__ bool dset_contains(const FastScratch &S, unsigned long long key)
+{
+    unsigned long long slot = dset_slot(key, S.dmask);
+    for (unsigned long long probe = 0; probe <= S.dmask; ++probe) {
+        const unsigned long long cur = __atomic_load_n(&S.dset[slot], __ATOMIC_RELAXED);
+        if (cur == key) return true;
+        if (cur == 0ull) return false;
+        slot = (slot + 1) & S.dmask;
+    }
+    return false;
+}
+
+// wave-uniform decision "insert (doc, field, P)": lane 0 inserts, every lane gets the answer
+__device__ __forceinline__ bool dset_insert_wave(const FastScratch &S, uint32_t doc, uint32_t P, uint32_t field)
+{
+    int ins = 0;
+    if (lane_id() == 0) ins = dset_insert(S, dset_key(doc, P, field)) ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(ins) != 0;
+}
+
+// append one record to a wave's task region (cnt is wave-uniform; lane 0 writes)
+__device__ __forceinline__ void task_push(uint4 *region, uint32_t cap, uint32_t &cnt, uint4 rec)
+{
+    if (cnt < cap && lane_id() == 0) region[cnt] = rec;
+    ++cnt;
+}
+
+struct TaskCounts {
+    uint32_t v, e, s, x;
+};
+
+// Finish an all-ASCII document in the scan kernel.  items: the wave's LDS item lists (field f at
+// f * FK_ITEMS), nf[f] items each.
+__device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D,
+                                 uint64_t *items, uint32_t n0, uint32_t n1, uint32_t flags, int64_t wave, OutCtx &O,
+                                 TaskCounts &TC)
+{
+    const int lane = lane_id();
+    uint4 *vq = S.vq + (size_t)wave * S.vcap, *eq = S.eq + (size_t)wave * S.ecap;
+    uint4 *sq = S.sq + (size_t)wave * S.scap, *xq = S.xq + (size_t)wave * S.xcap;
+    for (uint32_t f = 0; f < 2; ++f) {
+        FieldCtx F;
+        F.arena = D.arena;
+        F.fb = f ? D.t1 : D.t0;
+        F.fe = f ? D.t2 : D.t1;
+        F.n = (uint32_t)(F.fe - F.fb);
+        F.ascii = true;
+        F.cps = nullptr;
+        F.blkcnt = nullptr;
+        F.doc = D.doc;
+        F.field = f;
+        const uint32_t N = f ? n1 : n0;
+        uint64_t *its = items + f * FK_ITEMS;
+        if ((flags & (f ? DH_EDGE1 : DH_EDGE0)) && F.n >= EDGE_MIN_M + 1) task_push(eq, S.ecap, TC.e, make_uint4(D.doc, f, 0u, 0u));
+        if (F.n <= (uint32_t)MAXM) task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
+        if (N == 0) continue;
+        if (N > (uint32_t)WAVE) wave_sort_lds(its, N);
+        for (uint32_t bs = 0; bs < N;) {
+            uint32_t be = N;
+            if (N > (uint32_t)WAVE) {
+                be = bs + WAVE < N ? bs + WAVE : N;
+                if (be < N)
+                    while (be > bs && it_pat(its[be]) == it_pat(its[be - 1])) --be;
+                if (be == bs) be = bs + WAVE;   // (cannot happen: the scan defers such documents)
+            }
+            const uint32_t NB = be - bs;
+            uint64_t it = (lane < (int)NB) ? its[bs + lane] : ~0ull;
+            bs = be;
+            it = wave_sort_reg(it);
+            const bool valid = lane < (int)NB;
+            const uint32_t pat = valid ? it_pat(it) : 0xFFFFFu;
+            const uint32_t kind = it_kind(it);
+            const uint32_t bpos = it_pos(it);
+            const uint32_t use = it_use(it);
+            const uint32_t pi = valid ? FT.pat_info[pat] : 0u;
+            const uint32_t rxk = valid ? FT.pat_rxk[pat] : 0u;
+            const uint32_t m = pi_m(pi);
+            const bool fuzzy = (pi & PI_FUZZY) != 0;
+            const uint32_t prev_pat = (uint32_t)__shfl_up((int)pat, 1, WAVE);
+            const bool head = valid && (lane == 0 || prev_pat != pat);
+            const uint64_t heads = __ballot(head);
+            const uint64_t below = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+            const int gs = 63 - __builtin_clzll((heads & below) | 1ull);
+            const uint64_t after = heads & ~below;
+            const int ge = after ? __builtin_ctzll(after) : (int)NB;
+            const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
+            // the short path owns fuzzy names at least as long as the field
+            const bool live = valid && !(fuzzy && m >= F.n);
+            const uint64_t fullm = __ballot(live && kind == FU_FULL);
+            const bool decided = (fullm & gmask) != 0;
+            // pieces of undecided fuzzy names -> verify tasks (one per alignment base)
+            uint64_t vneed = __ballot(live && fuzzy && !decided && kind == FU_PIECE);
+            uint32_t last_P = 0xFFFFFFFFu;
+            int64_t last_base = -1;
+            while (vneed) {
+                const int l = __builtin_ctzll(vneed);
+                vneed &= vneed - 1;
+                const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pat, l);
+                const uint32_t uu = (uint32_t)__builtin_amdgcn_readlane((int)use, l);
+                const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)bpos, l);   // ASCII: byte = code point
+                const uint32_t info1 = FT.use_info1[uu];
+                const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
+                const int64_t base = (int64_t)q - (int64_t)o;
+                if (P == last_P && base == last_base) continue;
+                last_P = P;
+                last_base = base;
+                task_push(vq, S.vcap, TC.v, make_uint4(D.doc, (P << 1) | f, q, o | (pl << 8)));
+            }
+            // positions: uppercase names and exact occurrences of decided literal fuzzy names
+            const bool relevant = live && ((!fuzzy && kind == FU_UPPER) ||
+                                           (fuzzy && decided && rxk == RXK_LITERAL && kind == FU_FULL));
+            const uint32_t cpos = bpos;
+            const uint64_t relm = __ballot(relevant);
+            const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
+            const int pr = prevrel ? 63 - __builtin_clzll(prevrel) : -1;
+            const uint32_t pcpos = (uint32_t)__shfl((int)cpos, pr < 0 ? lane : pr, WAVE);
+            const bool overlap = relevant && pr >= 0 && cpos < pcpos + m;
+            uint64_t keep = relm;
+            if (__ballot(overlap)) {
+                keep = 0;
+                uint64_t mm2 = relm;
+                int cur_head = -1;
+                uint32_t last_end = 0;
+                while (mm2) {
+                    const int l = __builtin_ctzll(mm2);
+                    mm2 &= mm2 - 1;
+                    const int hh = __shfl(gs, l, WAVE);
+                    const uint32_t st = (uint32_t)__shfl((int)cpos, l, WAVE);
+                    const uint32_t len = (uint32_t)__shfl((int)m, l, WAVE);
+                    if (hh != cur_head) { cur_head = hh; keep |= 1ull << l; last_end = st + len; continue; }
+                    if (st >= last_end) { keep |= 1ull << l; last_end = st + len; }
+                }
+            }
+            emit_hits(O, GS, (keep >> lane) & 1ull, F.doc, pat, cpos, F.field);
+            // exactly decided fuzzy names: an edge window (11 <= m <= 20) may decide them again -> the set;
+            // regex-class ones get their re.finditer search
+            uint64_t dm = __ballot(head && live && fuzzy && decided);
+            while (dm) {
+                const int l = __builtin_ctzll(dm);
+                dm &= dm - 1;
+                const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pat, l);
+                const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
+                const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)rxk, l);
+                if (mm >= EDGE_MIN_M && mm <= EDGE_MAX_M) (void)dset_insert_wave(S, D.doc, P, f);
+                if (rk == RXK_REGEX) task_push(xq, S.xcap, TC.x, make_uint4(D.doc, (P << 1) | f, 0u, 0u));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- kernel: the tasks of the flat resolve
+// Task wave t works the task regions of scan wave t: verify, edge, short, then regex tasks.
+__device__ __forceinline__ void fk_field_ctx(FieldCtx &F, const uint8_t *arena, const int64_t *off, uint32_t doc,
+                                             uint32_t field)
+{
+    F.arena = arena;
+    F.fb = off[2 * (int64_t)doc + field];
+    F.fe = off[2 * (int64_t)doc + field + 1];
+    F.n = (uint32_t)(F.fe - F.fb);
+    F.ascii = true;
+    F.cps = nullptr;
+    F.blkcnt = nullptr;
+    F.doc = doc;
+    F.field = field;
+}
+
+// a decided regex-class name: re.finditer over the field, or `name: []`
+__device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTables &T, const DevScratch &GS,
+                                             const FieldCtx &F, OutCtx &O, uint32_t P, uint64_t *rxtab, uint8_t *txt,
+                                             unsigned long long &nrx, unsigned long long &nrx_bt,
+                                             unsigned long long &nrx_rounds)
+{
+    const int32_t r = FT.rxf_idx[P];
+    ++nrx;
+    nrx_bt += r < 0;
+    nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
+    const uint32_t cnt = (RK_SKIP & 8) ? 1u
+                         : (r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, txt)
+                                   : rx_positions(T, GS, F, O, P));
+    if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
+}
+
+// a name decided without an exact occurrence (piece window / edge window): first decision emits
+__device__ __forceinline__ void fk_decide_now(const FastTables &FT, const DevTables &T, const FastScratch &S,
+                                              const DevScratch &GS, const FieldCtx &F, OutCtx &O, uint32_t P,
+                                              uint64_t *rxtab, uint8_t *txt, unsigned long long &nrx,
+                                              unsigned long long &nrx_bt, unsigned long long &nrx_rounds)
+{
+    if (!dset_insert_wave(S, F.doc, P, F.field)) return;
+    if (FT.pat_rxk[P] == RXK_REGEX) fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+    else emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
+}
+
+// ---- lane-parallel verification of a piece of an ASCII name in an ASCII field (one lane = one task)
+// exact zero-byte flags (the high bit of every zero byte) of a 64-bit word
+__device__ __forceinline__ uint64_t zb64(uint64_t x)
+{
+    return ~(((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x | 0x7F7F7F7F7F7F7F7Full);
+}
+// the 8 byte flags of zb64 -> bits 0..7
+__device__ __forceinline__ uint32_t hb8(uint64_t z)
+{
+    return (uint32_t)((((z >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+}
+
+constexpr int LV_WIN = 23;   // dwords of text per lane in LDS (stride 23: no bank conflicts between lanes)
+
+// 8 text bytes at text position s (relative to the lane's window start A, 4-aligned)
+__device__ __forceinline__ uint64_t lv_text8(const uint32_t *win, int64_t d)
+{
+    const int k = (int)(d >> 2);
+    const uint32_t sh = (uint32_t)(d & 3);
+    const uint32_t x0 = win[k], x1 = win[k + 1], x2 = win[k + 2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
+}
+
+// positions of byte c in the name (bit i = name[i] == c), name in 8 little-endian words
+__device__ __forceinline__ uint64_t lv_match(const uint64_t (&NW)[8], uint32_t c, uint64_t needle)
+{
+    const uint64_t cc = (uint64_t)c * 0x0101010101010101ull;
+    uint64_t M = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) M |= (uint64_t)hb8(zb64(NW[w] ^ cc)) << (8 * w);
+    return M & needle;
+}
+
+// one lane's task: does some window of the partial_ratio family around this piece pass?
+// (the same family and rule as fk_verify_piece; text = field bytes [fb, fb + n))
+__device__ bool lv_verify(const uint8_t *__restrict__ arena, int64_t fb, uint32_t n, const uint64_t (&NW)[8], uint32_t m,
+                          uint32_t q, uint32_t o, uint32_t pl, uint32_t *win, unsigned long long &nwin)
+{
+    const uint64_t needle = low_mask(m);
+    const uint32_t k = kfull(m);
+    const int64_t base = (int64_t)q - (int64_t)o;
+    if (k > 0) {
+        // text window [base - 2k, base + m + 2k) of the field, staged at A (4-aligned) in this lane's LDS
+        const int64_t lo = base - 2 * (int64_t)k;
+        const int64_t A = (fb + lo) & ~(int64_t)3;
+        const int64_t fe = fb + n;
+#pragma unroll
+        for (int j = 0; j < LV_WIN; ++j) {   // only dwords that overlap the field (the rest never matches)
+            const int64_t ad = A + 4 * j;
+            win[j] = (ad + 4 > fb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+        }
+        uint32_t cnt = 0;
+        uint64_t hit[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                if (8 * w >= (int)m) break;
+                const int64_t s = base + 8 * w + t;   // field position of name byte 8w
+                uint64_t z = zb64(lv_text8(win, fb + s - A) ^ NW[w]);
+                // bytes outside the field never match
+                const int64_t first = s < 0 ? -s : 0, last = (int64_t)n - s;   // valid byte range [first, last)
+                if (first >= 8 || last <= 0) continue;
+                uint64_t vm = ~0ull;
+                if (first > 0) vm &= ~0ull << (8 * first);
+                if (last < 8) vm &= (1ull << (8 * last)) - 1;
+                hit[w] |= z & vm;
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cnt += (uint32_t)__popcll(hb8(hit[w]) & (uint32_t)((needle >> (8 * w)) & 0xFFu));
+        if (cnt + k >= m) {
+            int64_t pmin = base - k, pmax = base + k;
+            if (pmin < 0) pmin = 0;
+            if (pmax > (int64_t)(n - m)) pmax = (int64_t)(n - m);
+            for (int64_t p = pmin; p <= pmax; ++p) {
+                uint64_t V = ~0ull;
+                for (uint32_t j = 0; j < m; ++j) {
+                    const uint32_t c = (uint32_t)(lv_text8(win, fb + p + j - A) & 0xFFu);
+                    const uint64_t U = V & lv_match(NW, c, needle);
+                    V = (V + U) | (V - U);
+                }
+                ++nwin;
+                const uint32_t L = (uint32_t)__popcll(~V & needle);
+                if (20u * (m - L) < m) return true;
+            }
+        }
+    }
+    if (q + pl + 1 <= m) {   // prefixes text[:w], w in [1, m)
+        uint64_t V = ~0ull;
+        ++nwin;
+        for (uint32_t w = 1; w < m; ++w) {
+            const uint32_t c = arena[fb + w - 1];
+            const uint64_t U = V & lv_match(NW, c, needle);
+            V = (V + U) | (V - U);
+            if (passes((uint32_t)__popcll(~V & needle), m, w)) return true;
+        }
+    }
+    if (q + m > n) {         // suffixes text[i:], i in (n-m, n): reversed name and text
+        uint64_t V = ~0ull;
+        ++nwin;
+        for (uint32_t kk = 1; kk < m; ++kk) {
+            const uint32_t c = arena[fb + n - kk];
+            const uint64_t M = lv_match(NW, c, needle);
+            const uint64_t R = __builtin_bitreverse64(M) >> (64 - m);   // bit i = name[m - 1 - i] == c
+            const uint64_t U = V & R;
+            V = (V + U) | (V - U);
+            if (passes((uint32_t)__popcll(~V & needle), m, kk)) return true;
+        }
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(RK_BLOCK) void kw_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                           const int64_t *__restrict__ off, int n_regions,
+                                                           FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
+    __shared__ uint64_t rxtab_all[RK_WAVES * 128];
+    __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
+    __shared__ uint32_t cnt_all[RK_WAVES * 4];
+    __shared__ uint32_t lvwin_all[RK_BLOCK * LV_WIN];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    if (t >= n_regions) return;
+    uint64_t *eitems = items_all + wib * FK_ITEMS;
+    uint64_t *rxtab = rxtab_all + wib * 128;
+    uint8_t *txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
+    uint32_t *icnt = cnt_all + wib * 4;
+    OutCtx O;
+    O.out = S.tout + (size_t)t * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    unsigned long long nver = 0, nwin = 0, nedge = 0, nrx = 0, nrx_bt = 0, nrx_rounds = 0;
+    unsigned long long nver_w = 0, nwin_w = 0;   // wave-serial counts (every lane counts)
+    FieldCtx F;
+    // ---- verify tasks: lanes take 64 tasks at a time (ASCII names); other names wave-serially
+    {
+        const uint32_t nv = (TK_SKIP & 1) ? 0u : min(S.vcnt[t], S.vcap);
+        const uint4 *vq = S.vq + (size_t)t * S.vcap;
+        uint32_t *win = lvwin_all + threadIdx.x * LV_WIN;
+        for (uint32_t k0 = 0; k0 < nv; k0 += WAVE) {
+            const uint32_t kk = k0 + (uint32_t)lane;
+            const bool valid = kk < nv;
+            const uint4 tk = valid ? vq[kk] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t doc = tk.x, P = tk.y >> 1, field = tk.y & 1u;
+            bool todo = valid && !dset_contains(S, dset_key(doc, P, field));
+            const uint32_t pi = todo ? FT.pat_info[P] : 0u;
+            const uint32_t m = pi_m(pi);
+            const bool lanewise = todo && (pi & PI_ASCII) != 0;
+            bool pass = false;
+            int64_t fb = 0;
+            uint32_t n = 0;
+            if (todo) {
+                fb = off[2 * (int64_t)doc + field];
+                n = (uint32_t)(off[2 * (int64_t)doc + field + 1] - fb);
+            }
+            if (lanewise) {
+                uint64_t NW[8];
+                const int64_t nb = FT.pat_boff[P];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    uint64_t x = 0;
+                    if (8 * w < (int)m) x = load8(FT.pat_bytes, nb + 8 * w);
+                    const int rem = (int)m - 8 * w;
+                    if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
+                    NW[w] = x;
+                }
+                ++nver;
+                pass = lv_verify(arena, fb, n, NW, m, tk.z, tk.w & 0xFFu, (tk.w >> 8) & 0xFFu, win, nwin);
+            }
+            // decisions (and the names lanes cannot take) wave-serially
+            uint64_t wm = __ballot(pass || (todo && !lanewise));
+            while (wm) {
+                const int l = __builtin_ctzll(wm);
+                wm &= wm - 1;
+                const uint32_t ld = (uint32_t)__builtin_amdgcn_readlane((int)doc, l);
+                const uint32_t lP = (uint32_t)__builtin_amdgcn_readlane((int)P, l);
+                const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane((int)field, l);
+                const bool lpass = __builtin_amdgcn_readlane((int)pass, l) != 0;
+                fk_field_ctx(F, arena, off, ld, lf);
+                bool dec = lpass;
+                if (!lpass) {
+                    const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
+                    const uint32_t nm = (lane < (int)lm) ? FT.pat_cps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
+                    const uint32_t lw = (uint32_t)__builtin_amdgcn_readlane((int)tk.w, l);
+                    const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)tk.z, l);
+                    ++nver_w;
+                    dec = fk_verify_piece(F, nm, lm, lq, lw & 0xFFu, (lw >> 8) & 0xFFu, nwin_w);
+                }
+                if (dec) fk_decide_now(FT, T, S, GS, F, O, lP, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+            }
+        }
+    }
+    // ---- edge tasks: one-deletion edge windows of the 11..20-code-point names
+    {
+        const uint32_t ne = (TK_SKIP & 2) ? 0u : min(S.ecnt[t], S.ecap);
+        const uint4 *eq = S.eq + (size_t)t * S.ecap;
+        for (uint32_t k = 0; k < ne; ++k) {
+            const uint4 tk = eq[k];
+            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
+            if (lane < 4) icnt[lane] = 0;
+            wave_sync();
+            uint32_t added = fk_edge_items(FT, F, eitems, &icnt[0], &icnt[1]);
+            added = (uint32_t)wave_sum((int)added);
+            if (!added) continue;
+            nedge += added;
+            wave_sync();
+            const uint32_t n_it = min(__builtin_amdgcn_readfirstlane(icnt[0]), (uint32_t)FK_ITEMS);
+            for (uint32_t i = 0; i < n_it; ++i) {
+                const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)it_pat(eitems[i]));
+                fk_decide_now(FT, T, S, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+            }
+        }
+    }
+    // ---- short fields
+    {
+        const uint32_t ns = (TK_SKIP & 4) ? 0u : min(S.scnt[t], S.scap);
+        const uint4 *sq = S.sq + (size_t)t * S.scap;
+        for (uint32_t k = 0; k < ns; ++k) {
+            const uint4 tk = sq[k];
+            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
+            fk_short_field(FT, GS, F, O, nver, nwin, [&](uint32_t P) {
+                fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+            });
+        }
+    }
+    // ---- regex-class names decided by an exact occurrence
+    {
+        const uint32_t nx = (TK_SKIP & 8) ? 0u : min(S.xcnt[t], S.xcap);
+        const uint4 *xq = S.xq + (size_t)t * S.xcap;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint4 tk = xq[k];
+            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
+            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
+            fk_regex_now(FT, T, GS, F, O, y >> 1, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+        }
+    }
+    if (lane == 0) S.tout_cnt[t] = O.n;
+    unsigned long long v = nver, w = nwin;   // lane-parallel counts (one per task)
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        v += __shfl_xor(v, dd, WAVE);
+        w += __shfl_xor(w, dd, WAVE);
+    }
+    if (lane == 0) {
+        atomicAdd(&S.stats[2], w + nwin_w);   // nver_w / nwin_w: every lane holds the wave's count
+        atomicAdd(&S.stats[3], v + nver_w);
+        atomicAdd(&S.stats[7], nedge);
+        atomicAdd(&S.stats[10], nrx);
+        atomicAdd(&S.stats[11], nrx_bt);
+        atomicAdd(&S.stats[12], nrx_rounds);
+    }
+}
+
 // ---------------------------------------------------------------- kernel 1: the scan
 __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int64_t n_docs,
-                                                            FastScratch S)
+                                                            FastScratch S, DevScratch GS)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     uint32_t *filt = (uint32_t *)smem_raw;
@@ -836,6 +1414,11 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     uint32_t cursor = 0;                      // items this wave wrote to HBM
     unsigned long long ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;
     const bool has_t3 = FT.has_t3 != 0;
+    OutCtx O;                                 // hits of the documents this wave finishes itself
+    O.out = S.kout + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    TaskCounts TC = {0u, 0u, 0u, 0u};
 
     for (int64_t d = wave; d < n_docs; d += n_waves) {
         FastDoc D;
@@ -886,10 +1469,19 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             // a 2-byte match cannot start on the last byte of a field
             if (rel1 - 1 >= 0 && rel1 - 1 < 16) valid &= ~(1u << (rel1 - 1));
             if (rel2 - 1 >= 0 && rel2 - 1 < 16) valid &= ~(1u << (rel2 - 1));
-            // non-ASCII bytes: attribute to the field(s) this lane's chunk covers
-            if (((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) && valid) {
-                if (rel1 > 0) na0 = true;
-                if (rel1 < 16) na1 = true;
+            // non-ASCII bytes, attributed exactly to their field
+            if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
+                uint32_t hb = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t x = (W[k] >> 7) & 0x01010101u;   // bit 0 of each byte = its high bit
+                    hb |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
+                }
+                const int j1 = rel1 <= 0 ? 0 : (rel1 >= 16 ? 16 : (int)rel1);
+                const uint32_t in0 = ((1u << j1) - 1u) & ~((1u << jlo) - 1u);
+                const uint32_t in1 = (jhi > j1) ? (((1u << jhi) - 1u) & ~((1u << j1) - 1u)) : 0u;
+                if (hb & in0) na0 = true;
+                if (hb & in1) na1 = true;
             }
             uint32_t hit = 0;
 #pragma unroll
@@ -1007,8 +1599,12 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
                 else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
             }
+        } else if (!(flags & (DH_NA0 | DH_NA1))) {
+            // all ASCII: finished here, the rest as tasks (flat resolve)
+            if (FK_STAGE >= 2) fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+            h.y = n0 | (n1 << 8) | flags;
         } else {
-            // items -> HBM (field 0 then field 1)
+            // items -> HBM (field 0 then field 1) for the resolve kernel
             for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) gitems[cursor + i] = items[i];
             for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) gitems[cursor + n0 + i] = items[FK_ITEMS + i];
             cursor += n0 + n1;
@@ -1021,6 +1617,20 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         }
         if (lane == 0) S.hdr[d] = h;
         wave_sync();
+    }
+    if (lane == 0) {
+        S.kout_cnt[wave] = O.n;
+        S.vcnt[wave] = TC.v;
+        S.ecnt[wave] = TC.e;
+        S.scnt[wave] = TC.s;
+        S.xcnt[wave] = TC.x;
+        if (TC.v > S.vcap || TC.e > S.ecap || TC.s > S.scap || TC.x > S.xcap) {
+            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
+            atomicMax(&S.tmax[0], TC.v);
+            atomicMax(&S.tmax[1], TC.e);
+            atomicMax(&S.tmax[2], TC.s);
+            atomicMax(&S.tmax[3], TC.x);
+        }
     }
     unsigned long long a = nanchor, c1 = ncand;
 #pragma unroll
@@ -1145,7 +1755,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
         F.cps = cps;
         F.blkcnt = blkcnt;
         F.doc = d;
-        if (!F.ascii) decode_field(GS, arena, F.fb, F.fe, cps, blkcnt);
+        if (!F.ascii) decode_field_fast(arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
         const int32_t r = FT.rxf_idx[P];
         ++nrx;
         nrx_bt += r < 0;
