@@ -1050,7 +1050,14 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
         const int ntb = (nkb * FK_WAVES + RK_WAVES - 1) / RK_WAVES;
-        hipLaunchKernelGGL(kw_task_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+        // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up)
+        hipLaunchKernelGGL(kw_verify_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+                           nkb * FK_WAVES, h->FS, h->S);
+        hipLaunchKernelGGL(kw_edge_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+                           nkb * FK_WAVES, h->FS, h->S);
+        hipLaunchKernelGGL(kw_short_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+                           nkb * FK_WAVES, h->FS, h->S);
+        hipLaunchKernelGGL(kw_rx_task_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
                            nkb * FK_WAVES, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
         hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,

@@ -725,13 +725,18 @@ __device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const
     }
     const uint32_t allow = (2 * n - 1) / 20;   // unmatched field chars any passing window allows
     const uint32_t count = (uint32_t)FT.f_count_ge[n];
-    for (uint32_t c0 = 0; c0 < count; c0 += WAVE) {
-        const uint32_t idx = c0 + lane;
-        bool cand = false;
-        if (idx < count) {
-            const uint64_t ns = FT.pat_sig[FT.f_first + idx];
-            cand = (uint32_t)__popcll(fsig & ~ns) <= allow;
+    constexpr int SIG_U = 8;   // signature chunks in flight
+    for (uint32_t c00 = 0; c00 < count; c00 += SIG_U * WAVE) {
+        uint64_t nsig[SIG_U];
+#pragma unroll
+        for (int u = 0; u < SIG_U; ++u) {
+            const uint32_t idx = c00 + (uint32_t)(u * WAVE + lane);
+            nsig[u] = idx < count ? FT.pat_sig[FT.f_first + idx] : ~0ull;
         }
+#pragma unroll
+      for (int u = 0; u < SIG_U; ++u) {
+        const uint32_t c0 = c00 + (uint32_t)(u * WAVE);
+        const bool cand = c0 + (uint32_t)lane < count && (uint32_t)__popcll(fsig & ~nsig[u]) <= allow;
         uint64_t cm = __ballot(cand);
         while (cm) {
             const int l = __builtin_ctzll(cm);
@@ -745,6 +750,7 @@ __device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const
             if (FT.pat_rxk[P] == RXK_REGEX) on_regex(P);
             else emit_hits(O, GS, lane == 0, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
         }
+      }
     }
 }
 
@@ -898,7 +904,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
 // ---------------------------------------------------------------- flat resolve (all-ASCII documents)
 // The scan kernel finishes an all-ASCII document itself (fk_scan_epilogue): it sorts the document's
 // items, emits the positions of uppercase names and of exact occurrences of literal fuzzy names,
-// and leaves the rest as tasks in its wave's task regions for kw_task_kernel:
+// and leaves the rest as tasks in its wave's task regions for the task kernels (kw_verify_kernel, kw_edge_kernel, kw_short_kernel, kw_rx_task_kernel):
 //   vq  {doc, P << 1 | field, q, o | pl << 8}   a pigeonhole piece of an undecided fuzzy name
 //   eq  {doc, field, 0, 0}                       a field flagged by the edge prefilter
 //   sq  {doc, field, 0, 0}                       a field of <= 64 code points
@@ -1112,17 +1118,6 @@ __device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTabl
     if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
 }
 
-// a name decided without an exact occurrence (piece window / edge window): first decision emits
-__device__ __forceinline__ void fk_decide_now(const FastTables &FT, const DevTables &T, const FastScratch &S,
-                                              const DevScratch &GS, const FieldCtx &F, OutCtx &O, uint32_t P,
-                                              uint64_t *rxtab, uint8_t *txt, unsigned long long &nrx,
-                                              unsigned long long &nrx_bt, unsigned long long &nrx_rounds)
-{
-    if (!dset_insert_wave(S, F.doc, P, F.field)) return;
-    if (FT.pat_rxk[P] == RXK_REGEX) fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
-    else emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
-}
-
 // ---- lane-parallel verification of a piece of an ASCII name in an ASCII field (one lane = one task)
 // exact zero-byte flags (the high bit of every zero byte) of a 64-bit word
 __device__ __forceinline__ uint64_t zb64(uint64_t x)
@@ -1156,228 +1151,368 @@ __device__ __forceinline__ uint64_t lv_match(const uint64_t (&NW)[8], uint32_t c
     return M & needle;
 }
 
-// one lane's task: does some window of the partial_ratio family around this piece pass?
-// (the same family and rule as fk_verify_piece; text = field bytes [fb, fb + n))
-__device__ bool lv_verify(const uint8_t *__restrict__ arena, int64_t fb, uint32_t n, const uint64_t (&NW)[8], uint32_t m,
-                          uint32_t q, uint32_t o, uint32_t pl, uint32_t *win, unsigned long long &nwin)
+// Band test of one lane's verify task (the text [base - 2k, base + m + 2k) staged in the lane's
+// LDS window): every name byte matched by a passing full window lies within +-2k of its aligned
+// text byte.  Returns the number of full windows [pmin, pmin + nwj) left to evaluate.
+__device__ uint32_t lv_band(const uint8_t *__restrict__ arena, int64_t fb, uint32_t n, const uint64_t (&NW)[8],
+                            uint32_t m, int64_t base, uint32_t k, uint32_t *win, int64_t &pmin)
 {
+    pmin = 0;
+    if (k == 0) return 0;
     const uint64_t needle = low_mask(m);
-    const uint32_t k = kfull(m);
-    const int64_t base = (int64_t)q - (int64_t)o;
-    if (k > 0) {
-        // text window [base - 2k, base + m + 2k) of the field, staged at A (4-aligned) in this lane's LDS
-        const int64_t lo = base - 2 * (int64_t)k;
-        const int64_t A = (fb + lo) & ~(int64_t)3;
-        const int64_t fe = fb + n;
+    const int64_t lo = base - 2 * (int64_t)k;
+    const int64_t A = (fb + lo) & ~(int64_t)3;
+    const int64_t fe = fb + n;
 #pragma unroll
-        for (int j = 0; j < LV_WIN; ++j) {   // only dwords that overlap the field (the rest never matches)
-            const int64_t ad = A + 4 * j;
-            win[j] = (ad + 4 > fb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
-        }
-        uint32_t cnt = 0;
-        uint64_t hit[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) {
+    for (int j = 0; j < LV_WIN; ++j) {   // only dwords that overlap the field (the rest never matches)
+        const int64_t ad = A + 4 * j;
+        win[j] = (ad + 4 > fb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+    }
+    uint64_t hit[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) {
 #pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                if (8 * w >= (int)m) break;
-                const int64_t s = base + 8 * w + t;   // field position of name byte 8w
-                uint64_t z = zb64(lv_text8(win, fb + s - A) ^ NW[w]);
-                // bytes outside the field never match
-                const int64_t first = s < 0 ? -s : 0, last = (int64_t)n - s;   // valid byte range [first, last)
-                if (first >= 8 || last <= 0) continue;
-                uint64_t vm = ~0ull;
-                if (first > 0) vm &= ~0ull << (8 * first);
-                if (last < 8) vm &= (1ull << (8 * last)) - 1;
-                hit[w] |= z & vm;
-            }
-        }
-#pragma unroll
-        for (int w = 0; w < 8; ++w) cnt += (uint32_t)__popcll(hb8(hit[w]) & (uint32_t)((needle >> (8 * w)) & 0xFFu));
-        if (cnt + k >= m) {
-            int64_t pmin = base - k, pmax = base + k;
-            if (pmin < 0) pmin = 0;
-            if (pmax > (int64_t)(n - m)) pmax = (int64_t)(n - m);
-            for (int64_t p = pmin; p <= pmax; ++p) {
-                uint64_t V = ~0ull;
-                for (uint32_t j = 0; j < m; ++j) {
-                    const uint32_t c = (uint32_t)(lv_text8(win, fb + p + j - A) & 0xFFu);
-                    const uint64_t U = V & lv_match(NW, c, needle);
-                    V = (V + U) | (V - U);
-                }
-                ++nwin;
-                const uint32_t L = (uint32_t)__popcll(~V & needle);
-                if (20u * (m - L) < m) return true;
-            }
+        for (int w = 0; w < 8; ++w) {
+            if (8 * w >= (int)m) break;
+            const int64_t s = base + 8 * w + t;   // field position of name byte 8w
+            const uint64_t z = zb64(lv_text8(win, fb + s - A) ^ NW[w]);
+            // bytes outside the field never match
+            const int64_t first = s < 0 ? -s : 0, last = (int64_t)n - s;   // valid byte range [first, last)
+            if (first >= 8 || last <= 0) continue;
+            uint64_t vm = ~0ull;
+            if (first > 0) vm &= ~0ull << (8 * first);
+            if (last < 8) vm &= (1ull << (8 * last)) - 1;
+            hit[w] |= z & vm;
         }
     }
-    if (q + pl + 1 <= m) {   // prefixes text[:w], w in [1, m)
-        uint64_t V = ~0ull;
-        ++nwin;
-        for (uint32_t w = 1; w < m; ++w) {
-            const uint32_t c = arena[fb + w - 1];
-            const uint64_t U = V & lv_match(NW, c, needle);
-            V = (V + U) | (V - U);
-            if (passes((uint32_t)__popcll(~V & needle), m, w)) return true;
-        }
-    }
-    if (q + m > n) {         // suffixes text[i:], i in (n-m, n): reversed name and text
-        uint64_t V = ~0ull;
-        ++nwin;
-        for (uint32_t kk = 1; kk < m; ++kk) {
-            const uint32_t c = arena[fb + n - kk];
-            const uint64_t M = lv_match(NW, c, needle);
-            const uint64_t R = __builtin_bitreverse64(M) >> (64 - m);   // bit i = name[m - 1 - i] == c
-            const uint64_t U = V & R;
-            V = (V + U) | (V - U);
-            if (passes((uint32_t)__popcll(~V & needle), m, kk)) return true;
-        }
-    }
-    return false;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) cnt += (uint32_t)__popcll(hb8(hit[w]) & (uint32_t)((needle >> (8 * w)) & 0xFFu));
+    if (cnt + k < m) return 0;
+    int64_t pmax = base + k;
+    pmin = base - k;
+    if (pmin < 0) pmin = 0;
+    if (pmax > (int64_t)(n - m)) pmax = (int64_t)(n - m);
+    return pmax >= pmin ? (uint32_t)(pmax - pmin + 1) : 0u;
 }
 
-__global__ __launch_bounds__(RK_BLOCK) void kw_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                           const int64_t *__restrict__ off, int n_regions,
-                                                           FastScratch S, DevScratch GS)
+// regex-class names decided in the task kernels -> the region's regex queue (xq), lane-parallel
+struct XPush {
+    uint4 *q;
+    uint32_t cap, n;   // n: wave-uniform running count
+};
+
+__device__ __forceinline__ void xq_push(XPush &X, bool pred, uint32_t doc, uint32_t P, uint32_t field)
 {
-    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
-    __shared__ uint64_t rxtab_all[RK_WAVES * 128];
-    __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
-    __shared__ uint32_t cnt_all[RK_WAVES * 4];
+    const uint64_t m = __ballot(pred);
+    if (!m) return;
+    const uint32_t idx = X.n + mbcnt(m);
+    if (pred && idx < X.cap) X.q[idx] = make_uint4(doc, (P << 1) | field, 0u, 0u);
+    X.n += (uint32_t)__popcll(m);
+}
+
+__device__ __forceinline__ void xq_close(const FastScratch &S, const XPush &X, int64_t t)
+{
+    if (lane_id() == 0) {
+        S.xcnt[t] = X.n;
+        if (X.n > X.cap) {
+            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
+            atomicMax(&S.tmax[3], X.n);
+        }
+    }
+}
+
+// a name decided without an exact occurrence (edge window): the first decision emits `name: []`
+// or queues the regex search.  Wave-uniform.
+__device__ __forceinline__ void fk_decide_queue(const FastTables &FT, const FastScratch &S, const DevScratch &GS,
+                                                const FieldCtx &F, OutCtx &O, XPush &X, uint32_t P)
+{
+    if (!dset_insert_wave(S, F.doc, P, F.field)) return;
+    const bool rx = FT.pat_rxk[P] == RXK_REGEX;
+    xq_push(X, rx && lane_id() == 0, F.doc, P, F.field);
+    emit_hits(O, GS, !rx && lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
+}
+
+__device__ __forceinline__ void task_stats(const FastScratch &S, unsigned long long v, unsigned long long w,
+                                           unsigned long long e, unsigned long long rx, unsigned long long rxbt,
+                                           unsigned long long rxr)
+{
+    if (lane_id() == 0) {
+        if (w) atomicAdd(&S.stats[2], w);
+        if (v) atomicAdd(&S.stats[3], v);
+        if (e) atomicAdd(&S.stats[7], e);
+        if (rx) atomicAdd(&S.stats[10], rx);
+        if (rxbt) atomicAdd(&S.stats[11], rxbt);
+        if (rxr) atomicAdd(&S.stats[12], rxr);
+    }
+}
+
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v)
+{
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) v += __shfl_xor(v, dd, WAVE);
+    return v;
+}
+
+constexpr int LV_MAXJ = 16;   // window jobs per verify task: <= 2 kfull(64) + 1 full windows + prefix + suffix
+
+// ---------------------------------------------------------------- kernels: the tasks of the flat resolve
+// Task kernels run one wave per scan wave t over the task regions that scan wave wrote, in stream
+// order verify -> edge -> short -> regex; each appends to region t's result list (tout) and the
+// first three append regex-class decisions to region t's regex queue (xq).
+
+// Verify tasks.  Lanes take 64 tasks at a time: band test per lane, then the surviving windows
+// (full windows, prefixes, suffixes) of all 64 tasks as one flat job list, 64 jobs a round, each
+// job's text staged in its lane's LDS window.  Names with non-ASCII code points wave-serially.
+__global__ __launch_bounds__(RK_BLOCK) void kw_verify_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                             const int64_t *__restrict__ off, int n_regions,
+                                                             FastScratch S, DevScratch GS)
+{
     __shared__ uint32_t lvwin_all[RK_BLOCK * LV_WIN];
+    __shared__ uint16_t jobs_all[RK_BLOCK * LV_MAXJ];
+    __shared__ uint32_t okf_all[RK_BLOCK];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
     if (t >= n_regions) return;
+    (void)T;
+    uint32_t *win = lvwin_all + threadIdx.x * LV_WIN;
+    uint16_t *jobs = jobs_all + wib * WAVE * LV_MAXJ;
+    uint32_t *okf = okf_all + wib * WAVE;
+    OutCtx O;
+    O.out = S.tout + (size_t)t * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = S.tout_cnt[t];
+    XPush X = {S.xq + (size_t)t * S.xcap, S.xcap, S.xcnt[t]};
+    unsigned long long nver = 0, nwin = 0, nver_w = 0, nwin_w = 0;
+    const uint32_t nv = (TK_SKIP & 1) ? 0u : min(S.vcnt[t], S.vcap);
+    const uint4 *vq = S.vq + (size_t)t * S.vcap;
+    for (uint32_t k0 = 0; k0 < nv; k0 += WAVE) {
+        const uint32_t kk = k0 + (uint32_t)lane;
+        const bool valid = kk < nv;
+        const uint4 tk = valid ? vq[kk] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t doc = tk.x, P = tk.y >> 1, field = tk.y & 1u;
+        const bool todo = valid && !dset_contains(S, dset_key(doc, P, field));
+        const uint32_t pi = todo ? FT.pat_info[P] : 0u;
+        const uint32_t m = pi_m(pi);
+        const bool lanewise = todo && (pi & PI_ASCII) != 0;
+        int64_t fb = 0;
+        uint32_t n = 0;
+        if (todo) {
+            fb = off[2 * (int64_t)doc + field];
+            n = (uint32_t)(off[2 * (int64_t)doc + field + 1] - fb);
+        }
+        const uint32_t q = tk.z, o = tk.w & 0xFFu, pl = (tk.w >> 8) & 0xFFu;
+        uint64_t NW[8];
+        {
+            const int64_t nb = lanewise ? FT.pat_boff[P] : 0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                uint64_t x = 0;
+                if (lanewise && 8 * w < (int)m) x = load8(FT.pat_bytes, nb + 8 * w);
+                const int rem = (int)m - 8 * w;
+                if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
+                NW[w] = x;
+            }
+        }
+        // band test -> this lane's window jobs
+        int64_t pmin = 0;
+        uint32_t nwj = 0, pre = 0, cj = 0;
+        if (lanewise) {
+            ++nver;
+            nwj = lv_band(arena, fb, n, NW, m, (int64_t)q - (int64_t)o, kfull(m), win, pmin);
+            pre = q + pl + 1 <= m ? 1u : 0u;
+            cj = nwj + pre + (q + m > n ? 1u : 0u);
+        }
+        int J = 0;
+        const int ex = wave_excl_scan((int)cj, &J);
+        okf[lane] = 0;
+        for (uint32_t j = 0; j < cj; ++j) jobs[ex + j] = (uint16_t)(lane | (j << 6));
+        wave_sync();
+        for (int g0 = 0; g0 < J; g0 += WAVE) {
+            const int g = g0 + lane;
+            const bool jv = g < J;
+            const uint32_t e = jv ? jobs[g] : 0u;
+            const int l = (int)(e & 63u);
+            const uint32_t j = e >> 6;
+            // the owner's task (every lane shuffles)
+            const uint32_t jm = (uint32_t)__shfl((int)m, l, WAVE);
+            const uint32_t jn = (uint32_t)__shfl((int)n, l, WAVE);
+            const uint32_t jnwj = (uint32_t)__shfl((int)nwj, l, WAVE);
+            const uint32_t jpre = (uint32_t)__shfl((int)pre, l, WAVE);
+            const uint32_t jpmin = (uint32_t)__shfl((int)(uint32_t)pmin, l, WAVE);
+            const uint32_t fbl = (uint32_t)__shfl((int)(uint32_t)fb, l, WAVE);
+            const uint32_t fbh = (uint32_t)__shfl((int)(uint32_t)((uint64_t)fb >> 32), l, WAVE);
+            const int64_t jfb = (int64_t)(((uint64_t)fbh << 32) | fbl);
+            uint64_t JW[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const uint32_t x0 = (uint32_t)__shfl((int)(uint32_t)NW[w], l, WAVE);
+                const uint32_t x1 = (uint32_t)__shfl((int)(uint32_t)(NW[w] >> 32), l, WAVE);
+                JW[w] = ((uint64_t)x1 << 32) | x0;
+            }
+            if (!jv) continue;
+            // job kind: full window at pmin + j, prefix text[:w] (w < m), suffix text[i:] (reversed)
+            const bool full = j < jnwj;
+            const bool rev = !full && !(j == jnwj && jpre);
+            const uint32_t len = full ? jm : jm - 1;
+            const int64_t start = full ? (int64_t)jpmin + j : (rev ? (int64_t)jn - len : 0);
+            const int64_t A = (jfb + start) & ~(int64_t)3;
+            const int64_t fe = jfb + jn;
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                const int64_t ad = A + 4 * w;
+                win[w] = (ad + 4 > jfb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+            }
+            const uint32_t d0 = (uint32_t)(jfb + start - A);
+            const uint64_t needle = low_mask(jm);
+            uint64_t V = ~0ull;
+            bool ok = false;
+            for (uint32_t s2 = 0; s2 < len; ++s2) {
+                const uint32_t bi = d0 + (rev ? len - 1 - s2 : s2);
+                const uint32_t c = (win[bi >> 2] >> (8 * (bi & 3))) & 0xFFu;
+                uint64_t M = lv_match(JW, c, needle);
+                if (rev) M = __builtin_bitreverse64(M) >> (64 - jm);   // bit i = name[m - 1 - i] == c
+                const uint64_t U = V & M;
+                V = (V + U) | (V - U);
+                if (!full && passes((uint32_t)__popcll(~V & needle), jm, s2 + 1)) { ok = true; break; }
+            }
+            if (full) ok = 20u * (jm - (uint32_t)__popcll(~V & needle)) < jm;
+            ++nwin;
+            if (ok) okf[l] = 1u;
+        }
+        wave_sync();
+        bool pass = lanewise && okf[lane] != 0;
+        // names lanes cannot take (non-ASCII code points), wave-serially
+        uint64_t wm = __ballot(todo && !lanewise);
+        while (wm) {
+            const int l = __builtin_ctzll(wm);
+            wm &= wm - 1;
+            FieldCtx F;
+            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readlane((int)doc, l),
+                         (uint32_t)__builtin_amdgcn_readlane((int)field, l));
+            const uint32_t lP = (uint32_t)__builtin_amdgcn_readlane((int)P, l);
+            const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
+            const uint32_t nm = (lane < (int)lm) ? FT.pat_cps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
+            const uint32_t lw = (uint32_t)__builtin_amdgcn_readlane((int)tk.w, l);
+            const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)tk.z, l);
+            ++nver_w;
+            const bool dec = fk_verify_piece(F, nm, lm, lq, lw & 0xFFu, (lw >> 8) & 0xFFu, nwin_w);
+            if (lane == l) pass = dec;
+        }
+        // decisions, lane-parallel: the first decision of (doc, name, field) emits or queues the regex search
+        const bool first = pass && dset_insert(S, dset_key(doc, P, field));
+        const bool rx = first && FT.pat_rxk[P] == RXK_REGEX;
+        emit_hits(O, GS, first && !rx, doc, P, KW_NOPOS, field);
+        xq_push(X, rx, doc, P, field);
+    }
+    if (lane == 0) S.tout_cnt[t] = O.n;
+    xq_close(S, X, t);
+    task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
+}
+
+// Edge tasks: one-deletion edge windows of the 11..20-code-point names.
+__global__ __launch_bounds__(RK_BLOCK) void kw_edge_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                           const int64_t *__restrict__ off, int n_regions,
+                                                           FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
+    __shared__ uint32_t cnt_all[RK_WAVES * 4];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    if (t >= n_regions) return;
+    (void)T;
     uint64_t *eitems = items_all + wib * FK_ITEMS;
-    uint64_t *rxtab = rxtab_all + wib * 128;
-    uint8_t *txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
     uint32_t *icnt = cnt_all + wib * 4;
     OutCtx O;
     O.out = S.tout + (size_t)t * S.out_cap;
     O.cap = S.out_cap;
-    O.n = 0;
-    unsigned long long nver = 0, nwin = 0, nedge = 0, nrx = 0, nrx_bt = 0, nrx_rounds = 0;
-    unsigned long long nver_w = 0, nwin_w = 0;   // wave-serial counts (every lane counts)
+    O.n = S.tout_cnt[t];
+    XPush X = {S.xq + (size_t)t * S.xcap, S.xcap, S.xcnt[t]};
+    unsigned long long nedge = 0;
     FieldCtx F;
-    // ---- verify tasks: lanes take 64 tasks at a time (ASCII names); other names wave-serially
-    {
-        const uint32_t nv = (TK_SKIP & 1) ? 0u : min(S.vcnt[t], S.vcap);
-        const uint4 *vq = S.vq + (size_t)t * S.vcap;
-        uint32_t *win = lvwin_all + threadIdx.x * LV_WIN;
-        for (uint32_t k0 = 0; k0 < nv; k0 += WAVE) {
-            const uint32_t kk = k0 + (uint32_t)lane;
-            const bool valid = kk < nv;
-            const uint4 tk = valid ? vq[kk] : make_uint4(0u, 0u, 0u, 0u);
-            const uint32_t doc = tk.x, P = tk.y >> 1, field = tk.y & 1u;
-            bool todo = valid && !dset_contains(S, dset_key(doc, P, field));
-            const uint32_t pi = todo ? FT.pat_info[P] : 0u;
-            const uint32_t m = pi_m(pi);
-            const bool lanewise = todo && (pi & PI_ASCII) != 0;
-            bool pass = false;
-            int64_t fb = 0;
-            uint32_t n = 0;
-            if (todo) {
-                fb = off[2 * (int64_t)doc + field];
-                n = (uint32_t)(off[2 * (int64_t)doc + field + 1] - fb);
-            }
-            if (lanewise) {
-                uint64_t NW[8];
-                const int64_t nb = FT.pat_boff[P];
-#pragma unroll
-                for (int w = 0; w < 8; ++w) {
-                    uint64_t x = 0;
-                    if (8 * w < (int)m) x = load8(FT.pat_bytes, nb + 8 * w);
-                    const int rem = (int)m - 8 * w;
-                    if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
-                    NW[w] = x;
-                }
-                ++nver;
-                pass = lv_verify(arena, fb, n, NW, m, tk.z, tk.w & 0xFFu, (tk.w >> 8) & 0xFFu, win, nwin);
-            }
-            // decisions (and the names lanes cannot take) wave-serially
-            uint64_t wm = __ballot(pass || (todo && !lanewise));
-            while (wm) {
-                const int l = __builtin_ctzll(wm);
-                wm &= wm - 1;
-                const uint32_t ld = (uint32_t)__builtin_amdgcn_readlane((int)doc, l);
-                const uint32_t lP = (uint32_t)__builtin_amdgcn_readlane((int)P, l);
-                const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane((int)field, l);
-                const bool lpass = __builtin_amdgcn_readlane((int)pass, l) != 0;
-                fk_field_ctx(F, arena, off, ld, lf);
-                bool dec = lpass;
-                if (!lpass) {
-                    const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
-                    const uint32_t nm = (lane < (int)lm) ? FT.pat_cps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
-                    const uint32_t lw = (uint32_t)__builtin_amdgcn_readlane((int)tk.w, l);
-                    const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)tk.z, l);
-                    ++nver_w;
-                    dec = fk_verify_piece(F, nm, lm, lq, lw & 0xFFu, (lw >> 8) & 0xFFu, nwin_w);
-                }
-                if (dec) fk_decide_now(FT, T, S, GS, F, O, lP, rxtab, txt, nrx, nrx_bt, nrx_rounds);
-            }
-        }
-    }
-    // ---- edge tasks: one-deletion edge windows of the 11..20-code-point names
-    {
-        const uint32_t ne = (TK_SKIP & 2) ? 0u : min(S.ecnt[t], S.ecap);
-        const uint4 *eq = S.eq + (size_t)t * S.ecap;
-        for (uint32_t k = 0; k < ne; ++k) {
-            const uint4 tk = eq[k];
-            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
-                         (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
-            if (lane < 4) icnt[lane] = 0;
-            wave_sync();
-            uint32_t added = fk_edge_items(FT, F, eitems, &icnt[0], &icnt[1]);
-            added = (uint32_t)wave_sum((int)added);
-            if (!added) continue;
-            nedge += added;
-            wave_sync();
-            const uint32_t n_it = min(__builtin_amdgcn_readfirstlane(icnt[0]), (uint32_t)FK_ITEMS);
-            for (uint32_t i = 0; i < n_it; ++i) {
-                const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)it_pat(eitems[i]));
-                fk_decide_now(FT, T, S, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
-            }
-        }
-    }
-    // ---- short fields
-    {
-        const uint32_t ns = (TK_SKIP & 4) ? 0u : min(S.scnt[t], S.scap);
-        const uint4 *sq = S.sq + (size_t)t * S.scap;
-        for (uint32_t k = 0; k < ns; ++k) {
-            const uint4 tk = sq[k];
-            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
-                         (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
-            fk_short_field(FT, GS, F, O, nver, nwin, [&](uint32_t P) {
-                fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
-            });
-        }
-    }
-    // ---- regex-class names decided by an exact occurrence
-    {
-        const uint32_t nx = (TK_SKIP & 8) ? 0u : min(S.xcnt[t], S.xcap);
-        const uint4 *xq = S.xq + (size_t)t * S.xcap;
-        for (uint32_t k = 0; k < nx; ++k) {
-            const uint4 tk = xq[k];
-            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
-            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
-            fk_regex_now(FT, T, GS, F, O, y >> 1, rxtab, txt, nrx, nrx_bt, nrx_rounds);
-        }
+    const uint32_t ne = (TK_SKIP & 2) ? 0u : min(S.ecnt[t], S.ecap);
+    const uint4 *eq = S.eq + (size_t)t * S.ecap;
+    for (uint32_t k = 0; k < ne; ++k) {
+        const uint4 tk = eq[k];
+        fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
+        if (lane < 4) icnt[lane] = 0;
+        wave_sync();
+        uint32_t added = fk_edge_items(FT, F, eitems, &icnt[0], &icnt[1]);
+        added = (uint32_t)wave_sum((int)added);
+        if (!added) continue;
+        nedge += added;
+        wave_sync();
+        const uint32_t n_it = min(__builtin_amdgcn_readfirstlane(icnt[0]), (uint32_t)FK_ITEMS);
+        for (uint32_t i = 0; i < n_it; ++i)
+            fk_decide_queue(FT, S, GS, F, O, X, (uint32_t)__builtin_amdgcn_readfirstlane((int)it_pat(eitems[i])));
     }
     if (lane == 0) S.tout_cnt[t] = O.n;
-    unsigned long long v = nver, w = nwin;   // lane-parallel counts (one per task)
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-        v += __shfl_xor(v, dd, WAVE);
-        w += __shfl_xor(w, dd, WAVE);
+    xq_close(S, X, t);
+    task_stats(S, 0, 0, nedge, 0, 0, 0);
+}
+
+// Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
+__global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                            const int64_t *__restrict__ off, int n_regions,
+                                                            FastScratch S, DevScratch GS)
+{
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    if (t >= n_regions) return;
+    (void)T;
+    OutCtx O;
+    O.out = S.tout + (size_t)t * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = S.tout_cnt[t];
+    XPush X = {S.xq + (size_t)t * S.xcap, S.xcap, S.xcnt[t]};
+    unsigned long long nver_w = 0, nwin_w = 0;
+    FieldCtx F;
+    const uint32_t ns = (TK_SKIP & 4) ? 0u : min(S.scnt[t], S.scap);
+    const uint4 *sq = S.sq + (size_t)t * S.scap;
+    for (uint32_t k = 0; k < ns; ++k) {
+        const uint4 tk = sq[k];
+        fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
+        fk_short_field(FT, GS, F, O, nver_w, nwin_w,
+                       [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
     }
-    if (lane == 0) {
-        atomicAdd(&S.stats[2], w + nwin_w);   // nver_w / nwin_w: every lane holds the wave's count
-        atomicAdd(&S.stats[3], v + nver_w);
-        atomicAdd(&S.stats[7], nedge);
-        atomicAdd(&S.stats[10], nrx);
-        atomicAdd(&S.stats[11], nrx_bt);
-        atomicAdd(&S.stats[12], nrx_rounds);
+    if (lane == 0) S.tout_cnt[t] = O.n;
+    xq_close(S, X, t);
+    task_stats(S, nver_w, nwin_w, 0, 0, 0, 0);
+}
+
+// Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.
+__global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                              const int64_t *__restrict__ off, int n_regions,
+                                                              FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t rxtab_all[RK_WAVES * 128];
+    __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    if (t >= n_regions) return;
+    uint64_t *rxtab = rxtab_all + wib * 128;
+    uint8_t *txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
+    OutCtx O;
+    O.out = S.tout + (size_t)t * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = S.tout_cnt[t];
+    unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
+    FieldCtx F;
+    const uint32_t nx = (TK_SKIP & 8) ? 0u : min(S.xcnt[t], S.xcap);
+    const uint4 *xq = S.xq + (size_t)t * S.xcap;
+    for (uint32_t k = 0; k < nx; ++k) {
+        const uint4 tk = xq[k];
+        const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
+        fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
+        fk_regex_now(FT, T, GS, F, O, y >> 1, rxtab, txt, nrx, nrx_bt, nrx_rounds);
     }
+    if (lane == 0) S.tout_cnt[t] = O.n;
+    task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
 }
 
 // ---------------------------------------------------------------- kernel 1: the scan
