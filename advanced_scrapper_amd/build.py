@@ -61,14 +61,15 @@ def build_kwmatch_stage(stage: int, force: bool = False) -> str:
 
 
 def build_kwmatch_variant(tag: str, defines, force: bool = False) -> str:
-    """Profiling / tuning variant ``lib/libkwmatch_<tag>.so`` built with extra -D defines; bench only."""
+    """Profiling / tuning variant ``lib/libkwmatch_<tag>.so`` built with extra -D defines (entries
+    starting with '-' are passed as compiler flags); bench only."""
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, f'libkwmatch_{tag}.so')
     srcs = _kw_sources()
     if force or _stale(out, srcs):
         units = [s for s in srcs if s.endswith('.hip')]
         _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC'] +
-             [f'-D{d}' for d in defines] + ['-o', out] + units)
+             [d if d.startswith('-') else f'-D{d}' for d in defines] + ['-o', out] + units)
     return out
 
 

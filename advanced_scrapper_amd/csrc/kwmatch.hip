@@ -1050,15 +1050,20 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
         const int ntb = (nkb * FK_WAVES + RK_WAVES - 1) / RK_WAVES;
-        // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up)
-        hipLaunchKernelGGL(kw_verify_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
-                           nkb * FK_WAVES, h->FS, h->S);
-        hipLaunchKernelGGL(kw_edge_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
-                           nkb * FK_WAVES, h->FS, h->S);
-        hipLaunchKernelGGL(kw_short_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
-                           nkb * FK_WAVES, h->FS, h->S);
-        hipLaunchKernelGGL(kw_rx_task_kernel, dim3(ntb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
-                           nkb * FK_WAVES, h->FS, h->S);
+        // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up);
+        // G[k] waves share each scan wave's task region
+        int G[4] = {1, 4, 4, 1};
+        if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
+        auto task = [&](auto kern, int g) {
+            g = std::max(1, std::min(g, 16));
+            const int nb = (nkb * FK_WAVES * g + RK_WAVES - 1) / RK_WAVES;
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+                               nkb * FK_WAVES, g, h->FS, h->S);
+        };
+        task(kw_verify_kernel, G[0]);
+        task(kw_edge_kernel, G[1]);
+        task(kw_short_kernel, G[2]);
+        task(kw_rx_task_kernel, G[3]);
         HIPCHK(h, hipGetLastError());
         hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
                            n_docs, h->FS, h->S);
@@ -1154,6 +1159,8 @@ static int finish(kw_handle *h)
         h->stats[2] = fst[2] + gst[2];
         h->stats[3] = fst[3];
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
+        if (getenv("KW_DUMP_TIMING"))   // FK_TIMING builds: scan-kernel cycles summed over waves
+            fprintf(stderr, "KW_TIMING probe %llu epilogue %llu total %llu\n", fst[13], fst[14], fst[15]);
         h->n_hits = (int64_t)tot;
         h->fetched = true;
         return KW_OK;

@@ -26,6 +26,12 @@
 #define FK_NOPROBE 0
 #endif
 // waves per SIMD the resolve kernel is compiled for (register budget)
+#ifndef FK_TIMING   // developer aid: per-phase cycle counters of the scan kernel (stats 13..15)
+#define FK_TIMING 0
+#endif
+#define FK_T0(v) const unsigned long long v = FK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
+#define FK_TACC(acc, v) do { if (FK_TIMING) acc += __builtin_amdgcn_s_memtime() - (v); } while (0)
+
 #ifndef RK_OCC
 #define RK_OCC 4
 #endif
@@ -61,6 +67,14 @@ __device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], int j)
     if (j >= 8) { a = W[2]; b = W[3]; }
     if (j >= 12) { a = W[3]; b = W[4]; }
     return __builtin_amdgcn_alignbyte(b, a, j & 3);
+}
+
+// a 64-bit value of lane l (wave-uniform result)
+__device__ __forceinline__ int64_t rdlane64(int64_t v, int l)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ bool lds_bit(const uint32_t *t, uint32_t idx) { return (t[idx >> 5] >> (idx & 31)) & 1u; }
@@ -614,6 +628,24 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
     return emitted;
 }
 
+// sort the n <= 64 keys held by lanes [0, n) (the other lanes hold ~0): few keys by rank and an
+// LDS scatter into buf (n slots, this wave's), more by the register bitonic network
+__device__ __forceinline__ uint64_t wave_sort_few(uint64_t x, uint32_t n, uint64_t *buf)
+{
+    if (n > 24) return wave_sort_reg(x);
+    const int lane = lane_id();
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint64_t y = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
+        r += (y < x || (y == x && (int)j < lane)) ? 1u : 0u;
+    }
+    wave_sync();
+    if (lane < (int)n) buf[r] = x;
+    wave_sync();
+    return lane < (int)n ? buf[lane] : ~0ull;
+}
+
 // sort n <= FK_ITEMS u64 keys in this wave's LDS buffer (bitonic over the next power of two; pads with ~0)
 __device__ void wave_sort_lds(uint64_t *a, uint32_t n)
 {
@@ -1003,8 +1035,8 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             }
             const uint32_t NB = be - bs;
             uint64_t it = (lane < (int)NB) ? its[bs + lane] : ~0ull;
+            it = wave_sort_few(it, NB, its + bs);
             bs = be;
-            it = wave_sort_reg(it);
             const bool valid = lane < (int)NB;
             const uint32_t pat = valid ? it_pat(it) : 0xFFFFFu;
             const uint32_t kind = it_kind(it);
@@ -1027,16 +1059,17 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             const uint64_t fullm = __ballot(live && kind == FU_FULL);
             const bool decided = (fullm & gmask) != 0;
             // pieces of undecided fuzzy names -> verify tasks (one per alignment base)
-            uint64_t vneed = __ballot(live && fuzzy && !decided && kind == FU_PIECE);
+            const bool vpiece = live && fuzzy && !decided && kind == FU_PIECE;
+            const uint32_t vinfo = vpiece ? FT.use_info1[use] : 0u;   // all lanes' loads in flight at once
+            uint64_t vneed = __ballot(vpiece);
             uint32_t last_P = 0xFFFFFFFFu;
             int64_t last_base = -1;
             while (vneed) {
                 const int l = __builtin_ctzll(vneed);
                 vneed &= vneed - 1;
                 const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pat, l);
-                const uint32_t uu = (uint32_t)__builtin_amdgcn_readlane((int)use, l);
                 const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)bpos, l);   // ASCII: byte = code point
-                const uint32_t info1 = FT.use_info1[uu];
+                const uint32_t info1 = (uint32_t)__builtin_amdgcn_readlane((int)vinfo, l);
                 const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
                 const int64_t base = (int64_t)q - (int64_t)o;
                 if (P == last_P && base == last_base) continue;
@@ -1072,15 +1105,14 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             emit_hits(O, GS, (keep >> lane) & 1ull, F.doc, pat, cpos, F.field);
             // exactly decided fuzzy names: an edge window (11 <= m <= 20) may decide them again -> the set;
             // regex-class ones get their re.finditer search
-            uint64_t dm = __ballot(head && live && fuzzy && decided);
-            while (dm) {
-                const int l = __builtin_ctzll(dm);
-                dm &= dm - 1;
-                const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pat, l);
-                const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
-                const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)rxk, l);
-                if (mm >= EDGE_MIN_M && mm <= EDGE_MAX_M) (void)dset_insert_wave(S, D.doc, P, f);
-                if (rk == RXK_REGEX) task_push(xq, S.xcap, TC.x, make_uint4(D.doc, (P << 1) | f, 0u, 0u));
+            const bool dec_head = head && live && fuzzy && decided;
+            if (dec_head && m >= EDGE_MIN_M && m <= EDGE_MAX_M) (void)dset_insert(S, dset_key(D.doc, pat, f));
+            const bool xrx = dec_head && rxk == RXK_REGEX;
+            const uint64_t xm = __ballot(xrx);
+            if (xm) {
+                const uint32_t xi = TC.x + mbcnt(xm);
+                if (xrx && xi < S.xcap) xq[xi] = make_uint4(D.doc, (pat << 1) | f, 0u, 0u);
+                TC.x += (uint32_t)__popcll(xm);
             }
         }
     }
@@ -1195,30 +1227,55 @@ __device__ uint32_t lv_band(const uint8_t *__restrict__ arena, int64_t fb, uint3
     return pmax >= pmin ? (uint32_t)(pmax - pmin + 1) : 0u;
 }
 
-// regex-class names decided in the task kernels -> the region's regex queue (xq), lane-parallel
+// regex-class names decided in the task kernels -> the region's regex queue (xq), lane-parallel;
+// several waves may append to one region (atomic count)
 struct XPush {
     uint4 *q;
-    uint32_t cap, n;   // n: wave-uniform running count
+    uint32_t cap;
+    uint32_t *cnt;
+    uint32_t *tmax;
+    uint32_t *status;
 };
 
 __device__ __forceinline__ void xq_push(XPush &X, bool pred, uint32_t doc, uint32_t P, uint32_t field)
 {
     const uint64_t m = __ballot(pred);
     if (!m) return;
-    const uint32_t idx = X.n + mbcnt(m);
-    if (pred && idx < X.cap) X.q[idx] = make_uint4(doc, (P << 1) | field, 0u, 0u);
-    X.n += (uint32_t)__popcll(m);
-}
-
-__device__ __forceinline__ void xq_close(const FastScratch &S, const XPush &X, int64_t t)
-{
-    if (lane_id() == 0) {
-        S.xcnt[t] = X.n;
-        if (X.n > X.cap) {
-            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
-            atomicMax(&S.tmax[3], X.n);
+    uint32_t b = 0;
+    if (lane_id() == 0) b = atomicAdd(X.cnt, (uint32_t)__popcll(m));
+    b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+    const uint32_t idx = b + mbcnt(m);
+    if (pred) {
+        if (idx < X.cap) {
+            X.q[idx] = make_uint4(doc, (P << 1) | field, 0u, 0u);
+        } else {
+            atomicOr(X.status, ST_TASK_OVERFLOW);
+            atomicMax(X.tmax, idx + 1);
         }
     }
+}
+
+__device__ __forceinline__ XPush xq_region(const FastScratch &S, int64_t t)
+{
+    XPush X;
+    X.q = S.xq + (size_t)t * S.xcap;
+    X.cap = S.xcap;
+    X.cnt = S.xcnt + t;
+    X.tmax = S.tmax + 3;
+    X.status = S.status;
+    return X;
+}
+
+// region t's result list, shared by the waves working the region
+__device__ __forceinline__ OutCtx tout_region(const FastScratch &S, int64_t t)
+{
+    OutCtx O;
+    O.shared = nullptr;
+    O.out = S.tout + (size_t)t * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    O.shared = S.tout_cnt + t;
+    return O;
 }
 
 // a name decided without an exact occurrence (edge window): the first decision emits `name: []`
@@ -1263,8 +1320,8 @@ constexpr int LV_MAXJ = 16;   // window jobs per verify task: <= 2 kfull(64) + 1
 // Verify tasks.  Lanes take 64 tasks at a time: band test per lane, then the surviving windows
 // (full windows, prefixes, suffixes) of all 64 tasks as one flat job list, 64 jobs a round, each
 // job's text staged in its lane's LDS window.  Names with non-ASCII code points wave-serially.
-__global__ __launch_bounds__(RK_BLOCK) void kw_verify_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                             const int64_t *__restrict__ off, int n_regions,
+__global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                             const int64_t *__restrict__ off, int n_regions, int G,
                                                              FastScratch S, DevScratch GS)
 {
     __shared__ uint32_t lvwin_all[RK_BLOCK * LV_WIN];
@@ -1272,21 +1329,20 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_verify_kernel(FastTables FT, DevT
     __shared__ uint32_t okf_all[RK_BLOCK];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
-    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
+    const int64_t t = gw / G;
+    const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     (void)T;
     uint32_t *win = lvwin_all + threadIdx.x * LV_WIN;
     uint16_t *jobs = jobs_all + wib * WAVE * LV_MAXJ;
     uint32_t *okf = okf_all + wib * WAVE;
-    OutCtx O;
-    O.out = S.tout + (size_t)t * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = S.tout_cnt[t];
-    XPush X = {S.xq + (size_t)t * S.xcap, S.xcap, S.xcnt[t]};
+    OutCtx O = tout_region(S, t);
+    XPush X = xq_region(S, t);
     unsigned long long nver = 0, nwin = 0, nver_w = 0, nwin_w = 0;
     const uint32_t nv = (TK_SKIP & 1) ? 0u : min(S.vcnt[t], S.vcap);
     const uint4 *vq = S.vq + (size_t)t * S.vcap;
-    for (uint32_t k0 = 0; k0 < nv; k0 += WAVE) {
+    for (uint32_t k0 = sub * WAVE; k0 < nv; k0 += (uint32_t)G * WAVE) {
         const uint32_t kk = k0 + (uint32_t)lane;
         const bool valid = kk < nv;
         const uint4 tk = valid ? vq[kk] : make_uint4(0u, 0u, 0u, 0u);
@@ -1405,35 +1461,32 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_verify_kernel(FastTables FT, DevT
         emit_hits(O, GS, first && !rx, doc, P, KW_NOPOS, field);
         xq_push(X, rx, doc, P, field);
     }
-    if (lane == 0) S.tout_cnt[t] = O.n;
-    xq_close(S, X, t);
     task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
 }
 
 // Edge tasks: one-deletion edge windows of the 11..20-code-point names.
 __global__ __launch_bounds__(RK_BLOCK) void kw_edge_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                           const int64_t *__restrict__ off, int n_regions,
+                                                           const int64_t *__restrict__ off, int n_regions, int G,
                                                            FastScratch S, DevScratch GS)
 {
     __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
     __shared__ uint32_t cnt_all[RK_WAVES * 4];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
-    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
+    const int64_t t = gw / G;
+    const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     (void)T;
     uint64_t *eitems = items_all + wib * FK_ITEMS;
     uint32_t *icnt = cnt_all + wib * 4;
-    OutCtx O;
-    O.out = S.tout + (size_t)t * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = S.tout_cnt[t];
-    XPush X = {S.xq + (size_t)t * S.xcap, S.xcap, S.xcnt[t]};
+    OutCtx O = tout_region(S, t);
+    XPush X = xq_region(S, t);
     unsigned long long nedge = 0;
     FieldCtx F;
     const uint32_t ne = (TK_SKIP & 2) ? 0u : min(S.ecnt[t], S.ecap);
     const uint4 *eq = S.eq + (size_t)t * S.ecap;
-    for (uint32_t k = 0; k < ne; ++k) {
+    for (uint32_t k = sub; k < ne; k += (uint32_t)G) {
         const uint4 tk = eq[k];
         fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
@@ -1448,70 +1501,63 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_edge_kernel(FastTables FT, DevTab
         for (uint32_t i = 0; i < n_it; ++i)
             fk_decide_queue(FT, S, GS, F, O, X, (uint32_t)__builtin_amdgcn_readfirstlane((int)it_pat(eitems[i])));
     }
-    if (lane == 0) S.tout_cnt[t] = O.n;
-    xq_close(S, X, t);
     task_stats(S, 0, 0, nedge, 0, 0, 0);
 }
 
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
 __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                            const int64_t *__restrict__ off, int n_regions,
+                                                            const int64_t *__restrict__ off, int n_regions, int G,
                                                             FastScratch S, DevScratch GS)
 {
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
-    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
+    const int64_t t = gw / G;
+    const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     (void)T;
-    OutCtx O;
-    O.out = S.tout + (size_t)t * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = S.tout_cnt[t];
-    XPush X = {S.xq + (size_t)t * S.xcap, S.xcap, S.xcnt[t]};
+    OutCtx O = tout_region(S, t);
+    XPush X = xq_region(S, t);
     unsigned long long nver_w = 0, nwin_w = 0;
     FieldCtx F;
     const uint32_t ns = (TK_SKIP & 4) ? 0u : min(S.scnt[t], S.scap);
     const uint4 *sq = S.sq + (size_t)t * S.scap;
-    for (uint32_t k = 0; k < ns; ++k) {
+    for (uint32_t k = sub; k < ns; k += (uint32_t)G) {
         const uint4 tk = sq[k];
         fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
         fk_short_field(FT, GS, F, O, nver_w, nwin_w,
                        [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
     }
-    if (lane == 0) S.tout_cnt[t] = O.n;
-    xq_close(S, X, t);
     task_stats(S, nver_w, nwin_w, 0, 0, 0, 0);
 }
 
 // Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.
 __global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                              const int64_t *__restrict__ off, int n_regions,
+                                                              const int64_t *__restrict__ off, int n_regions, int G,
                                                               FastScratch S, DevScratch GS)
 {
     __shared__ uint64_t rxtab_all[RK_WAVES * 128];
     __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
-    const int64_t t = (int64_t)blockIdx.x * RK_WAVES + wib;
+    const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
+    const int64_t t = gw / G;
+    const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     uint64_t *rxtab = rxtab_all + wib * 128;
     uint8_t *txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
-    OutCtx O;
-    O.out = S.tout + (size_t)t * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = S.tout_cnt[t];
+    OutCtx O = tout_region(S, t);
     unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
     FieldCtx F;
     const uint32_t nx = (TK_SKIP & 8) ? 0u : min(S.xcnt[t], S.xcap);
     const uint4 *xq = S.xq + (size_t)t * S.xcap;
-    for (uint32_t k = 0; k < nx; ++k) {
+    for (uint32_t k = sub; k < nx; k += (uint32_t)G) {
         const uint4 tk = xq[k];
         const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
         fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
         fk_regex_now(FT, T, GS, F, O, y >> 1, rxtab, txt, nrx, nrx_bt, nrx_rounds);
     }
-    if (lane == 0) S.tout_cnt[t] = O.n;
     task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
 }
 
@@ -1550,21 +1596,41 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     unsigned long long ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;
     const bool has_t3 = FT.has_t3 != 0;
     OutCtx O;                                 // hits of the documents this wave finishes itself
+    O.shared = nullptr;
     O.out = S.kout + (size_t)wave * S.out_cap;
     O.cap = S.out_cap;
     O.n = 0;
     TaskCounts TC = {0u, 0u, 0u, 0u};
 
+    // the next document's offsets are loaded one document ahead (lanes 0..2)
+    int64_t pf_off = (lane < 3 && wave < n_docs) ? off[2 * wave + lane] : 0;
+    // the 2-byte gate's byte ranges as SWAR constants (wave-uniform, loaded once)
+    const int n_gate = FT.n_gate;
+    uint32_t gate_a[4], gate_b[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        gate_a[r] = (0x80u - FT.gate_lo[r]) * 0x01010101u;
+        gate_b[r] = (0x7Fu - FT.gate_hi[r]) * 0x01010101u;
+    }
+    unsigned long long t_probe = 0, t_epi = 0;
+    FK_T0(t_all0);
     for (int64_t d = wave; d < n_docs; d += n_waves) {
         FastDoc D;
         D.arena = arena;
-        D.t0 = off[2 * d];
-        D.t1 = off[2 * d + 1];
-        D.t2 = off[2 * d + 2];
+        D.t0 = rdlane64(pf_off, 0);
+        D.t1 = rdlane64(pf_off, 1);
+        D.t2 = rdlane64(pf_off, 2);
         D.doc = (uint32_t)d;
+        pf_off = (lane < 3 && d + n_waves < n_docs) ? off[2 * (d + n_waves) + lane] : 0;
         if (lane < 4) icnt[lane] = 0;
-        wave_sync();
         bool defer = (D.t1 - D.t0 > MAX_FIELD_BYTES) || (D.t2 - D.t1 > MAX_FIELD_BYTES);
+        const int64_t base = D.t0 & ~(int64_t)15;
+        // the first tile's loads, in flight with the edge prefilter's
+        uint4 nv = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t nw4 = 0;
+        if (base + lane * 16 < D.t2) nv = *(const uint4 *)(arena + base + lane * 16);
+        if (lane == WAVE - 1 && base + SCAN_TILE < D.t2) nw4 = *(const uint32_t *)(arena + base + SCAN_TILE);
+        wave_sync();
         // edge prefilter: first / last four bytes of each field (lanes 0..3)
         uint32_t flags = 0;
         {
@@ -1581,20 +1647,19 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         }
         bool na0 = false, na1 = false;
         uint32_t qh = 0, qt = 0;                 // ring head / tail (wave-uniform)
-        const int64_t base = D.t0 & ~(int64_t)15;
         for (int64_t blk = base; blk < D.t2 && !defer; blk += SCAN_TILE) {
             const int64_t lp = blk + lane * 16;
             uint32_t W[5];
-            if (lp < D.t2) {
-                const uint4 v = *(const uint4 *)(arena + lp);
-                W[0] = v.x; W[1] = v.y; W[2] = v.z; W[3] = v.w;
-            } else {
-                W[0] = W[1] = W[2] = W[3] = 0;
-            }
+            W[0] = nv.x; W[1] = nv.y; W[2] = nv.z; W[3] = nv.w;
             W[4] = (uint32_t)__shfl_down((int)W[0], 1, WAVE);
-            if (lane == WAVE - 1) {
-                const int64_t q = blk + SCAN_TILE;
-                W[4] = (q < D.t2) ? *(const uint32_t *)(arena + q) : 0u;
+            if (lane == WAVE - 1) W[4] = nw4;
+            // the next tile's loads (double buffer)
+            {
+                const int64_t nb = blk + SCAN_TILE;
+                nv = make_uint4(0u, 0u, 0u, 0u);
+                nw4 = 0;
+                if (nb + lane * 16 < D.t2) nv = *(const uint4 *)(arena + nb + lane * 16);
+                if (lane == WAVE - 1 && nb + SCAN_TILE < D.t2) nw4 = *(const uint32_t *)(arena + nb + SCAN_TILE);
             }
             // lane-local position masks
             const int64_t rel0 = D.t0 - lp, rel2 = D.t2 - lp, rel1 = D.t1 - lp;
@@ -1628,19 +1693,18 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             hit &= valid;
             // 2-byte anchors: byte-class gate, then the exact bigram table
             uint32_t gate = 0;
-            if (FT.n_gate != 0) {
+            if (n_gate != 0) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t w = W[k];
                     uint32_t in80 = 0;
-                    if (FT.n_gate < 0) {
+                    if (n_gate < 0) {
                         in80 = 0x80808080u;
                     } else {
                         const uint32_t t = w & 0x7F7F7F7Fu;
-                        for (int r = 0; r < FT.n_gate; ++r) {
-                            const uint32_t a = t + (0x80u - FT.gate_lo[r]) * 0x01010101u;
-                            const uint32_t bb = t + (0x7Fu - FT.gate_hi[r]) * 0x01010101u;
-                            in80 |= a & ~bb & ~w & 0x80808080u;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            if (r < n_gate) in80 |= (t + gate_a[r]) & ~(t + gate_b[r]) & ~w & 0x80808080u;
                         }
                     }
                     while (in80) {
@@ -1678,7 +1742,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             if (qt - qh + (uint32_t)total > (uint32_t)FK_Q) {
                 while (qh != qt) {
                     const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
+                    FK_T0(tp0);
                     fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+                    FK_TACC(t_probe, tp0);
                     qh += c;
                 }
                 wave_sync();
@@ -1701,7 +1767,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 const bool more = rb + FK_Q < total;
                 while (qt - qh >= 64u || (more && qh != qt)) {
                     const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
+                    FK_T0(tp0);
                     fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+                    FK_TACC(t_probe, tp0);
                     qh += c;
                 }
                 if (more) wave_sync();
@@ -1713,7 +1781,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         // the rest of the ring
         while (!defer && qh != qt) {
             const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
+            FK_T0(tp0);
             fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+            FK_TACC(t_probe, tp0);
             qh += c;
         }
         wave_sync();
@@ -1736,7 +1806,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             }
         } else if (!(flags & (DH_NA0 | DH_NA1))) {
             // all ASCII: finished here, the rest as tasks (flat resolve)
+            FK_T0(te0);
             if (FK_STAGE >= 2) fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+            FK_TACC(t_epi, te0);
             h.y = n0 | (n1 << 8) | flags;
         } else {
             // items -> HBM (field 0 then field 1) for the resolve kernel
@@ -1766,6 +1838,13 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             atomicMax(&S.tmax[2], TC.s);
             atomicMax(&S.tmax[3], TC.x);
         }
+    }
+    if (FK_TIMING && lane == 0) {
+        unsigned long long t_all = 0;
+        FK_TACC(t_all, t_all0);
+        atomicAdd(&S.stats[13], t_probe);
+        atomicAdd(&S.stats[14], t_epi);
+        atomicAdd(&S.stats[15], t_all);
     }
     unsigned long long a = nanchor, c1 = ncand;
 #pragma unroll
@@ -1805,6 +1884,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
     uint32_t *blkcnt = S.cpbase + (size_t)wave * (CP_CAP / 16 + 2);
     OutCtx O;
+    O.shared = nullptr;
     O.out = S.out + (size_t)wave * S.out_cap;
     O.cap = S.out_cap;
     O.n = 0;

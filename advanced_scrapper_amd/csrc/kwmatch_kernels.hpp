@@ -139,7 +139,8 @@ __device__ __forceinline__ uint32_t to_cp(const FieldCtx &F, uint32_t bpos)
 struct OutCtx {
     kw_hit *out;
     uint32_t cap;
-    uint32_t n;   // wave-uniform running count
+    uint32_t n;        // wave-uniform running count
+    uint32_t *shared;  // non-null: the count lives here and several waves append (atomics)
 };
 
 // every lane with `emit` appends one record (order: lane order)
@@ -149,6 +150,11 @@ __device__ __forceinline__ void emit_hits(OutCtx &O, const DevScratch &S, bool e
     uint64_t m = __ballot(emit);
     if (!m) return;
     uint32_t r = mbcnt(m);
+    if (O.shared) {
+        uint32_t b = 0;
+        if (lane_id() == 0) b = atomicAdd(O.shared, (uint32_t)__popcll(m));
+        O.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+    }
     uint32_t idx = O.n + r;
     if (emit) {
         if (idx < O.cap) {
@@ -793,6 +799,7 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
     uint32_t *blkcnt = S.blkcnt + (size_t)wave * (CP_CAP / 16 + 2);
 
     OutCtx O;
+    O.shared = nullptr;
     O.out = S.out + (size_t)wave * S.out_cap;
     O.cap = S.out_cap;
     O.n = 0;
