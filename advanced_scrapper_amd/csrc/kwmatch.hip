@@ -971,7 +971,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.defer_cnt = (uint32_t *)(q + 16);
     h->FS.tmax = (uint32_t *)(q + 32);                  // 4 x u32
     h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
-    h->FS.stats = (unsigned long long *)(q + 128);      // 16 x u64 (fast path)
+    h->FS.stats = (unsigned long long *)(q + 128);      // 32 x u64 (fast path; 13.. developer counters)
     uint32_t *cnts = (uint32_t *)(q + 1024);
     h->out_cnt_all = cnts;
     h->FS.kout_cnt = cnts;
@@ -1037,7 +1037,7 @@ static int launch_scan(kw_handle *h)
     int rc = ensure_scratch(h, w);
     if (rc) return rc;
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
-    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 256, st));
+    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 384, st));
     HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
@@ -1151,7 +1151,7 @@ static int finish(kw_handle *h)
         }
         unsigned long long tot = 0;
         HIPCHK(h, hipMemcpy(&tot, h->d_offs + h->launched_waves, sizeof(tot), hipMemcpyDeviceToHost));
-        unsigned long long gst[3], fst[16];
+        unsigned long long gst[3], fst[32];
         HIPCHK(h, hipMemcpy(gst, h->S.stats, sizeof(gst), hipMemcpyDeviceToHost));
         HIPCHK(h, hipMemcpy(fst, h->FS.stats, sizeof(fst), hipMemcpyDeviceToHost));
         h->stats[0] = fst[0] + gst[0];
@@ -1160,7 +1160,8 @@ static int finish(kw_handle *h)
         h->stats[3] = fst[3];
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
         if (getenv("KW_DUMP_TIMING"))   // FK_TIMING builds: scan-kernel cycles summed over waves
-            fprintf(stderr, "KW_TIMING probe %llu epilogue %llu total %llu\n", fst[13], fst[14], fst[15]);
+            fprintf(stderr, "KW_TIMING probe %llu epilogue %llu total %llu batches %llu rounds %llu pairs %llu chunks %llu "
+                            "inner %llu\n", fst[13], fst[14], fst[15], fst[16], fst[17], fst[18], fst[19], fst[20]);
         h->n_hits = (int64_t)tot;
         h->fetched = true;
         return KW_OK;

@@ -32,6 +32,10 @@
 #define FK_T0(v) const unsigned long long v = FK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
 #define FK_TACC(acc, v) do { if (FK_TIMING) acc += __builtin_amdgcn_s_memtime() - (v); } while (0)
 
+#ifndef FK_GATE_ALL   // 1: look up the bigram table at every position; 0: only behind the byte-class gate
+#define FK_GATE_ALL 1
+#endif
+
 #ifndef RK_OCC
 #define RK_OCC 4
 #endif
@@ -105,11 +109,16 @@ __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_
 // by a wave prefix sum, so a popular anchor with many uses does not serialise
 // one lane; each use compares the first / last 8 bytes of its span (and the
 // middle when the span is longer than 16 bytes), then \b for uppercase names.
+struct ProbeCounters {   // FK_TIMING builds: probe batches, stage-A rounds, stage-B pairs / chunks, stage-A steps
+    unsigned long long batches, rounds, pairs, chunks, inner;
+};
+
 __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const DevTables &T, const FastDoc &D,
                                                  const uint2 *ring, uint32_t head, uint32_t cnt, uint64_t *items,
-                                                 uint32_t *icnt, unsigned long long &nanchor)
+                                                 uint32_t *icnt, unsigned long long &nanchor, ProbeCounters &PC)
 {
     if (FK_STAGE < 1 || FK_NOPROBE) return;
+    if (FK_TIMING) ++PC.batches;
     const int lane = lane_id();
     const uint8_t *__restrict__ arena = D.arena;
     const bool valid = lane < (int)cnt;
@@ -118,13 +127,42 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
     const int64_t fe = p < D.t1 ? D.t1 : D.t2;
     const uint32_t hi = valid ? ld_u32_unaligned(arena, p + 4) : 0u;
     const uint64_t h8 = (uint64_t)e.y | ((uint64_t)hi << 32);
-    int L = 5;                       // next key length to look up is L - 1
-    uint32_t tcur = 0, tend = 0;     // anchor records of the current key
+    // the hash lookups of the lane's key lengths 4, 3, 2 (try bits 0, 1, 2) go out together
+    uint32_t rb[3], re[3];
+    {
+        uint4 hs[3];
+        uint64_t key[3];
+        uint32_t slot[3];
+        bool want[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int Lk = 4 - i;
+            want[i] = valid && ((e.x >> i) & 1u) && p + Lk <= fe;
+            key[i] = ((uint64_t)Lk << 32) | (h8 & ((1ull << (8 * Lk)) - 1));
+            slot[i] = fk_ht_slot(key[i], FT.ht_mask);
+            hs[i] = want[i] ? FT.ht4[slot[i]] : make_uint4(~0u, ~0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            rb[i] = re[i] = 0;
+            for (;;) {
+                const uint64_t kk = (uint64_t)hs[i].x | ((uint64_t)hs[i].y << 32);
+                if (kk == key[i]) { rb[i] = hs[i].z; re[i] = hs[i].z + hs[i].w; break; }
+                if (kk == ~0ull) break;
+                slot[i] = (slot[i] + 1) & FT.ht_mask;
+                hs[i] = FT.ht4[slot[i]];
+            }
+        }
+    }
+    // anchor records still to test: [tcur, tend), then [rb[1], re[1]), then [rb[2], re[2])
+    uint32_t tcur = rb[0], tend = re[0], b1 = rb[1], e1 = re[1], b2 = rb[2], e2 = re[2];
     bool more = valid;
     while (__ballot(more)) {
-        // stage A: this lane's next matching anchor
-        uint32_t ub = 0, uc = 0;
-        while (more) {
+        // stage A: up to two matching anchors of this lane's candidate
+        uint32_t ub = 0, uc = 0, ub1 = 0, uc1 = 0, nm = 0;
+        if (FK_TIMING) ++PC.rounds;
+        while (more && nm < 2) {
+            if (FK_TIMING) ++PC.inner;
             if (tcur < tend) {
                 const uint4 ar = FT.arec[tcur++];
                 const uint32_t alen = ar.w & 0xFFu;
@@ -132,27 +170,22 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
                 const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
                 if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) continue;
                 ++nanchor;
-                ub = ar.z;
-                uc = ar.w >> 8;
-                break;
+                if (nm == 0) { ub = ar.z; uc = ar.w >> 8; }
+                else { ub1 = ar.z; uc1 = ar.w >> 8; }
+                ++nm;
+                continue;
             }
-            --L;
-            if (L < 2) { more = false; break; }
-            if (!((e.x >> (4 - L)) & 1u) || p + L > fe) continue;   // try4 = bit 0, try3 = bit 1, try2 = bit 2
-            const uint64_t key = ((uint64_t)L << 32) | (h8 & ((1ull << (8 * L)) - 1));
-            uint32_t slot = fk_ht_slot(key, FT.ht_mask);
-            for (;;) {
-                const uint4 hs = FT.ht4[slot];
-                const uint64_t kk = (uint64_t)hs.x | ((uint64_t)hs.y << 32);
-                if (kk == key) { tcur = hs.z; tend = hs.z + hs.w; break; }
-                if (kk == ~0ull) break;
-                slot = (slot + 1) & FT.ht_mask;
-            }
+            if (b1 >= e1 && b2 >= e2) { more = false; break; }
+            tcur = b1; tend = e1;
+            b1 = b2; e1 = e2;
+            b2 = e2 = 0;
         }
         // stage B: (candidate, use) pairs over the lanes
         int total;
-        const int ex = wave_excl_scan((int)uc, &total);
+        const int ex = wave_excl_scan((int)(uc + uc1), &total);
+        if (FK_TIMING) PC.pairs += (unsigned long long)total;
         for (int c0 = 0; c0 < total; c0 += WAVE) {
+            if (FK_TIMING) ++PC.chunks;
             const int g = c0 + lane;
             int owner = 0;   // the last lane whose prefix <= g
 #pragma unroll
@@ -162,7 +195,11 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
                 if (cand < WAVE && exc <= g) owner = cand;
             }
             const int exo = __shfl(ex, owner, WAVE);
-            const uint32_t u = (uint32_t)__shfl((int)ub, owner, WAVE) + (uint32_t)(g - exo);
+            const uint32_t oub = (uint32_t)__shfl((int)ub, owner, WAVE);
+            const uint32_t ouc = (uint32_t)__shfl((int)uc, owner, WAVE);
+            const uint32_t oub1 = (uint32_t)__shfl((int)ub1, owner, WAVE);
+            const uint32_t loc = (uint32_t)(g - exo);
+            const uint32_t u = loc < ouc ? oub + loc : oub1 + (loc - ouc);
             const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)p, owner, WAVE);
             const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)p >> 32), owner, WAVE);
             if (g >= total) continue;
@@ -1613,6 +1650,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         gate_b[r] = (0x7Fu - FT.gate_hi[r]) * 0x01010101u;
     }
     unsigned long long t_probe = 0, t_epi = 0;
+    ProbeCounters PC = {0, 0, 0, 0, 0};
     FK_T0(t_all0);
     for (int64_t d = wave; d < n_docs; d += n_waves) {
         FastDoc D;
@@ -1683,17 +1721,29 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 if (hb & in0) na0 = true;
                 if (hb & in1) na1 = true;
             }
-            uint32_t hit = 0;
+            uint32_t hit = 0, gate = 0;
+            if (FK_GATE_ALL && n_gate != 0) {
+                // stage 1 and the exact bigram table of the 2-byte anchors at every position
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
-                const uint32_t w = filt[fk_word(key)];
-                hit |= ((w >> fk_bit(key)) & 1u) << j;
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
+                    const uint32_t w = filt[fk_word(key)];
+                    const uint32_t x = fk_b2_index(key);
+                    hit |= ((w >> fk_bit(key)) & 1u) << j;
+                    gate |= ((b2[x >> 5] >> (x & 31)) & 1u) << j;
+                }
+                gate &= valid;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
+                    const uint32_t w = filt[fk_word(key)];
+                    hit |= ((w >> fk_bit(key)) & 1u) << j;
+                }
             }
             hit &= valid;
             // 2-byte anchors: byte-class gate, then the exact bigram table
-            uint32_t gate = 0;
-            if (n_gate != 0) {
+            if (!FK_GATE_ALL && n_gate != 0) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t w = W[k];
@@ -1743,7 +1793,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 while (qh != qt) {
                     const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
                     FK_T0(tp0);
-                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor, PC);
                     FK_TACC(t_probe, tp0);
                     qh += c;
                 }
@@ -1768,7 +1818,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 while (qt - qh >= 64u || (more && qh != qt)) {
                     const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
                     FK_T0(tp0);
-                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor, PC);
                     FK_TACC(t_probe, tp0);
                     qh += c;
                 }
@@ -1782,7 +1832,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         while (!defer && qh != qt) {
             const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
             FK_T0(tp0);
-            fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor);
+            fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor, PC);
             FK_TACC(t_probe, tp0);
             qh += c;
         }
@@ -1845,6 +1895,14 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         atomicAdd(&S.stats[13], t_probe);
         atomicAdd(&S.stats[14], t_epi);
         atomicAdd(&S.stats[15], t_all);
+        atomicAdd(&S.stats[16], PC.batches);
+        atomicAdd(&S.stats[17], PC.rounds);
+        atomicAdd(&S.stats[18], PC.pairs);
+        atomicAdd(&S.stats[19], PC.chunks);
+    }
+    if (FK_TIMING) {
+        const unsigned long long inner = wave_sum64(PC.inner);
+        if (lane == 0) atomicAdd(&S.stats[20], inner);
     }
     unsigned long long a = nanchor, c1 = ncand;
 #pragma unroll
