@@ -521,19 +521,19 @@ __device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint6
             const uint32_t c = lane >= 10 ? ct : ch;
             if ((uint32_t)j < L) hh = hh * SUB_B + c;
         }
-    } else if (act) {
-        if (lane >= 10) {   // suffix: walk back L code points from the field end
-            b0 = F.fe;
-            for (uint32_t j = 0; j < L; ++j) {
-                --b0;
-                while ((a[b0] & 0xC0) == 0x80) --b0;
-            }
-        }
-        int64_t b = b0;
-        for (uint32_t j = 0; j < L; ++j) {
-            uint32_t c;
-            b += decode_at(a, b, F.fe, &c);
-            hh = hh * SUB_B + c;
+    } else {
+        // decoded field: the wave holds the first and the last 20 code points
+        const int t20 = F.n < 20u ? (int)F.n : 20;
+        const uint32_t head = (lane < t20) ? F.cps[lane] : 0u;
+        const uint32_t tail = (lane < t20) ? F.cps[F.n - t20 + lane] : 0u;
+        b0 = lane >= 10 ? (int64_t)F.n - (int64_t)L : 0;   // window start, in code points
+        const int tbase = t20 - (int)L;
+#pragma unroll
+        for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j) {
+            const uint32_t ch = (uint32_t)__shfl((int)head, j, WAVE);
+            const uint32_t ct = (uint32_t)__shfl((int)tail, (tbase + j) & 63, WAVE);
+            const uint32_t c = lane >= 10 ? ct : ch;
+            if ((uint32_t)j < L) hh = hh * SUB_B + c;
         }
     }
     uint32_t added = 0;
@@ -553,10 +553,8 @@ __device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint6
             if (pi_m(FT.pat_info[P]) != L + 1) continue;
             const uint32_t *nm = FT.pat_cps + FT.pat_cp_off[P];
             bool eq = true;
-            int64_t bb = b0;
             for (uint32_t j = 0; j < L && eq; ++j) {
-                uint32_t c;
-                bb += decode_at(a, bb, F.fe, &c);
+                const uint32_t c = F.ascii ? (uint32_t)a[b0 + j] : F.cps[b0 + j];
                 eq = c == nm[j < del ? j : j + 1];
             }
             if (!eq) continue;
@@ -609,6 +607,24 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
             }
             wave_sync();
         } else {
+            // code points [r0, r0 + 2048 + L - 1) as bytes: ASCII as is, the rest as the marker 0x80
+            tb = r0;
+            const int64_t a1 = r0 + 2048 + L - 1 < n ? r0 + 2048 + L - 1 : n;
+            wave_sync();
+            for (int c = lane; c < RX_TXT / 16; c += WAVE) {
+                const int64_t i0 = r0 + 16 * (int64_t)c;
+                uint32_t wv[4] = {0u, 0u, 0u, 0u};
+                if (i0 < a1) {
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) {
+                        const uint4 v = *(const uint4 *)(F.cps + i0 + 4 * k4);   // the buffer holds FK_CP_CAP code points
+                        const uint32_t cc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) wv[k4] |= (cc[k] < 128u ? cc[k] : 0x80u) << (8 * k);
+                    }
+                }
+                ((uint4 *)txt)[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+            }
             wave_sync();
         }
         const int64_t s_lo = r0 + (int64_t)lane * 32;
@@ -617,8 +633,8 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
             const int64_t s_hi = s_lo + 32 < nstarts ? s_lo + 32 : nstarts;
             const int c_cnt = (int)(s_hi + L - 1 - s_lo);
             uint64_t D = 0;
+            const uint8_t *t = txt + (s_lo - tb);
             if (F.ascii) {
-                const uint8_t *t = txt + (s_lo - tb);
 #pragma unroll 8
                 for (int k = 0; k < c_cnt; ++k) {
                     D = ((D << 1) | 1ull) & tab[t[k] & 0x7Fu];
@@ -626,11 +642,12 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
                 }
             } else {
                 for (int k = 0; k < c_cnt; ++k) {
-                    const uint32_t c = F.cps[s_lo + k];
+                    const uint32_t b = t[k];
                     uint64_t B;
-                    if (c < 128) {
-                        B = tab[c];
+                    if (b < 128) {
+                        B = tab[b];
                     } else {
+                        const uint32_t c = F.cps[s_lo + k];
                         B = anym;
                         for (uint32_t e = eb; e < ee; ++e)
                             if (FT.rxf_ext_cp[e] == c) B |= FT.rxf_ext_mask[e];
@@ -830,7 +847,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
                                  uint64_t *items_lds, uint32_t *icnt_f, uint32_t *dflag, uint32_t *cps,
                                  uint32_t *blkcnt, uint64_t *rxtab, RxQueue &RQ, bool maybe_nonascii, bool edge,
                                  unsigned long long &nver,
-                                 unsigned long long &nwin, unsigned long long &nedge)
+                                 unsigned long long &nwin, unsigned long long &nedge, unsigned long long *tacc)
 {
     const int lane = lane_id();
     // ---- field facts (code points, ASCII) on demand
@@ -838,12 +855,15 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     // the scan's non-ASCII flags are exact per field
     F.ascii = !maybe_nonascii;
     F.n = (uint32_t)flen;
+    FK_T0(tr0);
     if (!F.ascii) {
         if (flen > (int64_t)FK_CP_CAP) return 1;
         F.n = decode_field_fast(F.arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
         F.cps = cps;
         F.blkcnt = blkcnt;
     }
+    FK_TACC(tacc[0], tr0);
+    FK_T0(tr1);
     const bool is_short = !(RK_SKIP & 1) && F.n <= (uint32_t)MAXM;
     // ---- one-deletion edge windows of the 11..20-code-point names (prefiltered by the scan)
     if (!(RK_SKIP & 2) && edge && F.n >= EDGE_MIN_M + 1) {
@@ -856,6 +876,8 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         }
     }
     wave_sync();
+    FK_TACC(tacc[1], tr1);
+    FK_T0(tr2);
     const uint32_t N = __builtin_amdgcn_readfirstlane(*icnt_f);
     if (N == 0 && !is_short) return 0;
     if (N > (uint32_t)WAVE) {
@@ -873,8 +895,8 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         }
         const uint32_t NB = be - bs;
         uint64_t it = (lane < (int)NB) ? items_lds[bs + lane] : ~0ull;
+        it = wave_sort_few(it, NB, items_lds + bs);
         bs = be;
-        it = wave_sort_reg(it);
         const bool valid = lane < (int)NB;
         const uint32_t pat = valid ? it_pat(it) : 0xFFFFFu;
         const uint32_t kind = it_kind(it);
@@ -897,7 +919,11 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         const uint64_t fullm = __ballot(live && (kind == FU_FULL || kind == FU_EDGE));
         const bool decided_full = (fullm & gmask) != 0;
         // ---- verification of pieces of undecided fuzzy names (wave-serial over such items)
-        uint64_t vneed = __ballot(live && fuzzy && !decided_full && kind == FU_PIECE);
+        const bool vpiece = live && fuzzy && !decided_full && kind == FU_PIECE;
+        // every piece lane's use record and code point position at once
+        const uint32_t vinfo = vpiece ? FT.use_info1[use] : 0u;
+        const uint32_t vq = vpiece ? to_cp_fast(F, bpos) : 0u;
+        uint64_t vneed = __ballot(vpiece);
         uint64_t decided_v = 0;   // bit per lane: its group got decided by a window
         uint32_t last_P = 0xFFFFFFFFu, nm = 0xFFFFFFFDu;
         int64_t last_base = -1;
@@ -908,11 +934,9 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
             if (decided_v & lg) continue;                       // group already decided
             const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pat, l);
             const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
-            const uint32_t uu = (uint32_t)__builtin_amdgcn_readlane((int)use, l);
-            const uint32_t bp = (uint32_t)__builtin_amdgcn_readlane((int)bpos, l);
-            const uint32_t info1 = FT.use_info1[uu];
+            const uint32_t info1 = (uint32_t)__builtin_amdgcn_readlane((int)vinfo, l);
             const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
-            const uint32_t q = to_cp_fast(F, bp);
+            const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)vq, l);
             // pieces of one occurrence share the alignment base = q - o: verify it once
             const int64_t base = (int64_t)q - (int64_t)o;
             if (P == last_P && base == last_base) continue;
@@ -964,8 +988,11 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
             fk_regex_enqueue(GS, F, (uint32_t)__shfl((int)pat, l, WAVE), RQ);
         }
     }
+    FK_TACC(tacc[2], tr2);
     // ---- short field: the field is the needle, the longer names are the haystacks
+    FK_T0(tr3);
     if (is_short) fk_short_field(FT, GS, F, O, nver, nwin, [&](uint32_t P) { fk_regex_enqueue(GS, F, P, RQ); });
+    FK_TACC(tacc[3], tr3);
     return 0;
 }
 
@@ -1899,6 +1926,10 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         atomicAdd(&S.stats[17], PC.rounds);
         atomicAdd(&S.stats[18], PC.pairs);
         atomicAdd(&S.stats[19], PC.chunks);
+        atomicAdd(&S.stats[27], (unsigned long long)TC.v);
+        atomicAdd(&S.stats[28], (unsigned long long)TC.e);
+        atomicAdd(&S.stats[29], (unsigned long long)TC.s);
+        atomicAdd(&S.stats[30], (unsigned long long)TC.x);
     }
     if (FK_TIMING) {
         const unsigned long long inner = wave_sum64(PC.inner);
@@ -1953,6 +1984,8 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     RQ.txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
     unsigned long long nver = 0, nwin = 0, nedge = 0, ndefer = 0, ndef_cp = 0, ndef_items = 0, nres = 0;
     unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
+    unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0};   // FK_TIMING: decode, edge, items, short, regex, all
+    FK_T0(tall0);
 
     for (int64_t c0 = wave * WAVE; c0 < n_docs; c0 += n_waves * WAVE) {
         const int64_t dl = c0 + lane;
@@ -1989,7 +2022,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
                 const bool na = (hy & (f ? DH_NA1 : DH_NA0)) != 0;
                 const bool edge = (hy & (f ? DH_EDGE1 : DH_EDGE0)) != 0;
                 const int rs = FK_STAGE < 2 ? 0 : fk_resolve_field(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps,
-                                                                   blkcnt, rxtab, RQ, na, edge, nver, nwin, nedge);
+                                                                   blkcnt, rxtab, RQ, na, edge, nver, nwin, nedge, tacc);
                 if (rs) {
                     defer = true;
                     if (rs == 1) ++ndef_cp;
@@ -2013,6 +2046,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     wave_sync_global();
     if (RQ.n > RQ.cap && lane == 0) atomicMax(&GS.status[2], RQ.n);   // the queue size a rescan needs
     const uint32_t n_rx = RQ.n < RQ.cap ? RQ.n : RQ.cap;
+    FK_T0(trx0);
     for (uint32_t t = 0; t < n_rx; ++t) {
         const uint4 tk = RQ.q[t];
         const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x);
@@ -2037,6 +2071,10 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
                                                          : ((RK_SKIP & 16) ? 1u : rx_positions(T, GS, F, O, P)));
         if (cnt == 0) emit_hits(O, GS, lane == 0, d, P, KW_NOPOS, F.field);
     }
+    FK_TACC(tacc[4], trx0);
+    FK_TACC(tacc[5], tall0);
+    if (FK_TIMING && lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&S.stats[21 + i], tacc[i]);
     if (lane == 0) S.out_cnt[wave] = O.n;
     unsigned long long v = nver, w = nwin;
 #pragma unroll
