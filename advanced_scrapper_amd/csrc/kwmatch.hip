@@ -287,14 +287,17 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
                         if (j != del) hh = hh * SUB_B + cps[i][j];
                     const uint64_t key = (hh + (uint64_t)(m - 1) * 0x9E3779B97F4A7C15ull) | 1ull;
                     B.edge[key].push_back(((uint32_t)i << 5) | del);
-                    // prefilter keys: first / last four UTF-8 bytes of the variant
+                    // prefilter keys: first / last eight UTF-8 bytes of the variant (>= 10 code points)
                     std::string v;
                     v.append((const char *)s, utf8_offset(cps[i], del));
                     v.append((const char *)s + utf8_offset(cps[i], del + 1), bl - utf8_offset(cps[i], del + 1));
                     const uint8_t *vp = (const uint8_t *)v.data();
-                    const uint32_t kp = (uint32_t)vp[0] | ((uint32_t)vp[1] << 8) | ((uint32_t)vp[2] << 16) | ((uint32_t)vp[3] << 24);
-                    const uint8_t *ve = vp + v.size() - 4;
-                    const uint32_t ks = (uint32_t)ve[0] | ((uint32_t)ve[1] << 8) | ((uint32_t)ve[2] << 16) | ((uint32_t)ve[3] << 24);
+                    uint64_t kp = 0, ks = 0;
+                    const uint8_t *ve = vp + v.size() - 8;
+                    for (int k = 0; k < 8; ++k) {
+                        kp |= (uint64_t)vp[k] << (8 * k);
+                        ks |= (uint64_t)ve[k] << (8 * k);
+                    }
                     B.edge_pre[fk_edge_index(kp) >> 5] |= 1u << (fk_edge_index(kp) & 31);
                     B.edge_suf[fk_edge_index(ks) >> 5] |= 1u << (fk_edge_index(ks) & 31);
                 }
@@ -1061,7 +1064,6 @@ static int launch_scan(kw_handle *h)
                                nkb * FK_WAVES, g, h->FS, h->S);
         };
         task(kw_verify_kernel, G[0]);
-        task(kw_edge_kernel, G[1]);
         task(kw_short_kernel, G[2]);
         task(kw_rx_task_kernel, G[3]);
         HIPCHK(h, hipGetLastError());
@@ -1164,7 +1166,8 @@ static int finish(kw_handle *h)
                             "inner %llu | resolve decode %llu edge %llu items %llu short %llu regex %llu all %llu\n", fst[13], fst[14],
                     fst[15], fst[16], fst[17], fst[18], fst[19], fst[20], fst[21], fst[22], fst[23], fst[24], fst[25],
                     fst[26]);
-            fprintf(stderr, "KW_TASKS verify %llu edge %llu short %llu regex %llu\n", fst[27], fst[28], fst[29], fst[30]);
+            fprintf(stderr, "KW_TASKS verify %llu edge %llu short %llu regex %llu edge_docs %llu\n", fst[27], fst[28], fst[29],
+                    fst[30], fst[31]);
         h->n_hits = (int64_t)tot;
         h->fetched = true;
         return KW_OK;

@@ -38,7 +38,7 @@ constexpr int FK_FILT_WORDS = 8192;             // stage 1: 2^18 bits = 32 KB
 constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
 constexpr int FK_T3_BITS = 16;                  // stage 2, 3-byte keys: 8 KB
 constexpr int FK_B2_WORDS = 2048;               // exact bigram table: 8 KB
-constexpr int FK_EDGE_BITS = 15;                // edge prefix / suffix keys: 2 x 4 KB
+constexpr int FK_EDGE_BITS = 20;                // edge prefix / suffix 8-byte keys: 2 x 128 KB (global, L2)
 constexpr int FK_Q = 256;                       // per-wave ring of stage-2 survivors (power of 2)
 constexpr int FK_ITEMS = 128;                   // items per field on the fast path
 constexpr int FK_CP_CAP = 16384;                // bytes of a non-ASCII field the fast path decodes
@@ -170,9 +170,9 @@ __host__ __device__ __forceinline__ uint32_t fk_t3_index(uint32_t key4)
 {
     return ((key4 & 0xFFFFFFu) * FK_MUL3) >> (32 - FK_T3_BITS);
 }
-__host__ __device__ __forceinline__ uint32_t fk_edge_index(uint32_t key4)
+__host__ __device__ __forceinline__ uint32_t fk_edge_index(uint64_t key8)
 {
-    return (key4 * FK_MUL4) >> (32 - FK_EDGE_BITS);
+    return (uint32_t)((key8 * 0x9E3779B97F4A7C15ull) >> (64 - FK_EDGE_BITS));
 }
 __host__ __device__ __forceinline__ uint32_t fk_b2_index(uint32_t key2)
 {

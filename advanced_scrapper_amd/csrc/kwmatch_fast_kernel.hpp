@@ -36,6 +36,10 @@
 #define FK_GATE_ALL 1
 #endif
 
+#ifndef FK_EPI_EDGE   // developer aid: 3 = edge windows in the epilogue; 1 = code present, never run; 0 = absent
+#define FK_EPI_EDGE 3
+#endif
+
 #ifndef RK_OCC
 #define RK_OCC 4
 #endif
@@ -110,7 +114,7 @@ __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_
 // one lane; each use compares the first / last 8 bytes of its span (and the
 // middle when the span is longer than 16 bytes), then \b for uppercase names.
 struct ProbeCounters {   // FK_TIMING builds: probe batches, stage-A rounds, stage-B pairs / chunks, stage-A steps
-    unsigned long long batches, rounds, pairs, chunks, inner;
+    unsigned long long batches, rounds, pairs, chunks, inner, edge_docs;
 };
 
 __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const DevTables &T, const FastDoc &D,
@@ -1000,9 +1004,9 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
 // ---------------------------------------------------------------- flat resolve (all-ASCII documents)
 // The scan kernel finishes an all-ASCII document itself (fk_scan_epilogue): it sorts the document's
 // items, emits the positions of uppercase names and of exact occurrences of literal fuzzy names,
-// and leaves the rest as tasks in its wave's task regions for the task kernels (kw_verify_kernel, kw_edge_kernel, kw_short_kernel, kw_rx_task_kernel):
+// (edge windows included) and leaves the rest as tasks in its wave's task regions for the task kernels
+// (kw_verify_kernel, kw_short_kernel, kw_rx_task_kernel):
 //   vq  {doc, P << 1 | field, q, o | pl << 8}   a pigeonhole piece of an undecided fuzzy name
-//   eq  {doc, field, 0, 0}                       a field flagged by the edge prefilter
 //   sq  {doc, field, 0, 0}                       a field of <= 64 code points
 //   xq  {doc, P << 1 | field, 0, 0}              a regex-class name decided by an exact occurrence
 // A name can be decided by more than one source (an exact occurrence and an edge window; several
@@ -1070,7 +1074,7 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                                  TaskCounts &TC)
 {
     const int lane = lane_id();
-    uint4 *vq = S.vq + (size_t)wave * S.vcap, *eq = S.eq + (size_t)wave * S.ecap;
+    uint4 *vq = S.vq + (size_t)wave * S.vcap;
     uint4 *sq = S.sq + (size_t)wave * S.scap, *xq = S.xq + (size_t)wave * S.xcap;
     for (uint32_t f = 0; f < 2; ++f) {
         FieldCtx F;
@@ -1085,7 +1089,6 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
         F.field = f;
         const uint32_t N = f ? n1 : n0;
         uint64_t *its = items + f * FK_ITEMS;
-        if ((flags & (f ? DH_EDGE1 : DH_EDGE0)) && F.n >= EDGE_MIN_M + 1) task_push(eq, S.ecap, TC.e, make_uint4(D.doc, f, 0u, 0u));
         if (F.n <= (uint32_t)MAXM) task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
         if (N == 0) continue;
         if (N > (uint32_t)WAVE) wave_sort_lds(its, N);
@@ -1178,6 +1181,74 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                 if (xrx && xi < S.xcap) xq[xi] = make_uint4(D.doc, (pat << 1) | f, 0u, 0u);
                 TC.x += (uint32_t)__popcll(xm);
             }
+        }
+    }
+    // ---- one-deletion edge windows of the 11..20-code-point names, both fields at once:
+    // lane 20 f + 10 side + (L - 10) hashes the first (side 0) or last (side 1) L bytes of field f
+    if ((FK_EPI_EDGE & 1) && (flags & (DH_EDGE0 | DH_EDGE1)) && (FK_EPI_EDGE & 2)) {
+        const int f = lane >= 20 ? 1 : 0;
+        const int sidx = lane - 20 * f;
+        const uint32_t L = (EDGE_MIN_M - 1) + (uint32_t)(sidx % 10);
+        const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+        const bool act = lane < 40 && (flags & (f ? DH_EDGE1 : DH_EDGE0)) && fe - fb >= (int64_t)L + 2;
+        const int64_t w0 = sidx >= 10 ? fe - (int64_t)L : fb;
+        uint64_t hh = 0;
+        uint32_t wb[5] = {0u, 0u, 0u, 0u, 0u};   // the window's first 20 bytes
+        if (act) {
+            const int64_t a0 = w0 & ~(int64_t)3;
+            const uint32_t sh = (uint32_t)(w0 & 3);
+            uint32_t dw[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dw[i] = *(const uint32_t *)(D.arena + a0 + 4 * i);   // the arena is padded
+#pragma unroll
+            for (int i = 0; i < 5; ++i) wb[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+#pragma unroll
+            for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j)
+                if ((uint32_t)j < L) hh = hh * SUB_B + ((wb[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        }
+        uint32_t ecur = 0, eend = 0;
+        if (act) {
+            const uint64_t key = (hh + (uint64_t)L * 0x9E3779B97F4A7C15ull) | 1ull;
+            uint32_t slot = (uint32_t)(key >> 32) & FT.edge_mask;
+            for (;;) {
+                const uint64_t kk = FT.edge_key[slot];
+                if (kk == key) { ecur = FT.edge_begin[slot]; eend = ecur + FT.edge_cnt[slot]; break; }
+                if (kk == 0) break;
+                slot = (slot + 1) & FT.edge_mask;
+            }
+        }
+        // one matching variant per lane per round (a lane rarely has two)
+        while (__ballot(ecur < eend)) {
+            uint32_t P = 0;
+            bool hit = false;
+            while (ecur < eend && !hit) {
+                const uint32_t ent = FT.edge_ent[ecur++];
+                P = ent >> 5;
+                const uint32_t del = ent & 31u;
+                const uint32_t pi = FT.pat_info[P], co = FT.pat_cp_off[P];
+                if (pi_m(pi) != L + 1) continue;
+                // the name's code points, all loads in flight together; the window is in wb
+                uint32_t nmv[EDGE_MAX_M];
+#pragma unroll
+                for (int k = 0; k < (int)EDGE_MAX_M; ++k) nmv[k] = (uint32_t)k <= L ? FT.pat_cps[co + k] : 0u;
+                bool eq = true;
+#pragma unroll
+                for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j) {
+                    const uint32_t want = (uint32_t)j < del ? nmv[j] : nmv[j + 1];
+                    if ((uint32_t)j < L) eq = eq && ((wb[j >> 2] >> (8 * (j & 3))) & 0xFFu) == want;
+                }
+                hit = eq;
+            }
+            const bool first = hit && dset_insert(S, dset_key(D.doc, P, (uint32_t)f));
+            const bool rx = first && FT.pat_rxk[P] == RXK_REGEX;
+            emit_hits(O, GS, first && !rx, D.doc, P, KW_NOPOS, (uint32_t)f);
+            const uint64_t xm = __ballot(rx);
+            if (xm) {
+                const uint32_t xi = TC.x + mbcnt(xm);
+                if (rx && xi < S.xcap) xq[xi] = make_uint4(D.doc, (P << 1) | (uint32_t)f, 0u, 0u);
+                TC.x += (uint32_t)__popcll(xm);
+            }
+            TC.e += (uint32_t)__popcll(__ballot(hit));   // edge items found (statistics)
         }
     }
 }
@@ -1528,46 +1599,6 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
     task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
 }
 
-// Edge tasks: one-deletion edge windows of the 11..20-code-point names.
-__global__ __launch_bounds__(RK_BLOCK) void kw_edge_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                           const int64_t *__restrict__ off, int n_regions, int G,
-                                                           FastScratch S, DevScratch GS)
-{
-    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
-    __shared__ uint32_t cnt_all[RK_WAVES * 4];
-    const int lane = lane_id();
-    const int wib = threadIdx.x / WAVE;
-    const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
-    const int64_t t = gw / G;
-    const uint32_t sub = (uint32_t)(gw % G);
-    if (t >= n_regions) return;
-    (void)T;
-    uint64_t *eitems = items_all + wib * FK_ITEMS;
-    uint32_t *icnt = cnt_all + wib * 4;
-    OutCtx O = tout_region(S, t);
-    XPush X = xq_region(S, t);
-    unsigned long long nedge = 0;
-    FieldCtx F;
-    const uint32_t ne = (TK_SKIP & 2) ? 0u : min(S.ecnt[t], S.ecap);
-    const uint4 *eq = S.eq + (size_t)t * S.ecap;
-    for (uint32_t k = sub; k < ne; k += (uint32_t)G) {
-        const uint4 tk = eq[k];
-        fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
-                     (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
-        if (lane < 4) icnt[lane] = 0;
-        wave_sync();
-        uint32_t added = fk_edge_items(FT, F, eitems, &icnt[0], &icnt[1]);
-        added = (uint32_t)wave_sum((int)added);
-        if (!added) continue;
-        nedge += added;
-        wave_sync();
-        const uint32_t n_it = min(__builtin_amdgcn_readfirstlane(icnt[0]), (uint32_t)FK_ITEMS);
-        for (uint32_t i = 0; i < n_it; ++i)
-            fk_decide_queue(FT, S, GS, F, O, X, (uint32_t)__builtin_amdgcn_readfirstlane((int)it_pat(eitems[i])));
-    }
-    task_stats(S, 0, 0, nedge, 0, 0, 0);
-}
-
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
 __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int n_regions, int G,
@@ -1635,9 +1666,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     uint32_t *l2 = filt + FK_FILT_WORDS;
     uint32_t *t3 = l2 + FK_L2_WORDS;
     uint32_t *b2 = t3 + FK_T3_WORDS;
-    uint32_t *epre = b2 + FK_B2_WORDS;
-    uint32_t *esuf = epre + FK_EDGE_WORDS;
-    uint64_t *items_all = (uint64_t *)(esuf + FK_EDGE_WORDS);               // FK_WAVES * 2 * FK_ITEMS
+    uint64_t *items_all = (uint64_t *)(b2 + FK_B2_WORDS);                   // FK_WAVES * 2 * FK_ITEMS
     uint2 *ring_all = (uint2 *)(items_all + FK_WAVES * 2 * FK_ITEMS);        // FK_WAVES * FK_Q
     uint32_t *cnt_all = (uint32_t *)(ring_all + FK_WAVES * FK_Q);            // FK_WAVES * 4
 
@@ -1645,7 +1674,6 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     for (int i = threadIdx.x; i < FK_L2_WORDS; i += FK_BLOCK) l2[i] = FT.l2[i];
     for (int i = threadIdx.x; i < FK_T3_WORDS; i += FK_BLOCK) t3[i] = FT.t3[i];
     for (int i = threadIdx.x; i < FK_B2_WORDS; i += FK_BLOCK) b2[i] = FT.b2[i];
-    for (int i = threadIdx.x; i < FK_EDGE_WORDS; i += FK_BLOCK) { epre[i] = FT.edge_pre[i]; esuf[i] = FT.edge_suf[i]; }
     __syncthreads();
 
     const int lane = lane_id();
@@ -1677,7 +1705,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         gate_b[r] = (0x7Fu - FT.gate_hi[r]) * 0x01010101u;
     }
     unsigned long long t_probe = 0, t_epi = 0;
-    ProbeCounters PC = {0, 0, 0, 0, 0};
+    ProbeCounters PC = {0, 0, 0, 0, 0, 0};
     FK_T0(t_all0);
     for (int64_t d = wave; d < n_docs; d += n_waves) {
         FastDoc D;
@@ -1696,19 +1724,20 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         if (base + lane * 16 < D.t2) nv = *(const uint4 *)(arena + base + lane * 16);
         if (lane == WAVE - 1 && base + SCAN_TILE < D.t2) nw4 = *(const uint32_t *)(arena + base + SCAN_TILE);
         wave_sync();
-        // edge prefilter: first / last four bytes of each field (lanes 0..3)
+        // edge prefilter: first / last eight bytes of each field (lanes 0..3) against the global
+        // bitmaps; the word is fetched now and tested at the document's end
         uint32_t flags = 0;
+        uint32_t ebits = 0, ebit = 0;
         {
             const int f = lane >> 1;
             const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
-            bool e = false;
             if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
-                const uint32_t k = ld_u32_unaligned(arena, (lane & 1) ? fe - 4 : fb);
-                e = lds_bit((lane & 1) ? esuf : epre, fk_edge_index(k));
+                const int64_t a = (lane & 1) ? fe - 8 : fb;
+                const uint64_t k = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
+                const uint32_t idx = fk_edge_index(k);
+                ebit = idx & 31u;
+                ebits = ((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5];
             }
-            const uint64_t em = __ballot(e);
-            if (em & 3ull) flags |= DH_EDGE0;
-            if (em & 12ull) flags |= DH_EDGE1;
         }
         bool na0 = false, na1 = false;
         uint32_t qh = 0, qt = 0;                 // ring head / tail (wave-uniform)
@@ -1871,6 +1900,12 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         if (!defer && cursor + n0 + n1 > S.item_cap) { defer = true; ++ndef_items; }
         if (__ballot(na0)) flags |= DH_NA0;
         if (__ballot(na1)) flags |= DH_NA1;
+        {
+            const uint64_t em = __ballot((ebits >> ebit) & 1u);
+            if (em & 3ull) flags |= DH_EDGE0;
+            if (em & 12ull) flags |= DH_EDGE1;
+            if (FK_TIMING) PC.edge_docs += (flags & (DH_EDGE0 | DH_EDGE1)) ? 1u : 0u;
+        }
         uint2 h;
         h.x = (uint32_t)(wave * S.item_cap + cursor);
         if (defer) {
@@ -1905,13 +1940,12 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     if (lane == 0) {
         S.kout_cnt[wave] = O.n;
         S.vcnt[wave] = TC.v;
-        S.ecnt[wave] = TC.e;
+        if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);   // edge items (decided in the epilogue)
         S.scnt[wave] = TC.s;
         S.xcnt[wave] = TC.x;
-        if (TC.v > S.vcap || TC.e > S.ecap || TC.s > S.scap || TC.x > S.xcap) {
+        if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
             atomicOr(&S.status[0], ST_TASK_OVERFLOW);
             atomicMax(&S.tmax[0], TC.v);
-            atomicMax(&S.tmax[1], TC.e);
             atomicMax(&S.tmax[2], TC.s);
             atomicMax(&S.tmax[3], TC.x);
         }
@@ -1930,6 +1964,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         atomicAdd(&S.stats[28], (unsigned long long)TC.e);
         atomicAdd(&S.stats[29], (unsigned long long)TC.s);
         atomicAdd(&S.stats[30], (unsigned long long)TC.x);
+        atomicAdd(&S.stats[31], PC.edge_docs);
     }
     if (FK_TIMING) {
         const unsigned long long inner = wave_sum64(PC.inner);
@@ -1950,7 +1985,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     }
 }
 
-constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS + FK_B2_WORDS + 2 * FK_EDGE_WORDS) * 4 +
+constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS + FK_B2_WORDS) * 4 +
                              (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_Q * 8 + 4 * 4);
 
 // ---------------------------------------------------------------- kernel 2: resolve
