@@ -1161,13 +1161,14 @@ static int finish(kw_handle *h)
         h->stats[2] = fst[2] + gst[2];
         h->stats[3] = fst[3];
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
-        if (getenv("KW_DUMP_TIMING"))   // FK_TIMING builds: scan-kernel cycles summed over waves
+        if (getenv("KW_DUMP_TIMING")) {   // FK_TIMING builds: scan-kernel cycles summed over waves
             fprintf(stderr, "KW_TIMING probe %llu epilogue %llu total %llu batches %llu rounds %llu pairs %llu chunks %llu "
                             "inner %llu | resolve decode %llu edge %llu items %llu short %llu regex %llu all %llu\n", fst[13], fst[14],
                     fst[15], fst[16], fst[17], fst[18], fst[19], fst[20], fst[21], fst[22], fst[23], fst[24], fst[25],
                     fst[26]);
             fprintf(stderr, "KW_TASKS verify %llu edge %llu short %llu regex %llu edge_docs %llu\n", fst[27], fst[28], fst[29],
                     fst[30], fst[31]);
+        }
         h->n_hits = (int64_t)tot;
         h->fetched = true;
         return KW_OK;

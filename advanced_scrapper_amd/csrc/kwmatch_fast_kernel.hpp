@@ -40,6 +40,10 @@
 #define FK_EPI_EDGE 3
 #endif
 
+#ifndef FK_SHORT_LANES   // 1: lane-parallel short-field windows in the short task kernel; 0: wave-serial
+#define FK_SHORT_LANES 1
+#endif
+
 #ifndef RK_OCC
 #define RK_OCC 4
 #endif
@@ -1599,6 +1603,195 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
     task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------- lane-parallel short fields
+// An ASCII field of SHORT_EXACT_MAX < n <= 64 bytes against the fuzzy names at least as long
+// (the field is the needle).  Candidates come from the signature filter as in fk_short_field;
+// then every window of every candidate (full windows of the name, its prefixes, its suffixes and,
+// when m == n, the swapped run) is a job on its own lane: a bit-parallel LCS whose match vectors
+// come from the field's 128-entry table in LDS (pm), the candidate names staged in LDS (names,
+// SL_NAME bytes each).  Names with non-ASCII code points take the wave-serial fk_short_decide.
+constexpr int SL_NAME = 64;
+
+__device__ __forceinline__ void fk_short_run(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O,
+                                             XPush &X, const uint64_t *pm, uint8_t *names, uint32_t *cand,
+                                             uint32_t nc, uint32_t fc, unsigned long long &nver,
+                                             unsigned long long &nwin, unsigned long long &nwin_w)
+{
+    const int lane = lane_id();
+    const uint32_t n = F.n;
+    const uint64_t needle = low_mask(n);
+    // lane k holds candidate k
+    const bool has = lane < (int)nc;
+    const uint32_t P = has ? cand[lane] : 0u;
+    const uint32_t pi = has ? FT.pat_info[P] : 0u;
+    const uint32_t m = pi_m(pi);
+    const bool lanes_ok = has && (pi & PI_ASCII) != 0 && m <= (uint32_t)SL_NAME;
+    const int64_t boff = lanes_ok ? FT.pat_boff[P] : 0;
+    nver += has ? 1u : 0u;
+    // stage the names: 16 dwords per candidate
+    for (uint32_t i0 = 0; i0 < nc * (SL_NAME / 4); i0 += WAVE) {
+        const uint32_t idx = i0 + (uint32_t)lane;
+        const int k = (int)(idx / (SL_NAME / 4));
+        const uint32_t w = idx % (SL_NAME / 4);
+        const uint32_t blo = (uint32_t)__shfl((int)(uint32_t)boff, k & 63, WAVE);
+        const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)boff >> 32), k & 63, WAVE);
+        const int32_t km = __shfl((int)m, k & 63, WAVE);
+        if (idx < nc * (SL_NAME / 4) && 4 * w < (uint32_t)km)
+            ((uint32_t *)names)[idx] = ld_u32_unaligned(FT.pat_bytes, (int64_t)(((uint64_t)bhi << 32) | blo) + 4 * w);
+    }
+    // jobs per candidate: m - n + 1 full windows, the prefixes, the suffixes, the swapped run (m == n)
+    const uint32_t nj = lanes_ok ? (m - n + 3 + (m == n ? 1u : 0u)) : 0u;
+    int J = 0;
+    const int ex = wave_excl_scan((int)nj, &J);
+    uint32_t okm = 0, exm = 0;   // per candidate lane: decided / equal to the field
+    wave_sync();
+    for (int g0 = 0; g0 < J; g0 += WAVE) {
+        const int g = g0 + lane;
+        int owner = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+            const int c = owner + step;
+            const int e = __shfl(ex, c & 63, WAVE);
+            if (c < WAVE && e <= g) owner = c;
+        }
+        const int exo = __shfl(ex, owner, WAVE);
+        const uint32_t om = (uint32_t)__shfl((int)m, owner, WAVE);
+        bool ok = false, exact = false;
+        if (g < J) {
+            const uint32_t j = (uint32_t)(g - exo);
+            const uint8_t *nm = names + owner * SL_NAME;
+            const uint32_t nfull = om - n + 1;
+            uint64_t V = ~0ull;
+            ++nwin;
+            if (j < nfull) {
+                // full window name[j, j + n)
+                for (uint32_t s = 0; s < n; ++s) {
+                    const uint64_t U = V & pm[nm[j + s]];
+                    V = (V + U) | (V - U);
+                }
+                const uint32_t L = (uint32_t)__popcll(~V & needle);
+                ok = 20u * (n - L) < n;
+                exact = om == n && L == n;
+                if (!ok && om == n && j == 0) {   // swapped: needle = name, windows = prefixes of the field
+                    for (uint32_t i = 1; i < n && !ok; ++i) ok = passes((uint32_t)__popcll(~V & low_mask(i)), om, i);
+                }
+            } else if (j == nfull) {
+                // prefixes name[:i], i < n
+                for (uint32_t i = 1; i < n && !ok; ++i) {
+                    const uint64_t U = V & pm[nm[i - 1]];
+                    V = (V + U) | (V - U);
+                    ok = passes((uint32_t)__popcll(~V & needle), n, i);
+                }
+            } else {
+                // suffixes name[m-k:] (j == nfull + 1) or the swapped run over the whole reversed name:
+                // reversed needle
+                const bool sw = j == nfull + 2;
+                const uint32_t steps = sw ? om : n - 1;
+                for (uint32_t t = 1; t <= steps && !ok; ++t) {
+                    const uint64_t R = __builtin_bitreverse64(pm[nm[om - t]]) >> (64 - n);
+                    const uint64_t U = V & R;
+                    V = (V + U) | (V - U);
+                    if (!sw) ok = passes((uint32_t)__popcll(~V & needle), n, t);
+                }
+                if (sw) {   // needle = name, windows = suffixes of the field: field[i:] ~ fr[:n-i]
+                    for (uint32_t t = 1; t < n && !ok; ++t) ok = passes((uint32_t)__popcll(~V & low_mask(t)), om, t);
+                }
+            }
+        }
+        // fold the job results into the owners' bits
+        const uint64_t okb = __ballot(ok), exb = __ballot(exact);
+        uint64_t rest = okb | exb;
+        while (rest) {
+            const int l = __builtin_ctzll(rest);
+            rest &= rest - 1;
+            const int ow = __shfl(owner, l, WAVE);
+            if (lane == ow) {
+                if ((okb >> l) & 1ull) okm = 1u;
+                if ((exb >> l) & 1ull) exm = 1u;
+            }
+        }
+    }
+    // candidates lanes cannot take (non-ASCII names), wave-serially
+    uint64_t slow = __ballot(has && !lanes_ok);
+    while (slow) {
+        const int l = __builtin_ctzll(slow);
+        slow &= slow - 1;
+        const uint32_t lP = (uint32_t)__builtin_amdgcn_readlane((int)P, l);
+        const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
+        const uint32_t nmr = (lane < (int)lm) ? FT.pat_cps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
+        bool exact = false;
+        const bool dec = fk_short_decide(fc, n, nmr, lm, &exact, nwin_w);
+        if (lane == l) {
+            okm = dec ? 1u : 0u;
+            exm = exact ? 1u : 0u;
+        }
+    }
+    const bool dec = has && okm != 0;
+    const bool rx = dec && FT.pat_rxk[P] == RXK_REGEX;
+    emit_hits(O, GS, dec && !rx, F.doc, P, exm ? 0u : KW_NOPOS, F.field);
+    xq_push(X, rx, F.doc, P, F.field);
+    wave_sync();
+}
+
+__device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O, XPush &X,
+                               uint64_t *pm, uint8_t *names, uint32_t *cand, unsigned long long &nver,
+                               unsigned long long &nwin, unsigned long long &nver_w, unsigned long long &nwin_w)
+{
+    const int lane = lane_id();
+    const uint32_t n = F.n;
+    if (n <= (uint32_t)SHORT_EXACT_MAX) {
+        fk_short_field(FT, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
+        return;
+    }
+    const uint64_t needle = low_mask(n);
+    uint64_t FW[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        uint64_t x = 0;
+        if (8 * w < (int)n) x = load8(F.arena, F.fb + 8 * w);
+        const int rem = (int)n - 8 * w;
+        if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
+        FW[w] = x;
+    }
+    // the field's match vectors for every ASCII byte, and its signature
+    const uint64_t m0 = lv_match(FW, (uint32_t)lane, needle), m1 = lv_match(FW, (uint32_t)lane + 64, needle);
+    wave_sync();
+    pm[lane] = m0;
+    pm[lane + 64] = m1;
+    uint64_t fsig = (m0 ? 1ull << lane : 0ull) | (m1 ? 1ull << lane : 0ull);   // bit c & 63
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) fsig |= __shfl_xor(fsig, d, WAVE);
+    const uint32_t fc = (lane < (int)n) ? (uint32_t)F.arena[F.fb + lane] : 0xFFFFFFFCu;
+    wave_sync();
+    const uint32_t allow = (2 * n - 1) / 20;
+    const uint32_t count = (uint32_t)FT.f_count_ge[n];
+    uint32_t nc = 0;
+    constexpr int SIG_U = 8;
+    for (uint32_t c00 = 0; c00 < count; c00 += SIG_U * WAVE) {
+        uint64_t nsig[SIG_U];
+#pragma unroll
+        for (int u = 0; u < SIG_U; ++u) {
+            const uint32_t idx = c00 + (uint32_t)(u * WAVE + lane);
+            nsig[u] = idx < count ? FT.pat_sig[FT.f_first + idx] : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < SIG_U; ++u) {
+            const uint32_t c0 = c00 + (uint32_t)(u * WAVE);
+            const bool cnd = c0 + (uint32_t)lane < count && (uint32_t)__popcll(fsig & ~nsig[u]) <= allow;
+            const uint64_t cm = __ballot(cnd);
+            if (!cm) continue;
+            if (nc + (uint32_t)__popcll(cm) > (uint32_t)WAVE) {
+                fk_short_run(FT, GS, F, O, X, pm, names, cand, nc, fc, nver, nwin, nwin_w);
+                nc = 0;
+            }
+            if (cnd) cand[nc + mbcnt(cm)] = (uint32_t)FT.f_first + c0 + (uint32_t)lane;
+            nc += (uint32_t)__popcll(cm);
+            wave_sync();
+        }
+    }
+    if (nc) fk_short_run(FT, GS, F, O, X, pm, names, cand, nc, fc, nver, nwin, nwin_w);
+}
+
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
 __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int n_regions, int G,
@@ -1611,9 +1804,15 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
     const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     (void)T;
+    __shared__ uint64_t pm_all[RK_WAVES * 128];
+    __shared__ uint32_t names_all[RK_WAVES * WAVE * SL_NAME / 4];
+    __shared__ uint32_t cand_all[RK_WAVES * WAVE];
+    uint64_t *pm = pm_all + wib * 128;
+    uint8_t *names = (uint8_t *)(names_all + wib * WAVE * SL_NAME / 4);
+    uint32_t *cand = cand_all + wib * WAVE;
     OutCtx O = tout_region(S, t);
     XPush X = xq_region(S, t);
-    unsigned long long nver_w = 0, nwin_w = 0;
+    unsigned long long nver = 0, nwin = 0, nver_w = 0, nwin_w = 0;
     FieldCtx F;
     const uint32_t ns = (TK_SKIP & 4) ? 0u : min(S.scnt[t], S.scap);
     const uint4 *sq = S.sq + (size_t)t * S.scap;
@@ -1621,10 +1820,13 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
         const uint4 tk = sq[k];
         fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
-        fk_short_field(FT, GS, F, O, nver_w, nwin_w,
-                       [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
+        if (FK_SHORT_LANES)
+            fk_short_lanes(FT, GS, F, O, X, pm, names, cand, nver, nwin, nver_w, nwin_w);
+        else
+            fk_short_field(FT, GS, F, O, nver_w, nwin_w,
+                           [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
     }
-    task_stats(S, nver_w, nwin_w, 0, 0, 0, 0);
+    task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
 }
 
 // Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.
