@@ -44,8 +44,9 @@ def main():
     ap.add_argument('--gather-hits', action='store_true', help='also time the RCCL all-gather of hit records')
     ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'traffic_r01.json'),
                     help='per-launch HBM bytes from the rocprofv3 PMC passes (profiles/pmc_traffic.py)')
-    ap.add_argument('--workload', choices=('match', 'dedup'), default='match',
-                    help='match = BASELINE.json metric (config 2/3); dedup = CDX URL dedup (config 5)')
+    ap.add_argument('--workload', choices=('match', 'kb50k', 'dedup'), default='match',
+                    help='match = BASELINE.json metric (config 2/3); kb50k = ~50k-pattern synthetic KB '
+                         '(config 4); dedup = CDX URL dedup (config 5)')
     ap.add_argument('--rows-per-gpu', type=int, default=200_000_000, help='dedup: CDX rows per GPU')
     args = ap.parse_args()
     if args.workload == 'dedup':
@@ -61,7 +62,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
-    processed = golden_data.kb_processed()          # info/ticker KB (S&P500 subset), 216 tickers
+    if args.workload == 'kb50k':                     # config 4: synthetic Wikidata-style KB, ~52k names
+        from advanced_scrapper_amd.synth_kb import synthetic_kb
+        processed = synthetic_kb(2300, args.seed)
+    else:
+        processed = golden_data.kb_processed()      # info/ticker KB (S&P500 subset), 216 tickers
     ckb = compile_kb(processed)
     names, kinds = synth.injectable_names(ckb)
     n_local = args.docs_per_gpu
@@ -126,9 +131,22 @@ def main():
     achieved = local_bytes / (scan_avg * 1e-3) / 1e9
     cpu = None
     if world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(processed, corpus, args.cpu_sample, args.cpu_procs)
+        # the port walks every name per field: ~1.7 s per article at 52k names, so config 4 samples fewer
+        n_cpu = args.cpu_sample if args.workload == 'match' else min(args.cpu_sample, 96)
+        cpu = cpu_baseline(processed, corpus, n_cpu, args.cpu_procs)
+    if args.workload == 'kb50k':
+        n_act = ckb.n_patterns
+        workload = (f'config 4: synthetic Wikidata-style KB ({len(processed)} tickers, {n_act} active names, '
+                    f'all <= 64 code points) vs synthetic ~2 KB articles, {n_local} docs per GPU')
+        metric = 'article GB/s keyword-matched (~50k-pattern synthetic KB, config 4); % of HBM peak'
+        data = 'synthetic (seeded generators: csrc/synth.c articles, synth_kb.py KB)'
+    else:
+        workload = ('config 2: S&P500 KB (216 tickers, 2462 active names) vs synthetic ~2 KB articles, '
+                    f'{n_local} docs per GPU')
+        metric = METRIC
+        data = 'synthetic (seeded generator, csrc/synth.c; KB = reference info/ticker via tests/golden)'
     out = {
-        'metric': METRIC,
+        'metric': metric,
         'value': round(value, 2),
         'unit': 'GB/s',
         'n_gpus': world,
@@ -139,10 +157,9 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'u8',
-        'data': 'synthetic (seeded generator, csrc/synth.c; KB = reference info/ticker via tests/golden)',
+        'data': data,
         'config': {
-            'workload': 'config 2: S&P500 KB (216 tickers, 2462 active names) vs synthetic ~2 KB articles, '
-                        f'{n_local} docs per GPU',
+            'workload': workload,
             'docs_per_gpu': n_local, 'total_docs': n_local * world, 'bytes_per_gpu': local_bytes,
             'total_bytes': int(total_bytes), 'hits_total': int(sum(counts)) if counts else None,
             'parallelism': f'dp{world} (document shards, RCCL all-gather of counts)',
@@ -150,7 +167,8 @@ def main():
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
-            'traffic': pmc_traffic(args.traffic_json, 'kw_items_kernel', n_local, args.seed),
+            'traffic': (pmc_traffic(args.traffic_json, 'kw_items_kernel', n_local, args.seed)
+                        if args.workload == 'match' else None),
             'algorithmic_bytes_per_launch': local_bytes,
             'kernel': 'kw::kw_items_kernel', 'kernel_ms_avg': round(scan_avg, 4),
             'kernels_ms_avg': {k: round(v, 4) for k, v in kavg.items()},
