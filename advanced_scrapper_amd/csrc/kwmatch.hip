@@ -1055,7 +1055,7 @@ static int launch_scan(kw_handle *h)
         const int ntb = (nkb * FK_WAVES + RK_WAVES - 1) / RK_WAVES;
         // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up);
         // G[k] waves share each scan wave's task region
-        int G[4] = {1, 4, 4, 1};
+        int G[4] = {4, 4, 8, 4};   // measured on MI355X (1M docs): 12.10 ms vs 12.31 ms for {1, 4, 4, 1}
         if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
         auto task = [&](auto kern, int g) {
             g = std::max(1, std::min(g, 16));

@@ -32,7 +32,10 @@
 
 namespace kw {
 
-constexpr int FK_WAVES = 16;                    // waves per scan workgroup (1024 threads)
+#ifndef FK_WAVES_CFG
+#define FK_WAVES_CFG 16
+#endif
+constexpr int FK_WAVES = FK_WAVES_CFG;           // waves per scan workgroup (one workgroup per CU: LDS)
 constexpr int FK_BLOCK = FK_WAVES * WAVE;
 constexpr int FK_FILT_WORDS = 8192;             // stage 1: 2^18 bits = 32 KB
 constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB

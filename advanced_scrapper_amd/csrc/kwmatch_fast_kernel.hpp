@@ -32,6 +32,10 @@
 #define FK_T0(v) const unsigned long long v = FK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
 #define FK_TACC(acc, v) do { if (FK_TIMING) acc += __builtin_amdgcn_s_memtime() - (v); } while (0)
 
+#ifndef FK_SCHED   // 1: pin the stage-1 LDS reads into groups of eight (sched_group_barrier)
+#define FK_SCHED 0
+#endif
+
 #ifndef FK_GATE_ALL   // 1: look up the bigram table at every position; 0: only behind the byte-class gate
 #define FK_GATE_ALL 1
 #endif
@@ -123,7 +127,7 @@ struct ProbeCounters {   // FK_TIMING builds: probe batches, stage-A rounds, sta
 
 __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const DevTables &T, const FastDoc &D,
                                                  const uint2 *ring, uint32_t head, uint32_t cnt, uint64_t *items,
-                                                 uint32_t *icnt, unsigned long long &nanchor, ProbeCounters &PC)
+                                                 uint32_t *icnt, uint32_t &nanchor, ProbeCounters &PC)
 {
     if (FK_STAGE < 1 || FK_NOPROBE) return;
     if (FK_TIMING) ++PC.batches;
@@ -1859,6 +1863,31 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, Dev
 }
 
 // ---------------------------------------------------------------- kernel 1: the scan
+// tile shape for `rem` bytes left in the document: positions per lane (64 lanes x 16 / 8 / 4 bytes)
+__device__ __forceinline__ int fk_shape(int64_t rem) { return rem > 512 ? 16 : (rem > 256 ? 8 : 4); }
+
+// one tile's loads: S bytes per lane at blk + lane * S (blk is 16-byte aligned), and the word after
+// the tile for the last lane; zero past the document end
+__device__ __forceinline__ void fk_tile_load(const uint8_t *__restrict__ arena, int64_t blk, int S, int64_t end,
+                                             int lane, uint4 &nv, uint32_t &nw4)
+{
+    nv = make_uint4(0u, 0u, 0u, 0u);
+    nw4 = 0;
+    const int64_t a = blk + (int64_t)lane * S;
+    if (a < end) {
+        if (S == 16) {
+            nv = *(const uint4 *)(arena + a);
+        } else if (S == 8) {
+            const uint2 v = *(const uint2 *)(arena + a);
+            nv.x = v.x;
+            nv.y = v.y;
+        } else {
+            nv.x = *(const uint32_t *)(arena + a);
+        }
+    }
+    if (lane == WAVE - 1 && blk + (int64_t)WAVE * S < end) nw4 = *(const uint32_t *)(arena + blk + (int64_t)WAVE * S);
+}
+
 __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int64_t n_docs,
                                                             FastScratch S, DevScratch GS)
@@ -1887,7 +1916,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     uint32_t *icnt = cnt_all + wib * 4;       // [0],[1] item counts, [2] defer flag
     uint64_t *gitems = S.items + (size_t)wave * S.item_cap;
     uint32_t cursor = 0;                      // items this wave wrote to HBM
-    unsigned long long ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;
+    uint32_t ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;   // per-wave totals fit 32 bits
     const bool has_t3 = FT.has_t3 != 0;
     OutCtx O;                                 // hits of the documents this wave finishes itself
     O.shared = nullptr;
@@ -1921,10 +1950,10 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         bool defer = (D.t1 - D.t0 > MAX_FIELD_BYTES) || (D.t2 - D.t1 > MAX_FIELD_BYTES);
         const int64_t base = D.t0 & ~(int64_t)15;
         // the first tile's loads, in flight with the edge prefilter's
-        uint4 nv = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t nw4 = 0;
-        if (base + lane * 16 < D.t2) nv = *(const uint4 *)(arena + base + lane * 16);
-        if (lane == WAVE - 1 && base + SCAN_TILE < D.t2) nw4 = *(const uint32_t *)(arena + base + SCAN_TILE);
+        int shp = fk_shape(D.t2 - base);         // positions per lane of the tile in flight
+        uint4 nv;
+        uint32_t nw4;
+        fk_tile_load(arena, base, shp, D.t2, lane, nv, nw4);
         wave_sync();
         // edge prefilter: first / last eight bytes of each field (lanes 0..3) against the global
         // bitmaps; the word is fetched now and tested at the document's end
@@ -1943,28 +1972,33 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         }
         bool na0 = false, na1 = false;
         uint32_t qh = 0, qt = 0;                 // ring head / tail (wave-uniform)
-        for (int64_t blk = base; blk < D.t2 && !defer; blk += SCAN_TILE) {
-            const int64_t lp = blk + lane * 16;
+        for (int64_t blk = base, nblk = 0; blk < D.t2 && !defer; blk = nblk) {
+            // tile shape: Sc positions per lane (16, or 8 / 4 for a document's last few hundred bytes,
+            // so the tail tile does not pay for 1 KiB of filter work); ng words per lane
+            const int Sc = shp, ng = Sc >> 2;
+            const int64_t lp = blk + lane * Sc;
             uint32_t W[5];
-            W[0] = nv.x; W[1] = nv.y; W[2] = nv.z; W[3] = nv.w;
-            W[4] = (uint32_t)__shfl_down((int)W[0], 1, WAVE);
-            if (lane == WAVE - 1) W[4] = nw4;
-            // the next tile's loads (double buffer)
             {
-                const int64_t nb = blk + SCAN_TILE;
-                nv = make_uint4(0u, 0u, 0u, 0u);
-                nw4 = 0;
-                if (nb + lane * 16 < D.t2) nv = *(const uint4 *)(arena + nb + lane * 16);
-                if (lane == WAVE - 1 && nb + SCAN_TILE < D.t2) nw4 = *(const uint32_t *)(arena + nb + SCAN_TILE);
+                const uint32_t nx = (uint32_t)__shfl_down((int)nv.x, 1, WAVE);
+                const uint32_t tail = lane == WAVE - 1 ? nw4 : nx;
+                W[0] = nv.x;
+                W[1] = ng > 1 ? nv.y : tail;
+                W[2] = ng > 2 ? nv.z : (ng == 2 ? tail : 0u);
+                W[3] = ng > 2 ? nv.w : 0u;
+                W[4] = ng > 2 ? tail : 0u;
             }
+            // the next tile's loads (double buffer)
+            nblk = blk + (int64_t)WAVE * Sc;
+            shp = fk_shape(D.t2 - nblk);
+            fk_tile_load(arena, nblk, shp, D.t2, lane, nv, nw4);
             // lane-local position masks
             const int64_t rel0 = D.t0 - lp, rel2 = D.t2 - lp, rel1 = D.t1 - lp;
-            const int jlo = rel0 <= 0 ? 0 : (rel0 >= 16 ? 16 : (int)rel0);
-            const int jhi = rel2 <= 0 ? 0 : (rel2 >= 16 ? 16 : (int)rel2);
+            const int jlo = rel0 <= 0 ? 0 : (rel0 >= Sc ? Sc : (int)rel0);
+            const int jhi = rel2 <= 0 ? 0 : (rel2 >= Sc ? Sc : (int)rel2);
             uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
             // a 2-byte match cannot start on the last byte of a field
-            if (rel1 - 1 >= 0 && rel1 - 1 < 16) valid &= ~(1u << (rel1 - 1));
-            if (rel2 - 1 >= 0 && rel2 - 1 < 16) valid &= ~(1u << (rel2 - 1));
+            if (rel1 - 1 >= 0 && rel1 - 1 < Sc) valid &= ~(1u << (rel1 - 1));
+            if (rel2 - 1 >= 0 && rel2 - 1 < Sc) valid &= ~(1u << (rel2 - 1));
             // non-ASCII bytes, attributed exactly to their field
             if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
                 uint32_t hb = 0;
@@ -1973,7 +2007,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                     const uint32_t x = (W[k] >> 7) & 0x01010101u;   // bit 0 of each byte = its high bit
                     hb |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
                 }
-                const int j1 = rel1 <= 0 ? 0 : (rel1 >= 16 ? 16 : (int)rel1);
+                const int j1 = rel1 <= 0 ? 0 : (rel1 >= Sc ? Sc : (int)rel1);
                 const uint32_t in0 = ((1u << j1) - 1u) & ~((1u << jlo) - 1u);
                 const uint32_t in1 = (jhi > j1) ? (((1u << jhi) - 1u) & ~((1u << j1) - 1u)) : 0u;
                 if (hb & in0) na0 = true;
@@ -1981,19 +2015,33 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             }
             uint32_t hit = 0, gate = 0;
             if (FK_GATE_ALL && n_gate != 0) {
-                // stage 1 and the exact bigram table of the 2-byte anchors at every position
+                // stage 1 and the exact bigram table of the 2-byte anchors at every position; the
+                // LDS reads of four positions are issued together (eight in flight) before their bits
+                // are taken
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
-                    const uint32_t w = filt[fk_word(key)];
-                    const uint32_t x = fk_b2_index(key);
-                    hit |= ((w >> fk_bit(key)) & 1u) << j;
-                    gate |= ((b2[x >> 5] >> (x & 31)) & 1u) << j;
+                for (int g = 0; g < 4; ++g) {
+                    if (g >= ng) break;
+                    uint32_t fw[4], bw[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
+                        fw[jj] = filt[fk_word(key)];
+                        bw[jj] = b2[fk_b2_index(key) >> 5];
+                    }
+                    if (FK_SCHED) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const int j = 4 * g + jj;
+                        const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
+                        hit |= ((fw[jj] >> fk_bit(key)) & 1u) << j;
+                        gate |= ((bw[jj] >> (fk_b2_index(key) & 31u)) & 1u) << j;
+                    }
                 }
                 gate &= valid;
             } else {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
+                    if (j >= Sc) break;
                     const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
                     const uint32_t w = filt[fk_word(key)];
                     hit |= ((w >> fk_bit(key)) & 1u) << j;
@@ -2026,7 +2074,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 }
                 gate &= valid;
             }
-            ncand += (unsigned long long)__popc(hit);
+            ncand += (uint32_t)__popc(hit);
             // stage 2 on the stage-1 hits: independent hashes of the 4- and 3-byte keys
             uint32_t m4 = 0, m3 = 0;
             {
@@ -2045,7 +2093,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             int total;
             const int ex = wave_excl_scan(__popc(cm), &total);
             if (total == 0) continue;
-            ncand2 += (lane == 0) ? (unsigned long long)total : 0ull;
+            ncand2 += (lane == 0) ? (uint32_t)total : 0u;
             // survivors -> the ring; full batches of 64 are probed as they fill
             if (qt - qh + (uint32_t)total > (uint32_t)FK_Q) {
                 while (qh != qt) {
@@ -2172,7 +2220,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         const unsigned long long inner = wave_sum64(PC.inner);
         if (lane == 0) atomicAdd(&S.stats[20], inner);
     }
-    unsigned long long a = nanchor, c1 = ncand;
+    unsigned long long a = nanchor, c1 = ncand;   // summed over the wave in 64 bits
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) {
         a += __shfl_xor(a, dd, WAVE);
@@ -2181,9 +2229,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     if (lane == 0) {
         atomicAdd(&S.stats[0], c1);
         atomicAdd(&S.stats[1], a);
-        atomicAdd(&S.stats[4], ndefer);
-        atomicAdd(&S.stats[5], ndef_items);
-        atomicAdd(&S.stats[8], ncand2);
+        atomicAdd(&S.stats[4], (unsigned long long)ndefer);
+        atomicAdd(&S.stats[5], (unsigned long long)ndef_items);
+        atomicAdd(&S.stats[8], (unsigned long long)ncand2);
     }
 }
 

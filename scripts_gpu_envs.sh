@@ -1,14 +1,10 @@
 #!/bin/bash
-# Parity tests, then a short bench per environment setting: bash scripts_gpu_envs.sh "VAR=val ..." ...
+# Bench under each environment assignment given on the command line, e.g. KW_TASK_G=2,4,4,2
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-rc=$?; echo "pytest_rc=$rc" >> gpurun_out/gpu_tests.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-sample 0 > gpurun_out/bench_default.log 2>&1 || exit $?
 i=0
 for e in "$@"; do
   i=$((i+1))
-  env $e timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/bench_env$i.log 2>&1 || exit $?
-  echo "$e" >> gpurun_out/bench_env$i.log
+  env $e timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-sample 0 > gpurun_out/env_$i.log 2>&1 || exit $?
+  echo "$e" >> gpurun_out/env_$i.log
 done
