@@ -1015,7 +1015,11 @@ static int launch_scan(kw_handle *h)
     int nrb = (int)std::min<int64_t>((n_docs + (int64_t)RK_WAVES * WAVE - 1) / ((int64_t)RK_WAVES * WAVE),
                                      (int64_t)h->cus * h->resolve_blocks_per_cu);
     if (nrb < 1) nrb = 1;
-    const int ngb = std::max(1, std::min(h->cus, (int)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)));
+    // generic kernel: 4 blocks per CU (one resident, 1 wave / SIMD at 256 VGPRs): the deferred documents'
+    // costs vary by orders of magnitude, later blocks take the work of the slow ones
+    int gmul = 4;
+    if (const char *e = getenv("KW_GENERIC_BLOCKS_PER_CU")) gmul = std::max(1, atoi(e));
+    const int ngb = std::max(1, (int)std::min<int64_t>((int64_t)h->cus * gmul, (n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));
     ScratchCaps w;
     w.nk = nkb * FK_WAVES;
     w.nr = nrb * RK_WAVES;

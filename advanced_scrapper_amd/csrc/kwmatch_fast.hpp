@@ -42,8 +42,10 @@ constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
 constexpr int FK_T3_BITS = 16;                  // stage 2, 3-byte keys: 8 KB
 constexpr int FK_B2_WORDS = 2048;               // exact bigram table: 8 KB
 constexpr int FK_EDGE_BITS = 20;                // edge prefix / suffix 8-byte keys: 2 x 128 KB (global, L2)
-constexpr int FK_Q = 256;                       // per-wave ring of stage-2 survivors (power of 2)
-constexpr int FK_ITEMS = 128;                   // items per field on the fast path
+constexpr int FK_Q = 128;                       // per-wave ring of stage-2 survivors (power of 2)
+constexpr int FK_ITEMS0 = 512;                  // items of field 0 (text) on the fast path (power of 2: LDS sort)
+constexpr int FK_ITEMS1 = 64;                   // items of field 1 (title)
+constexpr int FK_ITEMS_MAX = FK_ITEMS0;         // one field's item buffer in the resolve kernel
 constexpr int FK_CP_CAP = 16384;                // bytes of a non-ASCII field the fast path decodes
 constexpr int RK_WAVES = 4;                     // waves per resolve workgroup
 constexpr int RK_BLOCK = RK_WAVES * WAVE;
@@ -65,12 +67,15 @@ constexpr uint32_t EDGE_MIN_M = 11, EDGE_MAX_M = 20;   // names with edge-only f
 // per-document header written by the scan kernel (uint2):
 //   x = index of the document's first item in FastScratch::items
 //   y = n0 [7:0] | n1 [15:8] | flags
-constexpr uint32_t DH_NEED = 1u << 16;          // the resolve kernel has work on this document
-constexpr uint32_t DH_EDGE0 = 1u << 17;         // field 0: edge prefilter hit (prefix or suffix)
-constexpr uint32_t DH_EDGE1 = 1u << 18;
-constexpr uint32_t DH_NA0 = 1u << 19;           // field 0 has non-ASCII bytes
-constexpr uint32_t DH_NA1 = 1u << 20;
-constexpr uint32_t DH_DEFER = 1u << 21;         // sent to the generic kernel by the scan
+// document header .y: n0 (bits 0..9) | n1 << DH_N1_SHIFT (bits 10..16) | flags
+constexpr uint32_t DH_N1_SHIFT = 10;
+constexpr uint32_t DH_NEED = 1u << 17;          // the resolve kernel has work on this document
+constexpr uint32_t DH_EDGE0 = 1u << 18;         // field 0: edge prefilter hit (prefix or suffix)
+constexpr uint32_t DH_EDGE1 = 1u << 19;
+constexpr uint32_t DH_NA0 = 1u << 20;           // field 0 has non-ASCII bytes
+constexpr uint32_t DH_NA1 = 1u << 21;
+constexpr uint32_t DH_DEFER = 1u << 22;         // sent to the generic kernel by the scan
+static_assert(FK_ITEMS0 < 1024 && FK_ITEMS1 < 128, "item counts must fit the document header");
 
 struct FastTables {
     const uint32_t *filt;       // FK_FILT_WORDS

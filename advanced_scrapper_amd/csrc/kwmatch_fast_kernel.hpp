@@ -7,7 +7,8 @@
 //                      field, decide fuzzy names (exact / edge / LCS-verified
 //                      pieces), report re.finditer positions
 //
-// Rare documents (more than FK_ITEMS items in a field, non-ASCII fields longer
+// Rare documents (more than FK_ITEMS0 / FK_ITEMS1 items in the text / title, one name with more than
+// 64 items in a field, non-ASCII fields longer
 // than FK_CP_CAP bytes) are handed to the generic kernel (kw_scan_kernel).
 #pragma once
 #include "kwmatch_fast.hpp"
@@ -246,7 +247,7 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
             const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(s0 - fb) << IT_POS_SHIFT) |
                                   ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
             const uint32_t idx = atomicAdd(&icnt[f], 1u);
-            if (idx < (uint32_t)FK_ITEMS) items[f * FK_ITEMS + idx] = item;
+            if (idx < (uint32_t)(f ? FK_ITEMS1 : FK_ITEMS0)) items[(f ? FK_ITEMS0 : 0) + idx] = item;
             else atomicOr(&icnt[2], 1u);
         }
     }
@@ -571,7 +572,7 @@ __device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint6
             }
             if (!eq) continue;
             const uint32_t idx = atomicAdd(icnt_f, 1u);
-            if (idx < (uint32_t)FK_ITEMS)
+            if (idx < (uint32_t)FK_ITEMS_MAX)
                 items[idx] = ((uint64_t)P << IT_PAT_SHIFT) | ((uint64_t)FU_EDGE << IT_KIND_SHIFT);
             else
                 atomicOr(dflag, 1u);
@@ -712,7 +713,7 @@ __device__ __forceinline__ uint64_t wave_sort_few(uint64_t x, uint32_t n, uint64
     return lane < (int)n ? buf[lane] : ~0ull;
 }
 
-// sort n <= FK_ITEMS u64 keys in this wave's LDS buffer (bitonic over the next power of two; pads with ~0)
+// sort n <= FK_ITEMS_MAX u64 keys in this wave's LDS buffer (bitonic over the next power of two; pads with ~0)
 __device__ void wave_sort_lds(uint64_t *a, uint32_t n)
 {
     const int lane = lane_id();
@@ -938,7 +939,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         uint64_t vneed = __ballot(vpiece);
         uint64_t decided_v = 0;   // bit per lane: its group got decided by a window
         uint32_t last_P = 0xFFFFFFFFu, nm = 0xFFFFFFFDu;
-        int64_t last_base = -1;
+        int64_t last_key = -1;
         while (vneed) {
             const int l = __builtin_ctzll(vneed);
             vneed &= vneed - 1;
@@ -950,11 +951,11 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
             const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
             const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)vq, l);
             // pieces of one occurrence share the alignment base = q - o: verify it once
-            const int64_t base = (int64_t)q - (int64_t)o;
-            if (P == last_P && base == last_base) continue;
+            const int64_t key = piece_window_key(q, o, pl, mm, F.n);
+            if (P == last_P && key == last_key) continue;
             if (P != last_P) nm = (lane < (int)mm) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
             last_P = P;
-            last_base = base;
+            last_key = key;
             ++nver;
             if (fk_verify_piece(F, nm, mm, q, o, pl, nwin)) decided_v |= lg;
         }
@@ -1075,13 +1076,26 @@ struct TaskCounts {
     uint32_t v, e, s, x;
 };
 
-// Finish an all-ASCII document in the scan kernel.  items: the wave's LDS item lists (field f at
-// f * FK_ITEMS), nf[f] items each.
-__device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D,
+// true iff some name has more than 64 items in the sorted list a[0, n) (lane-parallel)
+__device__ __forceinline__ bool fk_long_run(const uint64_t *a, uint32_t n)
+{
+    bool r = false;
+    for (uint32_t i = (uint32_t)lane_id(); i + WAVE < n; i += WAVE) r |= it_pat(a[i]) == it_pat(a[i + WAVE]);
+    return __ballot(r) != 0;
+}
+
+// Finish an all-ASCII document in the scan kernel.  items: the wave's LDS item lists (field 0 at 0,
+// field 1 at FK_ITEMS0), n0 / n1 items.  Returns false, before anything is emitted, when a name has
+// more than 64 items in the text (the generic kernel takes the document).
+__device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D,
                                  uint64_t *items, uint32_t n0, uint32_t n1, uint32_t flags, int64_t wave, OutCtx &O,
                                  TaskCounts &TC)
 {
     const int lane = lane_id();
+    if (n0 > (uint32_t)WAVE) {   // the text's items sorted first: the deferral test precedes every emission
+        wave_sort_lds(items, n0);
+        if (fk_long_run(items, n0)) return false;
+    }
     uint4 *vq = S.vq + (size_t)wave * S.vcap;
     uint4 *sq = S.sq + (size_t)wave * S.scap, *xq = S.xq + (size_t)wave * S.xcap;
     for (uint32_t f = 0; f < 2; ++f) {
@@ -1096,17 +1110,17 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
         F.doc = D.doc;
         F.field = f;
         const uint32_t N = f ? n1 : n0;
-        uint64_t *its = items + f * FK_ITEMS;
+        uint64_t *its = items + (f ? FK_ITEMS0 : 0);
         if (F.n <= (uint32_t)MAXM) task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
         if (N == 0) continue;
-        if (N > (uint32_t)WAVE) wave_sort_lds(its, N);
+        if (f && N > (uint32_t)WAVE) wave_sort_lds(its, N);   // (field 1 holds at most FK_ITEMS1 = 64)
         for (uint32_t bs = 0; bs < N;) {
             uint32_t be = N;
             if (N > (uint32_t)WAVE) {
                 be = bs + WAVE < N ? bs + WAVE : N;
                 if (be < N)
                     while (be > bs && it_pat(its[be]) == it_pat(its[be - 1])) --be;
-                if (be == bs) be = bs + WAVE;   // (cannot happen: the scan defers such documents)
+                if (be == bs) be = bs + WAVE;   // (cannot happen: fk_long_run deferred such documents)
             }
             const uint32_t NB = be - bs;
             uint64_t it = (lane < (int)NB) ? its[bs + lane] : ~0ull;
@@ -1138,7 +1152,7 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             const uint32_t vinfo = vpiece ? FT.use_info1[use] : 0u;   // all lanes' loads in flight at once
             uint64_t vneed = __ballot(vpiece);
             uint32_t last_P = 0xFFFFFFFFu;
-            int64_t last_base = -1;
+            int64_t last_key = -1;
             while (vneed) {
                 const int l = __builtin_ctzll(vneed);
                 vneed &= vneed - 1;
@@ -1146,10 +1160,11 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                 const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)bpos, l);   // ASCII: byte = code point
                 const uint32_t info1 = (uint32_t)__builtin_amdgcn_readlane((int)vinfo, l);
                 const uint32_t o = (info1 >> 16) & 0xFF, pl = info1 >> 24;
-                const int64_t base = (int64_t)q - (int64_t)o;
-                if (P == last_P && base == last_base) continue;
+                const uint32_t mP = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
+                const int64_t key = piece_window_key(q, o, pl, mP, F.n);
+                if (P == last_P && key == last_key) continue;
                 last_P = P;
-                last_base = base;
+                last_key = key;
                 task_push(vq, S.vcap, TC.v, make_uint4(D.doc, (P << 1) | f, q, o | (pl << 8)));
             }
             // positions: uppercase names and exact occurrences of decided literal fuzzy names
@@ -1259,6 +1274,7 @@ __device__ void fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             TC.e += (uint32_t)__popcll(__ballot(hit));   // edge items found (statistics)
         }
     }
+    return true;
 }
 
 // ---------------------------------------------------------------- kernel: the tasks of the flat resolve
@@ -1897,8 +1913,8 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     uint32_t *l2 = filt + FK_FILT_WORDS;
     uint32_t *t3 = l2 + FK_L2_WORDS;
     uint32_t *b2 = t3 + FK_T3_WORDS;
-    uint64_t *items_all = (uint64_t *)(b2 + FK_B2_WORDS);                   // FK_WAVES * 2 * FK_ITEMS
-    uint2 *ring_all = (uint2 *)(items_all + FK_WAVES * 2 * FK_ITEMS);        // FK_WAVES * FK_Q
+    uint64_t *items_all = (uint64_t *)(b2 + FK_B2_WORDS);                   // FK_WAVES * (FK_ITEMS0 + FK_ITEMS1)
+    uint2 *ring_all = (uint2 *)(items_all + FK_WAVES * (FK_ITEMS0 + FK_ITEMS1));   // FK_WAVES * FK_Q
     uint32_t *cnt_all = (uint32_t *)(ring_all + FK_WAVES * FK_Q);            // FK_WAVES * 4
 
     for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FK_BLOCK) filt[i] = FT.filt[i];
@@ -1911,7 +1927,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     const int wib = threadIdx.x / WAVE;
     const int64_t wave = (int64_t)blockIdx.x * FK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * FK_WAVES;
-    uint64_t *items = items_all + wib * 2 * FK_ITEMS;
+    uint64_t *items = items_all + wib * (FK_ITEMS0 + FK_ITEMS1);
     uint2 *ring = ring_all + wib * FK_Q;
     uint32_t *icnt = cnt_all + wib * 4;       // [0],[1] item counts, [2] defer flag
     uint64_t *gitems = S.items + (size_t)wave * S.item_cap;
@@ -2158,6 +2174,15 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         }
         uint2 h;
         h.x = (uint32_t)(wave * S.item_cap + cursor);
+        bool done = false;
+        if (!defer && !(flags & (DH_NA0 | DH_NA1))) {
+            // all ASCII: finished here, the rest as tasks (flat resolve); a name with more than 64
+            // text items sends the document to the generic kernel instead
+            FK_T0(te0);
+            done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+            FK_TACC(t_epi, te0);
+            if (!done) { defer = true; ++ndef_items; }
+        }
         if (defer) {
             ++ndefer;
             h.y = DH_DEFER;
@@ -2166,23 +2191,19 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                 if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
                 else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
             }
-        } else if (!(flags & (DH_NA0 | DH_NA1))) {
-            // all ASCII: finished here, the rest as tasks (flat resolve)
-            FK_T0(te0);
-            if (FK_STAGE >= 2) fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
-            FK_TACC(t_epi, te0);
-            h.y = n0 | (n1 << 8) | flags;
+        } else if (done) {
+            h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
         } else {
             // items -> HBM (field 0 then field 1) for the resolve kernel
             for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) gitems[cursor + i] = items[i];
-            for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) gitems[cursor + n0 + i] = items[FK_ITEMS + i];
+            for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) gitems[cursor + n0 + i] = items[FK_ITEMS0 + i];
             cursor += n0 + n1;
             // the resolve kernel has work: items, an edge candidate, or a field that may be short
             const int64_t l0 = D.t1 - D.t0, l1 = D.t2 - D.t1;
             const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
             const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
             const bool need = (n0 + n1) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
-            h.y = n0 | (n1 << 8) | flags | (need ? DH_NEED : 0u);
+            h.y = n0 | (n1 << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u);
         }
         if (lane == 0) S.hdr[d] = h;
         wave_sync();
@@ -2236,7 +2257,8 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
 }
 
 constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS + FK_B2_WORDS) * 4 +
-                             (size_t)FK_WAVES * (2 * FK_ITEMS * 8 + FK_Q * 8 + 4 * 4);
+                             (size_t)FK_WAVES * ((FK_ITEMS0 + FK_ITEMS1) * 8 + FK_Q * 8 + 4 * 4);
+static_assert(kItemsLds <= 160 * 1024, "scan workgroup LDS exceeds the CU's 160 KiB");
 
 // ---------------------------------------------------------------- kernel 2: resolve
 __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables FT, DevTables T,
@@ -2244,7 +2266,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
                                                               const int64_t *__restrict__ off, int64_t n_docs,
                                                               FastScratch S, DevScratch GS)
 {
-    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS];
+    __shared__ uint64_t items_all[RK_WAVES * FK_ITEMS_MAX];
     __shared__ uint64_t rxtab_all[RK_WAVES * 128];
     __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
     __shared__ uint32_t cnt_all[RK_WAVES * 4];
@@ -2252,7 +2274,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     const int wib = threadIdx.x / WAVE;
     const int64_t wave = (int64_t)blockIdx.x * RK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * RK_WAVES;
-    uint64_t *items = items_all + wib * FK_ITEMS;
+    uint64_t *items = items_all + wib * FK_ITEMS_MAX;
     uint64_t *rxtab = rxtab_all + wib * 128;
     uint32_t *icnt = cnt_all + wib * 4;
     uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
@@ -2284,7 +2306,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
             const uint32_t hx = (uint32_t)__shfl((int)hl.x, l, WAVE);
             const uint32_t hy = (uint32_t)__shfl((int)hl.y, l, WAVE);
             const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
-            const uint32_t nf[2] = {hy & 255u, (hy >> 8) & 255u};
+            const uint32_t nf[2] = {hy & 1023u, (hy >> DH_N1_SHIFT) & 127u};
             const uint32_t out_mark = O.n, rq_mark = RQ.n;
             bool defer = false;
             ++nres;

@@ -426,6 +426,21 @@ __device__ bool verify_piece(const DevTables &T, const FieldCtx &F, uint32_t P, 
     return false;
 }
 
+// Pieces of one occurrence of a name share its alignment base = q - o, and the window family a
+// piece is verified over depends only on the base and on whether prefix (q + pl + 1 <= m) or suffix
+// (q + m > n) windows can contain the piece: a piece whose key equals the last verified one is
+// skipped.
+__device__ __forceinline__ int64_t piece_window_key(uint32_t q, uint32_t o, uint32_t pl, uint32_t m, uint32_t n)
+{
+    const int64_t base = (int64_t)q - (int64_t)o;
+    const int64_t pre = q + pl + 1 <= m ? 1 : 0, suf = q + m > n ? 1 : 0;
+    return ((base + (1ll << 40)) << 2) | (pre << 1) | suf;
+}
+
+// the fast path's wave-cooperative verification (kwmatch_fast_kernel.hpp)
+__device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint32_t q, uint32_t o, uint32_t pl,
+                                unsigned long long &nwin);
+
 // ------------------------------------------------------------------ resolve
 __device__ void process_group(const DevTables &T, const DevScratch &S, const FieldCtx &F, OutCtx &O,
                               const uint64_t *items, uint32_t gs, uint32_t ge, uint32_t P, unsigned long long &nwin)
@@ -444,18 +459,30 @@ __device__ void process_group(const DevTables &T, const DevScratch &S, const Fie
         bool full = (i < ge) && it_kind(items[i]) == USE_FULL;
         decided = __ballot(full) != 0;
     }
+    // pieces wave-serially, each by the wave-cooperative bit-parallel LCS (name code points one per
+    // lane, match vectors by ballot); one verification per window key
+    const uint32_t nm = (lane < (int)m) ? T.pat_cps[T.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+    int64_t last_key = -1;
     for (uint32_t c = gs; c < ge && !decided; c += WAVE) {
-        uint32_t i = c + lane;
-        bool pass = false;
-        if (i < ge) {
-            uint64_t it = items[i];
-            if (it_kind(it) == USE_PIECE) {
-                uint32_t info = T.use_info[it_use(it)];
-                uint32_t o = (info >> 8) & 0xFF, plen = (info >> 16) & 0xFF;
-                pass = verify_piece(T, F, P, m, to_cp(F, it_pos(it)), o, plen, nwin);
-            }
+        const uint32_t i = c + lane;
+        const bool piece = i < ge && it_kind(items[i]) == USE_PIECE;
+        uint32_t q = 0, info = 0;
+        if (piece) {
+            q = to_cp(F, it_pos(items[i]));
+            info = T.use_info[it_use(items[i])];
         }
-        decided = __ballot(pass) != 0;
+        uint64_t pm = __ballot(piece);
+        while (pm && !decided) {
+            const int l = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)q, l);
+            const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)info, l);
+            const uint32_t o = (li >> 8) & 0xFF, plen = (li >> 16) & 0xFF;
+            const int64_t key = piece_window_key(lq, o, plen, m, F.n);
+            if (key == last_key) continue;
+            last_key = key;
+            decided = fk_verify_piece(F, nm, m, lq, o, plen, nwin);
+        }
     }
     if (!decided) return;
     uint32_t cnt = (pi & PI_LITERAL) ? emit_nonoverlap(S, F, O, items, gs, ge, USE_FULL, blen, P)
