@@ -800,6 +800,7 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
         uint32_t c = *list_cnt;
         n_docs = c < list_cap ? c : list_cap;
     }
+    if ((int64_t)blockIdx.x * WAVES_PER_BLOCK >= n_docs) return;   // no document for any wave of this block
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     uint32_t *filt = (uint32_t *)smem_raw;
     uint64_t *pm_all = (uint64_t *)(filt + FILT_WORDS);                 // WAVES*128

@@ -250,3 +250,76 @@ def test_item_capacity_boundaries_vs_oracle(env):
     bad = _compare(env['processed'], texts, titles, got)
     assert not bad, f"GPU differs from the oracle on many-item docs {bad[:20]}"
     assert env['m'].stats()['deferred_docs'] > 0     # the > 512-item texts took the generic kernel
+
+
+def _nonascii_near_names(ckb):
+    """Non-ASCII text fields (> 256 bytes) with near-miss fuzzy names and non-ASCII characters at every
+    distance from them: inside the window family, just outside, at the field edges, plus regex-class
+    names and uppercase names (code point positions after multi-byte characters)."""
+    rng = random.Random(31)
+    fz = [n for n, c in zip(ckb.names, ckb.classes) if c == 'F' and len(n) >= 11]
+    up = [n for n, c in zip(ckb.names, ckb.classes) if c == 'U']
+    words = ['market', 'shares', 'rose', 'the', 'company', 'said', 'on', 'Monday', 'analysts', 'quarter']
+    na_chars = ['é', '’', '—', '中', '€', 'ß', '😀']
+    texts, titles = [], []
+    for i in range(160):
+        n = rng.choice(fz)
+        k = rng.randrange(len(n))
+        near = n[:k] + n[k + 1:] if i % 3 else n[:k] + rng.choice('xyz') + n[k:]
+        pre = ' '.join(rng.choice(words) for _ in range(rng.randrange(0, 60)))
+        post = ' '.join(rng.choice(words) for _ in range(rng.randrange(0, 60)))
+        gap = rng.choice([0, 1, 2, 3, 5, 8, 13, 40])
+        c = rng.choice(na_chars)
+        parts = [pre, ' ' * gap if i % 2 else '', near, ' ' * gap, post]
+        t = ' '.join(parts)
+        pos = rng.choice(['before', 'after', 'inside', 'start', 'end', 'far'])
+        if pos == 'before':
+            t = t.replace(near, c + ' ' * gap + near, 1)
+        elif pos == 'after':
+            t = t.replace(near, near + ' ' * gap + c, 1)
+        elif pos == 'inside':
+            j = rng.randrange(1, len(near))
+            t = t.replace(near, near[:j] + c + near[j:], 1)
+        elif pos == 'start':
+            t = c + t
+        elif pos == 'end':
+            t = t + c
+        else:
+            t = c * 3 + ' ' + t + ' ' + c
+        t += ' ' + ' '.join(rng.choice(up) for _ in range(3)) + ' ' + c
+        while len(t.encode()) <= 300:
+            t = rng.choice(words) + ' ' + t
+        texts.append(t)
+        titles.append(rng.choice(['', n, near, 'plain title']))
+    return texts, titles
+
+
+def test_nonascii_fields_in_scan_epilogue_vs_oracle(env):
+    texts, titles = _nonascii_near_names(env['ckb'])
+    got = _gpu_maps(env['m'], texts, titles)
+    bad = _compare(env['processed'], texts, titles, got)
+    assert not bad, f"GPU differs from the oracle on non-ASCII docs {bad[:20]}"
+
+
+def test_nonascii_wildcard_and_regex_names_vs_oracle():
+    """Regex-class names decided in non-ASCII fields go to the resolve kernel; literal ones stay."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    names = _WILD_NAMES + ['International Business Machines', 'Alphabet Incorporated Class', 'Nestlé Holdings AG']
+    processed = {'TK': {'name': {n: (None, None) for n in names}}}
+    m = GpuMatcher(compile_kb(processed))
+    rng = random.Random(41)
+    texts, titles = [], []
+    for n in names:
+        for c in ('é', '中', '’'):
+            k = rng.randrange(len(n))
+            filler = ' '.join(['lorem'] * 50)
+            texts.append(f"{filler} {c} {n[:k] + n[k + 1:]} {filler} {n} {c}")
+            texts.append(f"{c}{filler} {n[:k] + n[k + 1:]}{c} {filler}")
+            titles += [n, c]
+    got = _gpu_maps(m, texts, titles)
+    bad = _compare(processed, texts, titles, got)
+    assert not bad, f"GPU differs from the oracle on non-ASCII wildcard docs {bad[:20]}"
