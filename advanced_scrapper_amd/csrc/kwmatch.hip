@@ -902,7 +902,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_scan_kernel, BLOCK, kScanLds));
     h->blocks_per_cu = bpc > 0 ? bpc : 1;
     bpc = 0;
-    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_items_kernel, FK_BLOCK, kItemsLds));
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_items_kernel, FK_BLOCK, 0));
     h->items_blocks_per_cu = bpc > 0 ? bpc : 1;
     bpc = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_resolve_kernel, RK_BLOCK, 0));
@@ -1050,7 +1050,7 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
     HIPCHK(h, hipEventRecord(h->ev0, st));
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_items_kernel, dim3(nkb), dim3(FK_BLOCK), kItemsLds, st, h->FT, h->T, h->arena,
+        hipLaunchKernelGGL(kw_items_kernel, dim3(nkb), dim3(FK_BLOCK), 0, st, h->FT, h->T, h->arena,
                            h->doc_off, n_docs, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }

@@ -94,7 +94,7 @@ __device__ __forceinline__ int64_t rdlane64(int64_t v, int l)
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ bool lds_bit(const uint32_t *t, uint32_t idx) { return (t[idx >> 5] >> (idx & 31)) & 1u; }
+__device__ __forceinline__ bool lds_bit(const uint32_t *t, uint32_t idx) { return __builtin_amdgcn_ubfe(t[idx >> 5], idx, 1) != 0u; }
 
 // byte-exact compare of text[p, p+len) with pat[0, len)
 __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_t p, const uint8_t *__restrict__ pat,
@@ -1904,18 +1904,27 @@ __device__ __forceinline__ void fk_tile_load(const uint8_t *__restrict__ arena, 
     if (lane == WAVE - 1 && blk + (int64_t)WAVE * S < end) nw4 = *(const uint32_t *)(arena + blk + (int64_t)WAVE * S);
 }
 
+struct __attribute__((aligned(16))) ItemsLds {
+    uint32_t filt[FK_FILT_WORDS];
+    uint32_t l2[FK_L2_WORDS];
+    uint32_t t3[FK_T3_WORDS];
+    uint32_t b2[FK_B2_WORDS];
+    uint64_t items[FK_WAVES * (FK_ITEMS0 + FK_ITEMS1)];
+    uint2 ring[FK_WAVES * FK_Q];
+    uint32_t cnt[FK_WAVES * 4];
+};
+
 __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int64_t n_docs,
                                                             FastScratch S, DevScratch GS)
 {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    uint32_t *filt = (uint32_t *)smem_raw;
-    uint32_t *l2 = filt + FK_FILT_WORDS;
-    uint32_t *t3 = l2 + FK_L2_WORDS;
-    uint32_t *b2 = t3 + FK_T3_WORDS;
-    uint64_t *items_all = (uint64_t *)(b2 + FK_B2_WORDS);                   // FK_WAVES * (FK_ITEMS0 + FK_ITEMS1)
-    uint2 *ring_all = (uint2 *)(items_all + FK_WAVES * (FK_ITEMS0 + FK_ITEMS1));   // FK_WAVES * FK_Q
-    uint32_t *cnt_all = (uint32_t *)(ring_all + FK_WAVES * FK_Q);            // FK_WAVES * 4
+    // one static LDS block, the filters first: their addresses are constants below 64 KiB that fold
+    // into the ds_read offset field (no per-position address add)
+    __shared__ ItemsLds L;
+    uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
+    uint64_t *items_all = L.items;
+    uint2 *ring_all = L.ring;
+    uint32_t *cnt_all = L.cnt;
 
     for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FK_BLOCK) filt[i] = FT.filt[i];
     for (int i = threadIdx.x; i < FK_L2_WORDS; i += FK_BLOCK) l2[i] = FT.l2[i];
@@ -1967,6 +1976,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         const int64_t base = D.t0 & ~(int64_t)15;
         // the first tile's loads, in flight with the edge prefilter's
         int shp = fk_shape(D.t2 - base);         // positions per lane of the tile in flight
+        const int32_t dl1 = (int32_t)(D.t1 - D.t0), dl2 = (int32_t)(D.t2 - D.t0);   // field ends, doc-relative
         uint4 nv;
         uint32_t nw4;
         fk_tile_load(arena, base, shp, D.t2, lane, nv, nw4);
@@ -2008,7 +2018,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
             shp = fk_shape(D.t2 - nblk);
             fk_tile_load(arena, nblk, shp, D.t2, lane, nv, nw4);
             // lane-local position masks
-            const int64_t rel0 = D.t0 - lp, rel2 = D.t2 - lp, rel1 = D.t1 - lp;
+            // document-relative 32-bit positions (a document is far below 2^31 bytes)
+            const int32_t lrel = (int32_t)(lp - D.t0);
+            const int32_t rel0 = -lrel, rel2 = dl2 - lrel, rel1 = dl1 - lrel;
             const int jlo = rel0 <= 0 ? 0 : (rel0 >= Sc ? Sc : (int)rel0);
             const int jhi = rel2 <= 0 ? 0 : (rel2 >= Sc ? Sc : (int)rel2);
             uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
@@ -2049,8 +2061,10 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                     for (int jj = 0; jj < 4; ++jj) {
                         const int j = 4 * g + jj;
                         const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
-                        hit |= ((fw[jj] >> fk_bit(key)) & 1u) << j;
-                        gate |= ((bw[jj] >> (fk_b2_index(key) & 31u)) & 1u) << j;
+                        // v_bfe_u32 + v_lshl_or_b32 per bit; the bfe offset is taken mod 32 (hardware and
+                        // LLVM agree), so the b2 bit index needs no mask
+                        hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit(key), 1) << j;
+                        gate |= __builtin_amdgcn_ubfe(bw[jj], fk_b2_index(key), 1) << j;
                     }
                 }
                 gate &= valid;
@@ -2099,9 +2113,9 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                     const int j = __ffs(hm) - 1;
                     hm &= hm - 1;
                     const uint32_t key = fk_key_at(W, j);
-                    const int64_t p = lp + j;
-                    const int64_t fe = p < D.t1 ? D.t1 : D.t2;
-                    if (p + 4 <= fe && lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
+                    const int32_t pr = lrel + j;
+                    const int32_t fer = pr < dl1 ? dl1 : dl2;
+                    if (pr + 4 <= fer && lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
                     if (has_t3 && lds_bit(t3, fk_t3_index(key))) m3 |= 1u << j;
                 }
             }
@@ -2130,7 +2144,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
                     if (k >= rb && k < rb + FK_Q) {
                         const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
                         ring[(qt + (uint32_t)(k - rb)) & (FK_Q - 1)] =
-                            make_uint2(((uint32_t)(lp + j - D.t0) << 3) | fl, fk_key_at(W, j));
+                            make_uint2(((uint32_t)(lrel + j) << 3) | fl, fk_key_at(W, j));
                     }
                     ++k;
                 }
@@ -2256,9 +2270,7 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
     }
 }
 
-constexpr size_t kItemsLds = (size_t)(FK_FILT_WORDS + FK_L2_WORDS + FK_T3_WORDS + FK_B2_WORDS) * 4 +
-                             (size_t)FK_WAVES * ((FK_ITEMS0 + FK_ITEMS1) * 8 + FK_Q * 8 + 4 * 4);
-static_assert(kItemsLds <= 160 * 1024, "scan workgroup LDS exceeds the CU's 160 KiB");
+static_assert(sizeof(ItemsLds) <= 160 * 1024, "scan workgroup LDS exceeds the CU's 160 KiB");
 
 // ---------------------------------------------------------------- kernel 2: resolve
 __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables FT, DevTables T,
