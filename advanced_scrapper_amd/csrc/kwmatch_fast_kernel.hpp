@@ -2366,6 +2366,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     if (RQ.n > RQ.cap && lane == 0) atomicMax(&GS.status[2], RQ.n);   // the queue size a rescan needs
     const uint32_t n_rx = RQ.n < RQ.cap ? RQ.n : RQ.cap;
     FK_T0(trx0);
+    uint32_t dec_d = 0xFFFFFFFFu, dec_f = 0;   // the field whose code points cps holds (tasks come in doc order)
     for (uint32_t t = 0; t < n_rx; ++t) {
         const uint4 tk = RQ.q[t];
         const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x);
@@ -2381,7 +2382,11 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
         F.cps = cps;
         F.blkcnt = blkcnt;
         F.doc = d;
-        if (!F.ascii) decode_field_fast(arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
+        if (!F.ascii && (d != dec_d || F.field != dec_f)) {
+            decode_field_fast(arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
+            dec_d = d;
+            dec_f = F.field;
+        }
         const int32_t r = FT.rxf_idx[P];
         ++nrx;
         nrx_bt += r < 0;
