@@ -64,6 +64,7 @@ namespace kw {
 struct FastDoc {
     const uint8_t *arena;
     int64_t t0, t1, t2;
+    int32_t l1, l2;   // t1 - t0, t2 - t0: field ends relative to the document
     uint32_t doc;
 };
 
@@ -136,8 +137,10 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
     const uint8_t *__restrict__ arena = D.arena;
     const bool valid = lane < (int)cnt;
     const uint2 e = valid ? ring[(head + (uint32_t)lane) & (FK_Q - 1)] : make_uint2(0u, 0u);
-    const int64_t p = D.t0 + (int64_t)(e.x >> 3);
-    const int64_t fe = p < D.t1 ? D.t1 : D.t2;
+    // document-relative 32-bit positions; p only for the loads
+    const int32_t pr = (int32_t)(e.x >> 3);
+    const int32_t fer = pr < D.l1 ? D.l1 : D.l2;
+    const int64_t p = D.t0 + pr;
     const uint32_t hi = valid ? ld_u32_unaligned(arena, p + 4) : 0u;
     const uint64_t h8 = (uint64_t)e.y | ((uint64_t)hi << 32);
     // the hash lookups of the lane's key lengths 4, 3, 2 (try bits 0, 1, 2) go out together
@@ -150,7 +153,7 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int Lk = 4 - i;
-            want[i] = valid && ((e.x >> i) & 1u) && p + Lk <= fe;
+            want[i] = valid && ((e.x >> i) & 1u) && pr + Lk <= fer;
             key[i] = ((uint64_t)Lk << 32) | (h8 & ((1ull << (8 * Lk)) - 1));
             slot[i] = fk_ht_slot(key[i], FT.ht_mask);
             hs[i] = want[i] ? FT.ht4[slot[i]] : make_uint4(~0u, ~0u, 0u, 0u);
@@ -179,7 +182,7 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
             if (tcur < tend) {
                 const uint4 ar = FT.arec[tcur++];
                 const uint32_t alen = ar.w & 0xFFu;
-                if (p + (int64_t)alen > fe) continue;
+                if (pr + (int32_t)alen > fer) continue;
                 const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
                 if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) continue;
                 ++nanchor;
@@ -213,18 +216,17 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
             const uint32_t oub1 = (uint32_t)__shfl((int)ub1, owner, WAVE);
             const uint32_t loc = (uint32_t)(g - exo);
             const uint32_t u = loc < ouc ? oub + loc : oub1 + (loc - ouc);
-            const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)p, owner, WAVE);
-            const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)p >> 32), owner, WAVE);
+            const int32_t ppr = __shfl(pr, owner, WAVE);
             if (g >= total) continue;
-            const int64_t pp = (int64_t)(((uint64_t)phi << 32) | plo);
-            const int f = pp < D.t1 ? 0 : 1;
-            const int64_t fb = f ? D.t1 : D.t0, fe2 = f ? D.t2 : D.t1;
+            const int f = ppr < D.l1 ? 0 : 1;
+            const int32_t fbr = f ? D.l1 : 0, fer2 = f ? D.l2 : D.l1;
             const uint4 ur = FT.urec[u];
             const uint32_t kind = ur.x & 0xFF, aoff = (ur.x >> 8) & 0xFF;
             const uint32_t sblen = ur.y & 0xFFFF;
             const uint32_t pat = ur.z;
-            const int64_t s0 = pp - (int64_t)aoff;
-            if (s0 < fb || s0 + (int64_t)sblen > fe2) continue;
+            const int32_t s0r = ppr - (int32_t)aoff;
+            if (s0r < fbr || s0r + (int32_t)sblen > fer2) continue;
+            const int64_t s0 = D.t0 + s0r, fb = D.t0 + fbr, fe2 = D.t0 + fer2;
             const uint4 u2 = FT.urec2[u];
             const uint32_t hl = sblen < 8 ? sblen : 8;
             const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
@@ -244,7 +246,7 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
                 }
                 if (wn == wl) continue;
             }
-            const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(s0 - fb) << IT_POS_SHIFT) |
+            const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(uint32_t)(s0r - fbr) << IT_POS_SHIFT) |
                                   ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
             const uint32_t idx = atomicAdd(&icnt[f], 1u);
             if (idx < (uint32_t)(f ? FK_ITEMS1 : FK_ITEMS0)) items[(f ? FK_ITEMS0 : 0) + idx] = item;
@@ -1970,13 +1972,15 @@ __global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTa
         D.t1 = rdlane64(pf_off, 1);
         D.t2 = rdlane64(pf_off, 2);
         D.doc = (uint32_t)d;
+        D.l1 = (int32_t)(D.t1 - D.t0);
+        D.l2 = (int32_t)(D.t2 - D.t0);
         pf_off = (lane < 3 && d + n_waves < n_docs) ? off[2 * (d + n_waves) + lane] : 0;
         if (lane < 4) icnt[lane] = 0;
         bool defer = (D.t1 - D.t0 > MAX_FIELD_BYTES) || (D.t2 - D.t1 > MAX_FIELD_BYTES);
         const int64_t base = D.t0 & ~(int64_t)15;
         // the first tile's loads, in flight with the edge prefilter's
         int shp = fk_shape(D.t2 - base);         // positions per lane of the tile in flight
-        const int32_t dl1 = (int32_t)(D.t1 - D.t0), dl2 = (int32_t)(D.t2 - D.t0);   // field ends, doc-relative
+        const int32_t dl1 = D.l1, dl2 = D.l2;   // field ends, doc-relative
         uint4 nv;
         uint32_t nw4;
         fk_tile_load(arena, base, shp, D.t2, lane, nv, nw4);
