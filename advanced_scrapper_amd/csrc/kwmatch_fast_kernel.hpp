@@ -180,15 +180,26 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
         while (more && nm < 2) {
             if (FK_TIMING) ++PC.inner;
             if (tcur < tend) {
-                const uint4 ar = FT.arec[tcur++];
-                const uint32_t alen = ar.w & 0xFFu;
-                if (pr + (int32_t)alen > fer) continue;
-                const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
-                if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) continue;
-                ++nanchor;
-                if (nm == 0) { ub = ar.z; uc = ar.w >> 8; }
-                else { ub1 = ar.z; uc1 = ar.w >> 8; }
-                ++nm;
+                // two anchor records per step, both loads in flight together
+                const uint4 ar0 = FT.arec[tcur];
+                const bool two = tcur + 1 < tend;
+                const uint4 ar1 = two ? FT.arec[tcur + 1] : make_uint4(0u, 0u, 0u, 0u);
+                auto take = [&](const uint4 &ar) {
+                    const uint32_t alen = ar.w & 0xFFu;
+                    if (pr + (int32_t)alen > fer) return;
+                    const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
+                    if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) return;
+                    ++nanchor;
+                    if (nm == 0) { ub = ar.z; uc = ar.w >> 8; }
+                    else { ub1 = ar.z; uc1 = ar.w >> 8; }
+                    ++nm;
+                };
+                take(ar0);
+                ++tcur;
+                if (two && nm < 2) {
+                    take(ar1);
+                    ++tcur;
+                }
                 continue;
             }
             if (b1 >= e1 && b2 >= e2) { more = false; break; }
@@ -227,14 +238,18 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
             const int32_t s0r = ppr - (int32_t)aoff;
             if (s0r < fbr || s0r + (int32_t)sblen > fer2) continue;
             const int64_t s0 = D.t0 + s0r, fb = D.t0 + fbr, fe2 = D.t0 + fer2;
+            // the use's head / tail words, the span's text and the name's info go out together (one
+            // memory latency instead of three dependent ones)
             const uint4 u2 = FT.urec2[u];
+            const uint64_t th = load8(arena, s0);
+            const uint64_t tt = load8(arena, s0 + (sblen > 8 ? sblen - 8 : 0));
+            const uint32_t pi = kind == FU_UPPER ? FT.pat_info[pat] : 0u;
             const uint32_t hl = sblen < 8 ? sblen : 8;
             const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
-            if ((load8(arena, s0) ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
-            if (sblen > 8 && load8(arena, s0 + sblen - 8) != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) continue;
+            if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
+            if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) continue;
             if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) continue;
             if (kind == FU_UPPER) {
-                const uint32_t pi = FT.pat_info[pat];
                 const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
                 const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
                 if (wp == wf) continue;
