@@ -244,6 +244,10 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
             const uint64_t th = load8(arena, s0);
             const uint64_t tt = load8(arena, s0 + (sblen > 8 ? sblen - 8 : 0));
             const uint32_t pi = kind == FU_UPPER ? FT.pat_info[pat] : 0u;
+            // the neighbours of an uppercase name (\b), fetched with the rest: ASCII ones need nothing more
+            const bool hasp = kind == FU_UPPER && s0 > fb, hasn = kind == FU_UPPER && s0 + (int64_t)sblen < fe2;
+            const uint32_t prevb = hasp ? (uint32_t)arena[s0 - 1] : 0u;
+            const uint32_t nextb = hasn ? (uint32_t)arena[s0 + sblen] : 0u;
             const uint32_t hl = sblen < 8 ? sblen : 8;
             const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
             if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
@@ -251,12 +255,13 @@ __device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const Dev
             if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) continue;
             if (kind == FU_UPPER) {
                 const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
-                const bool wp = (s0 > fb) ? is_word_cp(T, decode_before(arena, fb, s0)) : false;
+                bool wp = false;
+                if (hasp) wp = is_word_cp(T, prevb < 0x80u ? prevb : decode_before(arena, fb, s0));
                 if (wp == wf) continue;
                 bool wn = false;
-                if (s0 + (int64_t)sblen < fe2) {
-                    uint32_t ch;
-                    decode_at(arena, s0 + sblen, fe2, &ch);
+                if (hasn) {
+                    uint32_t ch = nextb;
+                    if (nextb >= 0x80u) decode_at(arena, s0 + sblen, fe2, &ch);
                     wn = is_word_cp(T, ch);
                 }
                 if (wn == wl) continue;
