@@ -1153,8 +1153,10 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             const uint32_t kind = it_kind(it);
             const uint32_t bpos = it_pos(it);
             const uint32_t use = it_use(it);
+            // the name's info, regex class and (pieces) use record: all lanes' loads in flight at once
             const uint32_t pi = valid ? FT.pat_info[pat] : 0u;
             const uint32_t rxk = valid ? FT.pat_rxk[pat] : 0u;
+            const uint32_t uinfo = (valid && kind == FU_PIECE) ? FT.use_info1[use] : 0u;
             const uint32_t m = pi_m(pi);
             const bool fuzzy = (pi & PI_FUZZY) != 0;
             const uint32_t prev_pat = (uint32_t)__shfl_up((int)pat, 1, WAVE);
@@ -1171,7 +1173,7 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             const bool decided = (fullm & gmask) != 0;
             // pieces of undecided fuzzy names -> verify tasks (one per alignment base)
             const bool vpiece = live && fuzzy && !decided && kind == FU_PIECE;
-            const uint32_t vinfo = vpiece ? FT.use_info1[use] : 0u;   // all lanes' loads in flight at once
+            const uint32_t vinfo = vpiece ? uinfo : 0u;
             uint64_t vneed = __ballot(vpiece);
             uint32_t last_P = 0xFFFFFFFFu;
             int64_t last_key = -1;
