@@ -1058,7 +1058,6 @@ static int launch_scan(kw_handle *h)
     }
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
-        const int ntb = (nkb * FK_WAVES + RK_WAVES - 1) / RK_WAVES;
         // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up);
         // G[k] waves share each scan wave's task region
         int G[4] = {4, 4, 8, 4};   // measured on MI355X (1M docs): 12.10 ms vs 12.31 ms for {1, 4, 4, 1}
