@@ -1,0 +1,81 @@
+"""Per-ticker CSV egress, byte-identical to the reference's row-at-a-time pandas appends.
+
+The reference writes every (article, ticker) match with
+``pd.DataFrame([row]).to_csv(path, mode='a', index=False, header=...)``
+(match_keywords.py:128-146): one single-row frame per output row, so each
+column's dtype is inferred from that one value.  pandas writes such a frame
+through the stdlib ``csv`` writer (QUOTE_MINIMAL, ``"`` quote char, doubled
+quotes, ``os.linesep`` line ends) after rendering each cell:
+
+* ``str``                          -> the string itself
+* ``int`` / numpy integer          -> ``str(int(v))``
+* ``None`` / float NaN             -> ``''`` (``na_rep``)
+
+Those are the only cell types a matched row of a read_csv chunk normally
+holds (text columns, the ``time_unix`` int, NaN for missing cells).  Any
+other cell (a non-NaN float, a bool, a timestamp ...) sends its row through
+the reference's own pandas call, so the bytes are identical by construction.
+
+What changes is the cost per row: no DataFrame per row, no ``chunk.iloc``
+per (article, ticker), no second ``dateutil`` parse per row (the article's
+date was already parsed once for the period filter, match_keywords.py:152),
+and one file open per ticker per chunk instead of one per row.
+"""
+from __future__ import annotations
+
+import csv
+import io
+import math
+import numbers
+import os
+from typing import Iterable, List, Sequence
+
+import numpy as np
+import pandas as pd
+
+
+def _cell(v):
+    """pandas' rendering of a one-value column, or ``None`` when the fast path does not cover ``v``."""
+    if isinstance(v, str):
+        return v
+    if v is None:
+        return ''
+    if isinstance(v, (bool, np.bool_)):
+        return None
+    if isinstance(v, (numbers.Integral, np.integer)):
+        return str(int(v))
+    if isinstance(v, (float, np.floating)) and math.isnan(v):
+        return ''
+    return None
+
+
+def _pandas_row_bytes(columns: Sequence[str], values: Sequence, header: bool) -> str:
+    """The reference's own call for one row (match_keywords.py:145-146), rendered to a string."""
+    buf = io.StringIO()
+    pd.DataFrame([dict(zip(columns, values))]).to_csv(buf, index=False, header=header)
+    return buf.getvalue()
+
+
+def append_rows(path: str, columns: Sequence[str], rows: Iterable[Sequence]) -> int:
+    """Append ``rows`` (value tuples in ``columns`` order) to ``path``; header iff the file is new.
+
+    Equivalent, byte for byte, to one ``pd.DataFrame([dict(zip(columns, r))]).to_csv(path, mode='a',
+    index=False, header=not os.path.exists(path))`` per row, in order.  Returns the rows written.
+    """
+    header = not os.path.exists(path)
+    n = 0
+    # newline='' so the csv writer's os.linesep terminator reaches the file unchanged (pandas does the same)
+    with open(path, 'a', newline='', encoding='utf-8') as fh:
+        w = csv.writer(fh, lineterminator=os.linesep, delimiter=',', quotechar='"',
+                       quoting=csv.QUOTE_MINIMAL, doublequote=True, escapechar=None)
+        for values in rows:
+            cells: List = [_cell(v) for v in values]
+            if any(c is None for c in cells):
+                fh.write(_pandas_row_bytes(columns, values, header))
+            else:
+                if header:
+                    w.writerow(columns)
+                w.writerow(cells)
+            header = False
+            n += 1
+    return n

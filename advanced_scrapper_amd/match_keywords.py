@@ -30,6 +30,7 @@ from typing import Dict, List, Optional
 import pandas as pd
 from dateutil import parser
 
+from . import egress
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
 from .matcher import GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits, pack_fields
@@ -64,9 +65,39 @@ def append_to_csv(source_name, ticker, matched_names, article):
 
 
 def _append_rows(source_name, ticker, rows):
-    path = _output_path(source_name, ticker)
-    header = not os.path.exists(path)
-    pd.DataFrame(rows).to_csv(path, mode='a', index=False, header=header)
+    """Append row dicts (or value tuples in ``OUTPUT_COLUMNS`` order), one reference append per row."""
+    values = (tuple(r[c] for c in OUTPUT_COLUMNS) if isinstance(r, dict) else r for r in rows)
+    egress.append_rows(_output_path(source_name, ticker), OUTPUT_COLUMNS, values)
+
+
+def _chunk_rows(chunk, results, dates):
+    """Output rows of a matched chunk grouped by ticker, in article order (value tuples, OUTPUT_COLUMNS order).
+
+    Equals ``_csv_row(matched, chunk.iloc[i])`` per (article, ticker): the cells are read from column lists
+    (one ``tolist`` per column instead of one ``iloc`` per row) and ``time_unix`` reuses the article's
+    period-filter parse (match_keywords.py:152 parses ``str(date_time)``, :131 parses ``date_time``; the two
+    agree when the cell is a ``str``, otherwise :131's own call runs).  A chunk without an object column
+    (``iloc`` would upcast its ints to floats) takes the ``iloc`` path.
+    """
+    rows_by_ticker: Dict[str, list] = {}
+    hit = [i for i, tm in enumerate(results) if tm]
+    if not hit:
+        return rows_by_ticker
+    if not any(dt == object for dt in chunk.dtypes):
+        for i in hit:
+            row = chunk.iloc[i]
+            for ticker, matched in results[i].items():
+                rows_by_ticker.setdefault(ticker, []).append(_csv_row(matched, row))
+        return rows_by_ticker
+    cols = {c: chunk[c].tolist() for c in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')}
+    for i in hit:
+        raw = cols['date_time'][i]
+        stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
+        tail = (cols['title'][i], cols['url'][i], cols['source'][i], cols['source_url'][i], cols['article_text'][i])
+        for ticker, matched in results[i].items():
+            rows_by_ticker.setdefault(ticker, []).append(
+                (stamp, raw, json.dumps(matched['text']), json.dumps(matched['title'])) + tail)
+    return rows_by_ticker
 
 
 # --------------------------------------------------------------------- matcher cache
@@ -102,6 +133,12 @@ def get_matcher(processed_data, device: Optional[int] = None, sample_texts=None)
 
 # --------------------------------------------------------------------- process_chunk
 def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
+    """``ticker_matches`` of every row of ``chunk`` and the parse error, if any (see :func:`_match`)."""
+    results, error, _ = _match(chunk, processed_data, matcher)
+    return results, error
+
+
+def _match(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     """``ticker_matches`` of every row of ``chunk`` (list aligned with the rows).
 
     Raises the reference's exceptions: a row whose ``date_time`` does not parse
@@ -110,7 +147,7 @@ def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     """
     n = len(chunk)
     if n == 0:
-        return [], None
+        return [], None, []
     texts = [field_str(v) for v in chunk['article_text'].tolist()]
     titles = [field_str(v) for v in chunk['title'].tolist()]
     dates: List = []
@@ -128,22 +165,14 @@ def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
         hits = matcher.match_strings(texts[:n_ok], titles[:n_ok])
         for doc, fields in group_hits(hits).items():
             results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
-    return results, error
+    return results, error, dates
 
 
 def process_chunk(source_name, chunk, processed_data):
     """Match every row of ``chunk`` and append the per-ticker CSV rows (match_keywords.py:148-192)."""
-    results, error = match_chunk(chunk, processed_data)
-    if results:
-        rows_by_ticker: Dict[str, list] = {}
-        for i, ticker_matches in enumerate(results):
-            if not ticker_matches:
-                continue
-            row = chunk.iloc[i]
-            for ticker, matched in ticker_matches.items():
-                rows_by_ticker.setdefault(ticker, []).append(_csv_row(matched, row))
-        for ticker, rows in rows_by_ticker.items():
-            _append_rows(source_name, ticker, rows)
+    results, error, dates = _match(chunk, processed_data)
+    for ticker, rows in _chunk_rows(chunk, results, dates).items():
+        _append_rows(source_name, ticker, rows)
     if error is not None:
         raise error
 
@@ -181,12 +210,8 @@ def main(argv=None):
     for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
         if matcher is None:
             matcher = get_matcher(processed, args.device, [field_str(v) for v in chunk['article_text'].tolist()])
-        results, error = match_chunk(chunk, processed, matcher)
-        rows_by_ticker: Dict[str, list] = {}
-        for i, tm in enumerate(results):
-            for ticker, matched in tm.items():
-                rows_by_ticker.setdefault(ticker, []).append(_csv_row(matched, chunk.iloc[i]))
-        for ticker, rows in rows_by_ticker.items():
+        results, error, dates = _match(chunk, processed, matcher)
+        for ticker, rows in _chunk_rows(chunk, results, dates).items():
             _append_rows(args.source, ticker, rows)
         if error is not None:
             raise error

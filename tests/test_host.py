@@ -205,6 +205,51 @@ def test_csv_egress_bytes(golden, tmp_path, monkeypatch):
             assert fh.read() == want[fn], fn
 
 
+def test_csv_egress_chunk_rows_bytes(golden, tmp_path, monkeypatch):
+    """The chunk-level egress (_chunk_rows: column lists, one date parse) == reference files after sort."""
+    from dateutil import parser as dparser
+    from advanced_scrapper_amd import match_keywords as mk
+    monkeypatch.chdir(tmp_path)
+    os.makedirs('yahoo_ticker_matched_articles')
+    want_m = golden.matches()
+    start = 0
+    for chunk in pd.read_csv(io.BytesIO(golden.articles_csv_bytes()), chunksize=golden.chunksize()):
+        results = want_m[start:start + len(chunk)]
+        dates = [dparser.parse(str(v)) if pd.notna(v) else None for v in chunk['date_time'].tolist()]
+        for ticker, rows in mk._chunk_rows(chunk, results, dates).items():
+            mk._append_rows('yahoo', ticker, rows)
+        start += len(chunk)
+    for fn in os.listdir('yahoo_ticker_matched_articles'):
+        mk.sort_matched_csv(f'yahoo_ticker_matched_articles/{fn}')
+    want = golden.outputs()
+    assert sorted(os.listdir('yahoo_ticker_matched_articles')) == sorted(want)
+    for fn in want:
+        with open(os.path.join('yahoo_ticker_matched_articles', fn), 'rb') as fh:
+            assert fh.read() == want[fn], fn
+
+
+def test_egress_append_rows_equals_pandas_per_row(tmp_path):
+    """egress.append_rows == one pd.DataFrame([row]).to_csv(mode='a') per row (match_keywords.py:145-146),
+    byte for byte, over quotes, commas, CR/LF, empty strings, unicode, NaN/None, ints, and the cell types
+    that take the pandas fallback (floats, bools)."""
+    import numpy as np
+    from advanced_scrapper_amd import egress
+    cols = ('time_unix', 'date_time', 'text_matches', 'title', 'url')
+    rng = np.random.default_rng(7)
+    atoms = ['', 'a', 'x,y', 'say "hi"', 'line\nbreak', 'cr\rlf\r\n', ' lead', 'trail ', 'é中文', '"',
+             float('nan'), None, 0, -17, np.int64(1700000000), 2 ** 70, 1.5, np.float64(2.25), True, 'NA']
+    rows = []
+    for _ in range(400):
+        rows.append(tuple(atoms[int(rng.integers(len(atoms)))] for _ in cols))
+    rows.append(tuple('' for _ in cols))
+    got, want = str(tmp_path / 'got.csv'), str(tmp_path / 'want.csv')
+    for k in range(0, len(rows), 37):       # several appends, header only on the first
+        egress.append_rows(got, cols, rows[k:k + 37])
+    for r in rows:
+        pd.DataFrame([dict(zip(cols, r))]).to_csv(want, mode='a', index=False, header=not os.path.exists(want))
+    assert open(got, 'rb').read() == open(want, 'rb').read()
+
+
 def test_append_to_csv_single_row(tmp_path, monkeypatch):
     from advanced_scrapper_amd import match_keywords as mk
     monkeypatch.chdir(tmp_path)
