@@ -31,6 +31,7 @@ import pandas as pd
 from dateutil import parser
 
 from . import egress
+from .dates import parse_date
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
 from .matcher import GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits, pack_fields
@@ -154,7 +155,7 @@ def _match(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     error = None
     for v in chunk['date_time'].tolist():
         try:
-            dates.append(parser.parse(str(v)) if pd.notna(v) else None)
+            dates.append(parse_date(str(v)) if pd.notna(v) else None)
         except Exception as exc:   # match_keywords.py:152 raises here for this row
             error = exc
             break

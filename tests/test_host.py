@@ -250,6 +250,34 @@ def test_egress_append_rows_equals_pandas_per_row(tmp_path):
     assert open(got, 'rb').read() == open(want, 'rb').read()
 
 
+def test_parse_date_equals_dateutil():
+    """dates.parse_date == dateutil.parser.parse on the dataset layout (random valid stamps) and on
+    edge strings (invalid fields, leap days, other layouts), including raising the same exception type."""
+    import numpy as np
+    from dateutil import parser as dparser
+    from advanced_scrapper_amd.dates import parse_date
+    rng = np.random.default_rng(11)
+    cases = []
+    for _ in range(3000):
+        y, mo, d = int(rng.integers(900, 2100)), int(rng.integers(0, 14)), int(rng.integers(0, 33))
+        hh, mi, ss = int(rng.integers(0, 26)), int(rng.integers(0, 62)), int(rng.integers(0, 62))
+        sep = ' ' if rng.random() < 0.8 else 'T'
+        cases.append(f'{y:04d}-{mo:02d}-{d:02d}{sep}{hh:02d}:{mi:02d}:{ss:02d}')
+    cases += ['2024-02-29 00:00:00', '2023-02-29 00:00:00', '1900-02-29 12:00:00', '2000-02-29 23:59:59',
+              '2020-13-01 00:00:00', '2020-01-13 00:00:00', '2020-12-31 24:00:00', '0999-01-01 00:00:00',
+              '2020-01-02 03:04:05.123', '2020-01-02 03:04:05Z', '2020-01-02 03:04:05+02:00', ' 2020-01-02 03:04:05',
+              '2020-01-02 03:04:05 ', '2020/01/02 03:04:05', 'Jan 2 2020', '2020-01-02', 'nan', '', '12']
+    for s in cases:
+        try:
+            want = dparser.parse(s)
+        except Exception as exc:   # noqa: BLE001
+            with pytest.raises(type(exc)):
+                parse_date(s)
+            continue
+        got = parse_date(s)
+        assert got == want and got.tzinfo == want.tzinfo, s
+
+
 def test_append_to_csv_single_row(tmp_path, monkeypatch):
     from advanced_scrapper_amd import match_keywords as mk
     monkeypatch.chdir(tmp_path)
