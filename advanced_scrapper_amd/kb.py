@@ -21,6 +21,7 @@ import json
 import os
 import re
 from dataclasses import dataclass, field
+from datetime import datetime
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -68,6 +69,28 @@ def is_within_period(article_date, start_date, end_date):
     if hi is not None:
         return a <= hi
     return True
+
+
+_EPOCH = datetime(1970, 1, 1, tzinfo=tzutc())
+_OPEN_LO, _OPEN_HI = -(1 << 63), 1 << 63
+
+
+def epoch_us(d) -> int:
+    """The instant ``is_within_period`` compares, as integer microseconds since 1970 (naive = UTC).
+
+    Exact for every datetime (timedelta arithmetic is integral), so ``lo <= a <= hi`` on these integers
+    equals the aware-datetime comparison of match_keywords.py:31-37.  Raises ``TypeError`` for a tzinfo
+    whose ``utcoffset`` is ``None`` (the reference's comparison raises for it too).
+    """
+    if d.tzinfo is None:
+        d = d.replace(tzinfo=_EPOCH.tzinfo)
+    td = d - _EPOCH
+    return (td.days * 86400 + td.seconds) * 1000000 + td.microseconds
+
+
+def period_us(start_date, end_date) -> Tuple[int, int]:
+    """(lo, hi) integer bounds of one KB period; a missing (falsy) bound is open (match_keywords.py:26-30)."""
+    return (epoch_us(start_date) if start_date else _OPEN_LO, epoch_us(end_date) if end_date else _OPEN_HI)
 
 
 # --------------------------------------------------------------------- a1
@@ -273,6 +296,18 @@ class CompiledKB:
     @property
     def n_patterns(self) -> int:
         return len(self.names)
+
+    def occurrences_us(self) -> Optional[List[List[Tuple[int, int, int, int]]]]:
+        """``occurrences`` with the periods as integer µs bounds (built once), or ``None`` when a bound has no
+        UTC offset and only the datetime comparison can decide."""
+        cached = self.__dict__.get('_occ_us', False)
+        if cached is False:
+            try:
+                cached = [[(ti, rank) + period_us(lo, hi) for (ti, rank, lo, hi) in occ] for occ in self.occurrences]
+            except TypeError:
+                cached = None
+            self.__dict__['_occ_us'] = cached
+        return cached
 
 
 def compile_kb(processed_data: Dict[str, Dict[str, Dict[str, tuple]]]) -> CompiledKB:

@@ -19,7 +19,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native
-from .kb import CompiledKB, compile_kb, is_within_period, word_bitmap
+from .kb import CompiledKB, compile_kb, epoch_us, is_within_period, word_bitmap
 
 ARENA_PAD = 64   # bytes readable past the last field (kw_scan reads 16-B tiles)
 
@@ -202,6 +202,13 @@ def assemble_ticker_matches(ckb: CompiledKB, doc_fields: Dict[int, Dict[int, Lis
     """
     if article_date is None:
         return {}
+    occ_us = ckb.occurrences_us()
+    a_us = None
+    if occ_us is not None:
+        try:
+            a_us = epoch_us(article_date)
+        except TypeError:
+            a_us = None
     per_ticker: Dict[int, Tuple[dict, dict]] = {}
     for field_idx in (0, 1):
         pats = doc_fields.get(field_idx)
@@ -209,11 +216,17 @@ def assemble_ticker_matches(ckb: CompiledKB, doc_fields: Dict[int, Dict[int, Lis
             continue
         for pat, positions in pats.items():
             best: Dict[int, int] = {}
-            for (ti, rank, start, end) in ckb.occurrences[pat]:
-                if ti in best:
-                    continue   # occurrences are in rank order: the first in-period one wins
-                if is_within_period(article_date, start, end):
-                    best[ti] = rank
+            if a_us is not None:
+                # integer form of is_within_period (kb.epoch_us): exact, no per-occurrence tz conversion
+                for (ti, rank, lo, hi) in occ_us[pat]:
+                    if lo <= a_us <= hi and ti not in best:
+                        best[ti] = rank
+            else:
+                for (ti, rank, start, end) in ckb.occurrences[pat]:
+                    if ti in best:
+                        continue   # occurrences are in rank order: the first in-period one wins
+                    if is_within_period(article_date, start, end):
+                        best[ti] = rank
             if best and ckb.invalid_regex[pat]:
                 # the reference's re.finditer(name, s) raises re.error here (:178/:180)
                 re.compile(ckb.names[pat])

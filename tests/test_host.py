@@ -278,6 +278,33 @@ def test_parse_date_equals_dateutil():
         assert got == want and got.tzinfo == want.tzinfo, s
 
 
+def test_period_us_equals_is_within_period():
+    """kb.period_us/epoch_us integer bounds decide exactly like is_within_period (match_keywords.py:17-37)
+    for naive and offset-aware dates, open bounds, equal bounds and microsecond neighbours."""
+    from datetime import datetime, timedelta, timezone
+    from advanced_scrapper_amd.kb import epoch_us, is_within_period, period_us
+    rng = random.Random(5)
+
+    def rnd():
+        d = datetime(rng.randint(1, 9999), rng.randint(1, 12), rng.randint(1, 28), rng.randint(0, 23),
+                     rng.randint(0, 59), rng.randint(0, 59), rng.choice([0, 1, 999999, rng.randint(0, 999999)]))
+        if rng.random() < 0.4:
+            try:
+                d = d.replace(tzinfo=timezone(timedelta(minutes=rng.randint(-900, 900))))
+                d - datetime(1970, 1, 1, tzinfo=timezone.utc)
+            except OverflowError:
+                d = d.replace(tzinfo=None)
+        return d
+
+    for _ in range(5000):
+        a = rnd()
+        lo = None if rng.random() < 0.2 else (a if rng.random() < 0.1 else rnd())
+        hi = None if rng.random() < 0.2 else (a + timedelta(microseconds=rng.choice([-1, 0, 1])) if
+                                              rng.random() < 0.2 and a.year < 9999 else rnd())
+        lo_us, hi_us = period_us(lo, hi)
+        assert (lo_us <= epoch_us(a) <= hi_us) == is_within_period(a, lo, hi), (a, lo, hi)
+
+
 def test_append_to_csv_single_row(tmp_path, monkeypatch):
     from advanced_scrapper_amd import match_keywords as mk
     monkeypatch.chdir(tmp_path)
