@@ -192,6 +192,11 @@ def group_hits(hits: np.ndarray) -> Dict[int, Dict[int, Dict[int, List[int]]]]:
     return out
 
 
+def _rank_order(d):
+    """Items of pattern -> (rank, positions) in rank order (dict order when there is at most one)."""
+    return sorted(d.items(), key=lambda kv: kv[1][0]) if len(d) > 1 else d.items()
+
+
 def assemble_ticker_matches(ckb: CompiledKB, doc_fields: Dict[int, Dict[int, List[int]]], article_date):
     """The reference's per-article ``ticker_matches`` (match_keywords.py:153-187).
 
@@ -238,7 +243,7 @@ def assemble_ticker_matches(ckb: CompiledKB, doc_fields: Dict[int, Dict[int, Lis
         text_d, title_d = per_ticker[ti]
         if not text_d and not title_d:
             continue
-        text = {ckb.names[p]: list(v[1]) for p, v in sorted(text_d.items(), key=lambda kv: kv[1][0])}
-        title = {ckb.names[p]: list(v[1]) for p, v in sorted(title_d.items(), key=lambda kv: kv[1][0])}
+        text = {ckb.names[p]: list(v[1]) for p, v in _rank_order(text_d)}
+        title = {ckb.names[p]: list(v[1]) for p, v in _rank_order(title_d)}
         result[ckb.tickers[ti]] = {'text': text, 'title': title}
     return result
