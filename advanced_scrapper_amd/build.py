@@ -82,8 +82,18 @@ def build_synth(force: bool = False) -> str:
     return out
 
 
+def build_kwrows(force: bool = False) -> str:
+    """``lib/libkwrows.so``: host C assembly of the output rows' JSON cells (csrc/kwrows.c)."""
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, 'libkwrows.so')
+    src = os.path.join(CSRC, 'kwrows.c')
+    if force or _stale(out, [src]):
+        _run(['gcc', '-O2', '-fPIC', '-shared', '-Wall', '-o', out, src])
+    return out
+
+
 def build_all(force: bool = False):
-    return build_kwmatch(force), build_synth(force)
+    return build_kwmatch(force), build_synth(force), build_kwrows(force)
 
 
 if __name__ == '__main__':

@@ -34,6 +34,7 @@ from . import egress
 from .dates import parse_date
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
+from .rows import assemble_json_rows
 from .matcher import GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits, pack_fields
 
 OUTPUT_COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source',
@@ -72,32 +73,44 @@ def _append_rows(source_name, ticker, rows):
 
 
 def _chunk_rows(chunk, results, dates):
-    """Output rows of a matched chunk grouped by ticker, in article order (value tuples, OUTPUT_COLUMNS order).
+    """Output rows of a matched chunk grouped by ticker, from ``ticker_matches`` dicts (see :func:`_cell_rows`)."""
+    cells = [(i, t, json.dumps(m['text']), json.dumps(m['title'])) for i, tm in enumerate(results)
+             for t, m in tm.items()]
+    return _cell_rows(chunk, cells, dates)
 
-    Equals ``_csv_row(matched, chunk.iloc[i])`` per (article, ticker): the cells are read from column lists
-    (one ``tolist`` per column instead of one ``iloc`` per row) and ``time_unix`` reuses the article's
-    period-filter parse (match_keywords.py:152 parses ``str(date_time)``, :131 parses ``date_time``; the two
-    agree when the cell is a ``str``, otherwise :131's own call runs).  A chunk without an object column
-    (``iloc`` would upcast its ints to floats) takes the ``iloc`` path.
+
+def _cell_rows(chunk, cells, dates):
+    """Output rows grouped by ticker, in article order (value tuples, OUTPUT_COLUMNS order).
+
+    ``cells`` = ``(row index, ticker, text_matches JSON, title_matches JSON)`` in article then ticker order
+    (rows.assemble_json_rows, or json.dumps of ``ticker_matches``).  Each row equals ``_csv_row(matched,
+    chunk.iloc[i])``: the cells are read from column lists (one ``tolist`` per column instead of one ``iloc``
+    per row) and ``time_unix`` reuses the article's period-filter parse (match_keywords.py:152 parses
+    ``str(date_time)``, :131 parses ``date_time``; the two agree when the cell is a ``str``, otherwise :131's
+    own call runs).  A chunk without an object column (``iloc`` would upcast its ints to floats) takes the
+    ``iloc`` path.
     """
     rows_by_ticker: Dict[str, list] = {}
-    hit = [i for i, tm in enumerate(results) if tm]
-    if not hit:
+    if not cells:
         return rows_by_ticker
     if not any(dt == object for dt in chunk.dtypes):
-        for i in hit:
+        for i, ticker, tj, tt in cells:
             row = chunk.iloc[i]
-            for ticker, matched in results[i].items():
-                rows_by_ticker.setdefault(ticker, []).append(_csv_row(matched, row))
+            stamp = int(parser.parse(row['date_time']).timestamp())
+            rows_by_ticker.setdefault(ticker, []).append(
+                (stamp, row['date_time'], tj, tt, row['title'], row['url'], row['source'], row['source_url'],
+                 row['article_text']))
         return rows_by_ticker
     cols = {c: chunk[c].tolist() for c in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')}
-    for i in hit:
-        raw = cols['date_time'][i]
-        stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
-        tail = (cols['title'][i], cols['url'][i], cols['source'][i], cols['source_url'][i], cols['article_text'][i])
-        for ticker, matched in results[i].items():
-            rows_by_ticker.setdefault(ticker, []).append(
-                (stamp, raw, json.dumps(matched['text']), json.dumps(matched['title'])) + tail)
+    last, stamp, tail = -1, None, None
+    for i, ticker, tj, tt in cells:
+        if i != last:
+            raw = cols['date_time'][i]
+            stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
+            tail = (cols['title'][i], cols['url'][i], cols['source'][i], cols['source_url'][i],
+                    cols['article_text'][i])
+            last = i
+        rows_by_ticker.setdefault(ticker, []).append((stamp, raw, tj, tt) + tail)
     return rows_by_ticker
 
 
@@ -140,7 +153,21 @@ def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
 
 
 def _match(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
-    """``ticker_matches`` of every row of ``chunk`` (list aligned with the rows).
+    """``ticker_matches`` of every row of ``chunk`` (list aligned with the rows), the error, the dates."""
+    hits, error, dates, matcher = _match_hits(chunk, processed_data, matcher)
+    return _results(matcher, hits, dates), error, dates
+
+
+def _results(matcher, hits, dates):
+    results: List[dict] = [{} for _ in range(len(dates))]
+    if hits is not None and len(hits):
+        for doc, fields in group_hits(hits).items():
+            results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
+    return results
+
+
+def _match_hits(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
+    """Device hit records of ``chunk``'s rows, the parse error (if any), the parsed dates and the matcher.
 
     Raises the reference's exceptions: a row whose ``date_time`` does not parse
     raises after the rows before it were matched (the returned ``error`` lets
@@ -148,7 +175,7 @@ def _match(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     """
     n = len(chunk)
     if n == 0:
-        return [], None, []
+        return None, None, [], matcher
     texts = [field_str(v) for v in chunk['article_text'].tolist()]
     titles = [field_str(v) for v in chunk['title'].tolist()]
     dates: List = []
@@ -161,21 +188,31 @@ def _match(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
             break
     n_ok = len(dates)
     matcher = matcher or get_matcher(processed_data, sample_texts=texts[:n_ok])
-    results: List[dict] = [{} for _ in range(n_ok)]
-    if n_ok:
-        hits = matcher.match_strings(texts[:n_ok], titles[:n_ok])
-        for doc, fields in group_hits(hits).items():
-            results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
-    return results, error, dates
+    hits = matcher.match_strings(texts[:n_ok], titles[:n_ok]) if n_ok else None
+    return hits, error, dates, matcher
+
+
+def _write_chunk(source_name, chunk, processed_data, matcher: Optional[GpuMatcher] = None):
+    """Match ``chunk`` and append its rows; the JSON cells come from libkwrows (rows.py), or from the
+    Python assembly when only it can decide (offset-less timezones, a non-compiling in-period name)."""
+    hits, error, dates, matcher = _match_hits(chunk, processed_data, matcher)
+    cells = None
+    if hits is not None:
+        cells = assemble_json_rows(matcher.ckb, hits, dates)
+    if cells is None:
+        by_ticker = _chunk_rows(chunk, _results(matcher, hits, dates), dates)
+    else:
+        by_ticker = _cell_rows(chunk, cells, dates)
+    for ticker, rows in by_ticker.items():
+        _append_rows(source_name, ticker, rows)
+    if error is not None:
+        raise error
+    return matcher
 
 
 def process_chunk(source_name, chunk, processed_data):
     """Match every row of ``chunk`` and append the per-ticker CSV rows (match_keywords.py:148-192)."""
-    results, error, dates = _match(chunk, processed_data)
-    for ticker, rows in _chunk_rows(chunk, results, dates).items():
-        _append_rows(source_name, ticker, rows)
-    if error is not None:
-        raise error
+    _write_chunk(source_name, chunk, processed_data)
 
 
 # --------------------------------------------------------------------- sort
@@ -211,11 +248,7 @@ def main(argv=None):
     for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
         if matcher is None:
             matcher = get_matcher(processed, args.device, [field_str(v) for v in chunk['article_text'].tolist()])
-        results, error, dates = _match(chunk, processed, matcher)
-        for ticker, rows in _chunk_rows(chunk, results, dates).items():
-            _append_rows(args.source, ticker, rows)
-        if error is not None:
-            raise error
+        matcher = _write_chunk(args.source, chunk, processed, matcher)
     print("All matched CSV files have been processed.")
     for name in os.listdir(out_dir):
         sort_matched_csv(f"{out_dir}/{name}")

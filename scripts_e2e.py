@@ -26,7 +26,8 @@ def main():
     import pandas as pd
     from advanced_scrapper_amd import match_keywords as mk, synth
     from advanced_scrapper_amd.kb import compile_kb
-    from advanced_scrapper_amd.matcher import field_str, group_hits, assemble_ticker_matches
+    from advanced_scrapper_amd.matcher import field_str
+    from advanced_scrapper_amd.rows import assemble_json_rows
     from advanced_scrapper_amd.dates import parse_date
     from tests import golden_data
     processed = golden_data.kb_processed()
@@ -55,11 +56,9 @@ def main():
         c3 = time.perf_counter()
         hits = matcher.match_strings(texts, titles)
         c4 = time.perf_counter(); t['gpu_match'] += c4 - c3
-        results = [{} for _ in range(len(chunk))]
-        for doc, fields in group_hits(hits).items():
-            results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
+        cells = assemble_json_rows(matcher.ckb, hits, dates)
         c5 = time.perf_counter(); t['assemble'] += c5 - c4
-        by = mk._chunk_rows(chunk, results, dates)
+        by = mk._cell_rows(chunk, cells, dates)
         c6 = time.perf_counter(); t['rows'] += c6 - c5
         for ticker, rows in by.items():
             mk._append_rows('yahoo', ticker, rows)

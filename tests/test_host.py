@@ -305,6 +305,37 @@ def test_period_us_equals_is_within_period():
         assert (lo_us <= epoch_us(a) <= hi_us) == is_within_period(a, lo, hi), (a, lo, hi)
 
 
+def test_native_json_rows_equal_python_assembly(golden):
+    """rows.assemble_json_rows (csrc/kwrows.c) == group_hits + assemble_ticker_matches + json.dumps on seeded
+    random hit records over the golden KB and articles (periods, both fields, position-less matches)."""
+    import json
+    from dateutil import parser as dparser
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import assemble_ticker_matches, group_hits
+    from advanced_scrapper_amd.rows import assemble_json_rows
+    ckb = compile_kb(golden.kb_processed())
+    frame = pd.read_csv(io.BytesIO(golden.articles_csv_bytes()))
+    dates = [dparser.parse(str(v)) if pd.notna(v) else None for v in frame['date_time'].tolist()]
+    valid = [p for p in range(len(ckb.names)) if not ckb.invalid_regex[p]]
+    rng = np.random.default_rng(3)
+    recs = []
+    for d in range(len(frame)):
+        for _ in range(int(rng.integers(0, 6))):
+            p, f, k = valid[int(rng.integers(len(valid)))], int(rng.integers(2)), int(rng.integers(0, 4))
+            if k == 0:
+                recs.append((d, p, _native.KW_NOPOS, f))
+            for q in rng.choice(5000, size=k, replace=False):
+                recs.append((d, p, int(q), f))
+    hits = np.array(recs, dtype=_native.HIT_DTYPE)
+    rng.shuffle(hits)
+    got = assemble_json_rows(ckb, hits, dates)
+    want = [(d, t, json.dumps(m['text']), json.dumps(m['title']))
+            for d, fields in sorted(group_hits(hits).items())
+            for t, m in assemble_ticker_matches(ckb, fields, dates[d]).items()]
+    assert len(want) > 500 and got == want
+
+
 def test_append_to_csv_single_row(tmp_path, monkeypatch):
     from advanced_scrapper_amd import match_keywords as mk
     monkeypatch.chdir(tmp_path)
