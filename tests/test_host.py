@@ -236,7 +236,7 @@ def test_egress_append_rows_equals_pandas_per_row(tmp_path):
     from advanced_scrapper_amd import egress
     cols = ('time_unix', 'date_time', 'text_matches', 'title', 'url')
     rng = np.random.default_rng(7)
-    atoms = ['', 'a', 'x,y', 'say "hi"', 'line\nbreak', 'cr\rlf\r\n', ' lead', 'trail ', 'é中文', '"',
+    atoms = ['', 'a', 'x,y', 'say "hi"', 'line\nbreak', 'cr\rlf\r\n', 'cr\ronly', 'tab\t', '\x1c', ' lead', 'trail ', 'é中文', '"',
              float('nan'), None, 0, -17, np.int64(1700000000), 2 ** 70, 1.5, np.float64(2.25), True, 'NA']
     rows = []
     for _ in range(400):
@@ -248,6 +248,13 @@ def test_egress_append_rows_equals_pandas_per_row(tmp_path):
     for r in rows:
         pd.DataFrame([dict(zip(cols, r))]).to_csv(want, mode='a', index=False, header=not os.path.exists(want))
     assert open(got, 'rb').read() == open(want, 'rb').read()
+    # a NUL cell: pandas' writer raises, and so does append_rows (the rows before it are written first)
+    bad = ('a', 'b\0c', 'x', 'y', 'z')
+    with pytest.raises(Exception) as want_exc:
+        pd.DataFrame([dict(zip(cols, bad))]).to_csv(str(tmp_path / 'w2.csv'), index=False)
+    with pytest.raises(type(want_exc.value)):
+        egress.append_rows(str(tmp_path / 'g2.csv'), cols, [('1', '2', '3', '4', '5'), bad])
+    assert open(str(tmp_path / 'g2.csv'), 'rb').read() == b'time_unix,date_time,text_matches,title,url\n1,2,3,4,5\n'
 
 
 def test_parse_date_equals_dateutil():
