@@ -69,13 +69,14 @@ def append_rows(path: str, columns: Sequence[str], rows: Iterable[Sequence]) -> 
     with open(path, 'a', newline='', encoding='utf-8') as fh:
         w = csv.writer(fh, lineterminator=os.linesep, delimiter=',', quotechar='"',
                        quoting=csv.QUOTE_MINIMAL, doublequote=True, escapechar=None)
+        head = _join(list(columns)) if header else None
         for values in rows:
-            cells: List = [_cell(v) for v in values]
-            line = None if any(c is None for c in cells) else _join(cells)
-            if line is None or (header and _join(columns) is None):
+            line = _line(values)
+            if line is None or (header and head is None):
                 if lines:
                     fh.write(''.join(lines))
                     lines.clear()
+                cells: List = [_cell(v) for v in values]
                 if any(c is None for c in cells):
                     fh.write(_pandas_row_bytes(columns, values, header))
                 else:
@@ -84,7 +85,7 @@ def append_rows(path: str, columns: Sequence[str], rows: Iterable[Sequence]) -> 
                     w.writerow(cells)
             else:
                 if header:
-                    lines.append(_join(columns))
+                    lines.append(head)
                 lines.append(line)
             header = False
             n += 1
@@ -95,6 +96,30 @@ def append_rows(path: str, columns: Sequence[str], rows: Iterable[Sequence]) -> 
 
 _LINESEP = os.linesep
 _QUOTE_TRIGGERS = tuple(dict.fromkeys((',', '"') + tuple(os.linesep)))
+
+
+def _line(values: Sequence):
+    """``_join`` of the rendered cells in one pass (``None`` when a cell needs the pandas or writer path)."""
+    if not _NL_ONLY:
+        cells = [_cell(v) for v in values]
+        return None if any(c is None for c in cells) else _join(cells)
+    out = []
+    for v in values:
+        if type(v) is not str:
+            v = _cell(v)
+            if v is None:
+                return None
+        if '\0' in v:
+            return None
+        if ',' in v or '"' in v or '\n' in v:
+            v = '"' + v.replace('"', '""') + '"'
+        out.append(v)
+    if len(out) == 1 and out[0] == '':
+        out[0] = '""'
+    return ','.join(out) + '\n'
+
+
+_NL_ONLY = os.linesep == '\n'
 
 
 def _join(cells: Sequence[str]):
