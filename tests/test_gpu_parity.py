@@ -93,10 +93,20 @@ def test_golden_ticker_level(env, golden):
             assert list(got[t]['title']) == list(want[d][t]['title']), (d, t)
 
 
-def test_dropin_process_chunk_csv_bytes(env, golden, tmp_path, monkeypatch):
-    """The drop-in driver writes byte-identical per-ticker CSVs (after the sort)."""
+@pytest.mark.parametrize('native_cells', [True, False])
+def test_dropin_process_chunk_csv_bytes(env, golden, tmp_path, monkeypatch, native_cells):
+    """The drop-in driver writes byte-identical per-ticker CSVs (after the sort), with the JSON cells from
+    libkwrows (checked to be the path taken) and with the Python assembly it falls back to."""
     from advanced_scrapper_amd import match_keywords as mk
     monkeypatch.chdir(tmp_path)
+    native = mk.assemble_json_rows
+    calls = []
+
+    def cells(ckb, hits, dates):
+        out = native(ckb, hits, dates) if native_cells else None
+        calls.append(out is not None)
+        return out
+    monkeypatch.setattr(mk, 'assemble_json_rows', cells)
     os.makedirs('yahoo_ticker_matched_articles')
     processed = env['processed']
     for chunk in pd.read_csv(io.BytesIO(golden.articles_csv_bytes()), chunksize=golden.chunksize()):
@@ -109,6 +119,7 @@ def test_dropin_process_chunk_csv_bytes(env, golden, tmp_path, monkeypatch):
     assert sorted(got) == sorted(want)
     for fn in want:
         assert got[fn] == want[fn], fn
+    assert calls and all(c == native_cells for c in calls)
 
 
 @pytest.mark.parametrize('seed', [7, 11])
