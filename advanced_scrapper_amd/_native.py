@@ -27,7 +27,9 @@ HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('fiel
 
 # every symbol include/kwmatch.h and include/kwdedup.h declare
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
-           'kw_last_kernel_times', 'kw_last_error', 'kw_destroy',
+           'kw_last_kernel_times', 'kw_doc_routes', 'kw_last_error', 'kw_destroy',
+           'kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_comm_last_error',
+           'kw_comm_destroy',
            'kw_dedup_create', 'kw_dedup_run', 'kw_dedup_counts', 'kw_dedup_kept_size', 'kw_dedup_kept_copy',
            'kw_dedup_last_ms', 'kw_dedup_last_error', 'kw_dedup_destroy', 'dedup_urls')
 
@@ -35,6 +37,8 @@ EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_l
 KW_URL_NO_HTML, KW_URL_KEPT, KW_URL_FILTERED, KW_URL_DUPLICATE = 0, 1, 2, 3
 KW_DEDUP_NORMALIZE = 1
 KW_N_STATS = 13
+KW_COMM_ID_BYTES = 128
+KW_ROUTE_SCAN, KW_ROUTE_RESOLVE, KW_ROUTE_GENERIC = 0, 1, 2
 
 
 class KwError(RuntimeError):
@@ -83,6 +87,17 @@ def lib() -> ctypes.CDLL:
     L.kw_last_kernel_ms.restype = ctypes.c_int
     L.kw_last_kernel_times.argtypes = [vp, vp, i32]
     L.kw_last_kernel_times.restype = ctypes.c_int
+    L.kw_doc_routes.argtypes = [vp, vp, i64]
+    L.kw_doc_routes.restype = ctypes.c_int
+    L.kw_comm_unique_id.argtypes = [vp]
+    L.kw_comm_init.argtypes = [i32, i32, vp, i32, ctypes.POINTER(vp)]
+    L.kw_allgather_counts.argtypes = [vp, i64, vp, vp]
+    L.kw_allgather_hits.argtypes = [vp, vp, i64, i64, i32, vp, i64, ctypes.POINTER(i64), vp, vp]
+    L.kw_comm_destroy.argtypes = [vp]
+    for f in ('kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_comm_destroy'):
+        getattr(L, f).restype = ctypes.c_int
+    L.kw_comm_last_error.argtypes = [vp]
+    L.kw_comm_last_error.restype = ctypes.c_char_p
     L.kw_last_error.argtypes = [vp]
     L.kw_last_error.restype = ctypes.c_char_p
     L.kw_destroy.argtypes = [vp]
@@ -94,6 +109,12 @@ def lib() -> ctypes.CDLL:
 def check(rc: int, handle=None) -> None:
     if rc != KW_OK:
         msg = lib().kw_last_error(handle)
+        raise KwError(rc, msg.decode('utf-8', 'replace') if msg else '')
+
+
+def check_comm(rc: int, comm=None) -> None:
+    if rc != KW_OK:
+        msg = lib().kw_comm_last_error(comm)
         raise KwError(rc, msg.decode('utf-8', 'replace') if msg else '')
 
 

@@ -37,7 +37,7 @@ def build_kwmatch(force: bool = False) -> str:
     if force or _stale(out, srcs):
         units = [s for s in srcs if s.endswith('.hip')]
         _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC', '-Wall',
-              '-o', out] + units)
+              '-o', out] + units + ['-ldl'])
     return out
 
 
@@ -56,7 +56,7 @@ def build_kwmatch_stage(stage: int, force: bool = False) -> str:
     if force or _stale(out, srcs):
         units = [s for s in srcs if s.endswith('.hip')]
         _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC', f'-DFK_STAGE={stage}',
-              '-o', out] + units)
+              '-o', out] + units + ['-ldl'])
     return out
 
 
@@ -69,7 +69,7 @@ def build_kwmatch_variant(tag: str, defines, force: bool = False) -> str:
     if force or _stale(out, srcs):
         units = [s for s in srcs if s.endswith('.hip')]
         _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC'] +
-             [d if d.startswith('-') else f'-D{d}' for d in defines] + ['-o', out] + units)
+             [d if d.startswith('-') else f'-D{d}' for d in defines] + ['-o', out] + units + ['-ldl'])
     return out
 
 

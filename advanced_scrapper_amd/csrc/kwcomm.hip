@@ -1,0 +1,224 @@
+// libkwmatch multi-GPU exchange: RCCL over xGMI, one process per GPU.
+//
+// Matching shards with no data-path exchange (every article is independent,
+// SURVEY.md §8(e)); the only collectives are the exchange of per-rank hit
+// counts and of the packed 16-byte hit records, so that the rank that writes
+// the output (or every rank) holds the records of the whole batch in document
+// order.  This replaces the reference's process pool + shared filesystem
+// (match_keywords.py:230-238: np.array_split + Pool.starmap), whose only
+// "exchange" is the per-ticker CSV files every worker appends to.
+//
+// RCCL is resolved at run time (dlopen): the copy torch has already loaded
+// (RTLD_NOLOAD, soname librccl.so.1) is reused so one process never holds two
+// RCCL runtimes; otherwise /opt/rocm's.  Without RCCL the kw_comm_* calls fail
+// with KW_EUNSUPPORTED; the single-GPU path never needs it.
+#include <hip/hip_runtime.h>
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kwmatch.h"
+
+namespace {
+
+// the subset of rccl.h this file calls (types are ABI-stable in NCCL 2.x)
+typedef struct ncclComm *ncclComm_t;
+typedef struct { char internal[128]; } ncclUniqueId;
+typedef int ncclResult_t;
+enum { nccl_int8 = 0, nccl_uint32 = 3, nccl_int64 = 4 };
+
+struct Rccl {
+    void *so = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+Rccl g_rccl;
+std::string g_comm_err;
+
+bool load_rccl(std::string &err)
+{
+    if (g_rccl.so) return true;
+    void *so = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!so) so = dlopen("librccl.so.1", RTLD_NOW);
+    if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!so) {
+        err = std::string("kw_comm: RCCL (librccl.so.1) not found: ") + dlerror();
+        return false;
+    }
+    Rccl r;
+    r.so = so;
+#define KW_SYM(field, name)                                                   \
+    do {                                                                      \
+        *(void **)(&r.field) = dlsym(so, name);                               \
+        if (!r.field) { err = "kw_comm: RCCL symbol missing: " name; return false; } \
+    } while (0)
+    KW_SYM(GetUniqueId, "ncclGetUniqueId");
+    KW_SYM(CommInitRank, "ncclCommInitRank");
+    KW_SYM(CommDestroy, "ncclCommDestroy");
+    KW_SYM(AllGather, "ncclAllGather");
+    KW_SYM(Send, "ncclSend");
+    KW_SYM(Recv, "ncclRecv");
+    KW_SYM(GroupStart, "ncclGroupStart");
+    KW_SYM(GroupEnd, "ncclGroupEnd");
+    KW_SYM(GetErrorString, "ncclGetErrorString");
+#undef KW_SYM
+    g_rccl = r;
+    return true;
+}
+
+// records of one rank -> global document ids (doc + base)
+__global__ void kw_rebase_kernel(const kw_hit *__restrict__ src, kw_hit *__restrict__ dst, int64_t n, uint32_t base)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        kw_hit r = src[i];
+        r.doc += base;
+        dst[i] = r;
+    }
+}
+
+}  // namespace
+
+struct kw_comm {
+    int nranks = 1, rank = 0, device = 0;
+    ncclComm_t comm = nullptr;
+    int64_t *d_counts = nullptr;   // [nranks + 1]: own count at [nranks], gathered at [0, nranks)
+    kw_hit *d_stage = nullptr;     // this rank's records, rebased
+    size_t stage_cap = 0;
+    std::string err;
+};
+
+#define CCHK(c, x)                                                                          \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) { (c)->err = std::string("HIP error ") + hipGetErrorString(e_) + " at " #x; return KW_EHIP; } \
+    } while (0)
+#define NCHK(c, x)                                                                          \
+    do {                                                                                    \
+        ncclResult_t r_ = (x);                                                              \
+        if (r_ != 0) { (c)->err = std::string("RCCL error: ") + g_rccl.GetErrorString(r_) + " at " #x; return KW_EHIP; } \
+    } while (0)
+
+extern "C" int kw_comm_unique_id(uint8_t *id_out)
+{
+    if (!id_out) return KW_EINVAL;
+    if (!load_rccl(g_comm_err)) return KW_EUNSUPPORTED;
+    ncclUniqueId id;
+    ncclResult_t r = g_rccl.GetUniqueId(&id);
+    if (r != 0) { g_comm_err = std::string("ncclGetUniqueId: ") + g_rccl.GetErrorString(r); return KW_EHIP; }
+    memcpy(id_out, id.internal, KW_COMM_ID_BYTES);
+    return KW_OK;
+}
+
+extern "C" int kw_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, int32_t device, kw_comm **out)
+{
+    if (!out) return KW_EINVAL;
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks || !id) { g_comm_err = "kw_comm_init: bad arguments"; return KW_EINVAL; }
+    if (!load_rccl(g_comm_err)) return KW_EUNSUPPORTED;
+    kw_comm *c = new kw_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    *out = c;   // the caller reads kw_comm_last_error and destroys it on failure
+    CCHK(c, hipSetDevice(device));
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, KW_COMM_ID_BYTES);
+    NCHK(c, g_rccl.CommInitRank(&c->comm, nranks, uid, rank));
+    CCHK(c, hipMalloc(&c->d_counts, sizeof(int64_t) * (nranks + 1)));
+    return KW_OK;
+}
+
+// all-gather one int64 per rank (blocking: the host needs the values)
+static int gather_counts(kw_comm *c, int64_t count, int64_t *counts, hipStream_t st)
+{
+    CCHK(c, hipMemcpyAsync(c->d_counts + c->nranks, &count, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    NCHK(c, g_rccl.AllGather(c->d_counts + c->nranks, c->d_counts, 1, nccl_int64, c->comm, st));
+    CCHK(c, hipMemcpyAsync(counts, c->d_counts, sizeof(int64_t) * c->nranks, hipMemcpyDeviceToHost, st));
+    CCHK(c, hipStreamSynchronize(st));
+    return KW_OK;
+}
+
+extern "C" int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, void *stream)
+{
+    if (!c || !counts) return KW_EINVAL;
+    CCHK(c, hipSetDevice(c->device));
+    return gather_counts(c, count, counts, (hipStream_t)stream);
+}
+
+extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
+                                 kw_hit *d_out, int64_t cap, int64_t *n_total, int64_t *counts, void *stream)
+{
+    if (!c || !n_total || n < 0 || (n > 0 && !d_local)) return KW_EINVAL;
+    if (root >= c->nranks || doc_base < 0) { c->err = "kw_allgather_hits: bad root or doc_base"; return KW_EINVAL; }
+    hipStream_t st = (hipStream_t)stream;
+    CCHK(c, hipSetDevice(c->device));
+    int rc;
+    std::vector<int64_t> cnt(c->nranks, 0);
+    rc = gather_counts(c, n, cnt.data(), st);
+    if (rc) return rc;
+    std::vector<int64_t> pre(c->nranks + 1, 0);
+    for (int r = 0; r < c->nranks; ++r) pre[r + 1] = pre[r] + cnt[r];
+    if (counts) memcpy(counts, cnt.data(), sizeof(int64_t) * c->nranks);
+    *n_total = pre[c->nranks];
+    const bool receive = root < 0 || root == c->rank;
+    if (receive && pre[c->nranks] > cap) { c->err = "kw_allgather_hits: destination too small"; return KW_EINVAL; }
+    if (receive && pre[c->nranks] > 0 && !d_out) { c->err = "kw_allgather_hits: null destination"; return KW_EINVAL; }
+    if (doc_base + n > 0xFFFFFFFFll) { c->err = "kw_allgather_hits: global document ids beyond 2^32"; return KW_EINVAL; }
+    // this rank's records, rebased: straight into its slot of the output when it receives, else into
+    // the staging buffer it sends from
+    kw_hit *mine = nullptr;
+    if (n > 0) {
+        if (receive) {
+            mine = d_out + pre[c->rank];
+        } else {
+            if ((size_t)n > c->stage_cap) {
+                if (c->d_stage) (void)hipFree(c->d_stage);
+                c->stage_cap = (size_t)n + (size_t)n / 4 + 1024;
+                CCHK(c, hipMalloc(&c->d_stage, c->stage_cap * sizeof(kw_hit)));
+            }
+            mine = c->d_stage;
+        }
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(kw_rebase_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d_local, mine, n, (uint32_t)doc_base);
+        CCHK(c, hipGetLastError());
+    }
+    if (c->nranks == 1) return KW_OK;
+    // point-to-point over the xGMI mesh: every (sender, receiver) pair moves exactly its records
+    NCHK(c, g_rccl.GroupStart());
+    for (int p = 0; p < c->nranks; ++p) {
+        if (p == c->rank) continue;
+        const bool p_receives = root < 0 || root == p;
+        if (p_receives && n > 0) NCHK(c, g_rccl.Send(mine, (size_t)n * 4, nccl_uint32, p, c->comm, st));
+        if (receive && cnt[p] > 0) NCHK(c, g_rccl.Recv(d_out + pre[p], (size_t)cnt[p] * 4, nccl_uint32, p, c->comm, st));
+    }
+    NCHK(c, g_rccl.GroupEnd());
+    return KW_OK;
+}
+
+extern "C" const char *kw_comm_last_error(kw_comm *c)
+{
+    return c ? c->err.c_str() : g_comm_err.c_str();
+}
+
+extern "C" int kw_comm_destroy(kw_comm *c)
+{
+    if (!c) return KW_OK;
+    (void)hipSetDevice(c->device);
+    if (c->comm) (void)g_rccl.CommDestroy(c->comm);
+    if (c->d_counts) (void)hipFree(c->d_counts);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    delete c;
+    return KW_OK;
+}

@@ -1238,6 +1238,22 @@ extern "C" int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n)
     return KW_OK;
 }
 
+extern "C" int kw_doc_routes(kw_handle *h, uint8_t *routes, int64_t n)
+{
+    if (!h || (n > 0 && !routes)) return KW_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = finish(h);
+    if (rc) return rc;
+    if (n != h->n_docs) { h->err = "kw_doc_routes: n differs from the scanned document count"; return KW_EINVAL; }
+    std::vector<uint2> hdr((size_t)n);
+    if (n > 0) HIPCHK(h, hipMemcpy(hdr.data(), h->FS.hdr, (size_t)n * sizeof(uint2), hipMemcpyDeviceToHost));
+    for (int64_t d = 0; d < n; ++d) {
+        const uint32_t y = hdr[d].y;
+        routes[d] = (y & DH_DEFER) ? KW_ROUTE_GENERIC : (y & (DH_NA0 | DH_NA1)) ? KW_ROUTE_RESOLVE : KW_ROUTE_SCAN;
+    }
+    return KW_OK;
+}
+
 extern "C" const char *kw_last_error(kw_handle *h)
 {
     if (!h) return g_err.c_str();

@@ -75,7 +75,7 @@ int64_t kwrows_assemble(const kw_hit_rec *h, int64_t n_hits, const int64_t *date
     int64_t *seen = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n_tickers > 0 ? n_tickers : 1));
     int64_t ecap = 1024, ne = 0, rows = 0, group = 0, rc = 0;
     entry_t *ent = (entry_t *)malloc(sizeof(entry_t) * (size_t)ecap);
-    if (!seen || !ent) { free(seen); free(ent); return -1; }
+    if (!seen || !ent) { free(seen); free(ent); return -3; }   /* allocation failure */
     for (int32_t t = 0; t < n_tickers; ++t) seen[t] = -1;
     sink_t s = {out, 0, out_cap, 0};
     out_off[0] = 0;
@@ -100,7 +100,7 @@ int64_t kwrows_assemble(const kw_hit_rec *h, int64_t n_hits, const int64_t *date
                 if (ne == ecap) {
                     ecap *= 2;
                     entry_t *ne_ = (entry_t *)realloc(ent, sizeof(entry_t) * (size_t)ecap);
-                    if (!ne_) { rc = -1; break; }
+                    if (!ne_) { rc = -3; break; }
                     ent = ne_;
                 }
                 ent[ne++] = (entry_t){t, (int32_t)h[g].field, occ_rank[o], (int32_t)p, g, ge};

@@ -8,8 +8,12 @@ documents and a full copy of the compiled KB.  The only collectives are
 * ``gather_hits``       — the packed 16-B hit records, padded to the largest
                           rank, all-gathered so any rank can write the output.
 
-With backend "nccl" torch.distributed is RCCL on ROCm; "gloo" is used for the
-CPU tests.
+On the GPU the exchange is libkwmatch's own RCCL communicator
+(:class:`KwComm`, ``kw_comm_*`` in include/kwmatch.h: counts all-gather, then
+point-to-point send/recv of the exact records over the xGMI mesh);
+torch.distributed only carries the communicator id and the barriers.  The
+torch-collective forms below (``allgather_counts`` / ``gather_hits``) are the
+same exchange over any backend, used by the ``gloo`` CPU tests.
 """
 from __future__ import annotations
 
@@ -39,6 +43,103 @@ def init(backend: str = 'nccl'):
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     return rank, world, local
+
+
+class KwComm:
+    """libkwmatch's RCCL communicator (kw_comm_init / kw_allgather_counts / kw_allgather_hits).
+
+    The id is made by rank 0 (ncclGetUniqueId) and broadcast over the
+    torch.distributed process group; every rank then joins on its device.
+    """
+
+    def __init__(self, rank: int, world: int, device: int):
+        import ctypes
+        import torch.distributed as td
+        from . import _native
+        self._n = _native
+        self.rank, self.world, self.device = rank, world, device
+        L = _native.lib()
+        idb = np.zeros(_native.KW_COMM_ID_BYTES, dtype=np.uint8)
+        if rank == 0:
+            _native.check_comm(L.kw_comm_unique_id(_native.ptr(idb)))
+        if world > 1:
+            obj = [idb.tobytes()]
+            td.broadcast_object_list(obj, src=0)
+            idb = np.frombuffer(obj[0], dtype=np.uint8).copy()
+        h = ctypes.c_void_p()
+        rc = L.kw_comm_init(world, rank, _native.ptr(idb), device, ctypes.byref(h))
+        if rc != _native.KW_OK:
+            msg = L.kw_comm_last_error(h if h.value else None)
+            if h.value:
+                L.kw_comm_destroy(h)
+            raise _native.KwError(rc, msg.decode() if msg else '')
+        self.h = h
+        self._out = None
+
+    def close(self):
+        if getattr(self, 'h', None) is not None and self.h.value:
+            self._n.lib().kw_comm_destroy(self.h)
+            self.h = None
+
+    @staticmethod
+    def _sp(stream):
+        import ctypes
+        return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, 'cuda_stream') else (stream or 0))
+
+    def allgather_counts(self, count: int, stream=None) -> List[int]:
+        out = np.zeros(self.world, dtype=np.int64)
+        self._n.check_comm(self._n.lib().kw_allgather_counts(self.h, int(count), self._n.ptr(out), self._sp(stream)),
+                           self.h)
+        return [int(x) for x in out]
+
+    def gather_hits(self, hits, doc_base: int, root: int = -1, stream=None):
+        """Exchange [n, 4] int32 device records (doc ids local to the rank's shard).  Returns
+        (records of every rank in document order with global doc ids -- on receiving ranks, else
+        None -- and the per-rank counts).  Asynchronous on ``stream`` after the counts exchange."""
+        import ctypes
+        import torch
+        n = int(hits.shape[0])
+        counts = self.allgather_counts(n, stream)
+        total = sum(counts)
+        receive = root < 0 or root == self.rank
+        if receive and (self._out is None or self._out.shape[0] < max(total, 1)):
+            self._out = torch.empty((max(total + total // 4, 1), 4), dtype=torch.int32,
+                                    device=torch.device('cuda', self.device))
+        out = self._out if receive else None
+        nt = ctypes.c_int64()
+        self._n.check_comm(self._n.lib().kw_allgather_hits(
+            self.h, self._n.ptr(hits) if n else None, n, int(doc_base), int(root),
+            self._n.ptr(out) if out is not None else None, int(out.shape[0]) if out is not None else 0,
+            ctypes.byref(nt), None, self._sp(stream)), self.h)
+        return (out[:total] if receive else None), counts
+
+
+class Exchange:
+    """Moves a rank's hit records ([n, 4] int32, doc ids local to its shard) to rank 0, the writer.
+
+    backend "nccl": libkwmatch's RCCL communicator (:class:`KwComm`, device tensors);
+    any other backend (the gloo CPU tests): the torch-collective :func:`gather_hits`."""
+
+    def __init__(self, rank: int, world: int, device, backend: str):
+        self.rank, self.world, self.backend = rank, world, backend
+        self.comm = KwComm(rank, world, device) if backend == 'nccl' and world > 1 else None
+
+    def gather(self, hits, doc_base: int):
+        """Records of every rank with batch-global doc ids, in document order, on rank 0 (None elsewhere)."""
+        if self.world == 1:
+            out = hits.clone()
+            if out.numel():
+                out[:, 0] += doc_base
+            return out
+        if self.comm is not None:
+            out, _ = self.comm.gather_hits(hits, doc_base, root=0)
+            return out
+        allh = gather_hits(hits, doc_base, hits.device)
+        return allh if self.rank == 0 else None
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
 
 
 def shard_range(n_docs: int, rank: int, world: int) -> Tuple[int, int]:

@@ -27,6 +27,7 @@ import os
 import sys
 from typing import Dict, List, Optional
 
+import numpy as np
 import pandas as pd
 from dateutil import parser
 
@@ -35,7 +36,8 @@ from .dates import parse_date
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
 from .rows import assemble_json_rows
-from .matcher import GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits, pack_fields
+from .matcher import (GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits,  # noqa: F401
+                      pack_fields, records_from_tensor)
 
 OUTPUT_COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source',
                   'source_url', 'article_text')
@@ -80,7 +82,8 @@ def _chunk_rows(chunk, results, dates):
 
 
 def _cell_rows(chunk, cells, dates):
-    """Output rows grouped by ticker, in article order (value tuples, OUTPUT_COLUMNS order).
+    """Output rows grouped by ticker, in article order (value tuples, OUTPUT_COLUMNS order), and the
+    exception of the first row whose cells raise (``None`` if none does).
 
     ``cells`` = ``(row index, ticker, text_matches JSON, title_matches JSON)`` in article then ticker order
     (rows.assemble_json_rows, or json.dumps of ``ticker_matches``).  Each row equals ``_csv_row(matched,
@@ -88,30 +91,38 @@ def _cell_rows(chunk, cells, dates):
     per row) and ``time_unix`` reuses the article's period-filter parse (match_keywords.py:152 parses
     ``str(date_time)``, :131 parses ``date_time``; the two agree when the cell is a ``str``, otherwise :131's
     own call runs).  A chunk without an object column (``iloc`` would upcast its ints to floats) takes the
-    ``iloc`` path.
+    ``iloc`` path.  When a row's ``time_unix`` raises (the reference raises in that article's first
+    ``append_to_csv``, :131-132), the rows of the articles before it are kept and the exception returned.
     """
     rows_by_ticker: Dict[str, list] = {}
     if not cells:
-        return rows_by_ticker
+        return rows_by_ticker, None
     if not any(dt == object for dt in chunk.dtypes):
+        last, stamp, row = -1, None, None
         for i, ticker, tj, tt in cells:
             row = chunk.iloc[i]
-            stamp = int(parser.parse(row['date_time']).timestamp())
+            try:
+                stamp = int(parser.parse(row['date_time']).timestamp())
+            except Exception as exc:   # noqa: BLE001 - the reference's own exception, re-raised by the caller
+                return rows_by_ticker, exc
             rows_by_ticker.setdefault(ticker, []).append(
                 (stamp, row['date_time'], tj, tt, row['title'], row['url'], row['source'], row['source_url'],
                  row['article_text']))
-        return rows_by_ticker
+        return rows_by_ticker, None
     cols = {c: chunk[c].tolist() for c in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')}
     last, stamp, tail = -1, None, None
     for i, ticker, tj, tt in cells:
         if i != last:
             raw = cols['date_time'][i]
-            stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
+            try:
+                stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
+            except Exception as exc:   # noqa: BLE001
+                return rows_by_ticker, exc
             tail = (cols['title'][i], cols['url'][i], cols['source'][i], cols['source_url'][i],
                     cols['article_text'][i])
             last = i
         rows_by_ticker.setdefault(ticker, []).append((stamp, raw, tj, tt) + tail)
-    return rows_by_ticker
+    return rows_by_ticker, None
 
 
 # --------------------------------------------------------------------- matcher cache
@@ -155,27 +166,29 @@ def match_chunk(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
 def _match(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     """``ticker_matches`` of every row of ``chunk`` (list aligned with the rows), the error, the dates."""
     hits, error, dates, matcher = _match_hits(chunk, processed_data, matcher)
-    return _results(matcher, hits, dates), error, dates
+    results, err_asm = _results(matcher, hits, dates)
+    if err_asm is not None:
+        raise err_asm
+    return results, error, dates
 
 
 def _results(matcher, hits, dates):
+    """``ticker_matches`` per row; stops at the first row whose assembly raises (an in-period fuzzy name
+    whose regex does not compile: the reference's ``re.error`` at :178) and returns the rows before it
+    with that exception."""
     results: List[dict] = [{} for _ in range(len(dates))]
     if hits is not None and len(hits):
-        for doc, fields in group_hits(hits).items():
-            results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
-    return results
+        for doc, fields in group_hits(hits).items():      # ascending document order
+            try:
+                results[doc] = assemble_ticker_matches(matcher.ckb, fields, dates[doc])
+            except Exception as exc:   # noqa: BLE001 - raised after the earlier rows are written
+                return results[:doc], exc
+    return results, None
 
 
-def _match_hits(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
-    """Device hit records of ``chunk``'s rows, the parse error (if any), the parsed dates and the matcher.
-
-    Raises the reference's exceptions: a row whose ``date_time`` does not parse
-    raises after the rows before it were matched (the returned ``error`` lets
-    ``process_chunk`` write those rows first, as the reference's row loop does).
-    """
-    n = len(chunk)
-    if n == 0:
-        return None, None, [], matcher
+def _prepare(chunk):
+    """The reference's per-row field prep (match_keywords.py:150-152) of a whole chunk: texts, titles, the
+    dates of the rows before the first unparseable ``date_time``, and that parse error (or ``None``)."""
     texts = [field_str(v) for v in chunk['article_text'].tolist()]
     titles = [field_str(v) for v in chunk['title'].tolist()]
     dates: List = []
@@ -186,26 +199,80 @@ def _match_hits(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
         except Exception as exc:   # match_keywords.py:152 raises here for this row
             error = exc
             break
+    return texts, titles, dates, error
+
+
+def _match_hits(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
+    """Device hit records of ``chunk``'s rows, the parse error (if any), the parsed dates and the matcher.
+
+    Raises the reference's exceptions: a row whose ``date_time`` does not parse
+    raises after the rows before it were matched (the returned ``error`` lets
+    ``process_chunk`` write those rows first, as the reference's row loop does).
+    """
+    if len(chunk) == 0:
+        return None, None, [], matcher
+    texts, titles, dates, error = _prepare(chunk)
     n_ok = len(dates)
     matcher = matcher or get_matcher(processed_data, sample_texts=texts[:n_ok])
     hits = matcher.match_strings(texts[:n_ok], titles[:n_ok]) if n_ok else None
     return hits, error, dates, matcher
 
 
+def _write_hits(source_name, chunk, matcher, hits, dates, error):
+    """Append the rows of a matched chunk and raise the first of its errors in the reference's row order:
+    a row whose output cells raise, an article whose assembly raises, then the date parse error (the
+    rows of the articles before the failing one are written first, as the reference's loop does)."""
+    cells = assemble_json_rows(matcher.ckb, hits, dates) if hits is not None else None
+    err_rows = None
+    if cells is None:
+        results, err_asm = _results(matcher, hits, dates)
+        by_ticker, err_rows = _chunk_rows(chunk, results, dates)
+    else:
+        err_asm = None
+        by_ticker, err_rows = _cell_rows(chunk, cells, dates)
+    for ticker, rows in by_ticker.items():
+        _append_rows(source_name, ticker, rows)
+    for exc in (err_rows, err_asm, error):
+        if exc is not None:
+            raise exc
+
+
 def _write_chunk(source_name, chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     """Match ``chunk`` and append its rows; the JSON cells come from libkwrows (rows.py), or from the
     Python assembly when only it can decide (offset-less timezones, a non-compiling in-period name)."""
     hits, error, dates, matcher = _match_hits(chunk, processed_data, matcher)
-    cells = None
-    if hits is not None:
-        cells = assemble_json_rows(matcher.ckb, hits, dates)
-    if cells is None:
-        by_ticker = _chunk_rows(chunk, _results(matcher, hits, dates), dates)
-    else:
-        by_ticker = _cell_rows(chunk, cells, dates)
-    for ticker, rows in by_ticker.items():
-        _append_rows(source_name, ticker, rows)
-    if error is not None:
+    _write_hits(source_name, chunk, matcher, hits, dates, error)
+    return matcher
+
+
+def shard_rows(texts, titles, n_rows: int, rank: int, world: int):
+    """Contiguous, byte-balanced row range [lo, hi) of ``rank`` over the first ``n_rows`` rows."""
+    from .dist import byte_balanced_ranges
+    off = np.zeros(2 * n_rows + 1, dtype=np.int64)
+    if n_rows:
+        lens = np.fromiter((len(s.encode('utf-8', 'surrogatepass')) for i in range(n_rows)
+                            for s in (texts[i], titles[i])), dtype=np.int64, count=2 * n_rows)
+        np.cumsum(lens, out=off[1:])
+    return byte_balanced_ranges(off, world)[rank]
+
+
+def _write_chunk_sharded(source_name, chunk, processed_data, matcher, exchange):
+    """``process_chunk`` over ``exchange.world`` GPUs (the reference's Pool over sub-chunks,
+    match_keywords.py:231-238): every rank matches its byte-balanced row range of the chunk, the hit
+    records move to rank 0 (RCCL), and rank 0 -- the single writer -- appends the rows in article order.
+    Every rank raises the chunk's first error after rank 0 has written the rows before it."""
+    if len(chunk) == 0:
+        return matcher
+    texts, titles, dates, error = _prepare(chunk)
+    n_ok = len(dates)
+    matcher = matcher or get_matcher(processed_data, sample_texts=texts[:n_ok])
+    lo, hi = shard_rows(texts, titles, n_ok, exchange.rank, exchange.world)
+    local = matcher.match_device(texts[lo:hi], titles[lo:hi])
+    allh = exchange.gather(local, lo)
+    if exchange.rank == 0:
+        hits = records_from_tensor(allh) if n_ok else None
+        _write_hits(source_name, chunk, matcher, hits, dates, error)
+    elif error is not None:
         raise error
     return matcher
 
@@ -232,23 +299,67 @@ def sort_matched_csv(file_path):
 
 
 # --------------------------------------------------------------------- CLI
-def main(argv=None):
-    """The reference's ``__main__`` (match_keywords.py:220-246) with its constants as defaults."""
+def _parse(argv):
     ap = argparse.ArgumentParser(description=__doc__.split('\n')[0])
     ap.add_argument('--source', default='yahoo')
     ap.add_argument('--info-dir', default='info/Icahn_filter')
     ap.add_argument('--articles', default='datasets/yahoo_articles_all_20250605.csv')
     ap.add_argument('--chunksize', type=int, default=20000)
-    ap.add_argument('--device', type=int, default=None)
-    args = ap.parse_args(argv)
+    ap.add_argument('--device', type=int, default=None, help='single GPU: the HIP device (default: current)')
+    ap.add_argument('--gpus', type=int, default=1,
+                    help='GPUs of this node; N > 1 starts one rank per GPU (torch.distributed.run) that '
+                         'matches a byte-balanced share of every chunk, rank 0 writes')
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    """The reference's ``__main__`` (match_keywords.py:220-246) with its constants as defaults."""
+    args = _parse(argv)
+    world_env = os.environ.get('WORLD_SIZE')
+    if world_env is None and args.gpus > 1:
+        # one process per GPU, started before this process touches the GPU
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(('127.0.0.1', 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+               '--master-addr', '127.0.0.1', f'--master-port={port}', '-m', 'advanced_scrapper_amd.match_keywords']
+        cmd += list(argv if argv is not None else sys.argv[1:])
+        return subprocess.call(cmd)
+    if world_env is not None and int(world_env) != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world_env}')
+    if args.gpus > 1:
+        from . import dist
+        rank, world, local = dist.init('nccl')
+        return run(args, rank, world, local, 'nccl')
+    return run(args, 0, 1, args.device, None)
+
+
+def run(args, rank: int, world: int, device, backend, matcher=None):
+    """The driver loop on one rank: read the chunks, match (sharded over the ranks when world > 1), write on
+    rank 0, then rank 0 sorts every output file (match_keywords.py:226-246)."""
     processed = read_and_process_json_files(args.info_dir)
     out_dir = f'{args.source}_ticker_matched_articles'
-    os.makedirs(out_dir, exist_ok=True)
-    matcher = None
-    for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
-        if matcher is None:
-            matcher = get_matcher(processed, args.device, [field_str(v) for v in chunk['article_text'].tolist()])
-        matcher = _write_chunk(args.source, chunk, processed, matcher)
+    if rank == 0:
+        os.makedirs(out_dir, exist_ok=True)
+    exchange = None
+    if world > 1:
+        from .dist import Exchange
+        exchange = Exchange(rank, world, device, backend)
+    try:
+        for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
+            if matcher is None:
+                matcher = get_matcher(processed, device, [field_str(v) for v in chunk['article_text'].tolist()])
+            if exchange is None:
+                matcher = _write_chunk(args.source, chunk, processed, matcher)
+            else:
+                matcher = _write_chunk_sharded(args.source, chunk, processed, matcher, exchange)
+    finally:
+        if exchange is not None:
+            exchange.close()
+    if rank != 0:
+        return 0
     print("All matched CSV files have been processed.")
     for name in os.listdir(out_dir):
         sort_matched_csv(f"{out_dir}/{name}")

@@ -136,11 +136,25 @@ class GpuMatcher:
                                                  ctypes.c_void_p(st.cuda_stream)), self.h)
         return out[:n]
 
+    def hits_copy_into(self, dst, stream=None) -> int:
+        """Copy the last scan's records into the device tensor ``dst`` ([cap, 4] int32) on ``stream``
+        (asynchronous); returns the record count."""
+        t = self.torch
+        st = stream if stream is not None else t.cuda.current_stream(self.device)
+        cnt = ctypes.c_int64()
+        _native.check(_native.lib().kw_hits_copy(self.h, _native.ptr(dst), int(dst.shape[0]), ctypes.byref(cnt),
+                                                 ctypes.c_void_p(st.cuda_stream)), self.h)
+        return int(cnt.value)
+
     def fetch(self) -> np.ndarray:
         """Records of the last scan on the host (structured HIT_DTYPE array)."""
-        d = self.hits_device()
-        host = d.cpu().numpy()
-        return host.view(np.uint32).reshape(-1, 4).copy().view(_native.HIT_DTYPE).reshape(-1)
+        return records_from_tensor(self.hits_device())
+
+    def doc_routes(self, n_docs: int) -> np.ndarray:
+        """Per document of the last scan: which kernel finished it (_native.KW_ROUTE_*)."""
+        out = np.zeros(max(n_docs, 1), dtype=np.uint8)
+        _native.check(_native.lib().kw_doc_routes(self.h, _native.ptr(out), int(n_docs)), self.h)
+        return out[:n_docs]
 
     STAT_KEYS = ('candidates', 'anchor_hits', 'lcs_windows', 'verifications', 'deferred_docs', 'deferred_items',
                  'deferred_long_nonascii', 'edge_items', 'candidates_stage2', 'resolved_docs', 'regex_searches',
@@ -166,10 +180,20 @@ class GpuMatcher:
 
     def match_strings(self, texts: Sequence[str], titles: Sequence[str]) -> np.ndarray:
         """Convenience: pack, upload, scan and fetch."""
+        return records_from_tensor(self.match_device(texts, titles))
+
+    def match_device(self, texts: Sequence[str], titles: Sequence[str]):
+        """Pack, upload and scan; the records as a device tensor [n, 4] (int32 view of kw_hit)."""
         arena, off = pack_fields(texts, titles)
         d_arena, d_off = self.upload(arena, off)
         self.scan(d_arena, d_off, len(texts))
-        return self.fetch()
+        return self.hits_device()
+
+
+def records_from_tensor(t) -> np.ndarray:
+    """[n, 4] int32 records (device or host tensor) -> structured HIT_DTYPE array on the host."""
+    host = t.cpu().numpy() if hasattr(t, 'cpu') else np.asarray(t)
+    return np.ascontiguousarray(host).view(np.uint32).reshape(-1, 4).copy().view(_native.HIT_DTYPE).reshape(-1)
 
 
 # --------------------------------------------------------------------- assembly

@@ -91,7 +91,7 @@ def assemble_json_rows(ckb: CompiledKB, hits: np.ndarray, dates: Sequence) -> Op
     off, ti, rank, lo, hi, invalid, key_buf, key_off = tables
     row_cap = max(1024, len(h))
     out_cap = max(1 << 16, 64 * len(h))
-    while True:
+    for _attempt in range(24):
         row_doc = np.empty(row_cap, dtype=np.int32)
         row_ti = np.empty(row_cap, dtype=np.int32)
         out = np.empty(out_cap, dtype=np.uint8)
@@ -102,11 +102,15 @@ def assemble_json_rows(ckb: CompiledKB, hits: np.ndarray, dates: Sequence) -> Op
                                    _ptr(out_off), out_cap)
         if n == -2:
             return None
-        if n == -1:
+        if n == -3:
+            raise MemoryError('kwrows_assemble: allocation failed')
+        if n == -1:                      # row or text capacity too small: grow and redo
             row_cap *= 2
             out_cap *= 2
             continue
         break
+    else:
+        raise RuntimeError('kwrows_assemble: output kept overflowing')
     text = out[:out_off[2 * n]].tobytes().decode('ascii')
     oo = out_off[:2 * n + 1].tolist()
     tickers = ckb.tickers

@@ -32,23 +32,70 @@ HBM_PEAK_GBS = 8000.0
 METRIC = "article GB/s keyword-matched (S&P500 set) at 1 & 8 GPUs; % of HBM peak"
 
 
-def main():
+def _parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--docs-per-gpu', type=int, default=1_000_000)
     ap.add_argument('--seed', type=int, default=20250905)
-    ap.add_argument('--cpu-sample', type=int, default=4096, help='docs timed on the CPU port (0 = skip)')
-    ap.add_argument('--cpu-procs', type=int, default=min(16, os.cpu_count() or 1))
-    ap.add_argument('--gather-hits', action='store_true', help='also time the RCCL all-gather of hit records')
-    ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'traffic_r01.json'),
+    ap.add_argument('--cpu-sample', type=int, default=3000,
+                    help='docs of the same corpus timed on the CPU port of the reference loop (0 = skip)')
+    ap.add_argument('--cpu-procs', type=int, default=0,
+                    help='CPU port processes (0 = the host share: min(16, os.cpu_count()))')
+    ap.add_argument('--hits', choices=('root', 'all', 'none'), default='root',
+                    help='N > 1: hit records exchanged every step over libkwmatch\'s RCCL communicator '
+                         '(root = to rank 0, the writer; all = all-gather; none = counts only)')
+    ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'traffic_r02.json'),
                     help='per-launch HBM bytes from the rocprofv3 PMC passes (profiles/pmc_traffic.py)')
     ap.add_argument('--workload', choices=('match', 'kb50k', 'dedup'), default='match',
                     help='match = BASELINE.json metric (config 2/3); kb50k = ~50k-pattern synthetic KB '
                          '(config 4); dedup = CDX URL dedup (config 5)')
-    ap.add_argument('--rows-per-gpu', type=int, default=200_000_000, help='dedup: CDX rows per GPU')
-    args = ap.parse_args()
+    ap.add_argument('--rows-per-gpu', type=int, default=500_000_000, help='dedup: CDX rows per GPU (config 5)')
+    return ap.parse_args()
+
+
+def _launch_ranks(args) -> int:
+    """``--gpus N`` without torchrun's environment: start N rank processes (torch.distributed.run) before
+    this process touches the GPU, and return their exit code.  With torchrun's environment, WORLD_SIZE must
+    equal --gpus."""
+    world = os.environ.get('WORLD_SIZE')
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+        return -1
+    if args.gpus <= 1:
+        return -1
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(('127.0.0.1', 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def hits_digest(hits) -> str:
+    """Order-independent 64-bit digest of [n, 4] int32 records (doc, pattern, pos, field) with global doc
+    ids: the wrapping sum of a mixed hash of every record, so shardings and record orders agree."""
+    import torch
+    if hits.numel() == 0:
+        return '0' * 16
+    h = hits.to(torch.int64) & 0xFFFFFFFF
+    x = (h[:, 0] * 0x9E3779B97F4A7C15 + h[:, 1] * 0x2545F4914F6CDD1D + h[:, 2] * 0x27D4EB2F165667C5 +
+         h[:, 3] * 0x165667B19E3779F9)
+    x = x ^ ((x >> 31) & 0x1FFFFFFFF)
+    x = x * -0x40A7B892E31B1A47
+    x = x ^ ((x >> 29) & 0x7FFFFFFFF)
+    return f'{int(x.sum().item()) & 0xFFFFFFFFFFFFFFFF:016x}'
+
+
+def main():
+    args = _parse()
+    rc = _launch_ranks(args)
+    if rc >= 0:
+        sys.exit(rc)
     if args.workload == 'dedup':
         return bench_dedup(args)
 
@@ -83,27 +130,55 @@ def main():
     t_up = time.perf_counter() - t_up
     local_bytes = corpus.n_bytes
 
-    def step():
-        m.scan(d_arena, d_off, n_local)
-        n = m.n_hits()                                   # waits for the scan, reads the count
-        return dist.allgather_counts(n, dev)
+    # N > 1: the hit records of step i move over libkwmatch's RCCL communicator on a stream of their own
+    # while step i + 1 scans (double-buffered staging copies; the counts exchange is the step's rendezvous)
+    comm = dist.KwComm(rank, world, local) if world > 1 else None
+    compute = torch.cuda.current_stream(dev)
+    comm_stream = torch.cuda.Stream(dev) if comm is not None else None
+    stage = [None, None]
+    copied = [torch.cuda.Event(), torch.cuda.Event()]
+    sent = [None, None]
+    last = {'gathered': None, 'counts': None}
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    def step(i):
+        m.scan(d_arena, d_off, n_local, compute)
+        n = m.n_hits()                                   # waits for the scan, reads the count
+        if comm is None:
+            return [n]
+        b = i & 1
+        if sent[b] is not None:
+            compute.wait_event(sent[b])                  # the exchange that read this staging buffer is done
+        if stage[b] is None or stage[b].shape[0] < max(n, 1):
+            stage[b] = torch.empty((max(n + n // 4, 1), 4), dtype=torch.int32, device=dev)
+        m.hits_copy_into(stage[b], compute)
+        copied[b].record(compute)
+        if args.hits == 'none':
+            return comm.allgather_counts(n, comm_stream)
+        comm_stream.wait_event(copied[b])
+        g, counts = comm.gather_hits(stage[b][:n], doc_base, root=0 if args.hits == 'root' else -1,
+                                     stream=comm_stream)
+        ev = torch.cuda.Event()
+        ev.record(comm_stream)
+        sent[b] = ev
+        last['gathered'], last['counts'] = g, counts
+        return counts
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    sync_all()
     ktimes = []
     t0 = time.perf_counter()
     counts = None
-    for _ in range(args.steps):
-        counts = step()
+    for i in range(args.steps):
+        counts = step(i)
         ktimes.append(m.kernel_times())
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync_all()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     nb = torch.tensor([float(local_bytes)], dtype=torch.float64, device=dev)
@@ -115,15 +190,16 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_bytes / (elapsed / args.steps) / 1e9
 
-    gather_ms = None
-    if args.gather_hits:
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        allh = dist.gather_hits(m.hits_device(), doc_base, dev)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - t) * 1e3
-
+    # the digest of every hit record of the whole job (global document ids), on rank 0
+    if comm is None:
+        digest = hits_digest(m.hits_device())
+    elif args.hits in ('root', 'all'):
+        digest = hits_digest(last['gathered']) if rank == 0 else None
+    else:
+        digest = None
     st = m.stats()
+    if comm is not None:
+        comm.close()
     if rank != 0:
         return
     kavg = {k: float(np.mean([t[k] for t in ktimes])) for k in ktimes[0]}
@@ -131,8 +207,8 @@ def main():
     achieved = local_bytes / (scan_avg * 1e-3) / 1e9
     cpu = None
     if world == 1 and args.cpu_sample > 0:
-        # the port walks every name per field: ~1.7 s per article at 52k names, so config 4 samples fewer
-        n_cpu = args.cpu_sample if args.workload == 'match' else min(args.cpu_sample, 96)
+        # the port walks every name occurrence per field: config 4's 52k names take ~1 s per article
+        n_cpu = args.cpu_sample if args.workload == 'match' else min(args.cpu_sample, 64)
         cpu = cpu_baseline(processed, corpus, n_cpu, args.cpu_procs)
     if args.workload == 'kb50k':
         n_act = ckb.n_patterns
@@ -141,10 +217,13 @@ def main():
         metric = 'article GB/s keyword-matched (~50k-pattern synthetic KB, config 4); % of HBM peak'
         data = 'synthetic (seeded generators: csrc/synth.c articles, synth_kb.py KB)'
     else:
-        workload = ('config 2: S&P500 KB (216 tickers, 2462 active names) vs synthetic ~2 KB articles, '
+        cfg = 'config 2' if world == 1 else 'config 3'
+        workload = (f'{cfg}: S&P500 KB (216 tickers, 2462 active names) vs synthetic ~2 KB articles, '
                     f'{n_local} docs per GPU')
         metric = METRIC
         data = 'synthetic (seeded generator, csrc/synth.c; KB = reference info/ticker via tests/golden)'
+    exch = {'root': 'RCCL send/recv of every hit record to rank 0',
+            'all': 'RCCL all-gather of every hit record', 'none': 'RCCL all-gather of counts'}[args.hits]
     out = {
         'metric': metric,
         'value': round(value, 2),
@@ -162,7 +241,9 @@ def main():
             'workload': workload,
             'docs_per_gpu': n_local, 'total_docs': n_local * world, 'bytes_per_gpu': local_bytes,
             'total_bytes': int(total_bytes), 'hits_total': int(sum(counts)) if counts else None,
-            'parallelism': f'dp{world} (document shards, RCCL all-gather of counts)',
+            'hits_digest': digest,
+            'parallelism': (f'dp{world} (contiguous document shards; per step: {exch}, overlapped with the '
+                            f'next scan)' if world > 1 else 'dp1'),
         },
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -177,8 +258,8 @@ def main():
         'cpu_baseline': cpu,
         'scan_stats': st,
         'host': {'generate_s': round(t_gen, 2), 'h2d_s': round(t_up, 3),
-                 'h2d_GBps_pcie_inclusive': round(local_bytes / t_up / 1e9, 2) if t_up > 0 else None},
-        'hits_allgather_ms': None if gather_ms is None else round(gather_ms, 3),
+                 'h2d_GBps_pcie_inclusive': round(local_bytes / t_up / 1e9, 2) if t_up > 0 else None,
+                 'os_cpu_count': os.cpu_count()},
     }
     print(json.dumps(out), flush=True)
 
@@ -292,9 +373,11 @@ def pmc_traffic(path: str, kernel: str, docs: int, seed: int):
 
 
 def cpu_baseline(processed, corpus, n_sample: int, procs: int):
-    """Time the oracle's CPU port on the first n_sample documents of the same corpus."""
-    from dateutil import parser
+    """Time the CPU port of the reference loop (oracle/cpu_port.py) on the first n_sample documents of the
+    same corpus, in the reference's pool shape; procs = the host share (min(16, os.cpu_count()))."""
     from oracle import cpu_port
+    ncpu = os.cpu_count() or 1
+    procs = procs or min(16, ncpu)
     n = min(n_sample, corpus.n_docs)
     rows = []
     nbytes = 0
@@ -302,12 +385,16 @@ def cpu_baseline(processed, corpus, n_sample: int, procs: int):
     for i in range(n):
         t, ti = corpus.text(i), corpus.title(i)
         nbytes += len(t.encode('utf-8', 'surrogatepass')) + len(ti.encode('utf-8', 'surrogatepass'))
-        rows.append((t, ti, parser.parse(str(base + np.timedelta64(1420 * (corpus.doc_base + i), 's')))))
+        rows.append((t, ti, str(base + np.timedelta64(1420 * (corpus.doc_base + i), 's')).replace('T', ' ')))
     secs, done = cpu_port.time_port(processed, rows, procs)
     return {'value': round(nbytes / secs / 1e9, 6), 'unit': 'GB/s', 'cores': procs, 'kind': 'port',
-            'sample': f'first {done} docs of the same corpus ({nbytes} bytes), oracle CPU port '
-                      f'(Python loop + CPython re + C partial_ratio), {procs} processes, {secs:.2f} s wall',
-            'docs_per_s': round(done / secs, 2), 'docs_per_s_per_core': round(done / secs / procs, 3)}
+            'sample': f'first {done} docs of the same corpus ({nbytes} bytes): the reference loop '
+                      f'(match_keywords.py:148-192: per name occurrence period check, re, partial_ratio '
+                      f'decisions by the oracle C restatement, per-hit pandas appends) in its pool shape '
+                      f'(:230-238), {procs} processes on a host with os.cpu_count() = {ncpu} (16 = the '
+                      f'GPU box CPU share), {secs:.2f} s wall',
+            'docs_per_s': round(done / secs, 2), 'docs_per_s_per_core': round(done / secs / procs, 3),
+            'host_cpu_count': ncpu}
 
 
 if __name__ == '__main__':

@@ -126,8 +126,57 @@ int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *to
  * (kw_items_kernel), [1] resolve, [2] generic, [3] result compaction, [4] total. */
 int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 
+/* Which kernel finished each document of the last scan (after kw_hits):
+ * routes[d] = KW_ROUTE_SCAN (the scan kernel's epilogue and its task kernels),
+ * KW_ROUTE_RESOLVE (the resolve kernel: non-ASCII fields) or KW_ROUTE_GENERIC
+ * (deferred to the generic kernel: capacity limits).  For tests and tuning. */
+#define KW_ROUTE_SCAN 0
+#define KW_ROUTE_RESOLVE 1
+#define KW_ROUTE_GENERIC 2
+int kw_doc_routes(kw_handle *h, uint8_t *routes, int64_t n);
+
 const char *kw_last_error(kw_handle *h);
 int kw_destroy(kw_handle *h);
+
+/* ---- multi-GPU exchange (RCCL over xGMI; advanced_scrapper_amd/csrc/kwcomm.hip)
+ *
+ * Replaces the reference's process pool over article sub-chunks
+ * (match_keywords.py:230-238, np.array_split + Pool.starmap; the workers'
+ * only exchange is the shared per-ticker CSV files).  Here each rank (one
+ * process per GPU) scans a contiguous, byte-balanced document range; the hit
+ * counts and the packed kw_hit records are then exchanged so that the writing
+ * rank holds the batch's records in document order.  RCCL is loaded at run
+ * time; without it these calls return KW_EUNSUPPORTED. */
+typedef struct kw_comm kw_comm;
+#define KW_COMM_ID_BYTES 128
+
+/* A fresh communicator id (ncclGetUniqueId), made by ONE rank and shared with
+ * the others by the caller (e.g. torch.distributed's store). */
+int kw_comm_unique_id(uint8_t *id_out /* KW_COMM_ID_BYTES */);
+
+/* Join the communicator `id` as `rank` of `nranks` on HIP device `device`. */
+int kw_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, int32_t device, kw_comm **out);
+
+/* All-gather one count per rank into counts[nranks] (host).  Blocking. */
+int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, void *stream);
+
+/* Exchange hit records (e.g. a kw_hits_copy of this rank's last scan: d_local,
+ * n records).  Every record's doc gets doc_base added (the rank's first global
+ * document).  root < 0: every rank receives all records; root >= 0: only rank
+ * `root` does (d_out may be NULL elsewhere).  The receiver's d_out (cap
+ * records) gets the ranks' records concatenated in rank order = global
+ * document order.  *n_total = records over all ranks; counts[nranks] (host,
+ * optional) the per-rank counts.  The counts exchange blocks (every rank must
+ * call); the records move asynchronously on `stream` (RCCL send/recv over the
+ * xGMI mesh), so the next kw_scan can run beside them on another stream.
+ * The receiver's cap must hold the total (size d_out from kw_allgather_counts
+ * first): a short d_out fails on that rank after the counts exchange and
+ * leaves its peers waiting.  Use one stream per communicator. */
+int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root, kw_hit *d_out,
+                      int64_t cap, int64_t *n_total, int64_t *counts, void *stream);
+
+const char *kw_comm_last_error(kw_comm *c);
+int kw_comm_destroy(kw_comm *c);
 
 #ifdef __cplusplus
 }

@@ -1,41 +1,108 @@
 """ORACLE — CPU port timed as bench.py's ``cpu_baseline`` (test infrastructure only).
 
-The reference's own driver shape (match_keywords.py:230-238): the chunk is
-split into ``n`` sub-chunks (``np.array_split``) and a process pool runs the
-per-article loop on each.  The per-article loop is the oracle's restatement
-(oracle/kwmatch_oracle.py: CPython ``re`` for the uppercase branch, the C
-restatement of rapidfuzz partial_ratio for the fuzzy branch).  It is kinder
-to the CPU than the reference: it decides each distinct name once per field
-instead of once per (ticker, attribute) occurrence and it skips the per-hit
-pandas CSV appends.
+The reference's matching run the way the reference runs it
+(match_keywords.py:148-192 per row, :230-238 for the pool): the rows are split
+into ``procs`` sub-chunks (``np.array_split``) and a process pool runs, per
+article, the triple loop ticker -> attribute -> name occurrence with
+``is_within_period`` on every occurrence, ``re.finditer`` of the ``\\b``
+pattern for uppercase names, the two ``partial_ratio(...) > 95`` decisions for
+every fuzzy-class occurrence, ``re.finditer(name, s)`` on a fuzzy hit, and one pandas ``DataFrame([row]).to_csv(mode='a')`` append per
+matched (article, ticker) into a scratch directory (:128-146).  Pool start-up
+is excluded.  rapidfuzz is absent from the image, so its C work is stood in
+for by the oracle's C restatement (oracle/partial_ratio.c) run once per field
+over the distinct fuzzy names (``pr_decide_many``); the per-occurrence loop
+then looks the decision up.  (Calling the restatement once per occurrence, as
+the reference calls rapidfuzz, measured ~235 ms per article per core here --
+slower than rapidfuzz is believed to be, so it would flatter the GPU.)
 """
 from __future__ import annotations
 
 import multiprocessing as mp
+import os
+import re
+import shutil
+import tempfile
 import time
-from typing import List, Sequence, Tuple
+from typing import Sequence, Tuple
 
 import numpy as np
 
-_ORACLE = None
+_STATE = {}
 
 
 def _init(processed):
-    global _ORACLE
-    from oracle.kwmatch_oracle import Oracle
-    _ORACLE = Oracle(processed)
+    from oracle import kwmatch_oracle as orc
+    _STATE['processed'] = processed
+    _STATE['orc'] = orc
+    _STATE['oracle'] = orc.Oracle(processed)
+    _STATE['dir'] = tempfile.mkdtemp(prefix='kw_cpu_port_')
+
+
+def _append(ticker, matched, row):
+    """append_to_csv (match_keywords.py:128-146) into the worker's scratch directory."""
+    import json
+    import pandas as pd
+    from dateutil import parser
+    path = os.path.join(_STATE['dir'], f'{ticker}_match.csv')
+    text, title, date_s = row
+    rec = {'time_unix': int(parser.parse(date_s).timestamp()), 'date_time': date_s,
+           'text_matches': json.dumps(matched['text']), 'title_matches': json.dumps(matched['title']),
+           'title': title, 'url': '', 'source': '', 'source_url': '', 'article_text': text}
+    pd.DataFrame([rec]).to_csv(path, mode='a', header=not os.path.exists(path), index=False)
+
+
+def _article(text, title, date_s):
+    from dateutil import parser
+    orc = _STATE['orc']
+    article_date = parser.parse(date_s)
+    O = _STATE['oracle']
+    fz_a = dict(zip(O.fuzzy, O.fset.decide(text)))     # partial_ratio(text, name) > 95, one C pass
+    fz_b = dict(zip(O.fuzzy, O.fset.decide(title)))
+    ticker_matches = {}
+    for ticker, attrs in _STATE['processed'].items():
+        tm, ti = {}, {}
+        for _attr, names in attrs.items():
+            for name, (start, end) in names.items():
+                if not orc.in_period(article_date, start, end):
+                    continue
+                if name.isupper():
+                    if len(name) > 1:
+                        pat = r'\b' + re.escape(name) + r'\b'
+                        a = [x.start() for x in re.finditer(pat, text)]
+                        b = [x.start() for x in re.finditer(pat, title)]
+                        if a:
+                            tm[name] = a
+                        if b:
+                            ti[name] = b
+                elif not (name.islower() and name.replace(' ', '').isalpha()):
+                    hit_a = fz_a[name]
+                    hit_b = fz_b[name]
+                    if hit_a:
+                        tm[name] = [x.start() for x in re.finditer(name, text)]
+                    if hit_b:
+                        ti[name] = [x.start() for x in re.finditer(name, title)]
+        if tm or ti:
+            ticker_matches[ticker] = {'text': tm, 'title': ti}
+    for ticker, matched in ticker_matches.items():
+        _append(ticker, matched, (text, title, date_s))
+    return len(ticker_matches)
 
 
 def _run(rows):
     n = 0
-    for text, title, date in rows:
-        _ORACLE.ticker_matches(text, title, date)
+    for text, title, date_s in rows:
+        _article(text, title, date_s)
         n += 1
     return n
 
 
-def time_port(processed, rows: Sequence[Tuple[str, str, object]], procs: int) -> Tuple[float, int]:
-    """Wall seconds to match `rows` with `procs` worker processes (pool start-up excluded)."""
+def _cleanup(_):
+    shutil.rmtree(_STATE.get('dir', ''), ignore_errors=True)
+    return 0
+
+
+def time_port(processed, rows: Sequence[Tuple[str, str, str]], procs: int) -> Tuple[float, int]:
+    """Wall seconds to match `rows` ((text, title, date string)) with `procs` worker processes."""
     ctx = mp.get_context('spawn')
     with ctx.Pool(procs, initializer=_init, initargs=(processed,)) as pool:
         pool.map(_run, [[] for _ in range(procs)])           # warm the workers (imports, KB)
@@ -43,4 +110,6 @@ def time_port(processed, rows: Sequence[Tuple[str, str, object]], procs: int) ->
         subs = [[rows[i] for i in p] for p in parts]
         t0 = time.perf_counter()
         done = sum(pool.map(_run, subs))
-        return time.perf_counter() - t0, done
+        secs = time.perf_counter() - t0
+        pool.map(_cleanup, range(procs))
+        return secs, done

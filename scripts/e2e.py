@@ -4,7 +4,7 @@ Generates N synthetic articles (config-2 corpus), writes them as the reference's
 drop-in main loop's phases on chunks of 20 000 rows and prints one JSON line with seconds per phase and the
 end-to-end articles/s (the reference's CPU path on the same rows is bench.py's cpu_baseline).
 
-    python scripts_e2e.py [--docs 100000] [--chunksize 20000]
+    python scripts/e2e.py [--docs 100000] [--chunksize 20000]
 """
 import argparse
 import json
@@ -14,7 +14,7 @@ import sys
 import tempfile
 import time
 
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
@@ -58,7 +58,7 @@ def main():
         c4 = time.perf_counter(); t['gpu_match'] += c4 - c3
         cells = assemble_json_rows(matcher.ckb, hits, dates)
         c5 = time.perf_counter(); t['assemble'] += c5 - c4
-        by = mk._cell_rows(chunk, cells, dates)
+        by, _err = mk._cell_rows(chunk, cells, dates)
         c6 = time.perf_counter(); t['rows'] += c6 - c5
         for ticker, rows in by.items():
             mk._append_rows('yahoo', ticker, rows)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Kernel-trace stats of short bench runs per library variant: bash scripts_gpu_ktrace.sh <outdir> tag... (default = lib)
+# Kernel-trace stats of short bench runs per library variant: bash scripts/gpu_ktrace.sh <outdir> tag... (default = lib)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 out=$1; shift

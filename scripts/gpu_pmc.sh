@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ instruction / cycle counters per kernel of a 250k-document bench run, two passes:
-#   bash scripts_gpu_pmc.sh <outdir> [library variant tag]
+#   bash scripts/gpu_pmc.sh <outdir> [library variant tag]
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -42,12 +42,23 @@ def _kb_processed_raw():
     return json.loads(gzip.decompress(_read('kb_processed.json.gz')))
 
 
-def kb_processed() -> Dict:
-    """The reference's processed_data, rebuilt with datetime periods."""
+def processed_from(kb_list) -> Dict:
+    """processed_data from its JSON form ([[ticker, [[attr, [[name, start, end], ...]], ...]], ...])."""
     out = {}
-    for ticker, attrs in _kb_processed_raw():
+    for ticker, attrs in kb_list:
         out[ticker] = {a: {n: (_dt(s), _dt(e)) for n, s, e in names} for a, names in attrs}
     return out
+
+
+def kb_processed() -> Dict:
+    """The reference's processed_data, rebuilt with datetime periods."""
+    return processed_from(_kb_processed_raw())
+
+
+@functools.lru_cache(maxsize=None)
+def error_cases() -> dict:
+    """tests/golden/error_golden.json.gz (make_error_golden.py): the reference's partial outputs."""
+    return json.loads(gzip.decompress(_read('error_golden.json.gz')))
 
 
 def articles_csv_bytes() -> bytes:

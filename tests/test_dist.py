@@ -83,6 +83,62 @@ def test_gloo_sharded_gather_equals_single_process():
         assert np.array_equal(got, single), rank
 
 
+def _main_worker(rank, world, port, work, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TZ='UTC')
+    import time
+    time.tzset()
+    from advanced_scrapper_amd import dist
+    from advanced_scrapper_amd import match_keywords as mk
+    from tests import golden_data
+    dist.init('gloo')
+    os.chdir(work)
+    processed = golden_data.kb_processed()
+    mk.read_and_process_json_files = lambda _d: processed      # the golden KB (fixed ticker order)
+    args = mk._parse(['--info-dir', 'unused', '--articles', os.path.join(work, 'articles.csv'),
+                      '--chunksize', str(golden_data.chunksize()), '--gpus', str(world)])
+    from tests.oracle_matcher import OracleMatcher
+    rc = mk.run(args, rank, world, None, 'gloo', matcher=OracleMatcher(processed))
+    q.put((rank, rc))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_main_sharded_equals_reference_outputs(tmp_path):
+    """match_keywords.main's multi-rank loop (byte-balanced row shards of every chunk, the records moved to
+    rank 0, rank 0 writes and sorts) over 2 gloo ranks, with only the scan stubbed by the oracle, writes the
+    reference's own per-ticker files byte for byte (tests/golden/out_c1)."""
+    from tests import golden_data
+    (tmp_path / 'articles.csv').write_bytes(golden_data.articles_csv_bytes())
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_main_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, 0), (1, 0)]
+    out = tmp_path / 'yahoo_ticker_matched_articles'
+    want = golden_data.outputs()
+    assert sorted(os.listdir(out)) == sorted(want)
+    for fn in want:
+        assert (out / fn).read_bytes() == want[fn], fn
+
+
+def test_shard_rows_balance_bytes():
+    from advanced_scrapper_amd.match_keywords import shard_rows
+    texts = ['a' * (i % 7) + 'é' * (i % 3) for i in range(50)]
+    titles = ['t' * (i % 5) for i in range(50)]
+    for world in (1, 2, 3, 8):
+        rr = [shard_rows(texts, titles, 40, r, world) for r in range(world)]
+        assert rr[0][0] == 0 and rr[-1][1] == 40
+        assert all(rr[i][1] == rr[i + 1][0] for i in range(world - 1))
+
+
 def test_byte_balanced_ranges_cover_and_balance():
     from advanced_scrapper_amd import dist
     rng = np.random.default_rng(5)

@@ -334,3 +334,31 @@ def test_nonascii_wildcard_and_regex_names_vs_oracle():
     got = _gpu_maps(m, texts, titles)
     bad = _compare(processed, texts, titles, got)
     assert not bad, f"GPU differs from the oracle on non-ASCII wildcard docs {bad[:20]}"
+
+
+@pytest.mark.parametrize('case', ['invalid_regex', 'bad_date', 'int_dates'])
+def test_dropin_error_paths_gpu(golden, tmp_path, monkeypatch, case):
+    """process_chunk on the GPU writes exactly the rows the reference wrote before raising, and raises the
+    same exception (tests/golden/make_error_golden.py ran the reference on these chunks)."""
+    import time
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import match_keywords as mk
+    monkeypatch.setenv('TZ', 'UTC')
+    time.tzset()
+    g = golden.error_cases()
+    c = g['cases'][case]
+    processed = golden.processed_from(g['kb_processed'])
+    monkeypatch.chdir(tmp_path)
+    os.makedirs('yahoo_ticker_matched_articles')
+    raised = None
+    try:
+        for chunk in pd.read_csv(io.StringIO(c['articles_csv']), chunksize=g['chunksize']):
+            mk.process_chunk('yahoo', chunk, processed)
+    except Exception as exc:   # noqa: BLE001
+        raised = type(exc).__name__
+    assert raised == c['exception']
+    got = {fn: open(os.path.join('yahoo_ticker_matched_articles', fn), encoding='utf-8').read()
+           for fn in os.listdir('yahoo_ticker_matched_articles')}
+    assert got == c['files']

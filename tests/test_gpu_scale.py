@@ -1,0 +1,120 @@
+"""Parity at bench scale: the bench's own config-2 corpus (1M synthetic ~2 KB articles, bench.py's seed).
+
+* a seeded sample of the corpus, a seeded sample of the documents the resolve
+  kernel finished (non-ASCII fields), every document the generic kernel
+  finished (capacity deferrals), and the documents closest to the capacity
+  boundaries (the most hit records, the longest fields) are checked against
+  the CPU oracle, field by field, positions included (the oracle takes ~60 ms
+  per article, so the 120k resolve-route documents are sampled, not all run);
+* config 3's sharding logic with the real kernels: the corpus is scanned as
+  2-, 4- and 8-way contiguous byte-balanced shards one after another on this
+  GPU, each shard's records are rebased to global document ids by
+  libkwmatch's RCCL exchange (kw_allgather_hits on a one-rank communicator)
+  and concatenated in rank order; the result must equal the one-shot scan
+  record for record, and its bench digest must match.
+"""
+import numpy as np
+import pytest
+
+from tests import oracle_pool
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20250905          # bench.py --seed default
+N_DOCS = 1_000_000       # bench.py --docs-per-gpu default (config 2)
+
+
+def _sorted(rec):
+    return rec[np.lexsort((rec['pos'], rec['pattern'], rec['field'], rec['doc']))]
+
+
+@pytest.fixture(scope='module')
+def bench_scan(golden):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher, background_sample, records_from_tensor
+    processed = golden.kb_processed()
+    ckb = compile_kb(processed)
+    names, kinds = synth.injectable_names(ckb)
+    corpus = synth.generate(N_DOCS, names, kinds, seed=SEED, doc_base=0)
+    bg = synth.generate(2000, names, kinds, seed=SEED + 7777, doc_base=0)
+    m = GpuMatcher(ckb, 0, background_sample(bg.texts() + bg.titles()))
+    d_arena, d_off = m.upload(corpus.arena, corpus.off)
+    m.scan(d_arena, d_off, N_DOCS)
+    hits = m.hits_device().clone()
+    routes = m.doc_routes(N_DOCS)
+    return {'processed': processed, 'ckb': ckb, 'corpus': corpus, 'm': m, 'd_arena': d_arena, 'd_off': d_off,
+            'hits': hits, 'rec': records_from_tensor(hits), 'routes': routes, 'stats': m.stats()}
+
+
+def test_bench_corpus_vs_oracle(bench_scan):
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd.matcher import group_hits
+    b = bench_scan
+    corpus, rec, routes = b['corpus'], b['rec'], b['routes']
+    rng = np.random.default_rng(SEED)
+    pick = set(rng.choice(N_DOCS, 2000, replace=False).tolist())
+    resolve = np.flatnonzero(routes == _native.KW_ROUTE_RESOLVE)
+    generic = np.flatnonzero(routes == _native.KW_ROUTE_GENERIC)
+    assert len(resolve) > 0
+    pick |= set(rng.choice(resolve, min(1500, len(resolve)), replace=False).tolist())
+    pick |= set(generic.tolist())
+    per_doc = np.bincount(rec['doc'].astype(np.int64), minlength=N_DOCS)
+    pick |= set(np.argsort(-per_doc, kind='stable')[:250].tolist())
+    off = corpus.off
+    text_len = off[1::2][:N_DOCS] - off[0::2][:N_DOCS]
+    title_len = off[2::2] - off[1::2][:N_DOCS]
+    pick |= set(np.argsort(-text_len, kind='stable')[:150].tolist())
+    pick |= set(np.argsort(-title_len, kind='stable')[:100].tolist())
+    docs = sorted(pick)
+    texts = [corpus.text(d) for d in docs]
+    titles = [corpus.title(d) for d in docs]
+    want_t = oracle_pool.field_results(b['processed'], texts)
+    want_i = oracle_pool.field_results(b['processed'], titles)
+    sel = rec[np.isin(rec['doc'], np.asarray(docs, dtype=np.uint32))]
+    g = group_hits(sel)
+    names = b['ckb'].names
+    bad = []
+    for k, d in enumerate(docs):
+        f = g.get(d, {})
+        got_t = {names[p]: v for p, v in f.get(0, {}).items()}
+        got_i = {names[p]: v for p, v in f.get(1, {}).items()}
+        if got_t != want_t[k] or got_i != want_i[k]:
+            bad.append(int(d))
+            if len(bad) <= 3:
+                print('doc', d, 'route', int(routes[d]),
+                      {n: (got_t.get(n), want_t[k].get(n)) for n in set(got_t) | set(want_t[k])
+                       if got_t.get(n) != want_t[k].get(n)},
+                      {n: (got_i.get(n), want_i[k].get(n)) for n in set(got_i) | set(want_i[k])
+                       if got_i.get(n) != want_i[k].get(n)})
+    print(f'checked {len(docs)} docs ({len(resolve)} resolve-route, {len(generic)} generic-route in the corpus)')
+    assert not bad, f'{len(bad)} of {len(docs)} documents differ from the oracle: {bad[:20]}'
+
+
+def test_sharded_scans_equal_one_shot(bench_scan):
+    import bench
+    from advanced_scrapper_amd import dist
+    from advanced_scrapper_amd.matcher import records_from_tensor
+    b = bench_scan
+    m, d_arena, d_off = b['m'], b['d_arena'], b['d_off']
+    one = _sorted(b['rec'])
+    digest = bench.hits_digest(b['hits'])
+    comm = dist.KwComm(0, 1, 0)
+    try:
+        for world in (2, 4, 8):
+            parts = []
+            for lo, hi in dist.byte_balanced_ranges(b['corpus'].off, world):
+                m.scan(d_arena, d_off[2 * lo:], hi - lo)
+                g, counts = comm.gather_hits(m.hits_device(), lo)
+                assert counts == [g.shape[0]]
+                parts.append(g.clone())
+            allh = np.concatenate([records_from_tensor(p) for p in parts])
+            assert len(allh) == len(one), world
+            assert np.array_equal(_sorted(allh), one), world
+            import torch
+            assert bench.hits_digest(torch.cat(parts)) == digest, world
+    finally:
+        comm.close()

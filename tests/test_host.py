@@ -216,7 +216,9 @@ def test_csv_egress_chunk_rows_bytes(golden, tmp_path, monkeypatch):
     for chunk in pd.read_csv(io.BytesIO(golden.articles_csv_bytes()), chunksize=golden.chunksize()):
         results = want_m[start:start + len(chunk)]
         dates = [dparser.parse(str(v)) if pd.notna(v) else None for v in chunk['date_time'].tolist()]
-        for ticker, rows in mk._chunk_rows(chunk, results, dates).items():
+        by_ticker, err = mk._chunk_rows(chunk, results, dates)
+        assert err is None
+        for ticker, rows in by_ticker.items():
             mk._append_rows('yahoo', ticker, rows)
         start += len(chunk)
     for fn in os.listdir('yahoo_ticker_matched_articles'):
@@ -407,3 +409,32 @@ def test_synth_is_shard_invariant(golden):
     c = synth.generate(300, names, kinds, seed=5)
     assert np.array_equal(a.arena, c.arena) and np.array_equal(a.off, c.off)
     assert 1500 < a.n_bytes / a.n_docs < 3500
+
+
+# ------------------------------------------------------------------ error paths (match_keywords.py:152, :131, :178)
+@pytest.mark.parametrize('case', ['invalid_regex', 'bad_date', 'int_dates'])
+def test_dropin_error_paths_write_reference_partial_output(golden, tmp_path, monkeypatch, case):
+    """When a chunk raises mid-way, the drop-in writes exactly the rows the reference wrote before raising
+    and raises the same exception (tests/golden/make_error_golden.py ran the reference); the scan is the
+    oracle stand-in (tests/oracle_matcher.py), everything above it is the product path."""
+    import time
+    from advanced_scrapper_amd import match_keywords as mk
+    from tests.oracle_matcher import OracleMatcher
+    monkeypatch.setenv('TZ', 'UTC')
+    time.tzset()
+    g = golden.error_cases()
+    c = g['cases'][case]
+    processed = golden.processed_from(g['kb_processed'])
+    monkeypatch.chdir(tmp_path)
+    os.makedirs('yahoo_ticker_matched_articles')
+    m = OracleMatcher(processed)
+    raised = None
+    try:
+        for chunk in pd.read_csv(io.StringIO(c['articles_csv']), chunksize=g['chunksize']):
+            mk._write_chunk('yahoo', chunk, processed, m)
+    except Exception as exc:   # noqa: BLE001
+        raised = type(exc).__name__
+    assert raised == c['exception']
+    got = {fn: open(os.path.join('yahoo_ticker_matched_articles', fn), encoding='utf-8').read()
+           for fn in os.listdir('yahoo_ticker_matched_articles')}
+    assert got == c['files']
