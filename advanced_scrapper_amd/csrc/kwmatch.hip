@@ -18,26 +18,31 @@
 
 #include "kwmatch_kernels.hpp"
 #include "kwmatch_fast_kernel.hpp"
+#include "kwmatch_split.hpp"
 
 using namespace kw;
 
 // Scratch sizes of one launch configuration (every field only grows over a handle's life).
 struct ScratchCaps {
-    int nk = 0, nr = 0, ng = 0;            // scan, resolve and generic waves (task waves = nk)
-    uint32_t item_cap = 0, out_cap = 0;    // per scan wave items, per wave result records
+    int nk = 0, nr = 0, ng = 0;            // epilogue, resolve and generic waves (task waves = nk)
+    int ns = 0;                            // filter regions (filter waves = probe waves)
+    uint32_t item_cap = 0, out_cap = 0;    // per filter region items, per wave result records
+    uint32_t cand_cap = 0;                 // per filter region candidates
     int64_t hdr_cap = 0;                   // documents
     uint32_t defer_cap = 0, rx_cap = 0;
     uint32_t vcap = 0, ecap = 0, scap = 0, xcap = 0;   // per scan wave task regions
     uint64_t dsize = 0;                    // decided-set slots (power of two)
     bool covers(const ScratchCaps &o) const
     {
-        return nk >= o.nk && nr >= o.nr && ng >= o.ng && item_cap >= o.item_cap && out_cap >= o.out_cap &&
+        return nk >= o.nk && nr >= o.nr && ng >= o.ng && ns >= o.ns && cand_cap >= o.cand_cap &&
+               item_cap >= o.item_cap && out_cap >= o.out_cap &&
                hdr_cap >= o.hdr_cap && defer_cap >= o.defer_cap && rx_cap >= o.rx_cap && vcap >= o.vcap &&
                ecap >= o.ecap && scap >= o.scap && xcap >= o.xcap && dsize >= o.dsize;
     }
     void grow(const ScratchCaps &o)
     {
-        nk = std::max(nk, o.nk); nr = std::max(nr, o.nr); ng = std::max(ng, o.ng);
+        nk = std::max(nk, o.nk); nr = std::max(nr, o.nr); ng = std::max(ng, o.ng); ns = std::max(ns, o.ns);
+        cand_cap = std::max(cand_cap, o.cand_cap);
         item_cap = std::max(item_cap, o.item_cap); out_cap = std::max(out_cap, o.out_cap);
         hdr_cap = std::max(hdr_cap, o.hdr_cap); defer_cap = std::max(defer_cap, o.defer_cap);
         rx_cap = std::max(rx_cap, o.rx_cap); vcap = std::max(vcap, o.vcap); ecap = std::max(ecap, o.ecap);
@@ -85,6 +90,9 @@ struct kw_handle {
     kw_hit *out_all = nullptr;
     int64_t hdr_cap = 0;
     int items_blocks_per_cu = 1, resolve_blocks_per_cu = 1;
+    int filter_blocks_per_cu = 1, probe_blocks_per_cu = 1, epi_blocks_per_cu = 1;
+    int ns = 0;                        // filter regions of the last launch
+    hipEvent_t evf = nullptr, evp = nullptr;   // after the filter / probe kernels
     int n_anchor_fast = 0;
     unsigned long long fstats[16] = {0};
     hipEvent_t evr = nullptr, evg = nullptr;
@@ -907,6 +915,17 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     bpc = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_resolve_kernel, RK_BLOCK, 0));
     h->resolve_blocks_per_cu = bpc > 0 ? bpc : 1;
+    bpc = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_filter_kernel, FS_BLOCK, 0));
+    h->filter_blocks_per_cu = bpc > 0 ? bpc : 1;
+    bpc = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_probe_kernel, PK_BLOCK, 0));
+    h->probe_blocks_per_cu = bpc > 0 ? bpc : 1;
+    bpc = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_epi_kernel, EK_BLOCK, 0));
+    h->epi_blocks_per_cu = bpc > 0 ? bpc : 1;
+    HIPCHK(h, hipEventCreate(&h->evf));
+    HIPCHK(h, hipEventCreate(&h->evp));
     HIPCHK(h, hipEventCreate(&h->ev0));
     HIPCHK(h, hipEventCreate(&h->ev1));
     HIPCHK(h, hipEventCreate(&h->evg));
@@ -934,7 +953,8 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     const size_t nw = (size_t)2 * c.nk + c.nr + c.ng;
     const size_t per_tasks = (size_t)(c.vcap + c.ecap + c.scap + c.xcap) * 16;
     size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_blk) +
-                   nw * per_out + (size_t)c.nk * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 4 +
+                   nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 4 +
+                   (size_t)c.ns * c.cand_cap * 16 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 8 + 3 * 256 +
                    (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
                    32 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
@@ -946,7 +966,11 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.cps = (uint32_t *)carve((size_t)c.nr * per_fcps);
     h->FS.cpbase = (uint32_t *)carve((size_t)c.nr * per_blk);
     kw_hit *outs = (kw_hit *)carve(nw * per_out);
-    h->FS.items = (uint64_t *)carve((size_t)c.nk * c.item_cap * 8);
+    h->FS.items = (uint64_t *)carve((size_t)c.ns * c.item_cap * 8);
+    h->FS.cand = (uint4 *)carve((size_t)c.ns * c.cand_cap * 16);
+    h->FS.cand_cap = c.cand_cap;
+    h->FS.ccnt = (uint32_t *)carve((size_t)c.ns * 4);
+    h->FS.ncnt = (uint2 *)carve((size_t)c.hdr_cap * 8);
     h->FS.hdr = (uint2 *)carve((size_t)c.hdr_cap * 8);
     h->FS.defer_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
     h->FS.rx_tasks = (uint4 *)carve((size_t)c.nr * c.rx_cap * 16);
@@ -973,6 +997,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.status = h->S.status;
     h->FS.defer_cnt = (uint32_t *)(q + 16);
     h->FS.tmax = (uint32_t *)(q + 32);                  // 4 x u32
+    h->FS.cmax = (uint32_t *)(q + 48);                  // 2 x u32
     h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
     h->FS.stats = (unsigned long long *)(q + 128);      // 32 x u64 (fast path; 13.. developer counters)
     uint32_t *cnts = (uint32_t *)(q + 1024);
@@ -1010,8 +1035,14 @@ static int launch_scan(kw_handle *h)
 {
     hipStream_t st = h->stream;
     const int64_t n_docs = h->n_docs;
-    int nkb = (int)std::min<int64_t>((n_docs + FK_WAVES - 1) / FK_WAVES, (int64_t)h->cus * h->items_blocks_per_cu);
-    if (nkb < 1) nkb = 1;
+    // split scan: filter regions (one wave each, resident at once), probe waves = filter regions,
+    // epilogue waves = task regions
+    int nsb = (int)std::min<int64_t>((n_docs + FS_WAVES - 1) / FS_WAVES, (int64_t)h->cus * h->filter_blocks_per_cu);
+    if (nsb < 1) nsb = 1;
+    int neb = (int)std::min<int64_t>((n_docs + EK_WAVES - 1) / EK_WAVES, (int64_t)h->cus * h->epi_blocks_per_cu);
+    if (neb < 1) neb = 1;
+    const int n_regions = nsb * FS_WAVES;
+    const int n_epi = neb * EK_WAVES;
     int rmul = 2;   // resolve blocks per resident slot: later blocks balance the uneven documents (measured: 2-3 % faster than 1)
     if (const char *e = getenv("KW_RESOLVE_MUL")) rmul = std::max(1, atoi(e));
     int nrb = (int)std::min<int64_t>((n_docs + (int64_t)RK_WAVES * WAVE - 1) / ((int64_t)RK_WAVES * WAVE),
@@ -1023,11 +1054,15 @@ static int launch_scan(kw_handle *h)
     if (const char *e = getenv("KW_GENERIC_BLOCKS_PER_CU")) gmul = std::max(1, atoi(e));
     const int ngb = std::max(1, (int)std::min<int64_t>((int64_t)h->cus * gmul, (n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));
     ScratchCaps w;
-    w.nk = nkb * FK_WAVES;
+    w.nk = n_epi;
+    w.ns = n_regions;
     w.nr = nrb * RK_WAVES;
     w.ng = ngb * WAVES_PER_BLOCK;
     const int64_t docs_per_k = (n_docs + w.nk - 1) / w.nk;
-    w.item_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_k * 40), (int64_t)1 << 24);
+    const int64_t docs_per_s = (n_docs + w.ns - 1) / w.ns;
+    w.item_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_s * 32), (int64_t)1 << 26);
+    w.cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_s * 40), (int64_t)1 << 26);
+    if (const char *e = getenv("KW_TEST_CAND_CAP")) w.cand_cap = w.item_cap = (uint32_t)std::max(1, atoi(e));
     const int64_t docs_per_r = (n_docs + w.nr - 1) / w.nr;
     w.out_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, std::max(docs_per_r, docs_per_k) * 48),
                                             (int64_t)1 << 26);
@@ -1051,11 +1086,20 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
     HIPCHK(h, hipEventRecord(h->ev0, st));
+    if (n_docs > 0)
+        hipLaunchKernelGGL(kw_filter_kernel, dim3(nsb), dim3(FS_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
+                           h->FS);
+    HIPCHK(h, hipEventRecord(h->evf, st));
+    if (n_docs > 0)
+        hipLaunchKernelGGL(kw_probe_kernel, dim3((n_regions + PK_WAVES - 1) / PK_WAVES), dim3(PK_BLOCK), 0, st, h->FT,
+                           h->T, h->arena, h->doc_off, n_regions, h->FS);
+    HIPCHK(h, hipEventRecord(h->evp, st));
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_items_kernel, dim3(nkb), dim3(FK_BLOCK), 0, st, h->FT, h->T, h->arena,
-                           h->doc_off, n_docs, h->FS, h->S);
+        hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
+                           h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
+    h->ns = n_regions;
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
         // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up);
@@ -1064,9 +1108,9 @@ static int launch_scan(kw_handle *h)
         if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
         auto task = [&](auto kern, int g) {
             g = std::max(1, std::min(g, 16));
-            const int nb = (nkb * FK_WAVES * g + RK_WAVES - 1) / RK_WAVES;
+            const int nb = (n_epi * g + RK_WAVES - 1) / RK_WAVES;
             hipLaunchKernelGGL(kern, dim3(nb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
-                               nkb * FK_WAVES, g, h->FS, h->S);
+                               n_epi, g, h->FS, h->S);
         };
         task(kw_verify_kernel, G[0]);
         task(kw_short_kernel, G[2]);
@@ -1130,7 +1174,7 @@ static int finish(kw_handle *h)
             h->err = buf;
             return KW_EOVERFLOW;
         }
-        if (status[0] & (ST_OUT_OVERFLOW | ST_RX_OVERFLOW | ST_TASK_OVERFLOW | ST_DSET_FULL)) {
+        if (status[0] & (ST_OUT_OVERFLOW | ST_RX_OVERFLOW | ST_TASK_OVERFLOW | ST_DSET_FULL | ST_CAND_OVERFLOW)) {
             // grow what overflowed (result regions to the largest count seen, queues to the largest need) and rescan
             ScratchCaps w = h->caps;
             if (status[0] & ST_OUT_OVERFLOW) {
@@ -1150,6 +1194,12 @@ static int finish(kw_handle *h)
                 w.xcap = std::max(w.xcap, tm[3]);
             }
             if (status[0] & ST_DSET_FULL) w.dsize *= 4;
+            if (status[0] & ST_CAND_OVERFLOW) {
+                uint32_t cm[2];
+                HIPCHK(h, hipMemcpy(cm, h->FS.cmax, sizeof(cm), hipMemcpyDeviceToHost));
+                w.cand_cap = std::max(w.cand_cap, cm[0] + cm[0] / 8 + 64);
+                w.item_cap = std::max(w.item_cap, cm[1] + cm[1] / 8 + 64);
+            }
             int rc = ensure_scratch(h, w);
             if (rc) return rc;
             rc = launch_scan(h);
@@ -1235,6 +1285,8 @@ extern "C" int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n)
     hipEvent_t ev[6] = {h->ev0, h->ev1, h->evr, h->evg, h->ev2, h->ev2};
     for (int i = 0; i < n && i < 4; ++i) HIPCHK(h, hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
     if (n > 4) HIPCHK(h, hipEventElapsedTime(&ms[4], h->ev0, h->ev2));
+    hipEvent_t sp[4] = {h->ev0, h->evf, h->evp, h->ev1};
+    for (int i = 0; i + 5 < n && i < 3; ++i) HIPCHK(h, hipEventElapsedTime(&ms[5 + i], sp[i], sp[i + 1]));
     return KW_OK;
 }
 
@@ -1273,6 +1325,8 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->ev2) (void)hipEventDestroy(h->ev2);
     if (h->evg) (void)hipEventDestroy(h->evg);
     if (h->evr) (void)hipEventDestroy(h->evr);
+    if (h->evf) (void)hipEventDestroy(h->evf);
+    if (h->evp) (void)hipEventDestroy(h->evp);
     delete h;
     return KW_OK;
 }

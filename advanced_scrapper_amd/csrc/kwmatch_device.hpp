@@ -104,5 +104,6 @@ constexpr uint32_t ST_FIELD_TOO_LONG = 8u;
 constexpr uint32_t ST_RX_OVERFLOW = 16u;     // a resolve wave queued more regex searches than rx_cap
 constexpr uint32_t ST_TASK_OVERFLOW = 32u;   // a scan wave made more tasks than a task region holds
 constexpr uint32_t ST_DSET_FULL = 64u;       // the decided-name set is full
+constexpr uint32_t ST_CAND_OVERFLOW = 128u;  // a filter region held more candidates, or a probe region more items, than fit
 
 }  // namespace kw

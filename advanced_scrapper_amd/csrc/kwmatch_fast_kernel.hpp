@@ -87,6 +87,14 @@ __device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], int j)
     return __builtin_amdgcn_alignbyte(b, a, j & 3);
 }
 
+// a 64-bit value of lane l, l varying per lane
+__device__ __forceinline__ int64_t rdlane64v(int64_t v, int l)
+{
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, WAVE);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)v >> 32), l, WAVE);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // a 64-bit value of lane l (wave-uniform result)
 __device__ __forceinline__ int64_t rdlane64(int64_t v, int l)
 {

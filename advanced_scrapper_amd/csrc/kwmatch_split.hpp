@@ -1,0 +1,486 @@
+// The fast path's byte scan as three kernels (gfx950).  Included after kwmatch_fast_kernel.hpp, whose
+// probe, epilogue and field helpers it reuses.
+//
+//   kw_filter_kernel  one wave per document (grid-stride): the LDS filters over every byte position; the
+//                     stage-2 survivors ("candidates") go to the wave's region in HBM in document and
+//                     position order, with the document's flags (non-ASCII fields, edge prefilter, field
+//                     too long) in its header.  Few registers, 64 KiB of LDS: two workgroups per CU.
+//   kw_probe_kernel   one wave per filter region: the region's candidates 64 at a time, whatever document
+//                     they belong to (a document averages ~13 candidates, so per-document batches left most
+//                     lanes idle): anchor hash probe, head compare, then the (candidate, use) pairs spread
+//                     over the lanes to compare spans and test \b.  Each lane's verified uses ("items") are
+//                     staged in LDS and written out in candidate order, so a document's items are
+//                     contiguous in HBM, the text's before the title's; the header gets the first item's
+//                     index, the per-field counts are added up in ncnt.
+//   kw_epi_kernel     one wave per document: all-ASCII documents are finished by the epilogue
+//                     (fk_scan_epilogue: sort, emit, queue the verify / short / regex tasks), the others get
+//                     their header for the resolve kernel, oversize ones go to the generic kernel.
+//
+// Reference: the per-article x per-name loop of match_keywords.py:159-180 (see kwmatch_fast.hpp for the
+// anchors and filters).
+#pragma once
+#include "kwmatch_fast_kernel.hpp"
+
+namespace kw {
+
+#ifndef FS_WAVES_CFG
+#define FS_WAVES_CFG 8
+#endif
+constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
+constexpr int FS_BLOCK = FS_WAVES * WAVE;
+constexpr int PK_WAVES = 4;              // waves per probe workgroup
+constexpr int PK_BLOCK = PK_WAVES * WAVE;
+constexpr int PK_PER_LANE = 16;          // items one candidate may stage (more: its document is deferred)
+constexpr int EK_WAVES = 8;              // waves per epilogue workgroup
+constexpr int EK_BLOCK = EK_WAVES * WAVE;
+
+struct __attribute__((aligned(16))) FilterLds {
+    uint32_t filt[FK_FILT_WORDS];
+    uint32_t l2[FK_L2_WORDS];
+    uint32_t t3[FK_T3_WORDS];
+    uint32_t b2[FK_B2_WORDS];
+};
+
+// ---------------------------------------------------------------- kernel 1: the filters
+__global__ __launch_bounds__(FS_BLOCK) void kw_filter_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+                                                             const int64_t *__restrict__ off, int64_t n_docs,
+                                                             FastScratch S)
+{
+    __shared__ FilterLds L;
+    uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
+    for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FS_BLOCK) filt[i] = FT.filt[i];
+    for (int i = threadIdx.x; i < FK_L2_WORDS; i += FS_BLOCK) l2[i] = FT.l2[i];
+    for (int i = threadIdx.x; i < FK_T3_WORDS; i += FS_BLOCK) t3[i] = FT.t3[i];
+    for (int i = threadIdx.x; i < FK_B2_WORDS; i += FS_BLOCK) b2[i] = FT.b2[i];
+    __syncthreads();
+
+    const int lane = lane_id();
+    const int64_t wave = (int64_t)blockIdx.x * FS_WAVES + threadIdx.x / WAVE;
+    const int64_t n_waves = (int64_t)gridDim.x * FS_WAVES;
+    uint4 *cand = S.cand + (size_t)wave * S.cand_cap;
+    const uint32_t ccap = S.cand_cap;
+    uint32_t ccur = 0;                                   // candidates of this wave's region (wave-uniform)
+    uint32_t ncand = 0, ncand2 = 0;
+    const bool has_t3 = FT.has_t3 != 0;
+    const bool gate_on = FT.n_gate != 0;
+    int64_t pf_off = (lane < 3 && wave < n_docs) ? off[2 * wave + lane] : 0;
+    for (int64_t d = wave; d < n_docs; d += n_waves) {
+        const int64_t t0 = rdlane64(pf_off, 0), t1 = rdlane64(pf_off, 1), t2 = rdlane64(pf_off, 2);
+        pf_off = (lane < 3 && d + n_waves < n_docs) ? off[2 * (d + n_waves) + lane] : 0;
+        const int32_t dl1 = (int32_t)(t1 - t0), dl2 = (int32_t)(t2 - t0);
+        const bool defer = (t1 - t0 > MAX_FIELD_BYTES) || (t2 - t1 > MAX_FIELD_BYTES);
+        const int64_t base = t0 & ~(int64_t)15;
+        int shp = fk_shape(t2 - base);
+        uint4 nv;
+        uint32_t nw4;
+        fk_tile_load(arena, base, shp, t2, lane, nv, nw4);
+        // edge prefilter: first / last eight bytes of each field (lanes 0..3)
+        uint32_t ebits = 0, ebit = 0;
+        {
+            const int f = lane >> 1;
+            const int64_t fb = f ? t1 : t0, fe = f ? t2 : t1;
+            if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+                const int64_t a = (lane & 1) ? fe - 8 : fb;
+                const uint64_t k = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
+                const uint32_t idx = fk_edge_index(k);
+                ebit = idx & 31u;
+                ebits = ((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5];
+            }
+        }
+        bool na0 = false, na1 = false;
+        for (int64_t blk = base, nblk = 0; blk < t2 && !defer; blk = nblk) {
+            const int Sc = shp, ng = Sc >> 2;
+            const int64_t lp = blk + lane * Sc;
+            uint32_t W[5];
+            {
+                const uint32_t nx = (uint32_t)__shfl_down((int)nv.x, 1, WAVE);
+                const uint32_t tail = lane == WAVE - 1 ? nw4 : nx;
+                W[0] = nv.x;
+                W[1] = ng > 1 ? nv.y : tail;
+                W[2] = ng > 2 ? nv.z : (ng == 2 ? tail : 0u);
+                W[3] = ng > 2 ? nv.w : 0u;
+                W[4] = ng > 2 ? tail : 0u;
+            }
+            nblk = blk + (int64_t)WAVE * Sc;
+            shp = fk_shape(t2 - nblk);
+            fk_tile_load(arena, nblk, shp, t2, lane, nv, nw4);
+            const int32_t lrel = (int32_t)(lp - t0);
+            const int32_t rel0 = -lrel, rel2 = dl2 - lrel, rel1 = dl1 - lrel;
+            const int jlo = rel0 <= 0 ? 0 : (rel0 >= Sc ? Sc : (int)rel0);
+            const int jhi = rel2 <= 0 ? 0 : (rel2 >= Sc ? Sc : (int)rel2);
+            uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
+            if (rel1 - 1 >= 0 && rel1 - 1 < Sc) valid &= ~(1u << (rel1 - 1));
+            if (rel2 - 1 >= 0 && rel2 - 1 < Sc) valid &= ~(1u << (rel2 - 1));
+            if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
+                uint32_t hb = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t x = (W[k] >> 7) & 0x01010101u;
+                    hb |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
+                }
+                const int j1 = rel1 <= 0 ? 0 : (rel1 >= Sc ? Sc : (int)rel1);
+                const uint32_t in0 = ((1u << j1) - 1u) & ~((1u << jlo) - 1u);
+                const uint32_t in1 = (jhi > j1) ? (((1u << jhi) - 1u) & ~((1u << j1) - 1u)) : 0u;
+                if (hb & in0) na0 = true;
+                if (hb & in1) na1 = true;
+            }
+            uint32_t hit = 0, gate = 0;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                if (g >= ng) break;
+                uint32_t fw[4], bw[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
+                    fw[jj] = filt[fk_word(key)];
+                    bw[jj] = gate_on ? b2[fk_b2_index(key) >> 5] : 0u;
+                }
+                if (FK_SCHED) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int j = 4 * g + jj;
+                    const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
+                    hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit(key), 1) << j;
+                    gate |= __builtin_amdgcn_ubfe(bw[jj], fk_b2_index(key), 1) << j;
+                }
+            }
+            gate &= valid;
+            hit &= valid;
+            ncand += (uint32_t)__popc(hit);
+            uint32_t m4 = 0, m3 = 0;
+            {
+                uint32_t hm = hit;
+                while (hm) {
+                    const int j = __ffs(hm) - 1;
+                    hm &= hm - 1;
+                    const uint32_t key = fk_key_at(W, j);
+                    const int32_t pr = lrel + j;
+                    const int32_t fer = pr < dl1 ? dl1 : dl2;
+                    if (pr + 4 <= fer && lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
+                    if (has_t3 && lds_bit(t3, fk_t3_index(key))) m3 |= 1u << j;
+                }
+            }
+            const uint32_t cm = m4 | m3 | gate;
+            int total;
+            const int ex = wave_excl_scan(__popc(cm), &total);
+            if (total == 0) continue;
+            ncand2 += (lane == 0) ? (uint32_t)total : 0u;
+            uint32_t k = ccur + (uint32_t)ex;
+            uint32_t mm = cm;
+            while (mm) {
+                const int j = __ffs(mm) - 1;
+                mm &= mm - 1;
+                const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
+                if (k < ccap) cand[k] = make_uint4((uint32_t)d, ((uint32_t)(lrel + j) << 3) | fl, fk_key_at(W, j), 0u);
+                ++k;
+            }
+            ccur += (uint32_t)total;
+        }
+        uint32_t flags = 0;
+        if (__ballot(na0)) flags |= DH_NA0;
+        if (__ballot(na1)) flags |= DH_NA1;
+        const uint64_t em = __ballot((ebits >> ebit) & 1u);
+        if (em & 3ull) flags |= DH_EDGE0;
+        if (em & 12ull) flags |= DH_EDGE1;
+        if (defer) flags |= DH_DEFER;
+        if (lane == 0) {
+            S.hdr[d] = make_uint2(0u, flags);
+            S.ncnt[d] = make_uint2(0u, 0u);
+        }
+    }
+    if (lane == 0) {
+        S.ccnt[wave] = ccur;
+        if (ccur > ccap) {
+            atomicOr(&S.status[0], ST_CAND_OVERFLOW);
+            atomicMax(&S.cmax[0], ccur);
+        }
+    }
+    unsigned long long c1 = ncand;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) c1 += __shfl_xor(c1, dd, WAVE);
+    if (lane == 0) {
+        atomicAdd(&S.stats[0], c1);
+        atomicAdd(&S.stats[8], (unsigned long long)ncand2);
+    }
+}
+
+// ---------------------------------------------------------------- kernel 2: the anchor probe
+__global__ __launch_bounds__(PK_BLOCK) void kw_probe_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                            const int64_t *__restrict__ off, int32_t n_regions,
+                                                            FastScratch S)
+{
+    __shared__ uint64_t stage_all[PK_WAVES * WAVE * PK_PER_LANE];
+    __shared__ uint32_t scnt_all[PK_WAVES * WAVE];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t region = (int64_t)blockIdx.x * PK_WAVES + wib;
+    if (region >= n_regions) return;
+    uint64_t *stage = stage_all + wib * WAVE * PK_PER_LANE;
+    uint32_t *scnt = scnt_all + wib * WAVE;
+    const uint4 *cand = S.cand + (size_t)region * S.cand_cap;
+    const uint32_t nc = min(S.ccnt[region], S.cand_cap);
+    uint64_t *items = S.items + (size_t)region * S.item_cap;
+    const uint32_t icap = S.item_cap;
+    const uint32_t ibase = (uint32_t)((size_t)region * S.item_cap);
+    uint32_t icur = 0;                      // items of this region (wave-uniform)
+    uint32_t last_doc = 0xFFFFFFFFu;        // document of the region's last item so far
+    uint32_t nanchor = 0;
+    scnt[lane] = 0;
+    for (uint32_t c0 = 0; c0 < nc; c0 += WAVE) {
+        const bool valid = c0 + (uint32_t)lane < nc;
+        const uint4 e = valid ? cand[c0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t doc = e.x;
+        const int64_t t0 = valid ? off[2 * (int64_t)doc] : 0;
+        const int64_t t1 = valid ? off[2 * (int64_t)doc + 1] : 0;
+        const int64_t t2 = valid ? off[2 * (int64_t)doc + 2] : 0;
+        const int32_t l1 = (int32_t)(t1 - t0), l2 = (int32_t)(t2 - t0);
+        const int32_t pr = (int32_t)(e.y >> 3);
+        const int f = pr < l1 ? 0 : 1;
+        const int32_t fbr = f ? l1 : 0, fer = f ? l2 : l1;
+        const int64_t p = t0 + pr;
+        const uint32_t hi = valid ? ld_u32_unaligned(arena, p + 4) : 0u;
+        const uint64_t h8 = (uint64_t)e.z | ((uint64_t)hi << 32);
+        // hash lookups of the lane's key lengths 4, 3, 2 (try bits 0, 1, 2), all in flight together
+        uint32_t rb[3], re[3];
+        {
+            uint4 hs[3];
+            uint64_t key[3];
+            uint32_t slot[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int Lk = 4 - i;
+                const bool want = valid && ((e.y >> i) & 1u) && pr + Lk <= fer;
+                key[i] = ((uint64_t)Lk << 32) | (h8 & ((1ull << (8 * Lk)) - 1));
+                slot[i] = fk_ht_slot(key[i], FT.ht_mask);
+                hs[i] = want ? FT.ht4[slot[i]] : make_uint4(~0u, ~0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                rb[i] = re[i] = 0;
+                for (;;) {
+                    const uint64_t kk = (uint64_t)hs[i].x | ((uint64_t)hs[i].y << 32);
+                    if (kk == key[i]) { rb[i] = hs[i].z; re[i] = hs[i].z + hs[i].w; break; }
+                    if (kk == ~0ull) break;
+                    slot[i] = (slot[i] + 1) & FT.ht_mask;
+                    hs[i] = FT.ht4[slot[i]];
+                }
+            }
+        }
+        uint32_t tcur = rb[0], tend = re[0], b1 = rb[1], e1 = re[1], b2 = rb[2], e2 = re[2];
+        bool more = valid;
+        bool ovf = false;
+        while (__ballot(more)) {
+            // stage A: up to two matching anchors of this lane's candidate
+            uint32_t ub = 0, uc = 0, ub1 = 0, uc1 = 0, nm = 0;
+            while (more && nm < 2) {
+                if (tcur < tend) {
+                    const uint4 ar0 = FT.arec[tcur];
+                    const bool two = tcur + 1 < tend;
+                    const uint4 ar1 = two ? FT.arec[tcur + 1] : make_uint4(0u, 0u, 0u, 0u);
+                    auto take = [&](const uint4 &ar) {
+                        const uint32_t alen = ar.w & 0xFFu;
+                        if (pr + (int32_t)alen > fer) return;
+                        const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
+                        if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) return;
+                        ++nanchor;
+                        if (nm == 0) { ub = ar.z; uc = ar.w >> 8; }
+                        else { ub1 = ar.z; uc1 = ar.w >> 8; }
+                        ++nm;
+                    };
+                    take(ar0);
+                    ++tcur;
+                    if (two && nm < 2) {
+                        take(ar1);
+                        ++tcur;
+                    }
+                    continue;
+                }
+                if (b1 >= e1 && b2 >= e2) { more = false; break; }
+                tcur = b1; tend = e1;
+                b1 = b2; e1 = e2;
+                b2 = e2 = 0;
+            }
+            // stage B: (candidate, use) pairs over the lanes
+            int total;
+            const int ex = wave_excl_scan((int)(uc + uc1), &total);
+            for (int g0 = 0; g0 < total; g0 += WAVE) {
+                const int g = g0 + lane;
+                int owner = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const int cnd = owner + step;
+                    const int exc = __shfl(ex, cnd & 63, WAVE);
+                    if (cnd < WAVE && exc <= g) owner = cnd;
+                }
+                const int exo = __shfl(ex, owner, WAVE);
+                const uint32_t oub = (uint32_t)__shfl((int)ub, owner, WAVE);
+                const uint32_t ouc = (uint32_t)__shfl((int)uc, owner, WAVE);
+                const uint32_t oub1 = (uint32_t)__shfl((int)ub1, owner, WAVE);
+                const uint32_t loc = (uint32_t)(g - exo);
+                const uint32_t u = loc < ouc ? oub + loc : oub1 + (loc - ouc);
+                const int32_t ppr = __shfl(pr, owner, WAVE);
+                const int32_t ofbr = __shfl(fbr, owner, WAVE), ofer = __shfl(fer, owner, WAVE);
+                const int64_t ot0 = rdlane64v(t0, owner);
+                if (g >= total) continue;
+                const uint4 ur = FT.urec[u];
+                const uint32_t kind = ur.x & 0xFF, aoff = (ur.x >> 8) & 0xFF;
+                const uint32_t sblen = ur.y & 0xFFFF;
+                const uint32_t pat = ur.z;
+                const int32_t s0r = ppr - (int32_t)aoff;
+                if (s0r < ofbr || s0r + (int32_t)sblen > ofer) continue;
+                const int64_t s0 = ot0 + s0r, fb = ot0 + ofbr, fe2 = ot0 + ofer;
+                const uint4 u2 = FT.urec2[u];
+                const uint64_t th = load8(arena, s0);
+                const uint64_t tt = load8(arena, s0 + (sblen > 8 ? sblen - 8 : 0));
+                const uint32_t pi = kind == FU_UPPER ? FT.pat_info[pat] : 0u;
+                const bool hasp = kind == FU_UPPER && s0 > fb, hasn = kind == FU_UPPER && s0 + (int64_t)sblen < fe2;
+                const uint32_t prevb = hasp ? (uint32_t)arena[s0 - 1] : 0u;
+                const uint32_t nextb = hasn ? (uint32_t)arena[s0 + sblen] : 0u;
+                const uint32_t hl = sblen < 8 ? sblen : 8;
+                const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
+                if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
+                if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) continue;
+                if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) continue;
+                if (kind == FU_UPPER) {
+                    const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
+                    bool wp = false;
+                    if (hasp) wp = is_word_cp(T, prevb < 0x80u ? prevb : decode_before(arena, fb, s0));
+                    if (wp == wf) continue;
+                    bool wn = false;
+                    if (hasn) {
+                        uint32_t ch = nextb;
+                        if (nextb >= 0x80u) decode_at(arena, s0 + sblen, fe2, &ch);
+                        wn = is_word_cp(T, ch);
+                    }
+                    if (wn == wl) continue;
+                }
+                const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(uint32_t)(s0r - ofbr) << IT_POS_SHIFT) |
+                                      ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
+                const uint32_t k = atomicAdd(&scnt[owner], 1u);
+                if (k < (uint32_t)PK_PER_LANE) stage[owner * PK_PER_LANE + k] = item;
+            }
+            wave_sync();
+        }
+        // the batch's items, in candidate order
+        uint32_t nmine = scnt[lane];
+        if (nmine > (uint32_t)PK_PER_LANE) { ovf = true; nmine = PK_PER_LANE; }
+        int itotal;
+        const int iex = wave_excl_scan((int)nmine, &itotal);
+        const uint64_t withm = __ballot(nmine > 0);
+        if (withm) {
+            const uint64_t below = (1ull << lane) - 1;
+            const uint64_t prevm = withm & below;
+            const uint32_t pdoc = (uint32_t)__shfl((int)doc, prevm ? 63 - __builtin_clzll(prevm) : 0, WAVE);
+            const uint32_t prev_doc = prevm ? pdoc : last_doc;
+            if (nmine > 0) {
+                if (doc != prev_doc) S.hdr[doc].x = ibase + icur + (uint32_t)iex;
+                atomicAdd(f ? &S.ncnt[doc].y : &S.ncnt[doc].x, scnt[lane]);
+                for (uint32_t k = 0; k < nmine; ++k) {
+                    const uint32_t idx = icur + (uint32_t)iex + k;
+                    if (idx < icap) items[idx] = stage[lane * PK_PER_LANE + k];
+                }
+            }
+            last_doc = (uint32_t)__shfl((int)doc, 63 - __builtin_clzll(withm), WAVE);
+        }
+        if (ovf) atomicOr(&S.hdr[doc].y, DH_DEFER);
+        icur += (uint32_t)itotal;
+        scnt[lane] = 0;
+        wave_sync();
+    }
+    if (lane == 0 && icur > icap) {
+        atomicOr(&S.status[0], ST_CAND_OVERFLOW);
+        atomicMax(&S.cmax[1], icur);
+    }
+    unsigned long long a = nanchor;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) a += __shfl_xor(a, dd, WAVE);
+    if (lane == 0) atomicAdd(&S.stats[1], a);
+}
+
+// ---------------------------------------------------------------- kernel 3: per-document epilogue
+__global__ __launch_bounds__(EK_BLOCK) void kw_epi_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+                                                          const int64_t *__restrict__ off, int64_t n_docs,
+                                                          FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items_all[EK_WAVES * (FK_ITEMS0 + FK_ITEMS1)];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t wave = (int64_t)blockIdx.x * EK_WAVES + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * EK_WAVES;
+    uint64_t *items = items_all + wib * (FK_ITEMS0 + FK_ITEMS1);
+    uint32_t ndefer = 0, ndef_items = 0;
+    OutCtx O;
+    O.shared = nullptr;
+    O.out = S.kout + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    TaskCounts TC = {0u, 0u, 0u, 0u};
+    for (int64_t d = wave; d < n_docs; d += n_waves) {
+        // lanes 0..2: offsets, lane 3: header, lane 4: item counts
+        const int64_t ov = lane < 3 ? off[2 * d + lane] : 0;
+        const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : make_uint2(0u, 0u));
+        FastDoc D;
+        D.arena = arena;
+        D.t0 = rdlane64(ov, 0);
+        D.t1 = rdlane64(ov, 1);
+        D.t2 = rdlane64(ov, 2);
+        D.doc = (uint32_t)d;
+        D.l1 = (int32_t)(D.t1 - D.t0);
+        D.l2 = (int32_t)(D.t2 - D.t0);
+        const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
+        uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 3);
+        const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
+        const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+        bool defer = (flags & DH_DEFER) != 0;
+        if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) { defer = true; ++ndef_items; }
+        flags &= ~DH_DEFER;
+        bool done = false;
+        if (!defer && !(flags & (DH_NA0 | DH_NA1))) {
+            const uint64_t *src = S.items + ibeg;
+            for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) items[i] = src[i];
+            for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
+            wave_sync();
+            done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+            if (!done) { defer = true; ++ndef_items; }
+        }
+        uint2 h;
+        h.x = ibeg;
+        if (defer) {
+            ++ndefer;
+            h.y = DH_DEFER;
+            if (lane == 0) {
+                const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
+                else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+            }
+        } else if (done) {
+            h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
+        } else {
+            // non-ASCII: the resolve kernel works on the document (items, an edge candidate, or a short field)
+            const int64_t l0 = D.t1 - D.t0, l1 = D.t2 - D.t1;
+            const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
+            const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
+            const bool need = (n0 + n1) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
+            h.y = n0 | (n1 << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u);
+        }
+        if (lane == 0) S.hdr[d] = h;
+        wave_sync();
+    }
+    if (lane == 0) {
+        S.kout_cnt[wave] = O.n;
+        S.vcnt[wave] = TC.v;
+        if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);
+        S.scnt[wave] = TC.s;
+        S.xcnt[wave] = TC.x;
+        if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
+            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
+            atomicMax(&S.tmax[0], TC.v);
+            atomicMax(&S.tmax[2], TC.s);
+            atomicMax(&S.tmax[3], TC.x);
+        }
+        atomicAdd(&S.stats[4], (unsigned long long)ndefer);
+        atomicAdd(&S.stats[5], (unsigned long long)ndef_items);
+    }
+}
+
+}  // namespace kw

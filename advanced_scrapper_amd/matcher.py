@@ -167,9 +167,10 @@ class GpuMatcher:
 
     def kernel_times(self) -> Dict[str, float]:
         """Per-kernel device times (ms) of the last scan."""
-        v = np.zeros(5, dtype=np.float32)
-        _native.check(_native.lib().kw_last_kernel_times(self.h, _native.ptr(v), 5), self.h)
-        return dict(zip(('scan', 'resolve', 'generic', 'compact', 'total'), (float(x) for x in v)))
+        keys = ('scan', 'resolve', 'generic', 'compact', 'total', 'filter', 'probe', 'epilogue')
+        v = np.zeros(len(keys), dtype=np.float32)
+        _native.check(_native.lib().kw_last_kernel_times(self.h, _native.ptr(v), len(keys)), self.h)
+        return dict(zip(keys, (float(x) for x in v)))
 
     def kernel_ms(self) -> Tuple[float, float, float]:
         """(fast kernel, generic kernel, all kernels incl. compaction) in ms for the last scan."""

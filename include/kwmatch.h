@@ -122,8 +122,10 @@ int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
  * compaction. */
 int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *total_ms);
 
-/* Per-kernel device times (ms) of the last kw_scan, up to 5 values: [0] scan
- * (kw_items_kernel), [1] resolve, [2] generic, [3] result compaction, [4] total. */
+/* Per-kernel device times (ms) of the last kw_scan, up to 8 values: [0] scan
+ * (filter + probe + epilogue kernels), [1] resolve (task kernels + resolve
+ * kernel), [2] generic, [3] result compaction, [4] total, [5] filter kernel,
+ * [6] probe kernel, [7] epilogue kernel. */
 int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 
 /* Which kernel finished each document of the last scan (after kw_hits):
