@@ -954,7 +954,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     const size_t per_tasks = (size_t)(c.vcap + c.ecap + c.scap + c.xcap) * 16;
     size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_blk) +
                    nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 4 +
-                   (size_t)c.ns * c.cand_cap * 16 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 8 + 3 * 256 +
+                   (size_t)c.ns * c.cand_cap * 16 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 12 + 4 * 256 +
                    (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
                    32 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
@@ -971,6 +971,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.cand_cap = c.cand_cap;
     h->FS.ccnt = (uint32_t *)carve((size_t)c.ns * 4);
     h->FS.ncnt = (uint2 *)carve((size_t)c.hdr_cap * 8);
+    h->FS.dflags = (uint32_t *)carve((size_t)c.hdr_cap * 4);
     h->FS.hdr = (uint2 *)carve((size_t)c.hdr_cap * 8);
     h->FS.defer_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
     h->FS.rx_tasks = (uint4 *)carve((size_t)c.nr * c.rx_cap * 16);
@@ -1085,6 +1086,10 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
+    if (n_docs > 0) {
+        HIPCHK(h, hipMemsetAsync(h->FS.ncnt, 0, (size_t)n_docs * 8, st));
+        HIPCHK(h, hipMemsetAsync(h->FS.dflags, 0, (size_t)n_docs * 4, st));
+    }
     HIPCHK(h, hipEventRecord(h->ev0, st));
     if (n_docs > 0)
         hipLaunchKernelGGL(kw_filter_kernel, dim3(nsb), dim3(FS_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,

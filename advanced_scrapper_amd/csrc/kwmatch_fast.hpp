@@ -166,6 +166,7 @@ struct FastScratch {
     uint32_t cand_cap;
     uint32_t *ccnt;             // per filter region: candidates written
     uint2 *ncnt;                // per document: items of field 0 / field 1 (the probe adds them up)
+    uint32_t *dflags;           // per document: DH_NA0 / DH_NA1 (the filter ORs them in) and DH_DEFER (probe)
     uint32_t *cmax;             // [2] largest candidate / item count a region needed (rescan sizing)
 };
 

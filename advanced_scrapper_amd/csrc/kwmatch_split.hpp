@@ -26,6 +26,12 @@ namespace kw {
 #ifndef FS_WAVES_CFG
 #define FS_WAVES_CFG 8
 #endif
+#ifndef FS_AHEAD
+#define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
+#endif
+#ifndef FS_MINW
+#define FS_MINW 1
+#endif
 constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
 constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
@@ -34,83 +40,92 @@ constexpr int PK_PER_LANE = 16;          // items one candidate may stage (more:
 constexpr int EK_WAVES = 8;              // waves per epilogue workgroup
 constexpr int EK_BLOCK = EK_WAVES * WAVE;
 
+constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range)
+
 struct __attribute__((aligned(16))) FilterLds {
     uint32_t filt[FK_FILT_WORDS];
     uint32_t l2[FK_L2_WORDS];
     uint32_t t3[FK_T3_WORDS];
     uint32_t b2[FK_B2_WORDS];
+    uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
+    uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
 };
 
-// ---------------------------------------------------------------- kernel 1: the filters
-__global__ __launch_bounds__(FS_BLOCK) void kw_filter_kernel(FastTables FT, const uint8_t *__restrict__ arena,
-                                                             const int64_t *__restrict__ off, int64_t n_docs,
-                                                             FastScratch S)
+// the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
+__device__ __forceinline__ uint32_t fg_doc(const uint32_t *dstart, uint32_t nd, uint32_t r)
 {
-    __shared__ FilterLds L;
-    uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
-    for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FS_BLOCK) filt[i] = FT.filt[i];
-    for (int i = threadIdx.x; i < FK_L2_WORDS; i += FS_BLOCK) l2[i] = FT.l2[i];
-    for (int i = threadIdx.x; i < FK_T3_WORDS; i += FS_BLOCK) t3[i] = FT.t3[i];
-    for (int i = threadIdx.x; i < FK_B2_WORDS; i += FS_BLOCK) b2[i] = FT.b2[i];
-    __syncthreads();
+    uint32_t lo = 0, n = nd;
+    while (n > 1) {
+        const uint32_t h = n >> 1;
+        if (dstart[lo + h] <= r) lo += h;
+        n -= h;
+    }
+    return lo;
+}
 
+// bigram-table bit index: the low 16 bits of a 24-bit product equal fk_b2_index's (key2 * 40503) & 0xFFFF
+__device__ __forceinline__ uint32_t fk_b2_mul(uint32_t key) { return __umul24(key, 40503u); }
+
+// ---------------------------------------------------------------- kernel 1: the filters
+// A wave takes groups of FG_DOCS consecutive documents and streams each group's bytes as one flat range
+// (1 KiB tiles, 16 bytes per lane, the next tile's loads in flight): no per-document tile shapes or
+// set-up.  Keys that run over a field or document end are kept (a superset): the probe checks every
+// anchor against its field.  Non-ASCII bytes mark their field in dflags (rare: an LDS lookup of the
+// document, one atomic per field).
+__device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds &L, const uint8_t *__restrict__ arena,
+                                                 const int64_t *__restrict__ off, int64_t n_docs, const FastScratch &S,
+                                                 int64_t wave, int64_t n_waves, int wib, uint32_t &ncand, uint32_t &ncand2,
+                                                 uint32_t &ccur)
+{
     const int lane = lane_id();
-    const int64_t wave = (int64_t)blockIdx.x * FS_WAVES + threadIdx.x / WAVE;
-    const int64_t n_waves = (int64_t)gridDim.x * FS_WAVES;
+    const uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
+    uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
     uint4 *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
-    uint32_t ccur = 0;                                   // candidates of this wave's region (wave-uniform)
-    uint32_t ncand = 0, ncand2 = 0;
     const bool has_t3 = FT.has_t3 != 0;
-    const bool gate_on = FT.n_gate != 0;
-    int64_t pf_off = (lane < 3 && wave < n_docs) ? off[2 * wave + lane] : 0;
-    for (int64_t d = wave; d < n_docs; d += n_waves) {
-        const int64_t t0 = rdlane64(pf_off, 0), t1 = rdlane64(pf_off, 1), t2 = rdlane64(pf_off, 2);
-        pf_off = (lane < 3 && d + n_waves < n_docs) ? off[2 * (d + n_waves) + lane] : 0;
-        const int32_t dl1 = (int32_t)(t1 - t0), dl2 = (int32_t)(t2 - t0);
-        const bool defer = (t1 - t0 > MAX_FIELD_BYTES) || (t2 - t1 > MAX_FIELD_BYTES);
-        const int64_t base = t0 & ~(int64_t)15;
-        int shp = fk_shape(t2 - base);
-        uint4 nv;
-        uint32_t nw4;
-        fk_tile_load(arena, base, shp, t2, lane, nv, nw4);
-        // edge prefilter: first / last eight bytes of each field (lanes 0..3)
-        uint32_t ebits = 0, ebit = 0;
-        {
-            const int f = lane >> 1;
-            const int64_t fb = f ? t1 : t0, fe = f ? t2 : t1;
-            if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
-                const int64_t a = (lane & 1) ? fe - 8 : fb;
-                const uint64_t k = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
-                const uint32_t idx = fk_edge_index(k);
-                ebit = idx & 31u;
-                ebits = ((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5];
-            }
+    const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
+    for (int64_t g = wave; g < n_groups; g += n_waves) {
+        const int64_t d0 = g * FG_DOCS;
+        const int nd = (int)(n_docs - d0 < FG_DOCS ? n_docs - d0 : FG_DOCS);
+        const int64_t o0 = lane <= nd ? off[2 * (d0 + lane)] : 0;
+        const int64_t o1 = lane < nd ? off[2 * (d0 + lane) + 1] : 0;
+        const int64_t gb = rdlane64(o0, 0), ge = rdlane64(o0, nd);
+        if (ge - gb > 0x7FFFFFFFll) {   // group-relative positions are 32-bit: such groups go to the generic kernel
+            if (lane < nd) atomicOr(&S.dflags[d0 + lane], DH_DEFER);
+            continue;
         }
-        bool na0 = false, na1 = false;
-        for (int64_t blk = base, nblk = 0; blk < t2 && !defer; blk = nblk) {
-            const int Sc = shp, ng = Sc >> 2;
-            const int64_t lp = blk + lane * Sc;
+        if (ge <= gb) continue;   // every field of the group is empty
+        wave_sync();
+        if (lane <= nd) dstart[lane] = (uint32_t)(o0 - gb);
+        if (lane < nd) dtitle[lane] = (uint32_t)(o1 - gb);
+        wave_sync();
+        int64_t blk = gb & ~(int64_t)15;
+        // Three tiles in flight per wave, each in its own registers (the loop is unrolled by three, so no
+        // register copy waits for a load).  Loads are unconditional: an address past the group's last
+        // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
+        // comes with the word after it (lane 63's fifth word).
+        const int64_t glast = (ge - 1) & ~(int64_t)15;
+        auto load = [&](uint4 &v, uint32_t &w, int64_t tb) {
+            const int64_t a = tb + 16 * (int64_t)lane, e = tb + 1024;
+            v = *(const uint4 *)(arena + (a < glast ? a : glast));
+            w = *(const uint32_t *)(arena + (e < glast ? e : glast));
+        };
+        auto tile = [&](const uint4 &v, uint32_t w4, int64_t tb) {
+            const int64_t lp = tb + 16 * (int64_t)lane;
             uint32_t W[5];
+            W[0] = v.x;
+            W[1] = v.y;
+            W[2] = v.z;
+            W[3] = v.w;
             {
-                const uint32_t nx = (uint32_t)__shfl_down((int)nv.x, 1, WAVE);
-                const uint32_t tail = lane == WAVE - 1 ? nw4 : nx;
-                W[0] = nv.x;
-                W[1] = ng > 1 ? nv.y : tail;
-                W[2] = ng > 2 ? nv.z : (ng == 2 ? tail : 0u);
-                W[3] = ng > 2 ? nv.w : 0u;
-                W[4] = ng > 2 ? tail : 0u;
+                const uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1, WAVE);
+                W[4] = lane == WAVE - 1 ? w4 : nx;
             }
-            nblk = blk + (int64_t)WAVE * Sc;
-            shp = fk_shape(t2 - nblk);
-            fk_tile_load(arena, nblk, shp, t2, lane, nv, nw4);
-            const int32_t lrel = (int32_t)(lp - t0);
-            const int32_t rel0 = -lrel, rel2 = dl2 - lrel, rel1 = dl1 - lrel;
-            const int jlo = rel0 <= 0 ? 0 : (rel0 >= Sc ? Sc : (int)rel0);
-            const int jhi = rel2 <= 0 ? 0 : (rel2 >= Sc ? Sc : (int)rel2);
-            uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
-            if (rel1 - 1 >= 0 && rel1 - 1 < Sc) valid &= ~(1u << (rel1 - 1));
-            if (rel2 - 1 >= 0 && rel2 - 1 < Sc) valid &= ~(1u << (rel2 - 1));
+            const int32_t rlo = (int32_t)(gb - lp), rhi = (int32_t)(ge - lp);   // |.| < 2^31: groups are
+            const int jlo = rlo <= 0 ? 0 : (rlo >= 16 ? 16 : rlo);                // capped at 2^31 bytes
+            const int jhi = rhi <= 0 ? 0 : (rhi >= 16 ? 16 : rhi);
+            const uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
+            const uint32_t rel = (uint32_t)(lp - gb);   // group-relative byte of this lane's position 0
             if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
                 uint32_t hb = 0;
 #pragma unroll
@@ -118,34 +133,40 @@ __global__ __launch_bounds__(FS_BLOCK) void kw_filter_kernel(FastTables FT, cons
                     const uint32_t x = (W[k] >> 7) & 0x01010101u;
                     hb |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
                 }
-                const int j1 = rel1 <= 0 ? 0 : (rel1 >= Sc ? Sc : (int)rel1);
-                const uint32_t in0 = ((1u << j1) - 1u) & ~((1u << jlo) - 1u);
-                const uint32_t in1 = (jhi > j1) ? (((1u << jhi) - 1u) & ~((1u << j1) - 1u)) : 0u;
-                if (hb & in0) na0 = true;
-                if (hb & in1) na1 = true;
+                hb &= valid;
+                while (hb) {   // one atomic per (document, field) the lane's non-ASCII bytes fall in
+                    const uint32_t r = rel + (uint32_t)(__ffs(hb) - 1);
+                    const uint32_t k = fg_doc(dstart, (uint32_t)nd, r);
+                    const uint32_t tb = dtitle[k];
+                    const bool title = r >= tb;
+                    atomicOr(&S.dflags[d0 + k], title ? DH_NA1 : DH_NA0);
+                    const uint32_t fend = title ? dstart[k + 1] : tb;   // group-relative end of that field
+                    const int64_t skip = (int64_t)fend - (lp - gb);
+                    hb &= skip >= 16 ? 0u : ~((1u << (uint32_t)skip) - 1u);
+                }
             }
             uint32_t hit = 0, gate = 0;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                if (g >= ng) break;
-                uint32_t fw[4], bw[4];
+            for (int q = 0; q < 4; ++q) {
+                uint32_t fw[4], bw[4], bm[4];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
-                    const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
+                    const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
                     fw[jj] = filt[fk_word(key)];
-                    bw[jj] = gate_on ? b2[fk_b2_index(key) >> 5] : 0u;
+                    bm[jj] = fk_b2_mul(key);
+                    bw[jj] = b2[(bm[jj] >> 5) & (FK_B2_WORDS - 1)];
                 }
                 if (FK_SCHED) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
-                    const int j = 4 * g + jj;
-                    const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
+                    const int j = 4 * q + jj;
+                    const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
                     hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit(key), 1) << j;
-                    gate |= __builtin_amdgcn_ubfe(bw[jj], fk_b2_index(key), 1) << j;
+                    gate |= __builtin_amdgcn_ubfe(bw[jj], bm[jj], 1) << j;
                 }
             }
-            gate &= valid;
             hit &= valid;
+            gate &= valid;
             ncand += (uint32_t)__popc(hit);
             uint32_t m4 = 0, m3 = 0;
             {
@@ -154,43 +175,70 @@ __global__ __launch_bounds__(FS_BLOCK) void kw_filter_kernel(FastTables FT, cons
                     const int j = __ffs(hm) - 1;
                     hm &= hm - 1;
                     const uint32_t key = fk_key_at(W, j);
-                    const int32_t pr = lrel + j;
-                    const int32_t fer = pr < dl1 ? dl1 : dl2;
-                    if (pr + 4 <= fer && lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
+                    if (lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
                     if (has_t3 && lds_bit(t3, fk_t3_index(key))) m3 |= 1u << j;
                 }
             }
             const uint32_t cm = m4 | m3 | gate;
             int total;
             const int ex = wave_excl_scan(__popc(cm), &total);
-            if (total == 0) continue;
+            if (total == 0) return;
             ncand2 += (lane == 0) ? (uint32_t)total : 0u;
-            uint32_t k = ccur + (uint32_t)ex;
+            uint32_t kk = ccur + (uint32_t)ex;
             uint32_t mm = cm;
             while (mm) {
                 const int j = __ffs(mm) - 1;
                 mm &= mm - 1;
+                const uint32_t r = rel + (uint32_t)j;
+                const uint32_t k = fg_doc(dstart, (uint32_t)nd, r);
                 const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
-                if (k < ccap) cand[k] = make_uint4((uint32_t)d, ((uint32_t)(lrel + j) << 3) | fl, fk_key_at(W, j), 0u);
-                ++k;
+                if (kk < ccap)
+                    cand[kk] = make_uint4((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl, fk_key_at(W, j), 0u);
+                ++kk;
             }
             ccur += (uint32_t)total;
-        }
-        uint32_t flags = 0;
-        if (__ballot(na0)) flags |= DH_NA0;
-        if (__ballot(na1)) flags |= DH_NA1;
-        const uint64_t em = __ballot((ebits >> ebit) & 1u);
-        if (em & 3ull) flags |= DH_EDGE0;
-        if (em & 12ull) flags |= DH_EDGE1;
-        if (defer) flags |= DH_DEFER;
-        if (lane == 0) {
-            S.hdr[d] = make_uint2(0u, flags);
-            S.ncnt[d] = make_uint2(0u, 0u);
+        };
+        uint4 v0, v1, v2;
+        uint32_t w0, w1, w2;
+        load(v0, w0, blk);
+        load(v1, w1, blk + 1024);
+        load(v2, w2, blk + 2048);
+        for (;;) {
+            if (blk >= ge) break;
+            tile(v0, w0, blk);
+            load(v0, w0, blk + 3072);
+            blk += 1024;
+            if (blk >= ge) break;
+            tile(v1, w1, blk);
+            load(v1, w1, blk + 3072);
+            blk += 1024;
+            if (blk >= ge) break;
+            tile(v2, w2, blk);
+            load(v2, w2, blk + 3072);
+            blk += 1024;
         }
     }
+}
+
+__global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+                                                             const int64_t *__restrict__ off, int64_t n_docs,
+                                                             FastScratch S)
+{
+    __shared__ FilterLds L;
+    for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FS_BLOCK) L.filt[i] = FT.filt[i];
+    for (int i = threadIdx.x; i < FK_L2_WORDS; i += FS_BLOCK) L.l2[i] = FT.l2[i];
+    for (int i = threadIdx.x; i < FK_T3_WORDS; i += FS_BLOCK) L.t3[i] = FT.t3[i];
+    for (int i = threadIdx.x; i < FK_B2_WORDS; i += FS_BLOCK) L.b2[i] = FT.b2[i];
+    __syncthreads();
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t wave = (int64_t)blockIdx.x * FS_WAVES + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * FS_WAVES;
+    uint32_t ncand = 0, ncand2 = 0, ccur = 0;
+    fk_filter_groups(FT, L, arena, off, n_docs, S, wave, n_waves, wib, ncand, ncand2, ccur);
     if (lane == 0) {
         S.ccnt[wave] = ccur;
-        if (ccur > ccap) {
+        if (ccur > S.cand_cap) {
             atomicOr(&S.status[0], ST_CAND_OVERFLOW);
             atomicMax(&S.cmax[0], ccur);
         }
@@ -227,12 +275,14 @@ __global__ __launch_bounds__(PK_BLOCK) void kw_probe_kernel(FastTables FT, DevTa
     uint32_t nanchor = 0;
     scnt[lane] = 0;
     for (uint32_t c0 = 0; c0 < nc; c0 += WAVE) {
-        const bool valid = c0 + (uint32_t)lane < nc;
-        const uint4 e = valid ? cand[c0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+        const bool inr = c0 + (uint32_t)lane < nc;
+        const uint4 e = inr ? cand[c0 + lane] : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t doc = e.x;
-        const int64_t t0 = valid ? off[2 * (int64_t)doc] : 0;
-        const int64_t t1 = valid ? off[2 * (int64_t)doc + 1] : 0;
-        const int64_t t2 = valid ? off[2 * (int64_t)doc + 2] : 0;
+        const int64_t t0 = inr ? off[2 * (int64_t)doc] : 0;
+        const int64_t t1 = inr ? off[2 * (int64_t)doc + 1] : 0;
+        const int64_t t2 = inr ? off[2 * (int64_t)doc + 2] : 0;
+        // fields beyond MAX_FIELD_BYTES (item positions are 23-bit) are the generic kernel's
+        const bool valid = inr && t1 - t0 <= MAX_FIELD_BYTES && t2 - t1 <= MAX_FIELD_BYTES;
         const int32_t l1 = (int32_t)(t1 - t0), l2 = (int32_t)(t2 - t0);
         const int32_t pr = (int32_t)(e.y >> 3);
         const int f = pr < l1 ? 0 : 1;
@@ -382,7 +432,7 @@ __global__ __launch_bounds__(PK_BLOCK) void kw_probe_kernel(FastTables FT, DevTa
             }
             last_doc = (uint32_t)__shfl((int)doc, 63 - __builtin_clzll(withm), WAVE);
         }
-        if (ovf) atomicOr(&S.hdr[doc].y, DH_DEFER);
+        if (ovf) atomicOr(&S.dflags[doc], DH_DEFER);
         icur += (uint32_t)itotal;
         scnt[lane] = 0;
         wave_sync();
@@ -416,9 +466,10 @@ __global__ __launch_bounds__(EK_BLOCK) void kw_epi_kernel(FastTables FT, const u
     O.n = 0;
     TaskCounts TC = {0u, 0u, 0u, 0u};
     for (int64_t d = wave; d < n_docs; d += n_waves) {
-        // lanes 0..2: offsets, lane 3: header, lane 4: item counts
+        // lanes 0..2: offsets, lane 3: header, lane 4: item counts, lane 5: flags (y)
         const int64_t ov = lane < 3 ? off[2 * d + lane] : 0;
-        const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : make_uint2(0u, 0u));
+        const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) :
+                                                                        make_uint2(0u, 0u)));
         FastDoc D;
         D.arena = arena;
         D.t0 = rdlane64(ov, 0);
@@ -428,10 +479,25 @@ __global__ __launch_bounds__(EK_BLOCK) void kw_epi_kernel(FastTables FT, const u
         D.l1 = (int32_t)(D.t1 - D.t0);
         D.l2 = (int32_t)(D.t2 - D.t0);
         const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
-        uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 3);
+        uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5);
         const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
         const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
-        bool defer = (flags & DH_DEFER) != 0;
+        // edge prefilter: first / last eight bytes of each field (lanes 0..3) against the global bitmaps
+        {
+            const int f = lane >> 1;
+            const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+            bool e = false;
+            if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+                const int64_t a = (lane & 1) ? fe - 8 : fb;
+                const uint64_t k = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
+                const uint32_t idx = fk_edge_index(k);
+                e = (((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u;
+            }
+            const uint64_t em = __ballot(e);
+            if (em & 3ull) flags |= DH_EDGE0;
+            if (em & 12ull) flags |= DH_EDGE1;
+        }
+        bool defer = (flags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
         if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) { defer = true; ++ndef_items; }
         flags &= ~DH_DEFER;
         bool done = false;
