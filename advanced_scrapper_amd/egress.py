@@ -69,9 +69,9 @@ def append_rows(path: str, columns: Sequence[str], rows: Iterable[Sequence]) -> 
     with open(path, 'a', newline='', encoding='utf-8') as fh:
         w = csv.writer(fh, lineterminator=os.linesep, delimiter=',', quotechar='"',
                        quoting=csv.QUOTE_MINIMAL, doublequote=True, escapechar=None)
-        head = _join(list(columns)) if header else None
+        head = _join(list(columns)) if header and _FAST_OK else None
         for values in rows:
-            line = _line(values)
+            line = _line(values) if _FAST_OK else None
             if line is None or (header and head is None):
                 if lines:
                     fh.write(''.join(lines))
@@ -122,6 +122,22 @@ def _line(values: Sequence):
 _NL_ONLY = os.linesep == '\n'
 
 
+def _fast_path_agrees() -> bool:
+    """True iff ``_line`` / ``_join`` write what this interpreter's ``csv`` writer writes (the QUOTE_MINIMAL
+    rule they hard-code is CPython 3.10's) on probe rows: CR-only, LF, CRLF, tab, quotes, commas, empty
+    cells, a lone empty cell, non-ASCII.  When they disagree every row goes through the writer."""
+    probes = [('a', 'b'), ('cr\ronly', 'x'), ('lf\nx', 'y'), ('crlf\r\n', 'z'), ('t\tab', ''), ('say "hi"', 'q'),
+              ('x,y', 'c'), ('', ''), ('',), (' lead', 'trail '), ('é中', '\x1c'), (1, 'int')]
+    for row in probes:
+        buf = io.StringIO()
+        csv.writer(buf, lineterminator=os.linesep, delimiter=',', quotechar='"', quoting=csv.QUOTE_MINIMAL,
+                   doublequote=True, escapechar=None).writerow([_cell(v) for v in row])
+        if _line(row) != buf.getvalue() or _join([_cell(v) for v in row]) != buf.getvalue():
+            return False
+    return True
+
+
+
 def _join(cells: Sequence[str]):
     """One CSV line as the ``csv`` writer above writes it (QUOTE_MINIMAL), or ``None`` for a cell it
     rejects (a NUL character: that row goes through the writer itself, which raises as pandas does).
@@ -143,3 +159,6 @@ def _join(cells: Sequence[str]):
     if len(out) == 1 and out[0] == '':
         out[0] = '""'
     return ','.join(out) + _LINESEP
+
+
+_FAST_OK = _fast_path_agrees()

@@ -39,7 +39,7 @@ def _parse():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--docs-per-gpu', type=int, default=1_000_000)
     ap.add_argument('--seed', type=int, default=20250905)
-    ap.add_argument('--cpu-sample', type=int, default=3000,
+    ap.add_argument('--cpu-sample', type=int, default=10000,
                     help='docs of the same corpus timed on the CPU port of the reference loop (0 = skip)')
     ap.add_argument('--cpu-procs', type=int, default=0,
                     help='CPU port processes (0 = the host share: min(16, os.cpu_count()))')

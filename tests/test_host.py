@@ -438,3 +438,16 @@ def test_dropin_error_paths_write_reference_partial_output(golden, tmp_path, mon
     got = {fn: open(os.path.join('yahoo_ticker_matched_articles', fn), encoding='utf-8').read()
            for fn in os.listdir('yahoo_ticker_matched_articles')}
     assert got == c['files']
+
+
+def test_egress_fast_path_probe(monkeypatch, tmp_path):
+    """The fast CSV line writer is checked against the interpreter's csv writer at import; with the check
+    failing, append_rows still writes the writer's bytes (every row through csv.writer)."""
+    from advanced_scrapper_amd import egress
+    assert egress._FAST_OK
+    rows = [('a\rb', 1, 'x,y'), ('', 'q"t', 'é')]
+    p1, p2 = tmp_path / 'a.csv', tmp_path / 'b.csv'
+    egress.append_rows(str(p1), ('c1', 'c2', 'c3'), rows)
+    monkeypatch.setattr(egress, '_FAST_OK', False)
+    egress.append_rows(str(p2), ('c1', 'c2', 'c3'), rows)
+    assert p1.read_bytes() == p2.read_bytes()
