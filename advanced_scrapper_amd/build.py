@@ -92,8 +92,18 @@ def build_kwrows(force: bool = False) -> str:
     return out
 
 
+def build_kwcsv(force: bool = False) -> str:
+    """``lib/libkwcsv.so``: host C CSV tokenizer of the article ingest and the output sort (csrc/kwcsv.c)."""
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, 'libkwcsv.so')
+    src = os.path.join(CSRC, 'kwcsv.c')
+    if force or _stale(out, [src]):
+        _run(['gcc', '-O2', '-fPIC', '-shared', '-Wall', '-o', out, src])
+    return out
+
+
 def build_all(force: bool = False):
-    return build_kwmatch(force), build_synth(force), build_kwrows(force)
+    return build_kwmatch(force), build_synth(force), build_kwrows(force), build_kwcsv(force)
 
 
 if __name__ == '__main__':

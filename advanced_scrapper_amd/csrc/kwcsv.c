@@ -1,0 +1,191 @@
+/*
+ * kwcsv.c -- host-side CSV tokenizer for the article ingest and the output sort (libkwcsv.so).
+ *
+ * The reference reads the article CSV with pandas' C parser in 20 000-row chunks
+ * (match_keywords.py:230) and later re-reads every per-ticker output file to sort it
+ * (:195-217).  This tokenizer reproduces the parser's default dialect for both: ',' delimiter,
+ * '"' quoting with doubled quotes, "\n", "\r\n" and lone "\r" record ends, blank lines skipped,
+ * and the default NA strings (pandas' STR_NA_VALUES, passed in by the caller) -- quoted or not --
+ * mark a cell as NaN.  It does not guess dtypes: every cell carries a flag telling whether it is a
+ * witness that its column stays text (a character no number or bool literal holds); the caller
+ * hands a chunk back to pandas when a needed column has no witness, and on any record it cannot
+ * tokenize exactly (a field count different from the header's, a character after a closing quote),
+ * so the fast path is only taken where its result equals pandas'.
+ *
+ * kwcsv_parse   records -> unescaped cell bytes + offsets + flags
+ * kwcsv_pack    the text / title cells of parsed records -> the matcher's byte arena (NaN -> "nan",
+ *               match_keywords.py:150-151) and its 2n+1 offsets
+ * kwcsv_utf8_ok validity of UTF-8 cells (pandas raises UnicodeDecodeError on the others)
+ */
+#include <stdint.h>
+#include <string.h>
+
+#define KWCSV_QUOTED 1u   /* the cell was quoted */
+#define KWCSV_NA 2u       /* the cell is one of the NA strings: NaN */
+#define KWCSV_TEXT 4u     /* the cell proves its column is text (see kwcsv_text_witness) */
+
+static int is_na(const uint8_t *s, int64_t n, const uint8_t *na, const int32_t *na_off, int32_t n_na)
+{
+    for (int32_t k = 0; k < n_na; ++k) {
+        const int32_t a = na_off[k], b = na_off[k + 1];
+        if (b - a == n && memcmp(na + a, s, (size_t)n) == 0) return 1;
+    }
+    return 0;
+}
+
+static int ieq(const uint8_t *s, int64_t n, const char *lit)
+{
+    const int64_t m = (int64_t)strlen(lit);
+    if (m != n) return 0;
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t c = s[i];
+        if (c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+        if (c != (uint8_t)lit[i]) return 0;
+    }
+    return 1;
+}
+
+/* A non-NA cell that neither a number (ints, floats with '.', exponent, sign, surrounding blanks,
+ * inf / infinity) nor a bool literal can be: its column keeps dtype object in pandas' inference. */
+static int kwcsv_text_witness(const uint8_t *s, int64_t n)
+{
+    int64_t a = 0, b = n;
+    while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+    while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t')) --b;
+    if (a == b) return 1;   /* blanks only: no number */
+    const uint8_t *t = s + a;
+    const int64_t m = b - a;
+    if (ieq(t, m, "true") || ieq(t, m, "false")) return 0;
+    int64_t i = (t[0] == '+' || t[0] == '-') ? 1 : 0;
+    if (ieq(t + i, m - i, "inf") || ieq(t + i, m - i, "infinity")) return 0;
+    for (int64_t k = 0; k < m; ++k) {
+        const uint8_t c = t[k];
+        if (!((c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.' || c == 'e' || c == 'E')) return 1;
+    }
+    return 0;
+}
+
+/*
+ * Parse up to max_rows records of buf[pos, len) with ncols fields each.  Cell bytes (quotes removed,
+ * doubled quotes undone) go to out (cap bytes); cell i of record r spans out[coff[r*ncols+i],
+ * coff[r*ncols+i+1]); cfl gets its KWCSV_* flags.  *pos_out = the position after the last record.
+ * Returns the records parsed (0 at the end of the input), -1 if out is too small, -2 for a record
+ * this tokenizer does not reproduce exactly (the caller falls back to pandas), -3 for a record whose
+ * field count differs from ncols.
+ */
+int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_rows, int32_t ncols,
+                    const uint8_t *na, const int32_t *na_off, int32_t n_na, uint8_t *out, int64_t cap,
+                    int64_t *coff, uint8_t *cfl, int64_t *pos_out)
+{
+    int64_t p = pos, o = 0, rows = 0;
+    coff[0] = 0;
+    while (rows < max_rows) {
+        /* blank lines -- empty or blanks only -- are skipped, as pandas' skip_blank_lines does */
+        for (;;) {
+            int64_t k = p;
+            while (k < len && (buf[k] == ' ' || buf[k] == '\t')) ++k;
+            if (k < len && (buf[k] == '\n' || buf[k] == '\r')) { p = k + 1; continue; }
+            if (k >= len) p = k;
+            break;
+        }
+        if (p >= len) break;
+        int32_t f = 0;
+        for (;;) {
+            const int64_t cell0 = o;
+            uint8_t flags = 0;
+            if (p < len && buf[p] == '"') {
+                flags |= KWCSV_QUOTED;
+                ++p;
+                for (;;) {
+                    const uint8_t *q = p < len ? (const uint8_t *)memchr(buf + p, '"', (size_t)(len - p)) : NULL;
+                    if (!q) return -2;   /* unterminated quote */
+                    const int64_t k = (int64_t)(q - buf);
+                    if (o + (k - p) + 1 > cap) return -1;
+                    memcpy(out + o, buf + p, (size_t)(k - p));
+                    o += k - p;
+                    p = k + 1;
+                    if (p < len && buf[p] == '"') { out[o++] = '"'; ++p; continue; }
+                    break;
+                }
+                if (p < len && buf[p] != ',' && buf[p] != '\n' && buf[p] != '\r') return -2;
+            } else {
+                int64_t k = p;
+                while (k < len && buf[k] != ',' && buf[k] != '\n' && buf[k] != '\r') ++k;
+                if (o + (k - p) > cap) return -1;
+                memcpy(out + o, buf + p, (size_t)(k - p));
+                o += k - p;
+                p = k;
+            }
+            if (f >= ncols) return -3;
+            if (is_na(out + cell0, o - cell0, na, na_off, n_na)) flags |= KWCSV_NA;
+            else if (kwcsv_text_witness(out + cell0, o - cell0)) flags |= KWCSV_TEXT;
+            cfl[rows * ncols + f] = flags;
+            coff[rows * ncols + f + 1] = o;
+            ++f;
+            if (p < len && buf[p] == ',') { ++p; continue; }
+            /* record end: "\n", "\r\n", "\r" or the end of the input */
+            if (p < len && buf[p] == '\r') ++p;
+            if (p < len && buf[p] == '\n' && buf[p - 1] != '\n') ++p;
+            break;
+        }
+        if (f != ncols) return -3;
+        ++rows;
+    }
+    *pos_out = p;
+    return rows;
+}
+
+/* Every cell of column `col` of rows [0, nrows) is valid UTF-8 (or NA).  Returns 1 / 0. */
+int32_t kwcsv_utf8_ok(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, int64_t nrows, int32_t ncols,
+                      int32_t col)
+{
+    for (int64_t r = 0; r < nrows; ++r) {
+        const int64_t c = r * ncols + col;
+        if (cfl[c] & KWCSV_NA) continue;
+        const uint8_t *s = out + coff[c];
+        const int64_t n = coff[c + 1] - coff[c];
+        for (int64_t i = 0; i < n;) {
+            const uint8_t b = s[i];
+            int64_t k;
+            uint32_t cp;
+            if (b < 0x80) { ++i; continue; }
+            if (b >= 0xC2 && b <= 0xDF) { k = 1; cp = b & 0x1F; }
+            else if (b >= 0xE0 && b <= 0xEF) { k = 2; cp = b & 0x0F; }
+            else if (b >= 0xF0 && b <= 0xF4) { k = 3; cp = b & 0x07; }
+            else return 0;
+            for (int64_t j = 1; j <= k; ++j) {
+                if (i + j >= n || (s[i + j] & 0xC0) != 0x80) return 0;
+                cp = (cp << 6) | (s[i + j] & 0x3F);
+            }
+            if ((k == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (k == 3 && (cp < 0x10000 || cp > 0x10FFFF)))
+                return 0;
+            i += k + 1;
+        }
+    }
+    return 1;
+}
+
+/*
+ * The matcher's arena for parsed rows: document r = text cell then title cell (column ct, ci); an NA
+ * cell is "nan" (str(NaN), match_keywords.py:150-151).  off gets 2*nrows+1 offsets.  Returns the
+ * arena bytes, or -1 if cap is too small.
+ */
+int64_t kwcsv_pack(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, int64_t nrows, int32_t ncols,
+                   int32_t ct, int32_t ci, uint8_t *arena, int64_t cap, int64_t *off)
+{
+    int64_t a = 0;
+    off[0] = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+        for (int k = 0; k < 2; ++k) {
+            const int64_t c = r * ncols + (k ? ci : ct);
+            const uint8_t *s = out + coff[c];
+            int64_t n = coff[c + 1] - coff[c];
+            if (cfl[c] & KWCSV_NA) { s = (const uint8_t *)"nan"; n = 3; }
+            if (a + n > cap) return -1;
+            memcpy(arena + a, s, (size_t)n);
+            a += n;
+            off[2 * r + k + 1] = a;
+        }
+    }
+    return a;
+}

@@ -93,6 +93,8 @@ struct kw_handle {
     int filter_blocks_per_cu = 1, probe_blocks_per_cu = 1, epi_blocks_per_cu = 1;
     int ns = 0;                        // filter regions of the last launch
     hipEvent_t evf = nullptr, evp = nullptr;   // after the filter / probe kernels
+    hipStream_t side = nullptr;                // the resolve kernel's stream (beside epilogue + tasks)
+    hipEvent_t evs0 = nullptr, evs1 = nullptr, evt = nullptr;   // resolve start / end (side), tasks end
     int n_anchor_fast = 0;
     unsigned long long fstats[16] = {0};
     hipEvent_t evr = nullptr, evg = nullptr;
@@ -924,6 +926,10 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     bpc = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_epi_kernel, EK_BLOCK, 0));
     h->epi_blocks_per_cu = bpc > 0 ? bpc : 1;
+    HIPCHK(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreate(&h->evs0));
+    HIPCHK(h, hipEventCreate(&h->evs1));
+    HIPCHK(h, hipEventCreate(&h->evt));
     HIPCHK(h, hipEventCreate(&h->evf));
     HIPCHK(h, hipEventCreate(&h->evp));
     HIPCHK(h, hipEventCreate(&h->ev0));
@@ -1099,6 +1105,16 @@ static int launch_scan(kw_handle *h)
         hipLaunchKernelGGL(kw_probe_kernel, dim3((n_regions + PK_WAVES - 1) / PK_WAVES), dim3(PK_BLOCK), 0, st, h->FT,
                            h->T, h->arena, h->doc_off, n_regions, h->FS);
     HIPCHK(h, hipEventRecord(h->evp, st));
+    // the documents with a non-ASCII field: the resolve kernel on the side stream, beside the epilogue and
+    // the task kernels (disjoint documents, disjoint result regions); joined before the generic kernel
+    HIPCHK(h, hipStreamWaitEvent(h->side, h->evp, 0));
+    HIPCHK(h, hipEventRecord(h->evs0, h->side));
+    if (n_docs > 0) {
+        hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, h->side, h->FT, h->T, h->arena, h->doc_off,
+                           n_docs, h->FS, h->S);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->evs1, h->side));
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
                            h->FS, h->S);
@@ -1107,8 +1123,8 @@ static int launch_scan(kw_handle *h)
     h->ns = n_regions;
     HIPCHK(h, hipEventRecord(h->ev1, st));
     if (n_docs > 0) {
-        // flat resolve tasks: verify -> edge -> short -> regex (regex decisions of the first three queue up);
-        // G[k] waves share each scan wave's task region
+        // flat resolve tasks: verify -> short -> regex (regex decisions of the first two queue up);
+        // G[k] waves share each epilogue wave's task region
         int G[4] = {4, 4, 8, 4};   // measured on MI355X (1M docs): 12.10 ms vs 12.31 ms for {1, 4, 4, 1}
         if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
         auto task = [&](auto kern, int g) {
@@ -1121,10 +1137,9 @@ static int launch_scan(kw_handle *h)
         task(kw_short_kernel, G[2]);
         task(kw_rx_task_kernel, G[3]);
         HIPCHK(h, hipGetLastError());
-        hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
-                           n_docs, h->FS, h->S);
-        HIPCHK(h, hipGetLastError());
     }
+    HIPCHK(h, hipEventRecord(h->evt, st));
+    HIPCHK(h, hipStreamWaitEvent(st, h->evs1, 0));
     HIPCHK(h, hipEventRecord(h->evr, st));
     if (n_docs > 0) {
         // the generic kernel redoes every document the fast path deferred
@@ -1292,6 +1307,8 @@ extern "C" int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n)
     if (n > 4) HIPCHK(h, hipEventElapsedTime(&ms[4], h->ev0, h->ev2));
     hipEvent_t sp[4] = {h->ev0, h->evf, h->evp, h->ev1};
     for (int i = 0; i + 5 < n && i < 3; ++i) HIPCHK(h, hipEventElapsedTime(&ms[5 + i], sp[i], sp[i + 1]));
+    if (n > 8) HIPCHK(h, hipEventElapsedTime(&ms[8], h->evs0, h->evs1));
+    if (n > 9) HIPCHK(h, hipEventElapsedTime(&ms[9], h->ev1, h->evt));
     return KW_OK;
 }
 
@@ -1331,6 +1348,10 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->evg) (void)hipEventDestroy(h->evg);
     if (h->evr) (void)hipEventDestroy(h->evr);
     if (h->evf) (void)hipEventDestroy(h->evf);
+    if (h->evs0) (void)hipEventDestroy(h->evs0);
+    if (h->evs1) (void)hipEventDestroy(h->evs1);
+    if (h->evt) (void)hipEventDestroy(h->evt);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->evp) (void)hipEventDestroy(h->evp);
     delete h;
     return KW_OK;

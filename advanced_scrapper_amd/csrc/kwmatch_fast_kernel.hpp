@@ -2341,9 +2341,49 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     FK_T0(tall0);
 
     for (int64_t c0 = wave * WAVE; c0 < n_docs; c0 += n_waves * WAVE) {
+        // lane = document: this kernel owns the documents with a non-ASCII field (the epilogue kernel the
+        // others); it runs beside the epilogue and task kernels, right after the probe
         const int64_t dl = c0 + lane;
         uint2 hl = make_uint2(0u, 0u);
-        if (dl < n_docs) hl = S.hdr[dl];
+        bool dfr = false, dfr_items = false;
+        {
+            const uint32_t fl = dl < n_docs ? S.dflags[dl] : 0u;
+            if (fl & (DH_NA0 | DH_NA1)) {
+                const uint2 nc = S.ncnt[dl];
+                const uint32_t ibeg = S.hdr[dl].x;
+                const int64_t t0 = off[2 * dl], t1 = off[2 * dl + 1], t2 = off[2 * dl + 2];
+                uint32_t flags = fl & (DH_NA0 | DH_NA1);
+                // edge prefilter: the first / last eight bytes of each field against the global bitmaps
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int f = k >> 1;
+                    const int64_t fb = f ? t1 : t0, fe = f ? t2 : t1;
+                    if (fe - fb < (int64_t)EDGE_MIN_M + 1) continue;
+                    const int64_t a = (k & 1) ? fe - 8 : fb;
+                    const uint64_t key8 = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
+                    const uint32_t idx = fk_edge_index(key8);
+                    if ((((k & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u) flags |= f ? DH_EDGE1 : DH_EDGE0;
+                }
+                const bool defer = (fl & DH_DEFER) || t1 - t0 > MAX_FIELD_BYTES || t2 - t1 > MAX_FIELD_BYTES ||
+                                   nc.x > (uint32_t)FK_ITEMS0 || nc.y > (uint32_t)FK_ITEMS1;
+                const int64_t l0 = t1 - t0, l1 = t2 - t1;
+                const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
+                const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
+                const bool need = (nc.x + nc.y) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
+                hl.x = ibeg;
+                hl.y = defer ? (DH_DEFER | flags) : (nc.x | (nc.y << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u));
+                S.hdr[dl] = hl;
+                if (defer) {
+                    const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                    if (i < S.defer_cap) S.defer_list[i] = (uint32_t)dl;
+                    else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+                }
+                dfr = defer;
+                dfr_items = defer && (nc.x > (uint32_t)FK_ITEMS0 || nc.y > (uint32_t)FK_ITEMS1);
+            }
+        }
+        ndefer += (unsigned long long)__popcll(__ballot(dfr));
+        ndef_items += (unsigned long long)__popcll(__ballot(dfr_items));
         uint64_t todo = __ballot((hl.y & DH_NEED) != 0 && (hl.y & DH_DEFER) == 0);
         while (todo) {
             const int l = __builtin_ctzll(todo);

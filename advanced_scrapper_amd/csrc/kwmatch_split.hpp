@@ -480,6 +480,7 @@ __global__ __launch_bounds__(EK_BLOCK) void kw_epi_kernel(FastTables FT, const u
         D.l2 = (int32_t)(D.t2 - D.t0);
         const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
         uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5);
+        if (flags & (DH_NA0 | DH_NA1)) continue;   // the resolve kernel's document
         const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
         const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
         // edge prefilter: first / last eight bytes of each field (lanes 0..3) against the global bitmaps
@@ -519,15 +520,8 @@ __global__ __launch_bounds__(EK_BLOCK) void kw_epi_kernel(FastTables FT, const u
                 if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
                 else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
             }
-        } else if (done) {
-            h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
         } else {
-            // non-ASCII: the resolve kernel works on the document (items, an edge candidate, or a short field)
-            const int64_t l0 = D.t1 - D.t0, l1 = D.t2 - D.t1;
-            const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
-            const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
-            const bool need = (n0 + n1) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
-            h.y = n0 | (n1 << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u);
+            h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
         }
         if (lane == 0) S.hdr[d] = h;
         wave_sync();

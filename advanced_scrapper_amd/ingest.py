@@ -1,0 +1,207 @@
+"""Article ingest without pandas on the hot path (reference match_keywords.py:230, :150-152).
+
+``read_chunks(path, chunksize)`` yields the article CSV in ``chunksize``-row chunks, like
+``pd.read_csv(path, chunksize=...)``.  Each chunk is tokenized by the C tokenizer (csrc/kwcsv.c,
+``lib/libkwcsv.so``) into unescaped cell bytes, offsets and per-cell flags; the matcher's byte arena
+(text then title of every row, NaN -> ``"nan"``) is packed in C straight from the cells, and the host
+only decodes the cells it needs as Python ``str`` (dates of every row, the output cells of matched
+rows).  A chunk comes back as a :class:`NativeChunk` when the tokenizer's result provably equals
+pandas' for the six columns the path reads -- every record has the header's field count, no
+malformed quoting, valid UTF-8, and each needed column holds a cell that keeps it dtype ``object``
+(pandas infers dtypes per chunk) -- and otherwise as the ``pandas.DataFrame`` pandas itself parses
+from the same bytes, so every consumer sees pandas' values.
+"""
+from __future__ import annotations
+
+import ctypes
+import io
+import math
+import os
+from typing import Iterator, List, Optional, Sequence, Union
+
+import numpy as np
+import pandas as pd
+
+NEEDED = ('article_text', 'title', 'date_time', 'url', 'source', 'source_url')
+QUOTED, NA, TEXT = 1, 2, 4
+
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib', 'libkwcsv.so')
+        if not os.path.exists(path):
+            raise RuntimeError(f'{path} is missing: run __graft_entry__.build()')
+        L = ctypes.CDLL(path)
+        P, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.kwcsv_parse.restype = i64
+        L.kwcsv_parse.argtypes = [P, i64, i64, i64, i32, P, P, i32, P, i64, P, P, P]
+        L.kwcsv_pack.restype = i64
+        L.kwcsv_pack.argtypes = [P, P, P, i64, i32, i32, i32, P, i64, P]
+        L.kwcsv_utf8_ok.restype = i32
+        L.kwcsv_utf8_ok.argtypes = [P, P, P, i64, i32, i32]
+        _LIB = L
+    return _LIB
+
+
+def _na_table():
+    """pandas' own default NA strings (the parser's STR_NA_VALUES) as one byte buffer + offsets."""
+    from pandas._libs.parsers import STR_NA_VALUES
+    vals = sorted(v.encode('utf-8') for v in STR_NA_VALUES)
+    off = np.zeros(len(vals) + 1, dtype=np.int32)
+    off[1:] = np.cumsum([len(v) for v in vals])
+    return np.frombuffer(b''.join(vals) or b'\0', dtype=np.uint8).copy(), off, len(vals)
+
+
+def _p(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Cells:
+    """Tokenized records of one chunk: cell c of row r is ``buf[off[r*ncols+c]:off[r*ncols+c+1]]``."""
+
+    def __init__(self, buf: np.ndarray, off: np.ndarray, flags: np.ndarray, nrows: int, ncols: int):
+        self.buf, self.off, self.flags, self.nrows, self.ncols = buf, off, flags, nrows, ncols
+        self._mv = memoryview(buf)
+
+    def value(self, r: int, c: int):
+        """The cell as pandas gives it in an object column: ``str``, or NaN for an NA string."""
+        k = r * self.ncols + c
+        if self.flags[k] & NA:
+            return math.nan
+        return bytes(self._mv[self.off[k]:self.off[k + 1]]).decode('utf-8')
+
+    def column(self, c: int) -> List:
+        off = self.off.tolist()
+        fl = self.flags.tolist()
+        mv, n = self._mv, self.ncols
+        out = []
+        for r in range(self.nrows):
+            k = r * n + c
+            out.append(math.nan if fl[k] & NA else bytes(mv[off[k]:off[k + 1]]).decode('utf-8'))
+        return out
+
+
+class NativeChunk:
+    """One chunk read by the native tokenizer (the columns the path reads, decoded on demand)."""
+
+    def __init__(self, cells: Cells, columns: Sequence[str], index0: int):
+        self.cells = cells
+        self.columns = list(columns)
+        self.col = {c: i for i, c in enumerate(self.columns)}
+        self.index0 = index0          # row number of the chunk's first row in the file (pandas' index)
+        self._cache = {}
+
+    def __len__(self):
+        return self.cells.nrows
+
+    def column_list(self, name: str) -> List:
+        v = self._cache.get(name)
+        if v is None:
+            v = self._cache[name] = self.cells.column(self.col[name])
+        return v
+
+    def value(self, r: int, name: str):
+        v = self._cache.get(name)
+        return v[r] if v is not None else self.cells.value(r, self.col[name])
+
+    def arena(self, pad: int = 64):
+        """The matcher's arena and 2n+1 offsets (text, title per row; NaN -> "nan")."""
+        c = self.cells
+        n = c.nrows
+        cap = int(c.off[-1]) + 3 * 2 * n + pad
+        arena = np.zeros(cap, dtype=np.uint8)
+        off = np.zeros(2 * n + 1, dtype=np.int64)
+        got = _lib().kwcsv_pack(_p(c.buf), _p(c.off), _p(c.flags), n, c.ncols, self.col['article_text'],
+                                self.col['title'], _p(arena), cap - pad, _p(off))
+        if got < 0:
+            raise RuntimeError('kwcsv_pack: arena too small')
+        return arena[:got + pad], off
+
+    def frame(self) -> pd.DataFrame:
+        """The chunk as pandas would give it (object columns; for the drop-in process_chunk API)."""
+        data = {name: self.column_list(name) for name in self.columns}
+        return pd.DataFrame(data, index=pd.RangeIndex(self.index0, self.index0 + len(self)))
+
+
+def _split_header(buf: bytes):
+    """Header fields and the byte position after the header record (simple unquoted or quoted names)."""
+    end = len(buf)
+    for i, ch in enumerate(buf):
+        if ch in (10, 13):
+            end = i
+            break
+    head = buf[:end].decode('utf-8')
+    pos = end
+    if buf[pos:pos + 2] == b'\r\n':
+        pos += 2
+    elif pos < len(buf):
+        pos += 1
+    import csv
+    names = next(csv.reader([head])) if head else []
+    return names, head, pos
+
+
+def read_chunks(path: str, chunksize: int) -> Iterator[Union[NativeChunk, pd.DataFrame]]:
+    """Chunks of the article CSV: :class:`NativeChunk` where the fast path equals pandas, else the
+    ``DataFrame`` pandas parses from the same rows (see the module doc)."""
+    with open(path, 'rb') as fh:
+        data = fh.read()
+    yield from read_chunks_bytes(data, chunksize)
+
+
+def read_chunks_bytes(data: bytes, chunksize: int) -> Iterator[Union[NativeChunk, pd.DataFrame]]:
+    names, head, pos = _split_header(data)
+    ncols = len(names)
+    if ncols == 0 or len(set(names)) != ncols or any(n not in names for n in NEEDED):
+        yield from pd.read_csv(io.BytesIO(data), chunksize=chunksize)
+        return
+    need_idx = [names.index(n) for n in NEEDED]
+    na_buf, na_off, n_na = _na_table()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    L = _lib()
+    index0 = 0
+    rest_pandas = False
+    while pos < len(data) and not rest_pandas:
+        # a chunk's cells take at most its bytes
+        cap = min(len(data) - pos, 1 << 62) + 16
+        out = np.empty(cap, dtype=np.uint8)
+        coff = np.empty(chunksize * ncols + 1, dtype=np.int64)
+        cfl = np.empty(chunksize * ncols, dtype=np.uint8)
+        newpos = ctypes.c_int64(pos)
+        # bound the scan: at most the bytes of chunksize records (unknown), so parse all that remains
+        rows = L.kwcsv_parse(_p(buf), len(data), pos, chunksize, ncols, _p(na_buf), _p(na_off), n_na, _p(out), cap,
+                             _p(coff), _p(cfl), ctypes.byref(newpos))
+        if rows == 0:
+            break
+        if rows < 0:
+            rest_pandas = True
+            break
+        flags = cfl[:rows * ncols].reshape(rows, ncols)
+        ok = all(bool((flags[:, c] & TEXT).any()) for c in need_idx)
+        cells = Cells(out, coff[:rows * ncols + 1], cfl[:rows * ncols], int(rows), ncols)
+        if ok:
+            ok = all(L.kwcsv_utf8_ok(_p(out), _p(coff), _p(cfl), rows, ncols, c) for c in need_idx)
+        if ok:
+            yield NativeChunk(cells, names, index0)
+        else:
+            # pandas on exactly these rows (dtype inference is per chunk): the header + this chunk's bytes
+            frame = pd.read_csv(io.BytesIO(data[:_header_end(data)] + data[pos:newpos.value]))
+            frame.index = pd.RangeIndex(index0, index0 + len(frame))
+            yield frame
+        index0 += int(rows)
+        pos = newpos.value
+    if rest_pandas:
+        # a record the tokenizer does not reproduce: pandas takes the rest of the file, chunk by chunk
+        tail = data[:_header_end(data)] + data[pos:]
+        for frame in pd.read_csv(io.BytesIO(tail), chunksize=chunksize):
+            frame.index = pd.RangeIndex(index0, index0 + len(frame))
+            index0 += len(frame)
+            yield frame
+
+
+def _header_end(data: bytes) -> int:
+    _names, _head, pos = _split_header(data)
+    return pos

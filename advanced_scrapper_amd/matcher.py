@@ -167,7 +167,7 @@ class GpuMatcher:
 
     def kernel_times(self) -> Dict[str, float]:
         """Per-kernel device times (ms) of the last scan."""
-        keys = ('scan', 'resolve', 'generic', 'compact', 'total', 'filter', 'probe', 'epilogue')
+        keys = ('scan', 'resolve', 'generic', 'compact', 'total', 'filter', 'probe', 'epilogue', 'resolve_kernel', 'tasks')
         v = np.zeros(len(keys), dtype=np.float32)
         _native.check(_native.lib().kw_last_kernel_times(self.h, _native.ptr(v), len(keys)), self.h)
         return dict(zip(keys, (float(x) for x in v)))

@@ -122,10 +122,12 @@ int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
  * compaction. */
 int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *total_ms);
 
-/* Per-kernel device times (ms) of the last kw_scan, up to 8 values: [0] scan
- * (filter + probe + epilogue kernels), [1] resolve (task kernels + resolve
- * kernel), [2] generic, [3] result compaction, [4] total, [5] filter kernel,
- * [6] probe kernel, [7] epilogue kernel. */
+/* Per-kernel device times (ms) of the last kw_scan, up to 10 values: [0] scan
+ * (filter + probe + epilogue kernels), [1] resolve phase (the task kernels,
+ * then the wait for the resolve kernel, which starts after the probe on a
+ * side stream), [2] generic, [3] result compaction, [4] total, [5] filter
+ * kernel, [6] probe kernel, [7] epilogue kernel, [8] resolve kernel (side
+ * stream), [9] task kernels. */
 int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 
 /* Which kernel finished each document of the last scan (after kw_hits):
