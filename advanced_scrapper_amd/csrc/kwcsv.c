@@ -23,6 +23,7 @@
 #define KWCSV_QUOTED 1u   /* the cell was quoted */
 #define KWCSV_NA 2u       /* the cell is one of the NA strings: NaN */
 #define KWCSV_TEXT 4u     /* the cell proves its column is text (see kwcsv_text_witness) */
+#define KWCSV_CANON 8u    /* quoted iff the value holds ',', '"' or '\n': the csv writer's QUOTE_MINIMAL form */
 
 static int is_na(const uint8_t *s, int64_t n, const uint8_t *na, const int32_t *na_off, int32_t n_na)
 {
@@ -71,11 +72,12 @@ static int kwcsv_text_witness(const uint8_t *s, int64_t n)
  * coff[r*ncols+i+1]); cfl gets its KWCSV_* flags.  *pos_out = the position after the last record.
  * Returns the records parsed (0 at the end of the input), -1 if out is too small, -2 for a record
  * this tokenizer does not reproduce exactly (the caller falls back to pandas), -3 for a record whose
- * field count differs from ncols.
+ * field count differs from ncols.  rspan (optional, 2 per record) gets each record's byte span without
+ * its terminator.
  */
 int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_rows, int32_t ncols,
                     const uint8_t *na, const int32_t *na_off, int32_t n_na, uint8_t *out, int64_t cap,
-                    int64_t *coff, uint8_t *cfl, int64_t *pos_out)
+                    int64_t *coff, uint8_t *cfl, int64_t *pos_out, int64_t *rspan)
 {
     int64_t p = pos, o = 0, rows = 0;
     coff[0] = 0;
@@ -89,6 +91,7 @@ int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_ro
             break;
         }
         if (p >= len) break;
+        if (rspan) rspan[2 * rows] = p;
         int32_t f = 0;
         for (;;) {
             const int64_t cell0 = o;
@@ -117,12 +120,19 @@ int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_ro
                 p = k;
             }
             if (f >= ncols) return -3;
+            {
+                const int64_t n = o - cell0;
+                const int needq = n > 0 && (memchr(out + cell0, ',', (size_t)n) || memchr(out + cell0, '"', (size_t)n) ||
+                                            memchr(out + cell0, '\n', (size_t)n));
+                if (needq == ((flags & KWCSV_QUOTED) != 0)) flags |= KWCSV_CANON;
+            }
             if (is_na(out + cell0, o - cell0, na, na_off, n_na)) flags |= KWCSV_NA;
             else if (kwcsv_text_witness(out + cell0, o - cell0)) flags |= KWCSV_TEXT;
             cfl[rows * ncols + f] = flags;
             coff[rows * ncols + f + 1] = o;
             ++f;
             if (p < len && buf[p] == ',') { ++p; continue; }
+            if (rspan) rspan[2 * rows + 1] = p;
             /* record end: "\n", "\r\n", "\r" or the end of the input */
             if (p < len && buf[p] == '\r') ++p;
             if (p < len && buf[p] == '\n' && buf[p - 1] != '\n') ++p;

@@ -23,7 +23,7 @@ import numpy as np
 import pandas as pd
 
 NEEDED = ('article_text', 'title', 'date_time', 'url', 'source', 'source_url')
-QUOTED, NA, TEXT = 1, 2, 4
+QUOTED, NA, TEXT, CANON = 1, 2, 4, 8
 
 _LIB = None
 
@@ -37,7 +37,7 @@ def _lib():
         L = ctypes.CDLL(path)
         P, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
         L.kwcsv_parse.restype = i64
-        L.kwcsv_parse.argtypes = [P, i64, i64, i64, i32, P, P, i32, P, i64, P, P, P]
+        L.kwcsv_parse.argtypes = [P, i64, i64, i64, i32, P, P, i32, P, i64, P, P, P, P]
         L.kwcsv_pack.restype = i64
         L.kwcsv_pack.argtypes = [P, P, P, i64, i32, i32, i32, P, i64, P]
         L.kwcsv_utf8_ok.restype = i32
@@ -173,7 +173,7 @@ def read_chunks_bytes(data: bytes, chunksize: int) -> Iterator[Union[NativeChunk
         newpos = ctypes.c_int64(pos)
         # bound the scan: at most the bytes of chunksize records (unknown), so parse all that remains
         rows = L.kwcsv_parse(_p(buf), len(data), pos, chunksize, ncols, _p(na_buf), _p(na_off), n_na, _p(out), cap,
-                             _p(coff), _p(cfl), ctypes.byref(newpos))
+                             _p(coff), _p(cfl), ctypes.byref(newpos), None)
         if rows == 0:
             break
         if rows < 0:
@@ -205,3 +205,27 @@ def read_chunks_bytes(data: bytes, chunksize: int) -> Iterator[Union[NativeChunk
 def _header_end(data: bytes) -> int:
     _names, _head, pos = _split_header(data)
     return pos
+
+
+def parse_all(data: bytes):
+    """Every record of a whole CSV file: (column names, Cells, record byte spans [n, 2]) or ``None``
+    when the tokenizer cannot reproduce pandas' split of the file (the caller falls back to pandas)."""
+    names, _head, pos = _split_header(data)
+    ncols = len(names)
+    if ncols == 0 or len(set(names)) != ncols:
+        return None
+    na_buf, na_off, n_na = _na_table()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    # records <= terminators + 1; cells <= bytes
+    max_rows = data.count(b'\n') + data.count(b'\r') + 1
+    out = np.empty(len(data) + 16, dtype=np.uint8)
+    coff = np.empty(max_rows * ncols + 1, dtype=np.int64)
+    cfl = np.empty(max(max_rows * ncols, 1), dtype=np.uint8)
+    span = np.empty(2 * max_rows + 2, dtype=np.int64)
+    newpos = ctypes.c_int64(pos)
+    rows = _lib().kwcsv_parse(_p(buf), len(data), pos, max_rows, ncols, _p(na_buf), _p(na_off), n_na, _p(out),
+                              len(data) + 16, _p(coff), _p(cfl), ctypes.byref(newpos), _p(span))
+    if rows < 0 or newpos.value != len(data):
+        return None
+    cells = Cells(out, coff[:rows * ncols + 1], cfl[:rows * ncols], int(rows), ncols)
+    return names, cells, span[:2 * rows].reshape(-1, 2)

@@ -31,7 +31,8 @@ import numpy as np
 import pandas as pd
 from dateutil import parser
 
-from . import egress
+from . import egress, ingest
+from .ingest import NativeChunk
 from .dates import parse_date
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
@@ -96,6 +97,20 @@ def _cell_rows(chunk, cells, dates):
     """
     rows_by_ticker: Dict[str, list] = {}
     if not cells:
+        return rows_by_ticker, None
+    if isinstance(chunk, NativeChunk):
+        # the native tokenizer's chunk (all six columns object-typed): only matched rows are decoded
+        last, stamp, tail, raw = -1, None, None, None
+        for i, ticker, tj, tt in cells:
+            if i != last:
+                raw = chunk.value(i, 'date_time')
+                try:
+                    stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
+                except Exception as exc:   # noqa: BLE001
+                    return rows_by_ticker, exc
+                tail = tuple(chunk.value(i, c) for c in ('title', 'url', 'source', 'source_url', 'article_text'))
+                last = i
+            rows_by_ticker.setdefault(ticker, []).append((stamp, raw, tj, tt) + tail)
         return rows_by_ticker, None
     if not any(dt == object for dt in chunk.dtypes):
         last, stamp, row = -1, None, None
@@ -186,19 +201,24 @@ def _results(matcher, hits, dates):
     return results, None
 
 
+def _dates(values):
+    """``dateutil.parse(str(v)) if notna(v) else None`` per row (match_keywords.py:152) up to the first row
+    that raises; returns the dates and that exception (or ``None``)."""
+    dates: List = []
+    for v in values:
+        try:
+            dates.append(parse_date(str(v)) if pd.notna(v) else None)
+        except Exception as exc:   # match_keywords.py:152 raises here for this row
+            return dates, exc
+    return dates, None
+
+
 def _prepare(chunk):
     """The reference's per-row field prep (match_keywords.py:150-152) of a whole chunk: texts, titles, the
     dates of the rows before the first unparseable ``date_time``, and that parse error (or ``None``)."""
     texts = [field_str(v) for v in chunk['article_text'].tolist()]
     titles = [field_str(v) for v in chunk['title'].tolist()]
-    dates: List = []
-    error = None
-    for v in chunk['date_time'].tolist():
-        try:
-            dates.append(parse_date(str(v)) if pd.notna(v) else None)
-        except Exception as exc:   # match_keywords.py:152 raises here for this row
-            error = exc
-            break
+    dates, error = _dates(chunk['date_time'].tolist())
     return texts, titles, dates, error
 
 
@@ -277,15 +297,108 @@ def _write_chunk_sharded(source_name, chunk, processed_data, matcher, exchange):
     return matcher
 
 
+def _native_sample(chunk: NativeChunk, limit: int = 4000):
+    """The first rows' article texts (the anchor statistics' sample; speed only)."""
+    col = chunk.col['article_text']
+    return [field_str(chunk.cells.value(i, col)) for i in range(min(len(chunk), limit))]
+
+
+def _native_match(chunk: NativeChunk, processed_data, matcher, exchange=None):
+    """Hits of a natively read chunk: the arena is packed in C from the tokenized cells (no per-row
+    ``str``); with an exchange, this rank matches its byte-balanced row range and rank 0 gets all."""
+    from .dist import byte_balanced_ranges
+    dates, error = _dates(chunk.column_list('date_time'))
+    n_ok = len(dates)
+    matcher = matcher or get_matcher(processed_data, sample_texts=_native_sample(chunk))
+    if n_ok == 0:
+        return None, dates, error, matcher
+    arena, off = chunk.arena()
+    off = off[:2 * n_ok + 1]
+    if exchange is None:
+        d_arena, d_off = matcher.upload(arena, off)
+        matcher.scan(d_arena, d_off, n_ok)
+        return matcher.fetch(), dates, error, matcher
+    lo, hi = byte_balanced_ranges(off, exchange.world)[exchange.rank]
+    d_arena, d_off = matcher.upload(arena, off)
+    matcher.scan(d_arena, d_off[2 * lo:], hi - lo)
+    allh = exchange.gather(matcher.hits_device(), lo)
+    return (records_from_tensor(allh) if exchange.rank == 0 else None), dates, error, matcher
+
+
+def _write_native(source_name, chunk: NativeChunk, processed_data, matcher, exchange=None):
+    hits, dates, error, matcher = _native_match(chunk, processed_data, matcher, exchange)
+    if exchange is None or exchange.rank == 0:
+        _write_hits(source_name, chunk, matcher, hits, dates, error)
+    elif error is not None:
+        raise error
+    return matcher
+
+
 def process_chunk(source_name, chunk, processed_data):
     """Match every row of ``chunk`` and append the per-ticker CSV rows (match_keywords.py:148-192)."""
     _write_chunk(source_name, chunk, processed_data)
 
 
 # --------------------------------------------------------------------- sort
+def _sort_native(file_path) -> bool:
+    """sort_matched_csv's re-read, sort and rewrite without pandas when the result is provably the same
+    bytes (§8(f)2); ``False`` (file untouched) hands the file to the pandas path.
+
+    pandas' re-read (match_keywords.py:198) keeps a column ``object`` when a cell proves it text, reads an
+    all-NA column as NaN, and makes ``time_unix`` int64 when every cell is a plain integer; NA strings
+    become NaN, which to_csv writes as an empty cell.  ``sort_values('time_unix')`` with the default
+    kind is ``np.argsort(kind='quicksort')`` on those integers (pandas' nargsort without NaNs), so ties
+    keep pandas' (unstable) order.  A record whose cells are already in the writer's QUOTE_MINIMAL form,
+    with no NA cell and a canonical integer, is copied as it stands; the others are rendered again.
+    """
+    from .ingest import CANON, NA, TEXT, parse_all
+    with open(file_path, 'rb') as fh:
+        data = fh.read()
+    parsed = parse_all(data)
+    if parsed is None:
+        return False
+    names, cells, span = parsed
+    if 'time_unix' not in names:
+        return False
+    n, nc = cells.nrows, cells.ncols
+    ti = names.index('time_unix')
+    fl = cells.flags.reshape(n, nc)
+    for c in range(nc):
+        if c != ti and n and not ((fl[:, c] & TEXT).any() or (fl[:, c] & NA).all()):
+            return False
+    raw = [bytes(cells._mv[cells.off[r * nc + ti]:cells.off[r * nc + ti + 1]]) for r in range(n)]
+    if n and (fl[:, ti] & (NA | TEXT)).any():
+        return False
+    try:
+        ints = [int(x) for x in raw]
+    except ValueError:
+        return False
+    if any(v >= (1 << 63) or v < -(1 << 63) for v in ints):
+        return False
+    order = np.argsort(np.asarray(ints, dtype=np.int64), kind='quicksort')
+    plain = (fl & CANON).all(axis=1) & ~(fl & NA).any(axis=1) if n else np.zeros(0, bool)
+    lines = [egress._join(list(names)).encode('utf-8')]
+    nl = os.linesep.encode()
+    for r in order.tolist():
+        if plain[r] and str(ints[r]).encode() == raw[r]:
+            lines.append(data[span[r, 0]:span[r, 1]] + nl)
+        else:
+            vals = [str(ints[r]) if c == ti else ('' if fl[r, c] & NA else cells.value(r, c)) for c in range(nc)]
+            line = egress._join(vals)
+            if line is None:
+                return False
+            lines.append(line.encode('utf-8'))
+    with open(file_path, 'wb') as fh:
+        fh.write(b''.join(lines))
+    return True
+
+
 def sort_matched_csv(file_path):
     """Re-read, sort by ``time_unix`` (pandas default quicksort) and rewrite (match_keywords.py:195-217)."""
     try:
+        if _sort_native(file_path):
+            print(f"Sorted and saved: {file_path}")
+            return
         frame = pd.read_csv(file_path)
         if 'time_unix' not in frame.columns:
             frame['date_time'] = frame['date_time'].apply(parser.parse)
@@ -348,7 +461,13 @@ def run(args, rank: int, world: int, device, backend, matcher=None):
         from .dist import Exchange
         exchange = Exchange(rank, world, device, backend)
     try:
-        for chunk in pd.read_csv(args.articles, chunksize=args.chunksize):
+        # the native tokenizer (ingest.py), chunk by chunk, with pandas' own chunks where it cannot be exact
+        for chunk in ingest.read_chunks(args.articles, args.chunksize):
+            if isinstance(chunk, NativeChunk):
+                if matcher is None:
+                    matcher = get_matcher(processed, device, _native_sample(chunk))
+                matcher = _write_native(args.source, chunk, processed, matcher, exchange)
+                continue
             if matcher is None:
                 matcher = get_matcher(processed, device, [field_str(v) for v in chunk['article_text'].tolist()])
             if exchange is None:

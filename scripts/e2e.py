@@ -1,10 +1,13 @@
-"""End-to-end drop-in timing: match_keywords' per-chunk host phases around the GPU scan.
+"""End-to-end drop-in timing: match_keywords.main's per-chunk phases around the GPU scan, then the sort.
 
 Generates N synthetic articles (config-2 corpus), writes them as the reference's article CSV, then runs the
-drop-in main loop's phases on chunks of 20 000 rows and prints one JSON line with seconds per phase and the
-end-to-end articles/s (the reference's CPU path on the same rows is bench.py's cpu_baseline).
+drop-in main loop's phases on chunks of 20 000 rows -- native CSV ingest (libkwcsv), date parse, arena +
+GPU match, JSON cells (libkwrows), row tuples, CSV egress -- and the final sort of every per-ticker file
+(match_keywords.py:243-244, native rewrite with the pandas fallback), and prints one JSON line with seconds
+per phase and the end-to-end articles/s (the reference's CPU path on the same rows is bench.py's
+cpu_baseline).
 
-    python scripts/e2e.py [--docs 100000] [--chunksize 20000]
+    python scripts/e2e.py [--docs 200000] [--chunksize 20000]
 """
 import argparse
 import json
@@ -20,15 +23,14 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--docs', type=int, default=100000)
+    ap.add_argument('--docs', type=int, default=200000)
     ap.add_argument('--chunksize', type=int, default=20000)
     args = ap.parse_args()
-    import pandas as pd
-    from advanced_scrapper_amd import match_keywords as mk, synth
+    os.environ.setdefault('TZ', 'UTC')
+    time.tzset()
+    from advanced_scrapper_amd import ingest, match_keywords as mk, synth
     from advanced_scrapper_amd.kb import compile_kb
-    from advanced_scrapper_amd.matcher import field_str
     from advanced_scrapper_amd.rows import assemble_json_rows
-    from advanced_scrapper_amd.dates import parse_date
     from tests import golden_data
     processed = golden_data.kb_processed()
     ckb = compile_kb(processed)
@@ -39,22 +41,30 @@ def main():
     synth.to_dataframe(corpus).to_csv(csv_path, index=False)
     os.chdir(work)
     os.makedirs('yahoo_ticker_matched_articles')
-    t = dict(read=0.0, prep=0.0, dates=0.0, gpu_match=0.0, assemble=0.0, rows=0.0, write=0.0)
+    t = dict(read=0.0, dates=0.0, arena=0.0, gpu_match=0.0, assemble=0.0, rows=0.0, write=0.0, sort=0.0)
     matcher = None
-    n_rows = 0
+    n_rows = n_native = n_chunks = 0
     t_all = time.perf_counter()
     c0 = time.perf_counter()
-    for chunk in pd.read_csv(csv_path, chunksize=args.chunksize):
+    for chunk in ingest.read_chunks(csv_path, args.chunksize):
         c1 = time.perf_counter(); t['read'] += c1 - c0
-        texts = [field_str(v) for v in chunk['article_text'].tolist()]
-        titles = [field_str(v) for v in chunk['title'].tolist()]
-        c2 = time.perf_counter(); t['prep'] += c2 - c1
-        dates = [parse_date(str(v)) if pd.notna(v) else None for v in chunk['date_time'].tolist()]
-        c3 = time.perf_counter(); t['dates'] += c3 - c2
+        n_chunks += 1
+        if not isinstance(chunk, ingest.NativeChunk):
+            matcher = mk._write_chunk('yahoo', chunk, processed, matcher)
+            c0 = time.perf_counter(); t['write'] += c0 - c1
+            continue
+        n_native += 1
+        dates, error = mk._dates(chunk.column_list('date_time'))
+        c2 = time.perf_counter(); t['dates'] += c2 - c1
         if matcher is None:
-            matcher = mk.get_matcher(processed, 0, texts)
-        c3 = time.perf_counter()
-        hits = matcher.match_strings(texts, titles)
+            matcher = mk.get_matcher(processed, 0, mk._native_sample(chunk))
+        c2 = time.perf_counter()
+        arena, off = chunk.arena()
+        off = off[:2 * len(dates) + 1]
+        c3 = time.perf_counter(); t['arena'] += c3 - c2
+        d_arena, d_off = matcher.upload(arena, off)
+        matcher.scan(d_arena, d_off, len(dates))
+        hits = matcher.fetch()
         c4 = time.perf_counter(); t['gpu_match'] += c4 - c3
         cells = assemble_json_rows(matcher.ckb, hits, dates)
         c5 = time.perf_counter(); t['assemble'] += c5 - c4
@@ -64,9 +74,17 @@ def main():
             mk._append_rows('yahoo', ticker, rows)
             n_rows += len(rows)
         c0 = time.perf_counter(); t['write'] += c0 - c6
+    c7 = time.perf_counter()
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        for name in os.listdir('yahoo_ticker_matched_articles'):
+            mk.sort_matched_csv(f'yahoo_ticker_matched_articles/{name}')
+    t['sort'] = time.perf_counter() - c7
     total = time.perf_counter() - t_all
-    out = {'docs': args.docs, 'chunksize': args.chunksize, 'rows': n_rows, 'total_s': round(total, 3),
-           'articles_per_s': round(args.docs / total, 1), 'phases_s': {k: round(v, 3) for k, v in t.items()}}
+    out = {'docs': args.docs, 'chunksize': args.chunksize, 'chunks': n_chunks, 'native_chunks': n_native,
+           'rows': n_rows, 'total_s': round(total, 3), 'articles_per_s': round(args.docs / total, 1),
+           'phases_s': {k: round(v, 3) for k, v in t.items()}}
     print(json.dumps(out), flush=True)
     os.chdir(REPO)
     shutil.rmtree(work, ignore_errors=True)

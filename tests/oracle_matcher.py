@@ -45,6 +45,24 @@ class OracleMatcher:
         a = np.asarray(rows, dtype=np.uint32).reshape(-1, 4)
         return torch.from_numpy(a.view(np.int32).copy())
 
+    # the kw_scan-shaped calls of the native ingest path: an arena + offsets "upload", a scan of n documents
+    # starting at an offsets slice, the records of the last scan
+    def upload(self, arena, off):
+        return arena, off
+
+    def scan(self, d_arena, d_off, n_docs, stream=None):
+        b = bytes(d_arena)
+        texts = [b[d_off[2 * i]:d_off[2 * i + 1]].decode('utf-8', 'surrogatepass') for i in range(n_docs)]
+        titles = [b[d_off[2 * i + 1]:d_off[2 * i + 2]].decode('utf-8', 'surrogatepass') for i in range(n_docs)]
+        self._last = self.match_device(texts, titles)
+
+    def hits_device(self):
+        return self._last
+
+    def fetch(self):
+        from advanced_scrapper_amd.matcher import records_from_tensor
+        return records_from_tensor(self._last)
+
     def match_strings(self, texts, titles):
         from advanced_scrapper_amd.matcher import records_from_tensor
         return records_from_tensor(self.match_device(texts, titles))

@@ -162,3 +162,30 @@ def test_shard_range_partitions():
             assert rr[0][0] == 0 and rr[-1][1] == n
             assert all(rr[i][1] == rr[i + 1][0] for i in range(world - 1))
             assert max(h - l for l, h in rr) - min(h - l for l, h in rr) <= 1
+
+
+def test_main_single_rank_equals_reference_outputs(tmp_path, monkeypatch):
+    """match_keywords.main's single-GPU loop -- native CSV ingest (libkwcsv), matching, libkwrows cells, CSV
+    egress, the final sort -- with only the scan stubbed by the oracle, writes the reference's own per-ticker
+    files byte for byte (tests/golden/out_c1)."""
+    import time
+    from advanced_scrapper_amd import ingest
+    from advanced_scrapper_amd import match_keywords as mk
+    from tests import golden_data
+    from tests.oracle_matcher import OracleMatcher
+    monkeypatch.setenv('TZ', 'UTC')
+    time.tzset()
+    (tmp_path / 'articles.csv').write_bytes(golden_data.articles_csv_bytes())
+    kinds = [type(c).__name__ for c in ingest.read_chunks(str(tmp_path / 'articles.csv'), golden_data.chunksize())]
+    assert 'NativeChunk' in kinds
+    monkeypatch.chdir(tmp_path)
+    processed = golden_data.kb_processed()
+    monkeypatch.setattr(mk, 'read_and_process_json_files', lambda _d: processed)
+    args = mk._parse(['--info-dir', 'unused', '--articles', str(tmp_path / 'articles.csv'),
+                      '--chunksize', str(golden_data.chunksize())])
+    assert mk.run(args, 0, 1, None, None, matcher=OracleMatcher(processed)) == 0
+    out = tmp_path / 'yahoo_ticker_matched_articles'
+    want = golden_data.outputs()
+    assert sorted(os.listdir(out)) == sorted(want)
+    for fn in want:
+        assert (out / fn).read_bytes() == want[fn], fn
