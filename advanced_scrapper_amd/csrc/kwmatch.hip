@@ -28,6 +28,7 @@ struct ScratchCaps {
     int ns = 0;                            // filter regions (filter waves = probe waves)
     uint32_t item_cap = 0, out_cap = 0;    // per filter region items, per wave result records
     uint32_t cand_cap = 0;                 // per filter region candidates
+    uint32_t gi_cap = ITEM_CAP, gc_cap = CP_CAP;   // generic kernel: items per field, code points per field
     int64_t hdr_cap = 0;                   // documents
     uint32_t defer_cap = 0, rx_cap = 0;
     uint32_t vcap = 0, ecap = 0, scap = 0, xcap = 0;   // per scan wave task regions
@@ -35,7 +36,7 @@ struct ScratchCaps {
     bool covers(const ScratchCaps &o) const
     {
         return nk >= o.nk && nr >= o.nr && ng >= o.ng && ns >= o.ns && cand_cap >= o.cand_cap &&
-               item_cap >= o.item_cap && out_cap >= o.out_cap &&
+               item_cap >= o.item_cap && out_cap >= o.out_cap && gi_cap >= o.gi_cap && gc_cap >= o.gc_cap &&
                hdr_cap >= o.hdr_cap && defer_cap >= o.defer_cap && rx_cap >= o.rx_cap && vcap >= o.vcap &&
                ecap >= o.ecap && scap >= o.scap && xcap >= o.xcap && dsize >= o.dsize;
     }
@@ -43,6 +44,7 @@ struct ScratchCaps {
     {
         nk = std::max(nk, o.nk); nr = std::max(nr, o.nr); ng = std::max(ng, o.ng); ns = std::max(ns, o.ns);
         cand_cap = std::max(cand_cap, o.cand_cap);
+        gi_cap = std::max(gi_cap, o.gi_cap); gc_cap = std::max(gc_cap, o.gc_cap);
         item_cap = std::max(item_cap, o.item_cap); out_cap = std::max(out_cap, o.out_cap);
         hdr_cap = std::max(hdr_cap, o.hdr_cap); defer_cap = std::max(defer_cap, o.defer_cap);
         rx_cap = std::max(rx_cap, o.rx_cap); vcap = std::max(vcap, o.vcap); ecap = std::max(ecap, o.ecap);
@@ -951,14 +953,15 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     if (h->d_scratch) { (void)hipFree(h->d_scratch); h->d_scratch = nullptr; }
     if (h->d_small) { (void)hipFree(h->d_small); h->d_small = nullptr; }
     if (h->d_hits) { (void)hipFree(h->d_hits); h->d_hits = nullptr; }
-    const size_t per_items = (size_t)2 * ITEM_CAP * sizeof(uint64_t);
-    const size_t per_cps = (size_t)CP_CAP * sizeof(uint32_t);
-    const size_t per_blk = (size_t)(CP_CAP / 16 + 2) * sizeof(uint32_t);
+    const size_t per_items = (size_t)2 * c.gi_cap * sizeof(uint64_t);
+    const size_t per_cps = (size_t)c.gc_cap * sizeof(uint32_t);
+    const size_t per_blk = (size_t)(c.gc_cap / 16 + 2) * sizeof(uint32_t);
+    const size_t per_fblk = (size_t)(CP_CAP / 16 + 2) * sizeof(uint32_t);
     const size_t per_fcps = (size_t)FK_CP_CAP * sizeof(uint32_t);
     const size_t per_out = (size_t)c.out_cap * sizeof(kw_hit);
     const size_t nw = (size_t)2 * c.nk + c.nr + c.ng;
     const size_t per_tasks = (size_t)(c.vcap + c.ecap + c.scap + c.xcap) * 16;
-    size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_blk) +
+    size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_fblk) +
                    nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 4 +
                    (size_t)c.ns * c.cand_cap * 16 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 12 + 4 * 256 +
                    (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
@@ -970,7 +973,9 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->S.cps = (uint32_t *)carve((size_t)c.ng * per_cps);
     h->S.blkcnt = (uint32_t *)carve((size_t)c.ng * per_blk);
     h->FS.cps = (uint32_t *)carve((size_t)c.nr * per_fcps);
-    h->FS.cpbase = (uint32_t *)carve((size_t)c.nr * per_blk);
+    h->FS.cpbase = (uint32_t *)carve((size_t)c.nr * per_fblk);
+    h->S.item_cap = c.gi_cap;
+    h->S.cp_cap = c.gc_cap;
     kw_hit *outs = (kw_hit *)carve(nw * per_out);
     h->FS.items = (uint64_t *)carve((size_t)c.ns * c.item_cap * 8);
     h->FS.cand = (uint4 *)carve((size_t)c.ns * c.cand_cap * 16);
@@ -1005,6 +1010,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.defer_cnt = (uint32_t *)(q + 16);
     h->FS.tmax = (uint32_t *)(q + 32);                  // 4 x u32
     h->FS.cmax = (uint32_t *)(q + 48);                  // 2 x u32
+    h->S.gmax = (uint32_t *)(q + 56);                   // 2 x u32
     h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
     h->FS.stats = (unsigned long long *)(q + 128);      // 32 x u64 (fast path; 13.. developer counters)
     uint32_t *cnts = (uint32_t *)(q + 1024);
@@ -1059,7 +1065,13 @@ static int launch_scan(kw_handle *h)
     // costs vary by orders of magnitude, later blocks take the work of the slow ones
     int gmul = 4;
     if (const char *e = getenv("KW_GENERIC_BLOCKS_PER_CU")) gmul = std::max(1, atoi(e));
-    const int ngb = std::max(1, (int)std::min<int64_t>((int64_t)h->cus * gmul, (n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));
+    int ngb = std::max(1, (int)std::min<int64_t>((int64_t)h->cus * gmul, (n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));
+    {   // a generic wave's scratch grows with the largest deferred field: fewer waves then, within a budget
+        const size_t per_wave = (size_t)2 * h->caps.gi_cap * 8 + (size_t)h->caps.gc_cap * 4 +
+                                (size_t)(h->caps.gc_cap / 16 + 2) * 4;
+        const size_t budget = (size_t)4 << 30;
+        ngb = std::max(1, std::min(ngb, (int)std::max<size_t>(1, budget / per_wave / WAVES_PER_BLOCK)));
+    }
     ScratchCaps w;
     w.nk = n_epi;
     w.ns = n_regions;
@@ -1185,14 +1197,35 @@ static int finish(kw_handle *h)
         uint32_t status[4];
         HIPCHK(h, hipMemcpy(status, h->S.status, sizeof(status), hipMemcpyDeviceToHost));
         if (h->n_docs == 0) { h->n_hits = 0; h->fetched = true; return KW_OK; }
-        if (status[0] & (ST_ITEM_OVERFLOW | ST_CP_OVERFLOW | ST_FIELD_TOO_LONG)) {
+        if (status[0] & ST_FIELD_TOO_LONG) {
             char buf[256];
-            snprintf(buf, sizeof(buf), "kw_scan: device work buffer overflow (status 0x%x: %s%s%s)", status[0],
-                     (status[0] & ST_ITEM_OVERFLOW) ? "more than 16384 anchor occurrences in one field; " : "",
-                     (status[0] & ST_CP_OVERFLOW) ? "non-ASCII field longer than 65536 code points; " : "",
-                     (status[0] & ST_FIELD_TOO_LONG) ? "field longer than 8 MiB; " : "");
+            snprintf(buf, sizeof(buf), "kw_scan: a field longer than %lld bytes (positions are 23-bit in the "
+                     "device item records; the reference has no such limit)", (long long)MAX_FIELD_BYTES);
             h->err = buf;
             return KW_EOVERFLOW;
+        }
+        if (status[0] & (ST_ITEM_OVERFLOW | ST_CP_OVERFLOW)) {
+            // a deferred field needs more anchor items or code points than the generic kernel's buffers hold:
+            // grow them to the need (fewer generic waves, within the scratch budget) and scan again
+            uint32_t gm[2];
+            HIPCHK(h, hipMemcpy(gm, h->S.gmax, sizeof(gm), hipMemcpyDeviceToHost));
+            ScratchCaps w = h->caps;
+            if (status[0] & ST_ITEM_OVERFLOW) {
+                uint32_t c = w.gi_cap;
+                while (c < gm[0] && c < (1u << 30)) c <<= 1;
+                if (c < gm[0]) { h->err = "kw_scan: a field with more than 2^30 anchor occurrences"; return KW_EOVERFLOW; }
+                w.gi_cap = c;
+            }
+            if (status[0] & ST_CP_OVERFLOW) w.gc_cap = std::max(w.gc_cap, gm[1] + 64);
+            const size_t per_wave = (size_t)2 * w.gi_cap * 8 + (size_t)w.gc_cap * 4 + (size_t)(w.gc_cap / 16 + 2) * 4;
+            const size_t budget = (size_t)4 << 30;
+            w.ng = (int)std::min<size_t>((size_t)w.ng, std::max<size_t>(WAVES_PER_BLOCK, budget / per_wave / WAVES_PER_BLOCK * WAVES_PER_BLOCK));
+            h->caps.ng = w.ng;   // the generic wave count may shrink
+            int rc = ensure_scratch(h, w);
+            if (rc) return rc;
+            rc = launch_scan(h);
+            if (rc) return rc;
+            continue;
         }
         if (status[0] & (ST_OUT_OVERFLOW | ST_RX_OVERFLOW | ST_TASK_OVERFLOW | ST_DSET_FULL | ST_CAND_OVERFLOW)) {
             // grow what overflowed (result regions to the largest count seen, queues to the largest need) and rescan

@@ -17,8 +17,8 @@ constexpr int FILT_BITS = 18;                       // 2^18-bit filter = 32 KB o
 constexpr int FILT_WORDS = 1 << (FILT_BITS - 5);
 constexpr int SCAN_TILE = 1024;                     // bytes per wave per scan step (16 B / lane)
 constexpr int CAND_CAP = SCAN_TILE;                 // candidates per tile (<= positions)
-constexpr int ITEM_CAP = 16384;                     // anchor uses per field per doc (power of 2)
-constexpr int CP_CAP = 65536;                       // decoded code points per non-ASCII field
+constexpr int ITEM_CAP = 16384;                     // anchor uses per field per doc, initial (grows)
+constexpr int CP_CAP = 65536;                       // decoded code points per non-ASCII field, initial (grows)
 constexpr int MAXM = 64;                            // longest fuzzy name (rapidfuzz short-needle path)
 constexpr int SHORT_EXACT_MAX = 10;                 // fields this short can only match exactly
 constexpr int RX_MAX_QUANT = 16;                    // quantified atoms per regex program
@@ -87,9 +87,12 @@ struct DevTables {
 };
 
 struct DevScratch {
-    uint64_t *items;               // per wave: 2 * ITEM_CAP
-    uint32_t *cps;                 // per wave: CP_CAP
-    uint32_t *blkcnt;              // per wave: CP_CAP/64*4 + 2 (cumulative lead bytes per 64 B)
+    uint64_t *items;               // per wave: 2 * item_cap
+    uint32_t *cps;                 // per wave: cp_cap
+    uint32_t *blkcnt;              // per wave: cp_cap/16 + 2 (cumulative lead bytes per 64 B)
+    uint32_t item_cap;             // anchor uses per field (grown by the host when a document needs more)
+    uint32_t cp_cap;               // decoded code points per non-ASCII field (likewise)
+    uint32_t *gmax;                // [2] largest item count / code point count a deferred field needed
     kw_hit *out;                   // per wave: out_cap
     uint32_t *out_cnt;             // per wave
     uint32_t *status;              // [0] error bits, [1] max item count seen

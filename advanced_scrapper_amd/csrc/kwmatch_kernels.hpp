@@ -705,15 +705,19 @@ __device__ uint32_t decode_field(const DevScratch &S, const uint8_t *__restrict_
         bool lead = valid && ((byte & 0xC0) != 0x80);
         uint64_t m = __ballot(lead);
         uint32_t idx = cnt + mbcnt(m);
-        if (lead && idx < (uint32_t)CP_CAP) {
+        if (lead && idx < S.cp_cap) {
             uint32_t cp;
             decode_at(arena, fb + i, fe, &cp);
             cps[idx] = cp;
         }
-        if (lane == 0 && (b0 >> 6) < (int64_t)(CP_CAP / 16)) blkcnt[b0 >> 6] = cnt;
+        if (lane == 0 && (b0 >> 6) < (int64_t)(S.cp_cap / 16)) blkcnt[b0 >> 6] = cnt;
         cnt += (uint32_t)__popcll(m);
     }
-    if ((cnt > (uint32_t)CP_CAP || L > (int64_t)CP_CAP * 4) && lane == 0) atomicOr(&S.status[0], ST_CP_OVERFLOW);
+    if ((cnt > S.cp_cap || L > (int64_t)S.cp_cap * 4) && lane == 0) {
+        // the host grows the code point buffers to the largest need and runs the scan again
+        atomicOr(&S.status[0], ST_CP_OVERFLOW);
+        atomicMax(&S.gmax[1], (uint32_t)(L < 0xFFFFFFFFll ? L : 0xFFFFFFFFll));
+    }
     wave_sync_global();
     return cnt;
 }
@@ -784,8 +788,8 @@ __device__ void process_candidate(const DevTables &T, const DevScratch &S, const
             const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(p - fb) << IT_POS_SHIFT) |
                                   ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
             const uint32_t idx = atomicAdd(&icnt[f], 1u);
-            if (idx < (uint32_t)ITEM_CAP) items[idx] = item;
-            else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+            if (idx < S.item_cap) items[idx] = item;
+            else { atomicOr(&S.status[0], ST_ITEM_OVERFLOW); atomicMax(&S.gmax[0], idx + 1); }   // grown + rescanned
         }
     }
 }
@@ -821,10 +825,10 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
     uint64_t *lext_mask = extm_all + wib * 64;
     uint32_t *lext_cp = extc_all + wib * 64;
     uint32_t *icnt = icnt_all + wib * 2;
-    uint64_t *items0 = S.items + (size_t)wave * 2 * ITEM_CAP;
-    uint64_t *items1 = items0 + ITEM_CAP;
-    uint32_t *cps = S.cps + (size_t)wave * CP_CAP;
-    uint32_t *blkcnt = S.blkcnt + (size_t)wave * (CP_CAP / 16 + 2);
+    uint64_t *items0 = S.items + (size_t)wave * 2 * S.item_cap;
+    uint64_t *items1 = items0 + S.item_cap;
+    uint32_t *cps = S.cps + (size_t)wave * S.cp_cap;
+    uint32_t *blkcnt = S.blkcnt + (size_t)wave * (S.cp_cap / 16 + 2);
 
     OutCtx O;
     O.shared = nullptr;
@@ -897,8 +901,8 @@ __global__ __launch_bounds__(BLOCK) void kw_scan_kernel(DevTables T, const uint8
         }
         wave_sync_global();
         uint32_t N0 = icnt[0], N1 = icnt[1];
-        if (N0 > (uint32_t)ITEM_CAP) N0 = ITEM_CAP;
-        if (N1 > (uint32_t)ITEM_CAP) N1 = ITEM_CAP;
+        if (N0 > S.item_cap) N0 = S.item_cap;
+        if (N1 > S.item_cap) N1 = S.item_cap;
         N0 = __builtin_amdgcn_readfirstlane(N0);
         N1 = __builtin_amdgcn_readfirstlane(N1);
         const uint32_t ncp0 = (uint32_t)wave_sum((int)cpt), ncp1 = (uint32_t)wave_sum((int)cpu);

@@ -362,3 +362,48 @@ def test_dropin_error_paths_gpu(golden, tmp_path, monkeypatch, case):
     got = {fn: open(os.path.join('yahoo_ticker_matched_articles', fn), encoding='utf-8').read()
            for fn in os.listdir('yahoo_ticker_matched_articles')}
     assert got == c['files']
+
+
+@pytest.mark.parametrize('case', ['items_over_16384', 'non_ascii_over_65536_cps'])
+def test_capacity_limits_grow_and_match_oracle(golden, case):
+    """Fields past the generic kernel's initial buffers (more than 16 384 anchor occurrences in one field; a
+    non-ASCII field of more than 65 536 code points) grow the buffers and rescan instead of failing, and give
+    the oracle's result (a small KB keeps the oracle fast)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher, group_hits
+    from oracle import kwmatch_oracle as orc
+    processed = golden.processed_from(golden.error_cases()['kb_processed'])
+    processed = {t: {a: {n: p for n, p in names.items() if n != 'Notepad++'} for a, names in attrs.items()}
+                 for t, attrs in processed.items()}
+    if case == 'items_over_16384':
+        text = 'ACME Roadrunner Holdings ' * 9000 + 'Acme Rocket Skates.'
+    else:
+        text = 'é' * 70000 + ' ACME and Birdseed Deluxe; ' + 'ü' * 1000 + ' Wile E. Coyote'
+    texts, titles = [text, 'RRN short', text[:5000]], ['ACME title', text[-3000:], 'nan']
+    m = GpuMatcher(compile_kb(processed))
+    g = group_hits(m.match_strings(texts, titles))
+    st = m.stats()
+    assert st['deferred_docs'] >= 1
+    o = orc.Oracle(processed)
+    for d in range(len(texts)):
+        for f, s in ((0, texts[d]), (1, titles[d])):
+            have = {m.ckb.names[p]: v for p, v in g.get(d, {}).get(f, {}).items()}
+            assert have == o.field_results(s), (case, d, f)
+
+
+def test_field_over_8mib_is_a_stated_limit():
+    """A field beyond 8 MiB is the one capacity the device path does not take (23-bit item positions):
+    kw_scan reports it by name instead of returning a wrong result."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    processed = {'ACM': {'aliases': {'ACME': (None, None)}}}
+    m = GpuMatcher(compile_kb(processed))
+    with pytest.raises(_native.KwError, match='longer than 8388607 bytes'):
+        m.match_strings(['x' * (9 << 20)], ['t'])
