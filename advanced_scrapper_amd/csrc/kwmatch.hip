@@ -96,6 +96,8 @@ struct kw_handle {
     int ns = 0;                        // filter regions of the last launch
     hipEvent_t evf = nullptr, evp = nullptr;   // after the filter / probe kernels
     hipStream_t side = nullptr;                // the resolve kernel's stream (beside epilogue + tasks)
+    hipStream_t side2 = nullptr;               // the short-field task kernel's stream (beside verify)
+    hipEvent_t eve = nullptr, evq = nullptr;   // after the epilogue (main); after the short kernel (side2)
     hipEvent_t evs0 = nullptr, evs1 = nullptr, evt = nullptr;   // resolve start / end (side), tasks end
     int n_anchor_fast = 0;
     unsigned long long fstats[16] = {0};
@@ -929,6 +931,9 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_epi_kernel, EK_BLOCK, 0));
     h->epi_blocks_per_cu = bpc > 0 ? bpc : 1;
     HIPCHK(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIPCHK(h, hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreateWithFlags(&h->eve, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->evq, hipEventDisableTiming));
     HIPCHK(h, hipEventCreate(&h->evs0));
     HIPCHK(h, hipEventCreate(&h->evs1));
     HIPCHK(h, hipEventCreate(&h->evt));
@@ -1139,15 +1144,21 @@ static int launch_scan(kw_handle *h)
         // G[k] waves share each epilogue wave's task region
         int G[4] = {4, 4, 8, 4};   // measured on MI355X (1M docs): 12.10 ms vs 12.31 ms for {1, 4, 4, 1}
         if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
-        auto task = [&](auto kern, int g) {
+        auto task = [&](auto kern, int g, hipStream_t s) {
             g = std::max(1, std::min(g, 16));
             const int nb = (n_epi * g + RK_WAVES - 1) / RK_WAVES;
-            hipLaunchKernelGGL(kern, dim3(nb), dim3(RK_BLOCK), 0, st, h->FT, h->T, h->arena, h->doc_off,
+            hipLaunchKernelGGL(kern, dim3(nb), dim3(RK_BLOCK), 0, s, h->FT, h->T, h->arena, h->doc_off,
                                n_epi, g, h->FS, h->S);
         };
-        task(kw_verify_kernel, G[0]);
-        task(kw_short_kernel, G[2]);
-        task(kw_rx_task_kernel, G[3]);
+        // verify and short-field tasks are independent (both only append decisions): side by side; the
+        // regex tasks they (and the epilogue) queued run after both
+        HIPCHK(h, hipEventRecord(h->eve, st));
+        HIPCHK(h, hipStreamWaitEvent(h->side2, h->eve, 0));
+        task(kw_short_kernel, G[2], h->side2);
+        HIPCHK(h, hipEventRecord(h->evq, h->side2));
+        task(kw_verify_kernel, G[0], st);
+        HIPCHK(h, hipStreamWaitEvent(st, h->evq, 0));
+        task(kw_rx_task_kernel, G[3], st);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->evt, st));
@@ -1385,6 +1396,9 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->evs1) (void)hipEventDestroy(h->evs1);
     if (h->evt) (void)hipEventDestroy(h->evt);
     if (h->side) (void)hipStreamDestroy(h->side);
+    if (h->side2) (void)hipStreamDestroy(h->side2);
+    if (h->eve) (void)hipEventDestroy(h->eve);
+    if (h->evq) (void)hipEventDestroy(h->evq);
     if (h->evp) (void)hipEventDestroy(h->evp);
     delete h;
     return KW_OK;
