@@ -8,10 +8,11 @@
 //   kw_probe_kernel   one wave per filter region: the region's candidates 64 at a time, whatever document
 //                     they belong to (a document averages ~13 candidates, so per-document batches left most
 //                     lanes idle): anchor hash probe, head compare, then the (candidate, use) pairs spread
-//                     over the lanes to compare spans and test \b.  Each lane's verified uses ("items") are
-//                     staged in LDS and written out in candidate order, so a document's items are
-//                     contiguous in HBM, the text's before the title's; the header gets the first item's
-//                     index, the per-field counts are added up in ncnt.
+//                     over the lanes to compare spans and test \b.  The batch's verified uses ("items") are
+//                     appended to a wave-wide LDS pool (ballot ranks, any candidate may own hundreds of
+//                     them: a 50k-name KB has pieces shared by many names) and scattered to HBM grouped by
+//                     candidate, so a document's items are contiguous, the text's before the title's; the
+//                     header gets the first item's index, the per-field counts are added up in ncnt.
 //   kw_epi_kernel     one wave per document: all-ASCII documents are finished by the epilogue
 //                     (fk_scan_epilogue: sort, emit, queue the verify / short / regex tasks), the others get
 //                     their header for the resolve kernel, oversize ones go to the generic kernel.
@@ -36,10 +37,10 @@ constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
 constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
 constexpr int PK_BLOCK = PK_WAVES * WAVE;
-#ifndef PK_PER_LANE_CFG
-#define PK_PER_LANE_CFG 16
+#ifndef PK_POOL_CFG
+#define PK_POOL_CFG 1024
 #endif
-constexpr int PK_PER_LANE = PK_PER_LANE_CFG;   // items one candidate may stage (more: its document is deferred)
+constexpr int PK_POOL = PK_POOL_CFG;     // items one batch of 64 candidates may stage (more: their documents defer)
 #ifndef EK_MINW
 #define EK_MINW 5   // 96 VGPRs, no spill: 5 waves per SIMD (measured 9.10 vs 9.35 ms per step)
 #endif
@@ -266,13 +267,15 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
                                                             const int64_t *__restrict__ off, int32_t n_regions,
                                                             FastScratch S)
 {
-    __shared__ uint64_t stage_all[PK_WAVES * WAVE * PK_PER_LANE];
+    __shared__ uint64_t pool_all[PK_WAVES * PK_POOL];
+    __shared__ uint8_t pown_all[PK_WAVES * PK_POOL];
     __shared__ uint32_t scnt_all[PK_WAVES * WAVE];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t region = (int64_t)blockIdx.x * PK_WAVES + wib;
     if (region >= n_regions) return;
-    uint64_t *stage = stage_all + wib * WAVE * PK_PER_LANE;
+    uint64_t *pool = pool_all + wib * PK_POOL;
+    uint8_t *pown = pown_all + wib * PK_POOL;
     uint32_t *scnt = scnt_all + wib * WAVE;
     const uint4 *cand = S.cand + (size_t)region * S.cand_cap;
     const uint32_t nc = min(S.ccnt[region], S.cand_cap);
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
         }
         uint32_t tcur = rb[0], tend = re[0], b1 = rb[1], e1 = re[1], b2 = rb[2], e2 = re[2];
         bool more = valid;
-        bool ovf = false;
+        uint32_t pn = 0;                    // items in the pool (wave-uniform)
         while (__ballot(more)) {
             // stage A: up to two matching anchors of this lane's candidate
             uint32_t ub = 0, uc = 0, ub1 = 0, uc1 = 0, nm = 0;
@@ -364,6 +367,8 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
             const int ex = wave_excl_scan((int)(uc + uc1), &total);
             for (int g0 = 0; g0 < total; g0 += WAVE) {
                 const int g = g0 + lane;
+                bool pass = false;
+                uint64_t item = 0;
                 int owner = 0;
 #pragma unroll
                 for (int step = 32; step >= 1; step >>= 1) {
@@ -380,13 +385,14 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
                 const int32_t ppr = __shfl(pr, owner, WAVE);
                 const int32_t ofbr = __shfl(fbr, owner, WAVE), ofer = __shfl(fer, owner, WAVE);
                 const int64_t ot0 = rdlane64v(t0, owner);
-                if (g >= total) continue;
+                do {
+                if (g >= total) break;
                 const uint4 ur = FT.urec[u];
                 const uint32_t kind = ur.x & 0xFF, aoff = (ur.x >> 8) & 0xFF;
                 const uint32_t sblen = ur.y & 0xFFFF;
                 const uint32_t pat = ur.z;
                 const int32_t s0r = ppr - (int32_t)aoff;
-                if (s0r < ofbr || s0r + (int32_t)sblen > ofer) continue;
+                if (s0r < ofbr || s0r + (int32_t)sblen > ofer) break;
                 const int64_t s0 = ot0 + s0r, fb = ot0 + ofbr, fe2 = ot0 + ofer;
                 const uint4 u2 = FT.urec2[u];
                 const uint64_t th = load8(arena, s0);
@@ -397,32 +403,41 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
                 const uint32_t nextb = hasn ? (uint32_t)arena[s0 + sblen] : 0u;
                 const uint32_t hl = sblen < 8 ? sblen : 8;
                 const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
-                if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
-                if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) continue;
-                if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) continue;
+                if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) break;
+                if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) break;
+                if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) break;
                 if (kind == FU_UPPER) {
                     const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
                     bool wp = false;
                     if (hasp) wp = is_word_cp(T, prevb < 0x80u ? prevb : decode_before(arena, fb, s0));
-                    if (wp == wf) continue;
+                    if (wp == wf) break;
                     bool wn = false;
                     if (hasn) {
                         uint32_t ch = nextb;
                         if (nextb >= 0x80u) decode_at(arena, s0 + sblen, fe2, &ch);
                         wn = is_word_cp(T, ch);
                     }
-                    if (wn == wl) continue;
+                    if (wn == wl) break;
                 }
-                const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(uint32_t)(s0r - ofbr) << IT_POS_SHIFT) |
-                                      ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
-                const uint32_t k = atomicAdd(&scnt[owner], 1u);
-                if (k < (uint32_t)PK_PER_LANE) stage[owner * PK_PER_LANE + k] = item;
+                item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(uint32_t)(s0r - ofbr) << IT_POS_SHIFT) |
+                       ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
+                pass = true;
+                } while (0);
+                // append to the pool: rank by ballot, the owner's count by an LDS atomic
+                const uint64_t pm = __ballot(pass);
+                if (pass) {
+                    const uint32_t k = pn + (uint32_t)__builtin_popcountll(pm & ((1ull << lane) - 1));
+                    if (k < (uint32_t)PK_POOL) { pool[k] = item; pown[k] = (uint8_t)owner; }
+                    atomicAdd(&scnt[owner], 1u);
+                }
+                pn += (uint32_t)__builtin_popcountll(pm);
             }
             wave_sync();
         }
-        // the batch's items, in candidate order
-        uint32_t nmine = scnt[lane];
-        if (nmine > (uint32_t)PK_PER_LANE) { ovf = true; nmine = PK_PER_LANE; }
+        // the batch's items grouped by candidate (candidate order; any order within a candidate, the
+        // epilogue sorts): lane L's items start at icur + (items of lanes < L)
+        const uint32_t nmine = scnt[lane];
+        const bool ovf = pn > (uint32_t)PK_POOL;   // the pool dropped items: the batch's documents defer
         int itotal;
         const int iex = wave_excl_scan((int)nmine, &itotal);
         const uint64_t withm = __ballot(nmine > 0);
@@ -433,15 +448,20 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
             const uint32_t prev_doc = prevm ? pdoc : last_doc;
             if (nmine > 0) {
                 if (doc != prev_doc) S.hdr[doc].x = ibase + icur + (uint32_t)iex;
-                atomicAdd(f ? &S.ncnt[doc].y : &S.ncnt[doc].x, scnt[lane]);
-                for (uint32_t k = 0; k < nmine; ++k) {
-                    const uint32_t idx = icur + (uint32_t)iex + k;
-                    if (idx < icap) items[idx] = stage[lane * PK_PER_LANE + k];
-                }
+                atomicAdd(f ? &S.ncnt[doc].y : &S.ncnt[doc].x, nmine);
+                if (ovf) atomicOr(&S.dflags[doc], DH_DEFER);
             }
             last_doc = (uint32_t)__shfl((int)doc, 63 - __builtin_clzll(withm), WAVE);
+            if (!ovf) {
+                scnt[lane] = icur + (uint32_t)iex;   // the next free slot of the lane's items
+                wave_sync();
+                for (uint32_t j = (uint32_t)lane; j < pn; j += WAVE) {
+                    const uint32_t idx = atomicAdd(&scnt[pown[j]], 1u);
+                    if (idx < icap) items[idx] = pool[j];
+                }
+                wave_sync();
+            }
         }
-        if (ovf) atomicOr(&S.dflags[doc], DH_DEFER);
         icur += (uint32_t)itotal;
         scnt[lane] = 0;
         wave_sync();
