@@ -76,6 +76,7 @@ struct kw_handle {
     bool fetched = false;
     int64_t n_hits = 0;
     unsigned long long stats[KW_N_STATS] = {0};
+    int rescans = 0;   // scans of the last kw_scan's batch redone after growing a buffer
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     int cus = 256;
     int blocks_per_cu = 2;
@@ -91,7 +92,7 @@ struct kw_handle {
     uint32_t *out_cnt_all = nullptr;   // counts of every result region (scan, task, resolve, generic)
     kw_hit *out_all = nullptr;
     int64_t hdr_cap = 0;
-    int items_blocks_per_cu = 1, resolve_blocks_per_cu = 1;
+    int resolve_blocks_per_cu = 1;
     int filter_blocks_per_cu = 1, probe_blocks_per_cu = 1, epi_blocks_per_cu = 1;
     int ns = 0;                        // filter regions of the last launch
     hipEvent_t evf = nullptr, evp = nullptr;   // after the filter / probe kernels
@@ -916,9 +917,6 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_scan_kernel, BLOCK, kScanLds));
     h->blocks_per_cu = bpc > 0 ? bpc : 1;
     bpc = 0;
-    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_items_kernel, FK_BLOCK, 0));
-    h->items_blocks_per_cu = bpc > 0 ? bpc : 1;
-    bpc = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_resolve_kernel, RK_BLOCK, 0));
     h->resolve_blocks_per_cu = bpc > 0 ? bpc : 1;
     bpc = 0;
@@ -967,7 +965,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     const size_t nw = (size_t)2 * c.nk + c.nr + c.ng;
     const size_t per_tasks = (size_t)(c.vcap + c.ecap + c.scap + c.xcap) * 16;
     size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_fblk) +
-                   nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 4 +
+                   nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 8 +
                    (size_t)c.ns * c.cand_cap * 16 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 12 + 4 * 256 +
                    (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
                    32 * 256;
@@ -990,6 +988,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.dflags = (uint32_t *)carve((size_t)c.hdr_cap * 4);
     h->FS.hdr = (uint2 *)carve((size_t)c.hdr_cap * 8);
     h->FS.defer_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
+    h->FS.big_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
     h->FS.rx_tasks = (uint4 *)carve((size_t)c.nr * c.rx_cap * 16);
     h->FS.rx_cap = c.rx_cap;
     h->FS.vq = (uint4 *)carve((size_t)c.nk * c.vcap * 16);
@@ -1013,6 +1012,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->S.status = (uint32_t *)q;                        // 4 x u32
     h->FS.status = h->S.status;
     h->FS.defer_cnt = (uint32_t *)(q + 16);
+    h->FS.big_cnt = (uint32_t *)(q + 20);               // 2 x u32: all-ASCII, non-ASCII big documents
     h->FS.tmax = (uint32_t *)(q + 32);                  // 4 x u32
     h->FS.cmax = (uint32_t *)(q + 48);                  // 2 x u32
     h->S.gmax = (uint32_t *)(q + 56);                   // 2 x u32
@@ -1129,12 +1129,19 @@ static int launch_scan(kw_handle *h)
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, h->side, h->FT, h->T, h->arena, h->doc_off,
                            n_docs, h->FS, h->S);
+        // its documents with more items than its LDS holds: one wave each, wave w in resolve wave w's regions
+        hipLaunchKernelGGL(kw_resolve_big_kernel, dim3(std::min(nrb * RK_WAVES, h->cus * 4)), dim3(WAVE), 0, h->side,
+                           h->FT, h->T, h->arena, h->doc_off, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->evs1, h->side));
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
                            h->FS, h->S);
+        // the documents with more items than the epilogue's LDS holds: one wave each (grid-stride), wave w in
+        // epilogue wave w's regions; one resident round of workgroups (most exit at once: the list is short)
+        hipLaunchKernelGGL(kw_epi_big_kernel, dim3(std::min(n_epi, h->cus * 4)), dim3(WAVE), 0, st, h->FT, h->arena,
+                           h->doc_off, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
     h->ns = n_regions;
@@ -1196,6 +1203,7 @@ extern "C" int kw_scan(kw_handle *h, const uint8_t *d_arena, const int64_t *d_do
     h->stream = (hipStream_t)stream;
     h->scanned = true;
     h->fetched = false;
+    h->rescans = 0;
     return launch_scan(h);
 }
 
@@ -1234,6 +1242,7 @@ static int finish(kw_handle *h)
             h->caps.ng = w.ng;   // the generic wave count may shrink
             int rc = ensure_scratch(h, w);
             if (rc) return rc;
+            ++h->rescans;
             rc = launch_scan(h);
             if (rc) return rc;
             continue;
@@ -1266,6 +1275,7 @@ static int finish(kw_handle *h)
             }
             int rc = ensure_scratch(h, w);
             if (rc) return rc;
+            ++h->rescans;
             rc = launch_scan(h);
             if (rc) return rc;
             continue;
@@ -1280,11 +1290,10 @@ static int finish(kw_handle *h)
         h->stats[2] = fst[2] + gst[2];
         h->stats[3] = fst[3];
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
-        if (getenv("KW_DUMP_TIMING")) {   // FK_TIMING builds: scan-kernel cycles summed over waves
-            fprintf(stderr, "KW_TIMING probe %llu epilogue %llu total %llu batches %llu rounds %llu pairs %llu chunks %llu "
-                            "inner %llu | resolve decode %llu edge %llu items %llu short %llu regex %llu all %llu\n", fst[13], fst[14],
-                    fst[15], fst[16], fst[17], fst[18], fst[19], fst[20], fst[21], fst[22], fst[23], fst[24], fst[25],
-                    fst[26]);
+        h->stats[17] = (unsigned long long)h->rescans;
+        if (getenv("KW_DUMP_TIMING")) {   // FK_TIMING builds: resolve-kernel cycles summed over waves
+            fprintf(stderr, "KW_TIMING resolve decode %llu edge %llu items %llu short %llu regex %llu all %llu\n", fst[21],
+                    fst[22], fst[23], fst[24], fst[25], fst[26]);
             fprintf(stderr, "KW_TASKS verify %llu edge %llu short %llu regex %llu edge_docs %llu\n", fst[27], fst[28], fst[29],
                     fst[30], fst[31]);
         }

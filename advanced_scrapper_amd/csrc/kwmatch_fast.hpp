@@ -1,4 +1,4 @@
-// Fast path of libkwmatch (gfx950): a lean byte scan (kw_items_kernel) that
+// Fast path of libkwmatch (gfx950): a lean byte scan (kwmatch_split.hpp: filter, probe, epilogue) that
 // turns every anchor occurrence into an item, and a resolve kernel
 // (kw_resolve_kernel) that decides the names of each field from its items.
 //
@@ -32,20 +32,16 @@
 
 namespace kw {
 
-#ifndef FK_WAVES_CFG
-#define FK_WAVES_CFG 16
-#endif
-constexpr int FK_WAVES = FK_WAVES_CFG;           // waves per scan workgroup (one workgroup per CU: LDS)
-constexpr int FK_BLOCK = FK_WAVES * WAVE;
 constexpr int FK_FILT_WORDS = 8192;             // stage 1: 2^18 bits = 32 KB
 constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
 constexpr int FK_T3_BITS = 16;                  // stage 2, 3-byte keys: 8 KB
 constexpr int FK_B2_WORDS = 2048;               // exact bigram table: 8 KB
 constexpr int FK_EDGE_BITS = 20;                // edge prefix / suffix 8-byte keys: 2 x 128 KB (global, L2)
-constexpr int FK_Q = 128;                       // per-wave ring of stage-2 survivors (power of 2)
 constexpr int FK_ITEMS0 = 512;                  // items of field 0 (text) on the fast path (power of 2: LDS sort)
 constexpr int FK_ITEMS1 = 64;                   // items of field 1 (title)
 constexpr int FK_ITEMS_MAX = FK_ITEMS0;         // one field's item buffer in the resolve kernel
+constexpr int FK_BIG0 = 4096;                   // items of the text / title in the big-document epilogue
+constexpr int FK_BIG1 = 512;                    //   (kw_epi_big_kernel, 36 KiB of LDS per wave)
 constexpr int FK_CP_CAP = 16384;                // bytes of a non-ASCII field the fast path decodes
 constexpr int RK_WAVES = 4;                     // waves per resolve workgroup
 constexpr int RK_BLOCK = RK_WAVES * WAVE;
@@ -146,6 +142,8 @@ struct FastScratch {
     uint32_t *defer_list;       // docs sent to the generic kernel
     uint32_t *defer_cnt;
     uint32_t defer_cap;
+    uint32_t *big_list;         // docs with more items than the epilogue / resolve kernels hold (defer_cap):
+    uint32_t *big_cnt;          //   all-ASCII ones from the head ([0]), non-ASCII ones from the tail ([1])
     uint32_t *status;
     unsigned long long *stats;  // see kw_stats
     uint4 *rx_tasks;            // per resolve wave: rx_cap regex-position tasks (doc, field|ascii, pattern, n)

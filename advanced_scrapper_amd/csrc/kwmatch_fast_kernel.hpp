@@ -1,8 +1,7 @@
 // Fast path kernels (see kwmatch_fast.hpp).  Included after kwmatch_kernels.hpp
 // (shares its wave/text helpers).
 //
-//   kw_items_kernel    one wave per document: LDS filters over every byte,
-//                      anchor probes, items -> HBM, per-document header
+//   (the byte scan -- filter, anchor probe, all-ASCII epilogue -- is kwmatch_split.hpp)
 //   kw_resolve_kernel  one wave per document with work: sort the items of a
 //                      field, decide fuzzy names (exact / edge / LCS-verified
 //                      pieces), report re.finditer positions
@@ -27,7 +26,7 @@
 #define FK_NOPROBE 0
 #endif
 // waves per SIMD the resolve kernel is compiled for (register budget)
-#ifndef FK_TIMING   // developer aid: per-phase cycle counters of the scan kernel (stats 13..15)
+#ifndef FK_TIMING   // developer aid: per-phase cycle counters of the resolve kernel (KW_DUMP_TIMING)
 #define FK_TIMING 0
 #endif
 #define FK_T0(v) const unsigned long long v = FK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
@@ -119,168 +118,6 @@ __device__ __forceinline__ bool span_equal(const uint8_t *__restrict__ a, int64_
     for (; i < len; ++i)
         if (a[p + i] != pat[i]) return false;
     return true;
-}
-
-// ---------------------------------------------------------------- probe a batch of candidates
-// Candidate entry (stage-2 survivor): x = position relative to the document << 3 | try2 << 2 | try3 << 1 |
-// try4 (which anchor lengths to look up), y = the 4 bytes at the position.
-//
-// Stage A (lane = candidate): hash-probe the anchor table and step to the
-// lane's next anchor whose <= 8 head bytes match the text.  Stage B (lane =
-// (candidate, use) pair): the matched anchors' uses are spread over the lanes
-// by a wave prefix sum, so a popular anchor with many uses does not serialise
-// one lane; each use compares the first / last 8 bytes of its span (and the
-// middle when the span is longer than 16 bytes), then \b for uppercase names.
-struct ProbeCounters {   // FK_TIMING builds: probe batches, stage-A rounds, stage-B pairs / chunks, stage-A steps
-    unsigned long long batches, rounds, pairs, chunks, inner, edge_docs;
-};
-
-__device__ __forceinline__ void fast_probe_batch(const FastTables &FT, const DevTables &T, const FastDoc &D,
-                                                 const uint2 *ring, uint32_t head, uint32_t cnt, uint64_t *items,
-                                                 uint32_t *icnt, uint32_t &nanchor, ProbeCounters &PC)
-{
-    if (FK_STAGE < 1 || FK_NOPROBE) return;
-    if (FK_TIMING) ++PC.batches;
-    const int lane = lane_id();
-    const uint8_t *__restrict__ arena = D.arena;
-    const bool valid = lane < (int)cnt;
-    const uint2 e = valid ? ring[(head + (uint32_t)lane) & (FK_Q - 1)] : make_uint2(0u, 0u);
-    // document-relative 32-bit positions; p only for the loads
-    const int32_t pr = (int32_t)(e.x >> 3);
-    const int32_t fer = pr < D.l1 ? D.l1 : D.l2;
-    const int64_t p = D.t0 + pr;
-    const uint32_t hi = valid ? ld_u32_unaligned(arena, p + 4) : 0u;
-    const uint64_t h8 = (uint64_t)e.y | ((uint64_t)hi << 32);
-    // the hash lookups of the lane's key lengths 4, 3, 2 (try bits 0, 1, 2) go out together
-    uint32_t rb[3], re[3];
-    {
-        uint4 hs[3];
-        uint64_t key[3];
-        uint32_t slot[3];
-        bool want[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int Lk = 4 - i;
-            want[i] = valid && ((e.x >> i) & 1u) && pr + Lk <= fer;
-            key[i] = ((uint64_t)Lk << 32) | (h8 & ((1ull << (8 * Lk)) - 1));
-            slot[i] = fk_ht_slot(key[i], FT.ht_mask);
-            hs[i] = want[i] ? FT.ht4[slot[i]] : make_uint4(~0u, ~0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            rb[i] = re[i] = 0;
-            for (;;) {
-                const uint64_t kk = (uint64_t)hs[i].x | ((uint64_t)hs[i].y << 32);
-                if (kk == key[i]) { rb[i] = hs[i].z; re[i] = hs[i].z + hs[i].w; break; }
-                if (kk == ~0ull) break;
-                slot[i] = (slot[i] + 1) & FT.ht_mask;
-                hs[i] = FT.ht4[slot[i]];
-            }
-        }
-    }
-    // anchor records still to test: [tcur, tend), then [rb[1], re[1]), then [rb[2], re[2])
-    uint32_t tcur = rb[0], tend = re[0], b1 = rb[1], e1 = re[1], b2 = rb[2], e2 = re[2];
-    bool more = valid;
-    while (__ballot(more)) {
-        // stage A: up to two matching anchors of this lane's candidate
-        uint32_t ub = 0, uc = 0, ub1 = 0, uc1 = 0, nm = 0;
-        if (FK_TIMING) ++PC.rounds;
-        while (more && nm < 2) {
-            if (FK_TIMING) ++PC.inner;
-            if (tcur < tend) {
-                // two anchor records per step, both loads in flight together
-                const uint4 ar0 = FT.arec[tcur];
-                const bool two = tcur + 1 < tend;
-                const uint4 ar1 = two ? FT.arec[tcur + 1] : make_uint4(0u, 0u, 0u, 0u);
-                auto take = [&](const uint4 &ar) {
-                    const uint32_t alen = ar.w & 0xFFu;
-                    if (pr + (int32_t)alen > fer) return;
-                    const uint64_t m8 = alen >= 8 ? ~0ull : ((1ull << (8 * alen)) - 1);
-                    if ((h8 ^ ((uint64_t)ar.x | ((uint64_t)ar.y << 32))) & m8) return;
-                    ++nanchor;
-                    if (nm == 0) { ub = ar.z; uc = ar.w >> 8; }
-                    else { ub1 = ar.z; uc1 = ar.w >> 8; }
-                    ++nm;
-                };
-                take(ar0);
-                ++tcur;
-                if (two && nm < 2) {
-                    take(ar1);
-                    ++tcur;
-                }
-                continue;
-            }
-            if (b1 >= e1 && b2 >= e2) { more = false; break; }
-            tcur = b1; tend = e1;
-            b1 = b2; e1 = e2;
-            b2 = e2 = 0;
-        }
-        // stage B: (candidate, use) pairs over the lanes
-        int total;
-        const int ex = wave_excl_scan((int)(uc + uc1), &total);
-        if (FK_TIMING) PC.pairs += (unsigned long long)total;
-        for (int c0 = 0; c0 < total; c0 += WAVE) {
-            if (FK_TIMING) ++PC.chunks;
-            const int g = c0 + lane;
-            int owner = 0;   // the last lane whose prefix <= g
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-                const int cand = owner + step;
-                const int exc = __shfl(ex, cand & 63, WAVE);
-                if (cand < WAVE && exc <= g) owner = cand;
-            }
-            const int exo = __shfl(ex, owner, WAVE);
-            const uint32_t oub = (uint32_t)__shfl((int)ub, owner, WAVE);
-            const uint32_t ouc = (uint32_t)__shfl((int)uc, owner, WAVE);
-            const uint32_t oub1 = (uint32_t)__shfl((int)ub1, owner, WAVE);
-            const uint32_t loc = (uint32_t)(g - exo);
-            const uint32_t u = loc < ouc ? oub + loc : oub1 + (loc - ouc);
-            const int32_t ppr = __shfl(pr, owner, WAVE);
-            if (g >= total) continue;
-            const int f = ppr < D.l1 ? 0 : 1;
-            const int32_t fbr = f ? D.l1 : 0, fer2 = f ? D.l2 : D.l1;
-            const uint4 ur = FT.urec[u];
-            const uint32_t kind = ur.x & 0xFF, aoff = (ur.x >> 8) & 0xFF;
-            const uint32_t sblen = ur.y & 0xFFFF;
-            const uint32_t pat = ur.z;
-            const int32_t s0r = ppr - (int32_t)aoff;
-            if (s0r < fbr || s0r + (int32_t)sblen > fer2) continue;
-            const int64_t s0 = D.t0 + s0r, fb = D.t0 + fbr, fe2 = D.t0 + fer2;
-            // the use's head / tail words, the span's text and the name's info go out together (one
-            // memory latency instead of three dependent ones)
-            const uint4 u2 = FT.urec2[u];
-            const uint64_t th = load8(arena, s0);
-            const uint64_t tt = load8(arena, s0 + (sblen > 8 ? sblen - 8 : 0));
-            const uint32_t pi = kind == FU_UPPER ? FT.pat_info[pat] : 0u;
-            // the neighbours of an uppercase name (\b), fetched with the rest: ASCII ones need nothing more
-            const bool hasp = kind == FU_UPPER && s0 > fb, hasn = kind == FU_UPPER && s0 + (int64_t)sblen < fe2;
-            const uint32_t prevb = hasp ? (uint32_t)arena[s0 - 1] : 0u;
-            const uint32_t nextb = hasn ? (uint32_t)arena[s0 + sblen] : 0u;
-            const uint32_t hl = sblen < 8 ? sblen : 8;
-            const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
-            if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) continue;
-            if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) continue;
-            if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) continue;
-            if (kind == FU_UPPER) {
-                const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
-                bool wp = false;
-                if (hasp) wp = is_word_cp(T, prevb < 0x80u ? prevb : decode_before(arena, fb, s0));
-                if (wp == wf) continue;
-                bool wn = false;
-                if (hasn) {
-                    uint32_t ch = nextb;
-                    if (nextb >= 0x80u) decode_at(arena, s0 + sblen, fe2, &ch);
-                    wn = is_word_cp(T, ch);
-                }
-                if (wn == wl) continue;
-            }
-            const uint64_t item = ((uint64_t)pat << IT_PAT_SHIFT) | ((uint64_t)(uint32_t)(s0r - fbr) << IT_POS_SHIFT) |
-                                  ((uint64_t)kind << IT_KIND_SHIFT) | (uint64_t)u;
-            const uint32_t idx = atomicAdd(&icnt[f], 1u);
-            if (idx < (uint32_t)(f ? FK_ITEMS1 : FK_ITEMS0)) items[(f ? FK_ITEMS0 : 0) + idx] = item;
-            else atomicOr(&icnt[2], 1u);
-        }
-    }
 }
 
 // ---------------------------------------------------------------- field helpers
@@ -540,6 +377,7 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, uint32_t nmr, uint32_t 
 // name needs an exact occurrence, which the FULL use finds).  Lanes 0..19 take
 // (side, L = m-1): hash the window, look it up among the one-deletion variants,
 // verify exactly and append an EDGE item.  Returns the number of items added.
+template <uint32_t ICAP>
 __device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint64_t *items, uint32_t *icnt_f,
                                   uint32_t *dflag)
 {
@@ -602,7 +440,7 @@ __device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint6
             }
             if (!eq) continue;
             const uint32_t idx = atomicAdd(icnt_f, 1u);
-            if (idx < (uint32_t)FK_ITEMS_MAX)
+            if (idx < ICAP)
                 items[idx] = ((uint64_t)P << IT_PAT_SHIFT) | ((uint64_t)FU_EDGE << IT_KIND_SHIFT);
             else
                 atomicOr(dflag, 1u);
@@ -886,6 +724,7 @@ __device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const
 // ---------------------------------------------------------------- fast resolve of one field
 // Returns 0 when done, 1 if the field is a long non-ASCII field and 3 if the
 // items overflowed: the document then goes to the generic kernel.
+template <uint32_t ICAP>
 __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const DevScratch &GS, FieldCtx &F, OutCtx &O,
                                  uint64_t *items_lds, uint32_t *icnt_f, uint32_t *dflag, uint32_t *cps,
                                  uint32_t *blkcnt, uint64_t *rxtab, RxQueue &RQ, bool maybe_nonascii, bool edge,
@@ -910,7 +749,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     const bool is_short = !(RK_SKIP & 1) && F.n <= (uint32_t)MAXM;
     // ---- one-deletion edge windows of the 11..20-code-point names (prefiltered by the scan)
     if (!(RK_SKIP & 2) && edge && F.n >= EDGE_MIN_M + 1) {
-        uint32_t added = fk_edge_items(FT, F, items_lds, icnt_f, dflag);
+        uint32_t added = fk_edge_items<ICAP>(FT, F, items_lds, icnt_f, dflag);
         added = (uint32_t)wave_sum((int)added);
         if (added) {
             nedge += added;
@@ -1115,16 +954,24 @@ __device__ __forceinline__ bool fk_long_run(const uint64_t *a, uint32_t n)
 }
 
 // Finish an all-ASCII document in the scan kernel.  items: the wave's LDS item lists (field 0 at 0,
-// field 1 at FK_ITEMS0), n0 / n1 items.  Returns false, before anything is emitted, when a name has
-// more than 64 items in the text (the generic kernel takes the document).
+// field 1 at f1off; each buffer holds the next power of two of its count), n0 / n1 items.  Returns
+// false, before anything is emitted, when a name has more than 64 items in a field (the generic kernel
+// takes the document).
+template <uint32_t F1OFF = FK_ITEMS0>
 __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D,
                                  uint64_t *items, uint32_t n0, uint32_t n1, uint32_t flags, int64_t wave, OutCtx &O,
                                  TaskCounts &TC)
 {
+    constexpr uint32_t f1off = F1OFF;
     const int lane = lane_id();
-    if (n0 > (uint32_t)WAVE) {   // the text's items sorted first: the deferral test precedes every emission
+    // the fields' items sorted first: the deferral test precedes every emission
+    if (n0 > (uint32_t)WAVE) {
         wave_sort_lds(items, n0);
         if (fk_long_run(items, n0)) return false;
+    }
+    if (F1OFF != FK_ITEMS0 && n1 > (uint32_t)WAVE) {   // (big documents only: the epilogue kernel holds <= 64)
+        wave_sort_lds(items + f1off, n1);
+        if (fk_long_run(items + f1off, n1)) return false;
     }
     uint4 *vq = S.vq + (size_t)wave * S.vcap;
     uint4 *sq = S.sq + (size_t)wave * S.scap, *xq = S.xq + (size_t)wave * S.xcap;
@@ -1140,10 +987,9 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
         F.doc = D.doc;
         F.field = f;
         const uint32_t N = f ? n1 : n0;
-        uint64_t *its = items + (f ? FK_ITEMS0 : 0);
+        uint64_t *its = items + (f ? f1off : 0);
         if (F.n <= (uint32_t)MAXM) task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
         if (N == 0) continue;
-        if (f && N > (uint32_t)WAVE) wave_sort_lds(its, N);   // (field 1 holds at most FK_ITEMS1 = 64)
         for (uint32_t bs = 0; bs < N;) {
             uint32_t be = N;
             if (N > (uint32_t)WAVE) {
@@ -1910,403 +1756,159 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, Dev
     task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
 }
 
-// ---------------------------------------------------------------- kernel 1: the scan
-// tile shape for `rem` bytes left in the document: positions per lane (64 lanes x 16 / 8 / 4 bytes)
-__device__ __forceinline__ int fk_shape(int64_t rem) { return rem > 512 ? 16 : (rem > 256 ? 8 : 4); }
-
-// one tile's loads: S bytes per lane at blk + lane * S (blk is 16-byte aligned), and the word after
-// the tile for the last lane; zero past the document end
-__device__ __forceinline__ void fk_tile_load(const uint8_t *__restrict__ arena, int64_t blk, int S, int64_t end,
-                                             int lane, uint4 &nv, uint32_t &nw4)
-{
-    nv = make_uint4(0u, 0u, 0u, 0u);
-    nw4 = 0;
-    const int64_t a = blk + (int64_t)lane * S;
-    if (a < end) {
-        if (S == 16) {
-            nv = *(const uint4 *)(arena + a);
-        } else if (S == 8) {
-            const uint2 v = *(const uint2 *)(arena + a);
-            nv.x = v.x;
-            nv.y = v.y;
-        } else {
-            nv.x = *(const uint32_t *)(arena + a);
-        }
-    }
-    if (lane == WAVE - 1 && blk + (int64_t)WAVE * S < end) nw4 = *(const uint32_t *)(arena + blk + (int64_t)WAVE * S);
-}
-
-struct __attribute__((aligned(16))) ItemsLds {
-    uint32_t filt[FK_FILT_WORDS];
-    uint32_t l2[FK_L2_WORDS];
-    uint32_t t3[FK_T3_WORDS];
-    uint32_t b2[FK_B2_WORDS];
-    uint64_t items[FK_WAVES * (FK_ITEMS0 + FK_ITEMS1)];
-    uint2 ring[FK_WAVES * FK_Q];
-    uint32_t cnt[FK_WAVES * 4];
-};
-
-__global__ __launch_bounds__(FK_BLOCK) void kw_items_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
-                                                            const int64_t *__restrict__ off, int64_t n_docs,
-                                                            FastScratch S, DevScratch GS)
-{
-    // one static LDS block, the filters first: their addresses are constants below 64 KiB that fold
-    // into the ds_read offset field (no per-position address add)
-    __shared__ ItemsLds L;
-    uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
-    uint64_t *items_all = L.items;
-    uint2 *ring_all = L.ring;
-    uint32_t *cnt_all = L.cnt;
-
-    for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FK_BLOCK) filt[i] = FT.filt[i];
-    for (int i = threadIdx.x; i < FK_L2_WORDS; i += FK_BLOCK) l2[i] = FT.l2[i];
-    for (int i = threadIdx.x; i < FK_T3_WORDS; i += FK_BLOCK) t3[i] = FT.t3[i];
-    for (int i = threadIdx.x; i < FK_B2_WORDS; i += FK_BLOCK) b2[i] = FT.b2[i];
-    __syncthreads();
-
-    const int lane = lane_id();
-    const int wib = threadIdx.x / WAVE;
-    const int64_t wave = (int64_t)blockIdx.x * FK_WAVES + wib;
-    const int64_t n_waves = (int64_t)gridDim.x * FK_WAVES;
-    uint64_t *items = items_all + wib * (FK_ITEMS0 + FK_ITEMS1);
-    uint2 *ring = ring_all + wib * FK_Q;
-    uint32_t *icnt = cnt_all + wib * 4;       // [0],[1] item counts, [2] defer flag
-    uint64_t *gitems = S.items + (size_t)wave * S.item_cap;
-    uint32_t cursor = 0;                      // items this wave wrote to HBM
-    uint32_t ncand = 0, ncand2 = 0, nanchor = 0, ndefer = 0, ndef_items = 0;   // per-wave totals fit 32 bits
-    const bool has_t3 = FT.has_t3 != 0;
-    OutCtx O;                                 // hits of the documents this wave finishes itself
-    O.shared = nullptr;
-    O.out = S.kout + (size_t)wave * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = 0;
-    TaskCounts TC = {0u, 0u, 0u, 0u};
-
-    // the next document's offsets are loaded one document ahead (lanes 0..2)
-    int64_t pf_off = (lane < 3 && wave < n_docs) ? off[2 * wave + lane] : 0;
-    // the 2-byte gate's byte ranges as SWAR constants (wave-uniform, loaded once)
-    const int n_gate = FT.n_gate;
-    uint32_t gate_a[4], gate_b[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        gate_a[r] = (0x80u - FT.gate_lo[r]) * 0x01010101u;
-        gate_b[r] = (0x7Fu - FT.gate_hi[r]) * 0x01010101u;
-    }
-    unsigned long long t_probe = 0, t_epi = 0;
-    ProbeCounters PC = {0, 0, 0, 0, 0, 0};
-    FK_T0(t_all0);
-    for (int64_t d = wave; d < n_docs; d += n_waves) {
-        FastDoc D;
-        D.arena = arena;
-        D.t0 = rdlane64(pf_off, 0);
-        D.t1 = rdlane64(pf_off, 1);
-        D.t2 = rdlane64(pf_off, 2);
-        D.doc = (uint32_t)d;
-        D.l1 = (int32_t)(D.t1 - D.t0);
-        D.l2 = (int32_t)(D.t2 - D.t0);
-        pf_off = (lane < 3 && d + n_waves < n_docs) ? off[2 * (d + n_waves) + lane] : 0;
-        if (lane < 4) icnt[lane] = 0;
-        bool defer = (D.t1 - D.t0 > MAX_FIELD_BYTES) || (D.t2 - D.t1 > MAX_FIELD_BYTES);
-        const int64_t base = D.t0 & ~(int64_t)15;
-        // the first tile's loads, in flight with the edge prefilter's
-        int shp = fk_shape(D.t2 - base);         // positions per lane of the tile in flight
-        const int32_t dl1 = D.l1, dl2 = D.l2;   // field ends, doc-relative
-        uint4 nv;
-        uint32_t nw4;
-        fk_tile_load(arena, base, shp, D.t2, lane, nv, nw4);
-        wave_sync();
-        // edge prefilter: first / last eight bytes of each field (lanes 0..3) against the global
-        // bitmaps; the word is fetched now and tested at the document's end
-        uint32_t flags = 0;
-        uint32_t ebits = 0, ebit = 0;
-        {
-            const int f = lane >> 1;
-            const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
-            if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
-                const int64_t a = (lane & 1) ? fe - 8 : fb;
-                const uint64_t k = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
-                const uint32_t idx = fk_edge_index(k);
-                ebit = idx & 31u;
-                ebits = ((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5];
-            }
-        }
-        bool na0 = false, na1 = false;
-        uint32_t qh = 0, qt = 0;                 // ring head / tail (wave-uniform)
-        for (int64_t blk = base, nblk = 0; blk < D.t2 && !defer; blk = nblk) {
-            // tile shape: Sc positions per lane (16, or 8 / 4 for a document's last few hundred bytes,
-            // so the tail tile does not pay for 1 KiB of filter work); ng words per lane
-            const int Sc = shp, ng = Sc >> 2;
-            const int64_t lp = blk + lane * Sc;
-            uint32_t W[5];
-            {
-                const uint32_t nx = (uint32_t)__shfl_down((int)nv.x, 1, WAVE);
-                const uint32_t tail = lane == WAVE - 1 ? nw4 : nx;
-                W[0] = nv.x;
-                W[1] = ng > 1 ? nv.y : tail;
-                W[2] = ng > 2 ? nv.z : (ng == 2 ? tail : 0u);
-                W[3] = ng > 2 ? nv.w : 0u;
-                W[4] = ng > 2 ? tail : 0u;
-            }
-            // the next tile's loads (double buffer)
-            nblk = blk + (int64_t)WAVE * Sc;
-            shp = fk_shape(D.t2 - nblk);
-            fk_tile_load(arena, nblk, shp, D.t2, lane, nv, nw4);
-            // lane-local position masks
-            // document-relative 32-bit positions (a document is far below 2^31 bytes)
-            const int32_t lrel = (int32_t)(lp - D.t0);
-            const int32_t rel0 = -lrel, rel2 = dl2 - lrel, rel1 = dl1 - lrel;
-            const int jlo = rel0 <= 0 ? 0 : (rel0 >= Sc ? Sc : (int)rel0);
-            const int jhi = rel2 <= 0 ? 0 : (rel2 >= Sc ? Sc : (int)rel2);
-            uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
-            // a 2-byte match cannot start on the last byte of a field
-            if (rel1 - 1 >= 0 && rel1 - 1 < Sc) valid &= ~(1u << (rel1 - 1));
-            if (rel2 - 1 >= 0 && rel2 - 1 < Sc) valid &= ~(1u << (rel2 - 1));
-            // non-ASCII bytes, attributed exactly to their field
-            if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
-                uint32_t hb = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t x = (W[k] >> 7) & 0x01010101u;   // bit 0 of each byte = its high bit
-                    hb |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
-                }
-                const int j1 = rel1 <= 0 ? 0 : (rel1 >= Sc ? Sc : (int)rel1);
-                const uint32_t in0 = ((1u << j1) - 1u) & ~((1u << jlo) - 1u);
-                const uint32_t in1 = (jhi > j1) ? (((1u << jhi) - 1u) & ~((1u << j1) - 1u)) : 0u;
-                if (hb & in0) na0 = true;
-                if (hb & in1) na1 = true;
-            }
-            uint32_t hit = 0, gate = 0;
-            if (FK_GATE_ALL && n_gate != 0) {
-                // stage 1 and the exact bigram table of the 2-byte anchors at every position; the
-                // LDS reads of four positions are issued together (eight in flight) before their bits
-                // are taken
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    if (g >= ng) break;
-                    uint32_t fw[4], bw[4];
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
-                        fw[jj] = filt[fk_word(key)];
-                        bw[jj] = b2[fk_b2_index(key) >> 5];
-                    }
-                    if (FK_SCHED) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const int j = 4 * g + jj;
-                        const uint32_t key = __builtin_amdgcn_alignbyte(W[g + 1], W[g], jj);
-                        // v_bfe_u32 + v_lshl_or_b32 per bit; the bfe offset is taken mod 32 (hardware and
-                        // LLVM agree), so the b2 bit index needs no mask
-                        hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit(key), 1) << j;
-                        gate |= __builtin_amdgcn_ubfe(bw[jj], fk_b2_index(key), 1) << j;
-                    }
-                }
-                gate &= valid;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    if (j >= Sc) break;
-                    const uint32_t key = __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3);
-                    const uint32_t w = filt[fk_word(key)];
-                    hit |= ((w >> fk_bit(key)) & 1u) << j;
-                }
-            }
-            hit &= valid;
-            // 2-byte anchors: byte-class gate, then the exact bigram table
-            if (!FK_GATE_ALL && n_gate != 0) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t w = W[k];
-                    uint32_t in80 = 0;
-                    if (n_gate < 0) {
-                        in80 = 0x80808080u;
-                    } else {
-                        const uint32_t t = w & 0x7F7F7F7Fu;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            if (r < n_gate) in80 |= (t + gate_a[r]) & ~(t + gate_b[r]) & ~w & 0x80808080u;
-                        }
-                    }
-                    while (in80) {
-                        const int bi = __builtin_ctz(in80) >> 3;
-                        in80 &= in80 - 1;
-                        const int j = 4 * k + bi;
-                        const uint32_t key = __builtin_amdgcn_alignbyte(W[k + 1], W[k], bi) & 0xFFFFu;
-                        const uint32_t x = fk_b2_index(key);
-                        if ((b2[x >> 5] >> (x & 31)) & 1u) gate |= 1u << j;
-                    }
-                }
-                gate &= valid;
-            }
-            ncand += (uint32_t)__popc(hit);
-            // stage 2 on the stage-1 hits: independent hashes of the 4- and 3-byte keys
-            uint32_t m4 = 0, m3 = 0;
-            {
-                uint32_t hm = FK_STAGE >= 1 ? hit : 0u;
-                while (hm) {
-                    const int j = __ffs(hm) - 1;
-                    hm &= hm - 1;
-                    const uint32_t key = fk_key_at(W, j);
-                    const int32_t pr = lrel + j;
-                    const int32_t fer = pr < dl1 ? dl1 : dl2;
-                    if (pr + 4 <= fer && lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
-                    if (has_t3 && lds_bit(t3, fk_t3_index(key))) m3 |= 1u << j;
-                }
-            }
-            const uint32_t cm = m4 | m3 | gate;
-            int total;
-            const int ex = wave_excl_scan(__popc(cm), &total);
-            if (total == 0) continue;
-            ncand2 += (lane == 0) ? (uint32_t)total : 0u;
-            // survivors -> the ring; full batches of 64 are probed as they fill
-            if (qt - qh + (uint32_t)total > (uint32_t)FK_Q) {
-                while (qh != qt) {
-                    const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
-                    FK_T0(tp0);
-                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor, PC);
-                    FK_TACC(t_probe, tp0);
-                    qh += c;
-                }
-                wave_sync();
-            }
-            for (int rb = 0; rb < total; rb += FK_Q) {
-                int k = ex;
-                uint32_t mm = cm;
-                while (mm) {
-                    const int j = __ffs(mm) - 1;
-                    mm &= mm - 1;
-                    if (k >= rb && k < rb + FK_Q) {
-                        const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
-                        ring[(qt + (uint32_t)(k - rb)) & (FK_Q - 1)] =
-                            make_uint2(((uint32_t)(lrel + j) << 3) | fl, fk_key_at(W, j));
-                    }
-                    ++k;
-                }
-                qt += (uint32_t)((total - rb) < FK_Q ? (total - rb) : FK_Q);
-                wave_sync();
-                const bool more = rb + FK_Q < total;
-                while (qt - qh >= 64u || (more && qh != qt)) {
-                    const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
-                    FK_T0(tp0);
-                    fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor, PC);
-                    FK_TACC(t_probe, tp0);
-                    qh += c;
-                }
-                if (more) wave_sync();
-            }
-            wave_sync();
-            defer = __builtin_amdgcn_readfirstlane((int)icnt[2]) != 0;
-            if (defer) ++ndef_items;
-        }
-        // the rest of the ring
-        while (!defer && qh != qt) {
-            const uint32_t c = qt - qh < 64u ? qt - qh : 64u;
-            FK_T0(tp0);
-            fast_probe_batch(FT, T, D, ring, qh, c, items, icnt, nanchor, PC);
-            FK_TACC(t_probe, tp0);
-            qh += c;
-        }
-        wave_sync();
-        if (!defer && icnt[2] != 0) { defer = true; ++ndef_items; }
-        defer = __builtin_amdgcn_readfirstlane((int)defer) != 0;
-        const uint32_t n0 = __builtin_amdgcn_readfirstlane(icnt[0]);
-        const uint32_t n1 = __builtin_amdgcn_readfirstlane(icnt[1]);
-        if (!defer && cursor + n0 + n1 > S.item_cap) { defer = true; ++ndef_items; }
-        if (__ballot(na0)) flags |= DH_NA0;
-        if (__ballot(na1)) flags |= DH_NA1;
-        {
-            const uint64_t em = __ballot((ebits >> ebit) & 1u);
-            if (em & 3ull) flags |= DH_EDGE0;
-            if (em & 12ull) flags |= DH_EDGE1;
-            if (FK_TIMING) PC.edge_docs += (flags & (DH_EDGE0 | DH_EDGE1)) ? 1u : 0u;
-        }
-        uint2 h;
-        h.x = (uint32_t)(wave * S.item_cap + cursor);
-        bool done = false;
-        if (!defer && !(flags & (DH_NA0 | DH_NA1))) {
-            // all ASCII: finished here, the rest as tasks (flat resolve); a name with more than 64
-            // text items sends the document to the generic kernel instead
-            FK_T0(te0);
-            done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
-            FK_TACC(t_epi, te0);
-            if (!done) { defer = true; ++ndef_items; }
-        }
-        if (defer) {
-            ++ndefer;
-            h.y = DH_DEFER;
-            if (lane == 0) {
-                const uint32_t i = atomicAdd(S.defer_cnt, 1u);
-                if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
-                else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
-            }
-        } else if (done) {
-            h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
-        } else {
-            // items -> HBM (field 0 then field 1) for the resolve kernel
-            for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) gitems[cursor + i] = items[i];
-            for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) gitems[cursor + n0 + i] = items[FK_ITEMS0 + i];
-            cursor += n0 + n1;
-            // the resolve kernel has work: items, an edge candidate, or a field that may be short
-            const int64_t l0 = D.t1 - D.t0, l1 = D.t2 - D.t1;
-            const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
-            const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
-            const bool need = (n0 + n1) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
-            h.y = n0 | (n1 << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u);
-        }
-        if (lane == 0) S.hdr[d] = h;
-        wave_sync();
-    }
-    if (lane == 0) {
-        S.kout_cnt[wave] = O.n;
-        S.vcnt[wave] = TC.v;
-        if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);   // edge items (decided in the epilogue)
-        S.scnt[wave] = TC.s;
-        S.xcnt[wave] = TC.x;
-        if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
-            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
-            atomicMax(&S.tmax[0], TC.v);
-            atomicMax(&S.tmax[2], TC.s);
-            atomicMax(&S.tmax[3], TC.x);
-        }
-    }
-    if (FK_TIMING && lane == 0) {
-        unsigned long long t_all = 0;
-        FK_TACC(t_all, t_all0);
-        atomicAdd(&S.stats[13], t_probe);
-        atomicAdd(&S.stats[14], t_epi);
-        atomicAdd(&S.stats[15], t_all);
-        atomicAdd(&S.stats[16], PC.batches);
-        atomicAdd(&S.stats[17], PC.rounds);
-        atomicAdd(&S.stats[18], PC.pairs);
-        atomicAdd(&S.stats[19], PC.chunks);
-        atomicAdd(&S.stats[27], (unsigned long long)TC.v);
-        atomicAdd(&S.stats[28], (unsigned long long)TC.e);
-        atomicAdd(&S.stats[29], (unsigned long long)TC.s);
-        atomicAdd(&S.stats[30], (unsigned long long)TC.x);
-        atomicAdd(&S.stats[31], PC.edge_docs);
-    }
-    if (FK_TIMING) {
-        const unsigned long long inner = wave_sum64(PC.inner);
-        if (lane == 0) atomicAdd(&S.stats[20], inner);
-    }
-    unsigned long long a = nanchor, c1 = ncand;   // summed over the wave in 64 bits
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-        a += __shfl_xor(a, dd, WAVE);
-        c1 += __shfl_xor(c1, dd, WAVE);
-    }
-    if (lane == 0) {
-        atomicAdd(&S.stats[0], c1);
-        atomicAdd(&S.stats[1], a);
-        atomicAdd(&S.stats[4], (unsigned long long)ndefer);
-        atomicAdd(&S.stats[5], (unsigned long long)ndef_items);
-        atomicAdd(&S.stats[8], (unsigned long long)ncand2);
-    }
-}
-
-static_assert(sizeof(ItemsLds) <= 160 * 1024, "scan workgroup LDS exceeds the CU's 160 KiB");
 
 // ---------------------------------------------------------------- kernel 2: resolve
+#ifndef RK_NOINLINE   // 1: the resolve kernels call fk_resolve_field (fewer spills, a call frame); 0: inlined
+#define RK_NOINLINE 0
+#endif
+template <uint32_t ICAP>
+__device__ __attribute__((noinline)) int fk_resolve_field_call(const FastTables &FT, const DevTables &T, const DevScratch &GS,
+                                                               FieldCtx &F, OutCtx &O, uint64_t *items_lds,
+                                                               uint32_t *icnt_f, uint32_t *dflag, uint32_t *cps,
+                                                               uint32_t *blkcnt, uint64_t *rxtab, RxQueue &RQ,
+                                                               bool maybe_nonascii, bool edge, unsigned long long &nver,
+                                                               unsigned long long &nwin, unsigned long long &nedge,
+                                                               unsigned long long *tacc)
+{
+    return fk_resolve_field<ICAP>(FT, T, GS, F, O, items_lds, icnt_f, dflag, cps, blkcnt, rxtab, RQ, maybe_nonascii, edge,
+                                  nver, nwin, nedge, tacc);
+}
+
+struct RkCounters {
+    unsigned long long nver, nwin, nedge, ndefer, ndef_cp, ndef_items, nres, nrx, nrx_bt, nrx_rounds;
+};
+
+// Resolve one document with a non-ASCII field (n0 / n1 items from hx in the probe's item list, header
+// flags hy), field by field through an ICAP-item LDS buffer; on a field the fast path cannot finish, the
+// document's records and regex tasks are rolled back and it goes to the generic kernel.
+template <uint32_t ICAP>
+__device__ __forceinline__ void rk_resolve_doc(const FastTables &FT, const DevTables &T, const DevScratch &GS,
+                                               const FastScratch &S, const uint8_t *__restrict__ arena,
+                                               const int64_t *__restrict__ off, int64_t d, uint32_t hx, uint32_t n0,
+                                               uint32_t n1, uint32_t hy, uint64_t *items, uint32_t *icnt, uint32_t *cps,
+                                               uint32_t *blkcnt, uint64_t *rxtab, OutCtx &O, RxQueue &RQ, RkCounters &C,
+                                               unsigned long long *tacc)
+{
+    const int lane = lane_id();
+    const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
+    const uint32_t nf[2] = {n0, n1};
+    const uint32_t out_mark = O.n, rq_mark = RQ.n;
+    bool defer = false;
+    ++C.nres;
+    for (int f = 0; f < 2 && !defer; ++f) {
+        const uint32_t N = nf[f];
+        const uint64_t *src = S.items + hx + (f ? nf[0] : 0u);
+        for (uint32_t i = (uint32_t)lane; i < N; i += WAVE) items[i] = src[i];
+        if (lane == 0) { icnt[0] = N; icnt[1] = 0; }
+        wave_sync();
+        FieldCtx F;
+        F.arena = arena;
+        F.fb = f ? t1 : t0;
+        F.fe = f ? t2 : t1;
+        F.cps = cps;
+        F.blkcnt = blkcnt;
+        F.doc = (uint32_t)d;
+        F.field = (uint32_t)f;
+        F.ascii = true;
+        F.n = 0;
+        const bool na = (hy & (f ? DH_NA1 : DH_NA0)) != 0;
+        const bool edge = (hy & (f ? DH_EDGE1 : DH_EDGE0)) != 0;
+        int rs = 0;
+        if (FK_STAGE >= 2) {
+            if constexpr (RK_NOINLINE)
+                rs = fk_resolve_field_call<ICAP>(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps, blkcnt, rxtab, RQ, na,
+                                                 edge, C.nver, C.nwin, C.nedge, tacc);
+            else
+                rs = fk_resolve_field<ICAP>(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps, blkcnt, rxtab, RQ, na, edge,
+                                            C.nver, C.nwin, C.nedge, tacc);
+        }
+        if (rs) {
+            defer = true;
+            if (rs == 1) ++C.ndef_cp;
+            else ++C.ndef_items;
+        }
+        wave_sync();
+    }
+    if (defer) {
+        O.n = out_mark;   // drop this doc's partial records; the generic kernel redoes it
+        RQ.n = rq_mark;
+        ++C.ndefer;
+        if (lane == 0) {
+            const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+            if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
+            else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+        }
+    }
+}
+
+// After a resolve wave's last document: its queued regex-position tasks, its record count, the statistics.
+__device__ __forceinline__ void rk_wave_tail(const FastTables &FT, const DevTables &T, const DevScratch &GS,
+                                             const FastScratch &S, const uint8_t *__restrict__ arena,
+                                             const int64_t *__restrict__ off, int64_t wave, uint32_t *cps,
+                                             uint32_t *blkcnt, uint64_t *rxtab, OutCtx &O, RxQueue &RQ, RkCounters &C,
+                                             unsigned long long *tacc, unsigned long long tall0)
+{
+    const int lane = lane_id();
+    wave_sync_global();
+    if (RQ.n > RQ.cap && lane == 0) atomicMax(&GS.status[2], RQ.n);   // the queue size a rescan needs
+    const uint32_t n_rx = RQ.n < RQ.cap ? RQ.n : RQ.cap;
+    FK_T0(trx0);
+    uint32_t dec_d = 0xFFFFFFFFu, dec_f = 0;   // the field whose code points cps holds (tasks come in doc order)
+    for (uint32_t t = 0; t < n_rx; ++t) {
+        const uint4 tk = RQ.q[t];
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x);
+        const uint32_t fy = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.z);
+        FieldCtx F;
+        F.arena = arena;
+        F.field = fy & 1u;
+        F.fb = off[2 * (int64_t)d + F.field];
+        F.fe = off[2 * (int64_t)d + F.field + 1];
+        F.ascii = (fy & 2u) != 0;
+        F.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.w);
+        F.cps = cps;
+        F.blkcnt = blkcnt;
+        F.doc = d;
+        if (!F.ascii && (d != dec_d || F.field != dec_f)) {
+            decode_field_fast(arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
+            dec_d = d;
+            dec_f = F.field;
+        }
+        const int32_t r = FT.rxf_idx[P];
+        ++C.nrx;
+        C.nrx_bt += r < 0;
+        C.nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
+        const uint32_t cnt = (RK_SKIP & 8) ? 1u : (r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, RQ.txt)
+                                                         : ((RK_SKIP & 16) ? 1u : rx_positions(T, GS, F, O, P)));
+        if (cnt == 0) emit_hits(O, GS, lane == 0, d, P, KW_NOPOS, F.field);
+    }
+    FK_TACC(tacc[4], trx0);
+    FK_TACC(tacc[5], tall0);
+    if (FK_TIMING && lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&S.stats[21 + i], tacc[i]);
+    if (lane == 0) S.out_cnt[wave] = O.n;
+    unsigned long long v = C.nver, w = C.nwin;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        v += __shfl_xor(v, dd, WAVE);
+        w += __shfl_xor(w, dd, WAVE);
+    }
+    if (lane == 0) {
+        atomicAdd(&S.stats[2], w / WAVE);
+        atomicAdd(&S.stats[3], v / WAVE);
+        atomicAdd(&S.stats[4], C.ndefer);
+        atomicAdd(&S.stats[5], C.ndef_items);
+        atomicAdd(&S.stats[6], C.ndef_cp);
+        atomicAdd(&S.stats[7], C.nedge);
+        atomicAdd(&S.stats[9], C.nres);
+        atomicAdd(&S.stats[10], C.nrx);
+        atomicAdd(&S.stats[11], C.nrx_bt);
+        atomicAdd(&S.stats[12], C.nrx_rounds);
+    }
+}
+
+
+
 __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables FT, DevTables T,
                                                               const uint8_t *__restrict__ arena,
                                                               const int64_t *__restrict__ off, int64_t n_docs,
@@ -2335,8 +1937,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     RQ.cap = S.rx_cap;
     RQ.n = 0;
     RQ.txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
-    unsigned long long nver = 0, nwin = 0, nedge = 0, ndefer = 0, ndef_cp = 0, ndef_items = 0, nres = 0;
-    unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
+    RkCounters C = {};
     unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0};   // FK_TIMING: decode, edge, items, short, regex, all
     FK_T0(tall0);
 
@@ -2364,14 +1965,28 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
                     const uint32_t idx = fk_edge_index(key8);
                     if ((((k & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u) flags |= f ? DH_EDGE1 : DH_EDGE0;
                 }
-                const bool defer = (fl & DH_DEFER) || t1 - t0 > MAX_FIELD_BYTES || t2 - t1 > MAX_FIELD_BYTES ||
-                                   nc.x > (uint32_t)FK_ITEMS0 || nc.y > (uint32_t)FK_ITEMS1;
+                const bool over = nc.x > (uint32_t)FK_ITEMS0 || nc.y > (uint32_t)FK_ITEMS1;
+                bool defer = (fl & DH_DEFER) || t1 - t0 > MAX_FIELD_BYTES || t2 - t1 > MAX_FIELD_BYTES;
+                bool big = false;
+                if (!defer && over) {
+                    // more items than this kernel's LDS holds: the big-document resolve (list at the tail end
+                    // of big_list, the epilogue's big documents fill it from the head), beyond it the generic kernel
+                    if (nc.x <= (uint32_t)FK_BIG0 && nc.y <= (uint32_t)FK_BIG0) {
+                        const uint32_t bi = atomicAdd(&S.big_cnt[1], 1u);
+                        if (bi < S.defer_cap) {
+                            S.big_list[S.defer_cap - 1 - bi] = (uint32_t)dl;
+                            big = true;
+                        }
+                    }
+                    defer = !big;
+                }
                 const int64_t l0 = t1 - t0, l1 = t2 - t1;
                 const bool s0 = l0 <= MAXM || ((flags & DH_NA0) && l0 <= 4 * MAXM);
                 const bool s1 = l1 <= MAXM || ((flags & DH_NA1) && l1 <= 4 * MAXM);
-                const bool need = (nc.x + nc.y) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1;
+                const bool need = !big && ((nc.x + nc.y) > 0 || (flags & (DH_EDGE0 | DH_EDGE1)) || s0 || s1);
                 hl.x = ibeg;
-                hl.y = defer ? (DH_DEFER | flags) : (nc.x | (nc.y << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u));
+                // (a big document's header keeps the flags only: its kernel reads the counts from ncnt)
+                hl.y = defer ? (DH_DEFER | flags) : big ? flags : (nc.x | (nc.y << DH_N1_SHIFT) | flags | (need ? DH_NEED : 0u));
                 S.hdr[dl] = hl;
                 if (defer) {
                     const uint32_t i = atomicAdd(S.defer_cnt, 1u);
@@ -2379,11 +1994,11 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
                     else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
                 }
                 dfr = defer;
-                dfr_items = defer && (nc.x > (uint32_t)FK_ITEMS0 || nc.y > (uint32_t)FK_ITEMS1);
+                dfr_items = defer && over;
             }
         }
-        ndefer += (unsigned long long)__popcll(__ballot(dfr));
-        ndef_items += (unsigned long long)__popcll(__ballot(dfr_items));
+        C.ndefer += (unsigned long long)__popcll(__ballot(dfr));
+        C.ndef_items += (unsigned long long)__popcll(__ballot(dfr_items));
         uint64_t todo = __ballot((hl.y & DH_NEED) != 0 && (hl.y & DH_DEFER) == 0);
         while (todo) {
             const int l = __builtin_ctzll(todo);
@@ -2391,107 +2006,51 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
             const int64_t d = c0 + l;
             const uint32_t hx = (uint32_t)__shfl((int)hl.x, l, WAVE);
             const uint32_t hy = (uint32_t)__shfl((int)hl.y, l, WAVE);
-            const int64_t t0 = off[2 * d], t1 = off[2 * d + 1], t2 = off[2 * d + 2];
-            const uint32_t nf[2] = {hy & 1023u, (hy >> DH_N1_SHIFT) & 127u};
-            const uint32_t out_mark = O.n, rq_mark = RQ.n;
-            bool defer = false;
-            ++nres;
-            for (int f = 0; f < 2 && !defer; ++f) {
-                const uint32_t N = nf[f];
-                const uint64_t *src = S.items + hx + (f ? nf[0] : 0u);
-                for (uint32_t i = (uint32_t)lane; i < N; i += WAVE) items[i] = src[i];
-                if (lane == 0) { icnt[0] = N; icnt[1] = 0; }
-                wave_sync();
-                FieldCtx F;
-                F.arena = arena;
-                F.fb = f ? t1 : t0;
-                F.fe = f ? t2 : t1;
-                F.cps = cps;
-                F.blkcnt = blkcnt;
-                F.doc = (uint32_t)d;
-                F.field = (uint32_t)f;
-                F.ascii = true;
-                F.n = 0;
-                const bool na = (hy & (f ? DH_NA1 : DH_NA0)) != 0;
-                const bool edge = (hy & (f ? DH_EDGE1 : DH_EDGE0)) != 0;
-                const int rs = FK_STAGE < 2 ? 0 : fk_resolve_field(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps,
-                                                                   blkcnt, rxtab, RQ, na, edge, nver, nwin, nedge, tacc);
-                if (rs) {
-                    defer = true;
-                    if (rs == 1) ++ndef_cp;
-                    else ++ndef_items;
-                }
-                wave_sync();
-            }
-            if (defer) {
-                O.n = out_mark;   // drop this doc's partial records; the generic kernel redoes it
-                RQ.n = rq_mark;
-                ++ndefer;
-                if (lane == 0) {
-                    const uint32_t i = atomicAdd(S.defer_cnt, 1u);
-                    if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
-                    else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
-                }
-            }
+            rk_resolve_doc<FK_ITEMS_MAX>(FT, T, GS, S, arena, off, d, hx, hy & 1023u, (hy >> DH_N1_SHIFT) & 127u, hy,
+                                         items, icnt, cps, blkcnt, rxtab, O, RQ, C, tacc);
         }
     }
-    // the queued regex-position tasks of this wave's documents
-    wave_sync_global();
-    if (RQ.n > RQ.cap && lane == 0) atomicMax(&GS.status[2], RQ.n);   // the queue size a rescan needs
-    const uint32_t n_rx = RQ.n < RQ.cap ? RQ.n : RQ.cap;
-    FK_T0(trx0);
-    uint32_t dec_d = 0xFFFFFFFFu, dec_f = 0;   // the field whose code points cps holds (tasks come in doc order)
-    for (uint32_t t = 0; t < n_rx; ++t) {
-        const uint4 tk = RQ.q[t];
-        const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x);
-        const uint32_t fy = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
-        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.z);
-        FieldCtx F;
-        F.arena = arena;
-        F.field = fy & 1u;
-        F.fb = off[2 * (int64_t)d + F.field];
-        F.fe = off[2 * (int64_t)d + F.field + 1];
-        F.ascii = (fy & 2u) != 0;
-        F.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.w);
-        F.cps = cps;
-        F.blkcnt = blkcnt;
-        F.doc = d;
-        if (!F.ascii && (d != dec_d || F.field != dec_f)) {
-            decode_field_fast(arena, F.fb, F.fe, cps, blkcnt, FK_CP_CAP);
-            dec_d = d;
-            dec_f = F.field;
-        }
-        const int32_t r = FT.rxf_idx[P];
-        ++nrx;
-        nrx_bt += r < 0;
-        nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-        const uint32_t cnt = (RK_SKIP & 8) ? 1u : (r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, RQ.txt)
-                                                         : ((RK_SKIP & 16) ? 1u : rx_positions(T, GS, F, O, P)));
-        if (cnt == 0) emit_hits(O, GS, lane == 0, d, P, KW_NOPOS, F.field);
-    }
-    FK_TACC(tacc[4], trx0);
-    FK_TACC(tacc[5], tall0);
-    if (FK_TIMING && lane == 0)
-        for (int i = 0; i < 6; ++i) atomicAdd(&S.stats[21 + i], tacc[i]);
-    if (lane == 0) S.out_cnt[wave] = O.n;
-    unsigned long long v = nver, w = nwin;
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-        v += __shfl_xor(v, dd, WAVE);
-        w += __shfl_xor(w, dd, WAVE);
-    }
-    if (lane == 0) {
-        atomicAdd(&S.stats[2], w / WAVE);
-        atomicAdd(&S.stats[3], v / WAVE);
-        atomicAdd(&S.stats[4], ndefer);
-        atomicAdd(&S.stats[5], ndef_items);
-        atomicAdd(&S.stats[6], ndef_cp);
-        atomicAdd(&S.stats[7], nedge);
-        atomicAdd(&S.stats[9], nres);
-        atomicAdd(&S.stats[10], nrx);
-        atomicAdd(&S.stats[11], nrx_bt);
-        atomicAdd(&S.stats[12], nrx_rounds);
-    }
+    rk_wave_tail(FT, T, GS, S, arena, off, wave, cps, blkcnt, rxtab, O, RQ, C, tacc, tall0);
 }
 
+// ---------------------------------------------------------------- kernel 2b: big non-ASCII documents
+// The documents with a non-ASCII field and more items than kw_resolve_kernel's LDS holds (FK_ITEMS0 in the
+// text, FK_ITEMS1 in the title), up to FK_BIG0 per field: the same per-document resolve with one wave per
+// workgroup and a 32 KiB item buffer.  Launched after kw_resolve_kernel on its stream, at most one
+// workgroup per resolve wave: wave w continues resolve wave w's hit region and regex queue.
+__global__ __launch_bounds__(WAVE) void kw_resolve_big_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+                                                            const int64_t *__restrict__ off, FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items[FK_BIG0];
+    __shared__ uint64_t rxtab[128];
+    __shared__ uint4 rxtxt[RX_TXT / 16];
+    __shared__ uint32_t icnt[4];
+    const int64_t wave = blockIdx.x;
+    const uint32_t nbig = min(S.big_cnt[1], S.defer_cap);
+    if (wave >= (int64_t)nbig) return;
+    uint32_t *cps = S.cps + (size_t)wave * FK_CP_CAP;
+    uint32_t *blkcnt = S.cpbase + (size_t)wave * (CP_CAP / 16 + 2);
+    OutCtx O;
+    O.shared = nullptr;
+    O.out = S.out + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = S.out_cnt[wave];
+    RxQueue RQ;
+    RQ.q = S.rx_tasks + (size_t)wave * S.rx_cap;
+    RQ.cap = S.rx_cap;
+    RQ.n = 0;
+    RQ.txt = (uint8_t *)rxtxt;
+    RkCounters C = {};
+    unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0};
+    FK_T0(tall0);
+    for (int64_t i = wave; i < (int64_t)nbig; i += gridDim.x) {
+        const uint32_t d = S.big_list[S.defer_cap - 1 - i];   // (the list's tail end: see kw_resolve_kernel)
+        const uint2 h = S.hdr[d];
+        const uint2 nc = S.ncnt[d];
+        rk_resolve_doc<FK_BIG0>(FT, T, GS, S, arena, off, d, h.x, nc.x, nc.y, h.y, items, icnt, cps, blkcnt, rxtab, O,
+                                RQ, C, tacc);
+    }
+    rk_wave_tail(FT, T, GS, S, arena, off, wave, cps, blkcnt, rxtab, O, RQ, C, tacc, tall0);
+    if (wave == 0 && lane_id() == 0) atomicAdd(&S.stats[16], (unsigned long long)nbig);
+}
 }  // namespace kw

@@ -476,6 +476,24 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     if (lane == 0) atomicAdd(&S.stats[1], a);
 }
 
+// the edge-prefilter flags of a document: first / last eight bytes of each field (lanes 0..3) against
+// the global one-deletion prefix / suffix bitmaps
+__device__ __forceinline__ uint32_t fk_edge_flags(const FastTables &FT, const FastDoc &D)
+{
+    const int lane = lane_id();
+    const int f = lane >> 1;
+    const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+    bool e = false;
+    if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+        const int64_t a = (lane & 1) ? fe - 8 : fb;
+        const uint64_t k = (uint64_t)ld_u32_unaligned(D.arena, a) | ((uint64_t)ld_u32_unaligned(D.arena, a + 4) << 32);
+        const uint32_t idx = fk_edge_index(k);
+        e = (((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u;
+    }
+    const uint64_t em = __ballot(e);
+    return ((em & 3ull) ? DH_EDGE0 : 0u) | ((em & 12ull) ? DH_EDGE1 : 0u);
+}
+
 // ---------------------------------------------------------------- kernel 3: per-document epilogue
 __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT, const uint8_t *__restrict__ arena,
                                                           const int64_t *__restrict__ off, int64_t n_docs,
@@ -512,23 +530,24 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         if (flags & (DH_NA0 | DH_NA1)) continue;   // the resolve kernel's document
         const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
         const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
-        // edge prefilter: first / last eight bytes of each field (lanes 0..3) against the global bitmaps
-        {
-            const int f = lane >> 1;
-            const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
-            bool e = false;
-            if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
-                const int64_t a = (lane & 1) ? fe - 8 : fb;
-                const uint64_t k = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
-                const uint32_t idx = fk_edge_index(k);
-                e = (((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u;
-            }
-            const uint64_t em = __ballot(e);
-            if (em & 3ull) flags |= DH_EDGE0;
-            if (em & 12ull) flags |= DH_EDGE1;
-        }
+        flags |= fk_edge_flags(FT, D);
         bool defer = (flags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
-        if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) { defer = true; ++ndef_items; }
+        if (defer && lane == 0) atomicAdd(&S.stats[15], 1ull);   // (rare: counted where they happen)
+        if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) {
+            // more items than this kernel's LDS holds: the big-document epilogue, beyond its caps the generic kernel
+            uint32_t bi = 0xFFFFFFFFu;
+            if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG1) {
+                if (lane == 0) bi = atomicAdd(S.big_cnt, 1u);
+                bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+            }
+            if (bi < S.defer_cap) {
+                if (lane == 0) S.big_list[bi] = (uint32_t)d;
+                continue;
+            }
+            defer = true;
+            ++ndef_items;
+            if (lane == 0) atomicAdd(&S.stats[14], 1ull);
+        }
         flags &= ~DH_DEFER;
         bool done = false;
         if (!defer && !(flags & (DH_NA0 | DH_NA1))) {
@@ -537,7 +556,11 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
             for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
             wave_sync();
             done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
-            if (!done) { defer = true; ++ndef_items; }
+            if (!done) {
+                defer = true;
+                ++ndef_items;
+                if (lane == 0) atomicAdd(&S.stats[13], 1ull);
+            }
         }
         uint2 h;
         h.x = ibeg;
@@ -572,4 +595,87 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
     }
 }
 
+
+// ---------------------------------------------------------------- kernel 3b: big all-ASCII documents
+// The all-ASCII documents with more items than kw_epi_kernel's LDS holds (FK_ITEMS0 / FK_ITEMS1; a
+// 50k-name KB has pieces that many names share), up to FK_BIG0 / FK_BIG1, finished by the same
+// epilogue with one wave per workgroup and 36 KiB of LDS.  Launched right after kw_epi_kernel on the
+// same stream with one workgroup per epilogue wave: wave w continues epilogue wave w's hit and task
+// regions (their counts are read back and written again), so the task kernels and the compaction see
+// the big documents' records like any other.
+__global__ __launch_bounds__(WAVE) void kw_epi_big_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+                                                        const int64_t *__restrict__ off, FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items[FK_BIG0 + FK_BIG1];
+    const int lane = lane_id();
+    const int64_t wave = blockIdx.x;
+    const uint32_t nbig = min(*S.big_cnt, S.defer_cap);
+    if (wave >= (int64_t)nbig) return;
+    OutCtx O;
+    O.shared = nullptr;
+    O.out = S.kout + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = S.kout_cnt[wave];
+    TaskCounts TC = {S.vcnt[wave], 0u, S.scnt[wave], S.xcnt[wave]};
+    uint32_t ndefer = 0;
+    for (int64_t i = wave; i < (int64_t)nbig; i += gridDim.x) {
+        const uint32_t d = S.big_list[i];
+        const int64_t ov = lane < 3 ? off[2 * (int64_t)d + lane] : 0;
+        const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) :
+                                                                        make_uint2(0u, 0u)));
+        FastDoc D;
+        D.arena = arena;
+        D.t0 = rdlane64(ov, 0);
+        D.t1 = rdlane64(ov, 1);
+        D.t2 = rdlane64(ov, 2);
+        D.doc = d;
+        D.l1 = (int32_t)(D.t1 - D.t0);
+        D.l2 = (int32_t)(D.t2 - D.t0);
+        const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
+        uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5) & ~DH_DEFER;
+        const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
+        const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+        flags |= fk_edge_flags(FT, D);
+        const uint64_t *src = S.items + ibeg;
+        for (uint32_t k = (uint32_t)lane; k < n0; k += WAVE) items[k] = src[k];
+        for (uint32_t k = (uint32_t)lane; k < n1; k += WAVE) items[FK_BIG0 + k] = src[n0 + k];
+        wave_sync();
+        const bool done = fk_scan_epilogue<FK_BIG0>(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+        uint2 h;
+        h.x = ibeg;
+        if (!done) {
+            ++ndefer;
+            h.y = DH_DEFER;
+            if (lane == 0) {
+                const uint32_t j = atomicAdd(S.defer_cnt, 1u);
+                if (j < S.defer_cap) S.defer_list[j] = d;
+                else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+            }
+        } else {
+            // (the header's counts saturate: informational only past the resolve kernel)
+            h.y = min(n0, 1023u) | (min(n1, 127u) << DH_N1_SHIFT) | flags;
+        }
+        if (lane == 0) S.hdr[d] = h;
+        wave_sync();
+    }
+    if (lane == 0) {
+        S.kout_cnt[wave] = O.n;
+        S.vcnt[wave] = TC.v;
+        if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);
+        S.scnt[wave] = TC.s;
+        S.xcnt[wave] = TC.x;
+        if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
+            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
+            atomicMax(&S.tmax[0], TC.v);
+            atomicMax(&S.tmax[2], TC.s);
+            atomicMax(&S.tmax[3], TC.x);
+        }
+        if (ndefer) {
+            atomicAdd(&S.stats[4], (unsigned long long)ndefer);
+            atomicAdd(&S.stats[5], (unsigned long long)ndefer);
+            atomicAdd(&S.stats[13], (unsigned long long)ndefer);
+        }
+        if (wave == 0) atomicAdd(&S.stats[16], (unsigned long long)nbig);
+    }
+}
 }  // namespace kw

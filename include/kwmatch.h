@@ -112,8 +112,14 @@ int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void
  * passed the stage-2 filter, [9] documents the resolve kernel worked on,
  * [10] regex-position searches of decided regex-class names, of which [11]
  * ran the backtracking engine (quantified atoms), [12] 2048-position rounds of
- * the shift-and search. */
-#define KW_N_STATS 13
+ * the shift-and search; the all-ASCII documents the epilogue deferred because
+ * [13] a name had more than 64 items in a field, [14] a field had more items
+ * than the fast path holds, [15] the probe or filter flagged them (an item batch
+ * beyond the probe's pool, a field beyond 8 MiB); [16] all-ASCII documents
+ * finished by the big-document epilogue (more than 512 / 64 items); [17] times
+ * the batch was scanned again after a device buffer grew (0 once the buffers
+ * fit the workload: growth persists across kw_scan calls). */
+#define KW_N_STATS 18
 int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
 /* Device times (ms) of the last kw_scan, from HIP events on the scan's stream

@@ -237,7 +237,8 @@ def test_regex_queue_overflow_rescans(monkeypatch):
 
 
 def _many_item_docs(ckb):
-    """Fields around the fast path's item capacities (text 512, title 64, 64 items of one name)."""
+    """Fields around the fast path's item capacities (text 512, title 64: the epilogue kernel's LDS; beyond
+    them the big-document epilogue up to 4096 / 512; 64 items of one name: the generic kernel)."""
     rng = random.Random(23)
     fz = [n for n, c in zip(ckb.names, ckb.classes) if c == 'F' and n and len(n) >= 4]
     up = [n for n, c in zip(ckb.names, ckb.classes) if c == 'U']
@@ -247,7 +248,7 @@ def _many_item_docs(ckb):
         for reps in (63, 64, 65, 80, 200):                 # one name: the > 64-items-per-name deferral
             texts.append(' '.join([one] * reps) + na)
             titles.append('t')
-        for k in (60, 130, 300, 511, 520, 700):            # many names: below / above the text capacity
+        for k in (60, 130, 300, 511, 520, 700, 1500):      # many names: below / above the text capacity
             texts.append(' , '.join(rng.choice(fz + up) for _ in range(k)) + na)
             titles.append(' '.join(rng.choice(up) for _ in range(k // 8)) + na)   # title capacity 64
         texts.append(' '.join(rng.choice(up) for _ in range(100)) + na)
@@ -260,7 +261,9 @@ def test_item_capacity_boundaries_vs_oracle(env):
     got = _gpu_maps(env['m'], texts, titles)
     bad = _compare(env['processed'], texts, titles, got)
     assert not bad, f"GPU differs from the oracle on many-item docs {bad[:20]}"
-    assert env['m'].stats()['deferred_docs'] > 0     # the > 512-item texts took the generic kernel
+    st = env['m'].stats()
+    assert st['big_docs'] > 0          # the > 512-item all-ASCII texts took the big-document epilogue
+    assert st['deferred_docs'] > 0     # > 64 items of one name: the generic kernel
 
 
 def _nonascii_near_names(ckb):
