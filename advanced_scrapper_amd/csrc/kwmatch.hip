@@ -1138,10 +1138,6 @@ static int launch_scan(kw_handle *h)
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
                            h->FS, h->S);
-        // the documents with more items than the epilogue's LDS holds: one wave each (grid-stride), wave w in
-        // epilogue wave w's regions; one resident round of workgroups (most exit at once: the list is short)
-        hipLaunchKernelGGL(kw_epi_big_kernel, dim3(std::min(n_epi, h->cus * 4)), dim3(WAVE), 0, st, h->FT, h->arena,
-                           h->doc_off, h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
     h->ns = n_regions;

@@ -40,8 +40,8 @@ constexpr int FK_EDGE_BITS = 20;                // edge prefix / suffix 8-byte k
 constexpr int FK_ITEMS0 = 512;                  // items of field 0 (text) on the fast path (power of 2: LDS sort)
 constexpr int FK_ITEMS1 = 64;                   // items of field 1 (title)
 constexpr int FK_ITEMS_MAX = FK_ITEMS0;         // one field's item buffer in the resolve kernel
-constexpr int FK_BIG0 = 4096;                   // items of the text / title in the big-document epilogue
-constexpr int FK_BIG1 = 512;                    //   (kw_epi_big_kernel, 36 KiB of LDS per wave)
+constexpr int FK_BIG0 = 4096;                   // items of the text / title of a big document (epilogue:
+constexpr int FK_BIG1 = 512;                    //   the workgroup's 36 KiB of LDS; resolve: FK_BIG0 per field)
 constexpr int FK_CP_CAP = 16384;                // bytes of a non-ASCII field the fast path decodes
 constexpr int RK_WAVES = 4;                     // waves per resolve workgroup
 constexpr int RK_BLOCK = RK_WAVES * WAVE;
@@ -142,8 +142,8 @@ struct FastScratch {
     uint32_t *defer_list;       // docs sent to the generic kernel
     uint32_t *defer_cnt;
     uint32_t defer_cap;
-    uint32_t *big_list;         // docs with more items than the epilogue / resolve kernels hold (defer_cap):
-    uint32_t *big_cnt;          //   all-ASCII ones from the head ([0]), non-ASCII ones from the tail ([1])
+    uint32_t *big_list;         // non-ASCII docs with more items than the resolve kernel holds (defer_cap; filled
+    uint32_t *big_cnt;          //   from the tail end, count in big_cnt[1])
     uint32_t *status;
     unsigned long long *stats;  // see kw_stats
     uint4 *rx_tasks;            // per resolve wave: rx_cap regex-position tasks (doc, field|ascii, pattern, n)

@@ -377,8 +377,16 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, uint32_t nmr, uint32_t 
 // name needs an exact occurrence, which the FULL use finds).  Lanes 0..19 take
 // (side, L = m-1): hash the window, look it up among the one-deletion variants,
 // verify exactly and append an EDGE item.  Returns the number of items added.
+#ifndef RK_EDGE_NOINLINE   // 1: fk_edge_items as a called function (its registers stay out of the resolve loop)
+#define RK_EDGE_NOINLINE 0
+#endif
 template <uint32_t ICAP>
-__device__ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint64_t *items, uint32_t *icnt_f,
+#if RK_EDGE_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__
+#endif
+uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint64_t *items, uint32_t *icnt_f,
                                   uint32_t *dflag)
 {
     const int lane = lane_id();
@@ -1774,8 +1782,9 @@ __device__ __attribute__((noinline)) int fk_resolve_field_call(const FastTables 
                                   nver, nwin, nedge, tacc);
 }
 
-struct RkCounters {
-    unsigned long long nver, nwin, nedge, ndefer, ndef_cp, ndef_items, nres, nrx, nrx_bt, nrx_rounds;
+struct RkCounters {   // (per wave: the uniform ones in 32 bits, fewer scalar registers to spill)
+    unsigned long long nver, nwin, nedge;
+    uint32_t ndefer, ndef_cp, ndef_items, nres, nrx, nrx_bt, nrx_rounds;
 };
 
 // Resolve one document with a non-ASCII field (n0 / n1 items from hx in the probe's item list, header
@@ -1896,14 +1905,14 @@ __device__ __forceinline__ void rk_wave_tail(const FastTables &FT, const DevTabl
     if (lane == 0) {
         atomicAdd(&S.stats[2], w / WAVE);
         atomicAdd(&S.stats[3], v / WAVE);
-        atomicAdd(&S.stats[4], C.ndefer);
-        atomicAdd(&S.stats[5], C.ndef_items);
-        atomicAdd(&S.stats[6], C.ndef_cp);
+        atomicAdd(&S.stats[4], (unsigned long long)C.ndefer);
+        atomicAdd(&S.stats[5], (unsigned long long)C.ndef_items);
+        atomicAdd(&S.stats[6], (unsigned long long)C.ndef_cp);
         atomicAdd(&S.stats[7], C.nedge);
-        atomicAdd(&S.stats[9], C.nres);
-        atomicAdd(&S.stats[10], C.nrx);
-        atomicAdd(&S.stats[11], C.nrx_bt);
-        atomicAdd(&S.stats[12], C.nrx_rounds);
+        atomicAdd(&S.stats[9], (unsigned long long)C.nres);
+        atomicAdd(&S.stats[10], (unsigned long long)C.nrx);
+        atomicAdd(&S.stats[11], (unsigned long long)C.nrx_bt);
+        atomicAdd(&S.stats[12], (unsigned long long)C.nrx_rounds);
     }
 }
 
@@ -1997,8 +2006,8 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
                 dfr_items = defer && over;
             }
         }
-        C.ndefer += (unsigned long long)__popcll(__ballot(dfr));
-        C.ndef_items += (unsigned long long)__popcll(__ballot(dfr_items));
+        C.ndefer += (uint32_t)__popcll(__ballot(dfr));
+        C.ndef_items += (uint32_t)__popcll(__ballot(dfr_items));
         uint64_t todo = __ballot((hl.y & DH_NEED) != 0 && (hl.y & DH_DEFER) == 0);
         while (todo) {
             const int l = __builtin_ctzll(todo);

@@ -15,7 +15,9 @@
 //                     header gets the first item's index, the per-field counts are added up in ncnt.
 //   kw_epi_kernel     one wave per document: all-ASCII documents are finished by the epilogue
 //                     (fk_scan_epilogue: sort, emit, queue the verify / short / regex tasks), the others get
-//                     their header for the resolve kernel, oversize ones go to the generic kernel.
+//                     their header for the resolve kernel; documents with more items than a wave's LDS
+//                     holds are finished after the workgroup's loop with the whole workgroup's LDS
+//                     (epi_big_doc), oversize ones go to the generic kernel.
 //
 // Reference: the per-article x per-name loop of match_keywords.py:159-180 (see kwmatch_fast.hpp for the
 // anchors and filters).
@@ -48,6 +50,7 @@ constexpr int PK_POOL = PK_POOL_CFG;     // items one batch of 64 candidates may
 #define PK_MINW 1
 #endif
 constexpr int EK_WAVES = 8;              // waves per epilogue workgroup
+constexpr int EK_BIGQ = 64;              // big documents one epilogue workgroup finishes itself (more: generic)
 constexpr int EK_BLOCK = EK_WAVES * WAVE;
 
 constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range)
@@ -494,12 +497,77 @@ __device__ __forceinline__ uint32_t fk_edge_flags(const FastTables &FT, const Fa
     return ((em & 3ull) ? DH_EDGE0 : 0u) | ((em & 12ull) ? DH_EDGE1 : 0u);
 }
 
+// ---------------------------------------------------------------- big all-ASCII documents
+// An all-ASCII document with more items than one epilogue wave's LDS holds (FK_ITEMS0 / FK_ITEMS1; a
+// 50k-name KB has pieces that many names share), up to FK_BIG0 / FK_BIG1: finished by the same epilogue
+// after the workgroup's loop, by its wave 0 with the whole workgroup's LDS (items), in wave 0's hit and
+// task regions.  Returns 1 if the document went to the generic kernel (a name with > 64 items).
+#ifndef EK_BIG_NOINLINE   // 1: epi_big_doc as a called function (a call frame; 0: inlined into the epilogue)
+#define EK_BIG_NOINLINE 0
+#endif
+#if EK_BIG_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__ __forceinline__
+#endif
+uint32_t epi_big_doc(const FastTables &FT, const FastScratch &S, const DevScratch &GS,
+                                                          const uint8_t *__restrict__ arena, const int64_t *__restrict__ off,
+                                                          uint32_t d, uint64_t *items, int64_t wave, OutCtx &O,
+                                                          TaskCounts &TC)
+{
+    const int lane = lane_id();
+    const int64_t ov = lane < 3 ? off[2 * (int64_t)d + lane] : 0;
+    const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) :
+                                                                    make_uint2(0u, 0u)));
+    FastDoc D;
+    D.arena = arena;
+    D.t0 = rdlane64(ov, 0);
+    D.t1 = rdlane64(ov, 1);
+    D.t2 = rdlane64(ov, 2);
+    D.doc = d;
+    D.l1 = (int32_t)(D.t1 - D.t0);
+    D.l2 = (int32_t)(D.t2 - D.t0);
+    const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
+    uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5) & ~DH_DEFER;
+    const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
+    const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+    flags |= fk_edge_flags(FT, D);
+    const uint64_t *src = S.items + ibeg;
+    for (uint32_t k = (uint32_t)lane; k < n0; k += WAVE) items[k] = src[k];
+    for (uint32_t k = (uint32_t)lane; k < n1; k += WAVE) items[FK_BIG0 + k] = src[n0 + k];
+    wave_sync();
+    const bool done = fk_scan_epilogue<FK_BIG0>(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+    uint2 h;
+    h.x = ibeg;
+    if (!done) {
+        h.y = DH_DEFER;
+        if (lane == 0) {
+            const uint32_t j = atomicAdd(S.defer_cnt, 1u);
+            if (j < S.defer_cap) S.defer_list[j] = d;
+            else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+            atomicAdd(&S.stats[5], 1ull);
+            atomicAdd(&S.stats[13], 1ull);
+        }
+    } else {
+        // (the header's counts saturate: informational only past the resolve kernel)
+        h.y = min(n0, 1023u) | (min(n1, 127u) << DH_N1_SHIFT) | flags;
+    }
+    if (lane == 0) S.hdr[d] = h;
+    wave_sync();
+    return done ? 0u : 1u;
+}
+
 // ---------------------------------------------------------------- kernel 3: per-document epilogue
 __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT, const uint8_t *__restrict__ arena,
                                                           const int64_t *__restrict__ off, int64_t n_docs,
                                                           FastScratch S, DevScratch GS)
 {
     __shared__ uint64_t items_all[EK_WAVES * (FK_ITEMS0 + FK_ITEMS1)];
+    __shared__ uint32_t blk_docs[EK_BIGQ];   // this workgroup's big documents (finished after its loop)
+    __shared__ uint32_t blk_n;
+    static_assert(EK_WAVES * (FK_ITEMS0 + FK_ITEMS1) >= FK_BIG0 + FK_BIG1, "a big document needs the block's LDS");
+    if (threadIdx.x == 0) blk_n = 0;
+    __syncthreads();
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t wave = (int64_t)blockIdx.x * EK_WAVES + wib;
@@ -537,11 +605,11 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
             // more items than this kernel's LDS holds: the big-document epilogue, beyond its caps the generic kernel
             uint32_t bi = 0xFFFFFFFFu;
             if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG1) {
-                if (lane == 0) bi = atomicAdd(S.big_cnt, 1u);
+                if (lane == 0) bi = atomicAdd(&blk_n, 1u);
                 bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
             }
-            if (bi < S.defer_cap) {
-                if (lane == 0) S.big_list[bi] = (uint32_t)d;
+            if (bi < (uint32_t)EK_BIGQ) {
+                if (lane == 0) blk_docs[bi] = (uint32_t)d;
                 continue;
             }
             defer = true;
@@ -578,6 +646,13 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         if (lane == 0) S.hdr[d] = h;
         wave_sync();
     }
+    // the workgroup's big documents: wave 0 with the whole workgroup's LDS as one 4096 + 512-item buffer
+    __syncthreads();
+    const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
+    if (wib == 0 && nb) {
+        for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC);
+        if (lane == 0) atomicAdd(&S.stats[16], (unsigned long long)nb);
+    }
     if (lane == 0) {
         S.kout_cnt[wave] = O.n;
         S.vcnt[wave] = TC.v;
@@ -596,86 +671,4 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
 }
 
 
-// ---------------------------------------------------------------- kernel 3b: big all-ASCII documents
-// The all-ASCII documents with more items than kw_epi_kernel's LDS holds (FK_ITEMS0 / FK_ITEMS1; a
-// 50k-name KB has pieces that many names share), up to FK_BIG0 / FK_BIG1, finished by the same
-// epilogue with one wave per workgroup and 36 KiB of LDS.  Launched right after kw_epi_kernel on the
-// same stream with one workgroup per epilogue wave: wave w continues epilogue wave w's hit and task
-// regions (their counts are read back and written again), so the task kernels and the compaction see
-// the big documents' records like any other.
-__global__ __launch_bounds__(WAVE) void kw_epi_big_kernel(FastTables FT, const uint8_t *__restrict__ arena,
-                                                        const int64_t *__restrict__ off, FastScratch S, DevScratch GS)
-{
-    __shared__ uint64_t items[FK_BIG0 + FK_BIG1];
-    const int lane = lane_id();
-    const int64_t wave = blockIdx.x;
-    const uint32_t nbig = min(*S.big_cnt, S.defer_cap);
-    if (wave >= (int64_t)nbig) return;
-    OutCtx O;
-    O.shared = nullptr;
-    O.out = S.kout + (size_t)wave * S.out_cap;
-    O.cap = S.out_cap;
-    O.n = S.kout_cnt[wave];
-    TaskCounts TC = {S.vcnt[wave], 0u, S.scnt[wave], S.xcnt[wave]};
-    uint32_t ndefer = 0;
-    for (int64_t i = wave; i < (int64_t)nbig; i += gridDim.x) {
-        const uint32_t d = S.big_list[i];
-        const int64_t ov = lane < 3 ? off[2 * (int64_t)d + lane] : 0;
-        const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) :
-                                                                        make_uint2(0u, 0u)));
-        FastDoc D;
-        D.arena = arena;
-        D.t0 = rdlane64(ov, 0);
-        D.t1 = rdlane64(ov, 1);
-        D.t2 = rdlane64(ov, 2);
-        D.doc = d;
-        D.l1 = (int32_t)(D.t1 - D.t0);
-        D.l2 = (int32_t)(D.t2 - D.t0);
-        const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
-        uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5) & ~DH_DEFER;
-        const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
-        const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
-        flags |= fk_edge_flags(FT, D);
-        const uint64_t *src = S.items + ibeg;
-        for (uint32_t k = (uint32_t)lane; k < n0; k += WAVE) items[k] = src[k];
-        for (uint32_t k = (uint32_t)lane; k < n1; k += WAVE) items[FK_BIG0 + k] = src[n0 + k];
-        wave_sync();
-        const bool done = fk_scan_epilogue<FK_BIG0>(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
-        uint2 h;
-        h.x = ibeg;
-        if (!done) {
-            ++ndefer;
-            h.y = DH_DEFER;
-            if (lane == 0) {
-                const uint32_t j = atomicAdd(S.defer_cnt, 1u);
-                if (j < S.defer_cap) S.defer_list[j] = d;
-                else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
-            }
-        } else {
-            // (the header's counts saturate: informational only past the resolve kernel)
-            h.y = min(n0, 1023u) | (min(n1, 127u) << DH_N1_SHIFT) | flags;
-        }
-        if (lane == 0) S.hdr[d] = h;
-        wave_sync();
-    }
-    if (lane == 0) {
-        S.kout_cnt[wave] = O.n;
-        S.vcnt[wave] = TC.v;
-        if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);
-        S.scnt[wave] = TC.s;
-        S.xcnt[wave] = TC.x;
-        if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
-            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
-            atomicMax(&S.tmax[0], TC.v);
-            atomicMax(&S.tmax[2], TC.s);
-            atomicMax(&S.tmax[3], TC.x);
-        }
-        if (ndefer) {
-            atomicAdd(&S.stats[4], (unsigned long long)ndefer);
-            atomicAdd(&S.stats[5], (unsigned long long)ndefer);
-            atomicAdd(&S.stats[13], (unsigned long long)ndefer);
-        }
-        if (wave == 0) atomicAdd(&S.stats[16], (unsigned long long)nbig);
-    }
-}
 }  // namespace kw
