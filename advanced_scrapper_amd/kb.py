@@ -201,6 +201,7 @@ def classify_name(name: str) -> str:
 
 # --------------------------------------------------------------------- regex atoms
 _META = set('.^$*+?{}[]\\|()')
+_DOT = {'.'}
 RX_LIT, RX_ANY = 0, 1
 
 
@@ -218,8 +219,17 @@ def regex_atoms(name: str):
     ``? * + {m,n}`` on a single literal or ``.``, and unquantified groups.
     Anything else raises :class:`UnsupportedPattern`.
     """
-    if not (_META & set(name)):
+    meta = _META & set(name)
+    if not meta:
         return None
+    if meta == _DOT:
+        # only '.': every other character is a literal (the sre_parse walk gives the same atoms, ~50x slower)
+        return [(RX_ANY, 0, 1, 1) if ch == '.' else (RX_LIT, ord(ch), 1, 1) for ch in name]
+    return regex_atoms_sre(name)
+
+
+def regex_atoms_sre(name: str):
+    """regex_atoms through sre_parse (any name with a metacharacter)."""
     try:
         parsed = _sre_p.parse(name)
     except re.error:
@@ -310,23 +320,62 @@ class CompiledKB:
         return cached
 
 
-def compile_kb(processed_data: Dict[str, Dict[str, Dict[str, tuple]]]) -> CompiledKB:
+PAR_MIN_REGEX = 65536  # regex-bearing names from which compile_kb parses the programs in worker processes
+                       # (process start-up costs ~1 s: a 52k-name KB parses faster in one process)
+
+
+def _atoms_of(names: List[str]):
+    """Worker: regex_atoms of each name (UnsupportedPattern propagates to the caller)."""
+    return [regex_atoms(n) for n in names]
+
+
+def regex_programs(names: List[str], fuzzy: List[bool], workers: Optional[int] = None) -> list:
+    """regex_atoms of every fuzzy-class name (None for the others), in order.  Only names with a regex
+    metacharacter need sre_parse; from PAR_MIN_REGEX of them (a Wikidata-scale KB, config 4) they are
+    parsed by ``workers`` spawned processes (default min(16, os.cpu_count())) in contiguous chunks, so
+    the first unsupported name in KB order is the one reported, as in the serial loop."""
+    progs: list = [None] * len(names)
+    todo = [i for i, n in enumerate(names) if fuzzy[i] and (_META & set(n))]
+    if workers is None:
+        workers = min(16, os.cpu_count() or 1)
+    if workers > 1 and len(todo) >= PAR_MIN_REGEX:
+        import multiprocessing
+        from concurrent.futures import ProcessPoolExecutor
+        k = min(workers, max(1, len(todo) // 1024))
+        bounds = [len(todo) * j // k for j in range(k + 1)]
+        chunks = [todo[bounds[j]:bounds[j + 1]] for j in range(k)]
+        with ProcessPoolExecutor(k, mp_context=multiprocessing.get_context('spawn')) as ex:
+            futs = [ex.submit(_atoms_of, [names[i] for i in ch]) for ch in chunks]
+            for ch, fut in zip(chunks, futs):
+                for i, prog in zip(ch, fut.result()):
+                    progs[i] = prog
+    else:
+        for i in todo:
+            progs[i] = regex_atoms(names[i])
+    return progs
+
+
+def compile_kb(processed_data: Dict[str, Dict[str, Dict[str, tuple]]], workers: Optional[int] = None) -> CompiledKB:
     """Patterns of the active names in the reference's traversal order.
 
     The traversal ticker -> attribute -> name (match_keywords.py:159-163)
     assigns every occurrence a rank; a name's dict position inside a ticker's
     ``text_matches``/``title_matches`` is the rank of its first in-period
     occurrence there.  Patterns are ordered for the device: uppercase names
-    first, then fuzzy names by decreasing code-point length (stable).
+    first, then fuzzy names by decreasing code-point length (stable).  The
+    regex programs of a large KB are parsed in parallel (regex_programs).
     """
     tickers = list(processed_data.keys())
     first_seen: Dict[str, int] = {}
     occ_by_name: Dict[str, list] = {}
+    cls_of: Dict[str, str] = {}
     rank = 0
     for ti, ticker in enumerate(tickers):
         for _attr, names in processed_data[ticker].items():
             for name, (start, end) in names.items():
-                cls = classify_name(name)
+                cls = cls_of.get(name)
+                if cls is None:
+                    cls = cls_of[name] = classify_name(name)
                 if cls in (CLASS_UPPER, CLASS_FUZZY):
                     if name not in first_seen:
                         first_seen[name] = len(first_seen)
@@ -334,8 +383,8 @@ def compile_kb(processed_data: Dict[str, Dict[str, Dict[str, tuple]]]) -> Compil
                     occ_by_name[name].append((ti, rank, start, end))
                 rank += 1
     uniq = list(first_seen.keys())
-    upper = [n for n in uniq if classify_name(n) == CLASS_UPPER]
-    fuzzy = [n for n in uniq if classify_name(n) == CLASS_FUZZY]
+    upper = [n for n in uniq if cls_of[n] == CLASS_UPPER]
+    fuzzy = [n for n in uniq if cls_of[n] == CLASS_FUZZY]
     fuzzy.sort(key=lambda n: -len(n))
     ordered = upper + fuzzy
     enc = [n.encode('utf-8', 'surrogatepass') for n in ordered]
@@ -343,14 +392,14 @@ def compile_kb(processed_data: Dict[str, Dict[str, Dict[str, tuple]]]) -> Compil
     pat_off = np.zeros(len(enc) + 1, dtype=np.int64)
     np.cumsum(lens, out=pat_off[1:])
     pat_bytes = np.frombuffer(b''.join(enc), dtype=np.uint8).copy() if enc else np.zeros(0, np.uint8)
-    classes = [classify_name(n) for n in ordered]
+    classes = [cls_of[n] for n in ordered]
     pat_class = np.frombuffer(''.join(classes).encode('ascii'), dtype=np.uint8).copy()
     atoms: List[Tuple[int, int, int, int]] = []
     rx_off = np.zeros(len(ordered) + 1, dtype=np.int64)
     invalid = []
-    for i, name in enumerate(ordered):
+    progs = regex_programs(ordered, [c == CLASS_FUZZY for c in classes], workers)
+    for i, prog in enumerate(progs):
         rx_off[i] = len(atoms)
-        prog = regex_atoms(name) if classes[i] == CLASS_FUZZY else None
         invalid.append(prog == 'invalid')
         if isinstance(prog, list):
             atoms.extend(prog)

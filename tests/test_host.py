@@ -144,6 +144,26 @@ def test_regex_atoms_match_python_re(golden):
             assert _atoms_finditer(atoms, s) == want, (name, s)
 
 
+def test_regex_atoms_dot_fast_path_and_parallel_compile():
+    """The '.'-only fast path equals the sre_parse walk, and the parallel regex parse equals the serial one
+    (config-4 KB: ~52k names)."""
+    from advanced_scrapper_amd.synth_kb import synthetic_kb
+    processed = synthetic_kb(600, 11)
+    serial = compile_kb(processed, workers=1)
+    dots = [n for n in serial.names if set(n) & kb._META == {'.'}]
+    assert len(dots) > 100
+    for name in dots + ['.', 'a.b', '..', 'é.ü']:
+        assert kb.regex_atoms(name) == kb.regex_atoms_sre(name), name
+    old = kb.PAR_MIN_REGEX
+    kb.PAR_MIN_REGEX = 1
+    try:
+        par = compile_kb(processed, workers=2)
+    finally:
+        kb.PAR_MIN_REGEX = old
+    assert par.names == serial.names and par.invalid_regex == serial.invalid_regex
+    assert np.array_equal(par.rx_atoms, serial.rx_atoms) and np.array_equal(par.rx_off, serial.rx_off)
+
+
 def test_regex_atoms_classification():
     assert kb.regex_atoms('Apple Inc') is None
     assert kb.regex_atoms('C++') == 'invalid'
