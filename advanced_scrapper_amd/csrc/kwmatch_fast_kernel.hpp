@@ -76,6 +76,17 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *__restrict__
     return __builtin_amdgcn_alignbyte(x1, x0, s);
 }
 
+// the 8 bytes at any byte position (three aligned words)
+__device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t *__restrict__ a, int64_t p)
+{
+    const int64_t a0 = p & ~(int64_t)3;
+    const uint32_t s = (uint32_t)(p & 3);
+    const uint32_t x0 = *(const uint32_t *)(a + a0);
+    const uint32_t x1 = *(const uint32_t *)(a + a0 + 4);
+    const uint32_t x2 = *(const uint32_t *)(a + a0 + 8);
+    return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s) << 32);
+}
+
 // the 4-byte key at position j (0..15) of a lane's 16-byte chunk W[0..4]
 __device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], int j)
 {

@@ -2,8 +2,8 @@
 // probe, epilogue and field helpers it reuses.
 //
 //   kw_filter_kernel  one wave per document (grid-stride): the LDS filters over every byte position; the
-//                     stage-2 survivors ("candidates") go to the wave's region in HBM in document and
-//                     position order, with the document's flags (non-ASCII fields, edge prefilter, field
+//                     stage-2 survivors ("candidates", 8 bytes: document, position << 3 | key lengths to
+//                     probe) go to the wave's region in HBM in document and position order, with the document's flags (non-ASCII fields, edge prefilter, field
 //                     too long) in its header.  Few registers, 64 KiB of LDS: two workgroups per CU.
 //   kw_probe_kernel   one wave per filter region: the region's candidates 64 at a time, whatever document
 //                     they belong to (a document averages ~13 candidates, so per-document batches left most
@@ -93,7 +93,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const int lane = lane_id();
     const uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
-    uint4 *cand = S.cand + (size_t)wave * S.cand_cap;
+    uint2 *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const bool has_t3 = FT.has_t3 != 0;
     const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
@@ -206,7 +206,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 const uint32_t k = fg_doc(dstart, (uint32_t)nd, r);
                 const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
                 if (kk < ccap)
-                    cand[kk] = make_uint4((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl, fk_key_at(W, j), 0u);
+                    cand[kk] = make_uint2((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl);
                 ++kk;
             }
             ccur += (uint32_t)total;
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     uint64_t *pool = pool_all + wib * PK_POOL;
     uint8_t *pown = pown_all + wib * PK_POOL;
     uint32_t *scnt = scnt_all + wib * WAVE;
-    const uint4 *cand = S.cand + (size_t)region * S.cand_cap;
+    const uint2 *cand = S.cand + (size_t)region * S.cand_cap;
     const uint32_t nc = min(S.ccnt[region], S.cand_cap);
     uint64_t *items = S.items + (size_t)region * S.item_cap;
     const uint32_t icap = S.item_cap;
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     scnt[lane] = 0;
     for (uint32_t c0 = 0; c0 < nc; c0 += WAVE) {
         const bool inr = c0 + (uint32_t)lane < nc;
-        const uint4 e = inr ? cand[c0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+        const uint2 e = inr ? cand[c0 + lane] : make_uint2(0u, 0u);
         const uint32_t doc = e.x;
         const int64_t t0 = inr ? off[2 * (int64_t)doc] : 0;
         const int64_t t1 = inr ? off[2 * (int64_t)doc + 1] : 0;
@@ -303,8 +303,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
         const int f = pr < l1 ? 0 : 1;
         const int32_t fbr = f ? l1 : 0, fer = f ? l2 : l1;
         const int64_t p = t0 + pr;
-        const uint32_t hi = valid ? ld_u32_unaligned(arena, p + 4) : 0u;
-        const uint64_t h8 = (uint64_t)e.z | ((uint64_t)hi << 32);
+        const uint64_t h8 = valid ? ld_u64_unaligned(arena, p) : 0ull;
         // hash lookups of the lane's key lengths 4, 3, 2 (try bits 0, 1, 2), all in flight together
         uint32_t rb[3], re[3];
         {
