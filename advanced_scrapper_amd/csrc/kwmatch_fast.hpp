@@ -171,12 +171,23 @@ struct FastScratch {
 // host + device hashes of the LDS tables
 __host__ __device__ __forceinline__ uint32_t fk_word(uint32_t key4)
 {
-    return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;    // depends on bytes 0..2
+    // bits 19..31 of the product of bytes 0..2 (the high half would hardly depend on byte 0)
+    return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;
 }
 __host__ __device__ __forceinline__ uint32_t fk_bit(uint32_t key4)
 {
-    const uint32_t b3 = key4 >> 24;
-    return (b3 ^ (b3 >> 5)) & 31u;
+    return ((key4 >> 24) + (key4 >> 29)) & 31u;   // byte 3 folded to 5 bits (v_lshr_add_u32)
+}
+// device: the stage-1 word's LDS byte offset (= 4 * fk_word) and a bit offset whose low 5 bits are fk_bit
+// (v_bfe_u32 reads only those)
+__device__ __forceinline__ uint32_t fk_word_byte(uint32_t key4)
+{
+    return (__umul24(key4, FK_MUL1) >> 17) & (4u * FK_FILT_WORDS - 4u);
+}
+__device__ __forceinline__ uint32_t fk_bit_raw(uint32_t key4) { return (key4 >> 24) + (key4 >> 29); }
+__device__ __forceinline__ uint32_t lds_word_at(const uint32_t *t, uint32_t byte_off)
+{
+    return *(const uint32_t *)((const uint8_t *)t + byte_off);
 }
 __host__ __device__ __forceinline__ uint32_t fk_l2_index(uint32_t key4) { return (key4 * FK_MUL2) >> (32 - FK_L2_BITS); }
 __host__ __device__ __forceinline__ uint32_t fk_t3_index(uint32_t key4)

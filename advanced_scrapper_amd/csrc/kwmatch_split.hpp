@@ -113,6 +113,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         if (lane < nd) dtitle[lane] = (uint32_t)(o1 - gb);
         wave_sync();
         int64_t blk = gb & ~(int64_t)15;
+        uint32_t kdoc = 0;   // document of the current tile's first byte (candidate emission)
         // Three tiles in flight per wave, each in its own registers (the loop is unrolled by three, so no
         // register copy waits for a load).  Loads are unconditional: an address past the group's last
         // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
@@ -165,7 +166,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
-                    fw[jj] = filt[fk_word(key)];
+                    fw[jj] = lds_word_at(filt, fk_word_byte(key));
                     bm[jj] = fk_b2_mul(key);
                     bw[jj] = b2[(bm[jj] >> 5) & (FK_B2_WORDS - 1)];
                 }
@@ -174,7 +175,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 for (int jj = 0; jj < 4; ++jj) {
                     const int j = 4 * q + jj;
                     const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
-                    hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit(key), 1) << j;
+                    hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit_raw(key), 1) << j;
                     gate |= __builtin_amdgcn_ubfe(bw[jj], bm[jj], 1) << j;
                 }
             }
@@ -197,13 +198,21 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const int ex = wave_excl_scan(__popc(cm), &total);
             if (total == 0) return;
             ncand2 += (lane == 0) ? (uint32_t)total : 0u;
+            // the document of the tile's first byte (wave-uniform, advanced from the previous tile's), then
+            // each candidate's by a short forward walk (documents are longer than a tile: mostly one step)
+            {
+                const int64_t r0 = tb - gb;
+                const uint32_t rt = r0 > 0 ? (uint32_t)r0 : 0u;
+                while (dstart[kdoc + 1] <= rt) ++kdoc;
+            }
             uint32_t kk = ccur + (uint32_t)ex;
             uint32_t mm = cm;
             while (mm) {
                 const int j = __ffs(mm) - 1;
                 mm &= mm - 1;
                 const uint32_t r = rel + (uint32_t)j;
-                const uint32_t k = fg_doc(dstart, (uint32_t)nd, r);
+                uint32_t k = kdoc;
+                while (dstart[k + 1] <= r) ++k;
                 const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
                 if (kk < ccap)
                     cand[kk] = make_uint2((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl);
