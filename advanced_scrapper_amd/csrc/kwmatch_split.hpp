@@ -35,6 +35,9 @@ namespace kw {
 #ifndef FS_MINW
 #define FS_MINW 1
 #endif
+#ifndef FS_COMPACT   // 1: stage 2 of the filter over wave-compacted positions; 0: per-lane loops
+#define FS_COMPACT 1
+#endif
 constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
 constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
@@ -62,6 +65,7 @@ struct __attribute__((aligned(16))) FilterLds {
     uint32_t b2[FK_B2_WORDS];
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
+    uint2 stg[FS_WAVES][WAVE];                // stage-2 positions of one round (key, lane << 4 | j | flags)
 };
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
@@ -93,6 +97,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const int lane = lane_id();
     const uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
+    uint2 *stg = L.stg[wib];
     uint2 *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const bool has_t3 = FT.has_t3 != 0;
@@ -182,6 +187,57 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             hit &= valid;
             gate &= valid;
             ncand += (uint32_t)__popc(hit);
+#if FS_COMPACT
+            // stage 2 over the wave: the tile's stage-1 and bigram-gate positions compacted into 64-entry
+            // rounds (lane = position; usually one round), both LDS lookups at once, then the survivors
+            // ("candidates") ranked by ballot and written with their document
+            const uint32_t sm = hit | gate;
+            int ts;
+            const int sx = wave_excl_scan(__popc(sm), &ts);
+            if (ts == 0) return;
+            {
+                const int64_t r0 = tb - gb;
+                const uint32_t rt = r0 > 0 ? (uint32_t)r0 : 0u;
+                while (dstart[kdoc + 1] <= rt) ++kdoc;
+            }
+            const uint32_t rtile = (uint32_t)(tb - gb);   // group-relative byte of lane 0's position 0 (wraps
+                                                          // below the group start: only valid positions are read)
+            for (int c0 = 0; c0 < ts; c0 += WAVE) {
+                {
+                    uint32_t hm = sm;
+                    int rk = sx;
+                    while (hm) {
+                        const int j = __ffs(hm) - 1;
+                        hm &= hm - 1;
+                        if (rk >= c0 + WAVE) break;
+                        if (rk >= c0)
+                            stg[rk - c0] = make_uint2(fk_key_at(W, j), ((uint32_t)lane << 4) | (uint32_t)j |
+                                                                    (((hit >> j) & 1u) << 10) | (((gate >> j) & 1u) << 11));
+                        ++rk;
+                    }
+                }
+                wave_sync();
+                const bool act = c0 + lane < ts;
+                const uint2 e = act ? stg[lane] : make_uint2(0u, 0u);
+                wave_sync();
+                const bool h1 = (e.y >> 10) & 1u;
+                const uint32_t b4 = lds_bit(l2, fk_l2_index(e.x)) ? 1u : 0u;
+                const uint32_t b3 = (has_t3 && lds_bit(t3, fk_t3_index(e.x))) ? 2u : 0u;
+                const uint32_t fl = (h1 ? (b4 | b3) : 0u) | (((e.y >> 11) & 1u) << 2);
+                const bool pass = act && fl != 0u;
+                const uint64_t pm = __ballot(pass);
+                if (pass) {
+                    const uint32_t r = rtile + 16u * ((e.y >> 4) & 63u) + (e.y & 15u);
+                    uint32_t k = kdoc;
+                    while (dstart[k + 1] <= r) ++k;
+                    const uint32_t kk = ccur + mbcnt(pm);
+                    if (kk < ccap) cand[kk] = make_uint2((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl);
+                }
+                const uint32_t np = (uint32_t)__popcll(pm);
+                ccur += np;
+                ncand2 += (lane == 0) ? np : 0u;
+            }
+#else
             uint32_t m4 = 0, m3 = 0;
             {
                 uint32_t hm = hit;
@@ -219,6 +275,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 ++kk;
             }
             ccur += (uint32_t)total;
+#endif
         };
         uint4 v0, v1, v2;
         uint32_t w0, w1, w2;
