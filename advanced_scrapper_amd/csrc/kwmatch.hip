@@ -966,7 +966,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     const size_t per_tasks = (size_t)(c.vcap + c.ecap + c.scap + c.xcap) * 16;
     size_t total = (size_t)c.ng * (per_items + per_cps + per_blk) + (size_t)c.nr * (per_fcps + per_fblk) +
                    nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 8 +
-                   (size_t)c.ns * c.cand_cap * 8 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 12 + 4 * 256 +
+                   (size_t)c.ns * c.cand_cap * 4 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 12 + 4 * 256 +
                    (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
                    32 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
@@ -981,7 +981,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->S.cp_cap = c.gc_cap;
     kw_hit *outs = (kw_hit *)carve(nw * per_out);
     h->FS.items = (uint64_t *)carve((size_t)c.ns * c.item_cap * 8);
-    h->FS.cand = (uint2 *)carve((size_t)c.ns * c.cand_cap * 8);
+    h->FS.cand = (uint32_t *)carve((size_t)c.ns * c.cand_cap * 4);
     h->FS.cand_cap = c.cand_cap;
     h->FS.ccnt = (uint32_t *)carve((size_t)c.ns * 4);
     h->FS.ncnt = (uint2 *)carve((size_t)c.hdr_cap * 8);

@@ -160,7 +160,7 @@ struct FastScratch {
     unsigned long long *dset;   // decided (doc, field, pattern) set: open addressing, 0 = empty
     unsigned long long dmask;
     // split scan (kwmatch_split.hpp): filter regions -> candidates -> items
-    uint2 *cand;                // per filter region: cand_cap candidates {doc, pos << 3 | try bits, 4 bytes, 0}
+    uint32_t *cand;                // per filter region: cand_cap records (group headers, candidates: kwmatch_split.hpp)
     uint32_t cand_cap;
     uint32_t *ccnt;             // per filter region: candidates written
     uint2 *ncnt;                // per document: items of field 0 / field 1 (the probe adds them up)

@@ -2,8 +2,9 @@
 // probe, epilogue and field helpers it reuses.
 //
 //   kw_filter_kernel  one wave per document (grid-stride): the LDS filters over every byte position; the
-//                     stage-2 survivors ("candidates", 8 bytes: document, position << 3 | key lengths to
-//                     probe) go to the wave's region in HBM in document and position order, with the document's flags (non-ASCII fields, edge prefilter, field
+//                     stage-2 survivors ("candidates", 4 bytes: position in the document << 8 | document
+//                     in its group << 3 | key lengths to probe, after a header record per group) go to the
+//                     wave's region in HBM in document and position order, with the document's flags (non-ASCII fields, edge prefilter, field
 //                     too long) in its header.  Few registers, 64 KiB of LDS: two workgroups per CU.
 //   kw_probe_kernel   one wave per filter region: the region's candidates 64 at a time, whatever document
 //                     they belong to (a document averages ~13 candidates, so per-document batches left most
@@ -35,9 +36,6 @@ namespace kw {
 #ifndef FS_MINW
 #define FS_MINW 1
 #endif
-#ifndef FS_COMPACT   // 1: stage 2 of the filter over wave-compacted positions; 0: per-lane loops
-#define FS_COMPACT 1
-#endif
 constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
 constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
@@ -56,7 +54,7 @@ constexpr int EK_WAVES = 8;              // waves per epilogue workgroup
 constexpr int EK_BIGQ = 64;              // big documents one epilogue workgroup finishes itself (more: generic)
 constexpr int EK_BLOCK = EK_WAVES * WAVE;
 
-constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range)
+constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range; 5 bits of a candidate)
 
 struct __attribute__((aligned(16))) FilterLds {
     uint32_t filt[FK_FILT_WORDS];
@@ -98,7 +96,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
     uint2 *stg = L.stg[wib];
-    uint2 *cand = S.cand + (size_t)wave * S.cand_cap;
+    uint32_t *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const bool has_t3 = FT.has_t3 != 0;
     const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
@@ -119,6 +117,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         wave_sync();
         int64_t blk = gb & ~(int64_t)15;
         uint32_t kdoc = 0;   // document of the current tile's first byte (candidate emission)
+        bool ghdr = true;    // the group's header record is not written yet
         // Three tiles in flight per wave, each in its own registers (the loop is unrolled by three, so no
         // register copy waits for a load).  Loads are unconditional: an address past the group's last
         // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
@@ -187,7 +186,6 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             hit &= valid;
             gate &= valid;
             ncand += (uint32_t)__popc(hit);
-#if FS_COMPACT
             // stage 2 over the wave: the tile's stage-1 and bigram-gate positions compacted into 64-entry
             // rounds (lane = position; usually one round), both LDS lookups at once, then the survivors
             // ("candidates") ranked by ballot and written with their document
@@ -225,57 +223,29 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 const uint32_t b3 = (has_t3 && lds_bit(t3, fk_t3_index(e.x))) ? 2u : 0u;
                 const uint32_t fl = (h1 ? (b4 | b3) : 0u) | (((e.y >> 11) & 1u) << 2);
                 const bool pass = act && fl != 0u;
-                const uint64_t pm = __ballot(pass);
+                uint32_t k = kdoc, pd = 0;
+                bool keep = pass;
                 if (pass) {
                     const uint32_t r = rtile + 16u * ((e.y >> 4) & 63u) + (e.y & 15u);
-                    uint32_t k = kdoc;
                     while (dstart[k + 1] <= r) ++k;
+                    pd = r - dstart[k];
+                    keep = pd < (1u << 24);   // (a longer document has a field over 8 MiB: the generic kernel's)
+                }
+                const uint64_t pm = __ballot(keep);
+                if (pm) {
+                    // the group's header record precedes its first candidate (fl = 0: the group index)
+                    if (ghdr) {
+                        if (lane == 0 && ccur < ccap) cand[ccur] = (uint32_t)g << 3;
+                        ++ccur;
+                        ghdr = false;
+                    }
                     const uint32_t kk = ccur + mbcnt(pm);
-                    if (kk < ccap) cand[kk] = make_uint2((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl);
+                    if (keep && kk < ccap) cand[kk] = (pd << 8) | (k << 3) | fl;
                 }
                 const uint32_t np = (uint32_t)__popcll(pm);
                 ccur += np;
                 ncand2 += (lane == 0) ? np : 0u;
             }
-#else
-            uint32_t m4 = 0, m3 = 0;
-            {
-                uint32_t hm = hit;
-                while (hm) {
-                    const int j = __ffs(hm) - 1;
-                    hm &= hm - 1;
-                    const uint32_t key = fk_key_at(W, j);
-                    if (lds_bit(l2, fk_l2_index(key))) m4 |= 1u << j;
-                    if (has_t3 && lds_bit(t3, fk_t3_index(key))) m3 |= 1u << j;
-                }
-            }
-            const uint32_t cm = m4 | m3 | gate;
-            int total;
-            const int ex = wave_excl_scan(__popc(cm), &total);
-            if (total == 0) return;
-            ncand2 += (lane == 0) ? (uint32_t)total : 0u;
-            // the document of the tile's first byte (wave-uniform, advanced from the previous tile's), then
-            // each candidate's by a short forward walk (documents are longer than a tile: mostly one step)
-            {
-                const int64_t r0 = tb - gb;
-                const uint32_t rt = r0 > 0 ? (uint32_t)r0 : 0u;
-                while (dstart[kdoc + 1] <= rt) ++kdoc;
-            }
-            uint32_t kk = ccur + (uint32_t)ex;
-            uint32_t mm = cm;
-            while (mm) {
-                const int j = __ffs(mm) - 1;
-                mm &= mm - 1;
-                const uint32_t r = rel + (uint32_t)j;
-                uint32_t k = kdoc;
-                while (dstart[k + 1] <= r) ++k;
-                const uint32_t fl = ((m4 >> j) & 1u) | (((m3 >> j) & 1u) << 1) | (((gate >> j) & 1u) << 2);
-                if (kk < ccap)
-                    cand[kk] = make_uint2((uint32_t)(d0 + k), ((r - dstart[k]) << 3) | fl);
-                ++kk;
-            }
-            ccur += (uint32_t)total;
-#endif
         };
         uint4 v0, v1, v2;
         uint32_t w0, w1, w2;
@@ -346,7 +316,8 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     uint64_t *pool = pool_all + wib * PK_POOL;
     uint8_t *pown = pown_all + wib * PK_POOL;
     uint32_t *scnt = scnt_all + wib * WAVE;
-    const uint2 *cand = S.cand + (size_t)region * S.cand_cap;
+    const uint32_t *cand = S.cand + (size_t)region * S.cand_cap;
+    int32_t cur_group = -1;                 // group of the region's last header record so far (wave-uniform)
     const uint32_t nc = min(S.ccnt[region], S.cand_cap);
     uint64_t *items = S.items + (size_t)region * S.item_cap;
     const uint32_t icap = S.item_cap;
@@ -356,16 +327,28 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     uint32_t nanchor = 0;
     scnt[lane] = 0;
     for (uint32_t c0 = 0; c0 < nc; c0 += WAVE) {
-        const bool inr = c0 + (uint32_t)lane < nc;
-        const uint2 e = inr ? cand[c0 + lane] : make_uint2(0u, 0u);
-        const uint32_t doc = e.x;
+        const bool inb = c0 + (uint32_t)lane < nc;
+        const uint32_t e = inb ? cand[c0 + lane] : 0u;
+        // records: a group header (low 3 bits 0: the group index above them) before the group's candidates
+        // (position in the document << 8 | document in the group << 3 | key lengths to probe)
+        const bool is_hdr = inb && (e & 7u) == 0u;
+        int32_t grp = is_hdr ? (int32_t)(e >> 3) : -1;
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {   // the last header at or before each lane (groups ascend)
+            const int32_t y = __shfl_up(grp, d, WAVE);
+            if (lane >= d) grp = max(grp, y);
+        }
+        grp = max(grp, cur_group);
+        cur_group = __shfl(grp, WAVE - 1, WAVE);
+        const bool inr = inb && !is_hdr;
+        const uint32_t doc = (uint32_t)grp * FG_DOCS + ((e >> 3) & (FG_DOCS - 1));
         const int64_t t0 = inr ? off[2 * (int64_t)doc] : 0;
         const int64_t t1 = inr ? off[2 * (int64_t)doc + 1] : 0;
         const int64_t t2 = inr ? off[2 * (int64_t)doc + 2] : 0;
         // fields beyond MAX_FIELD_BYTES (item positions are 23-bit) are the generic kernel's
         const bool valid = inr && t1 - t0 <= MAX_FIELD_BYTES && t2 - t1 <= MAX_FIELD_BYTES;
         const int32_t l1 = (int32_t)(t1 - t0), l2 = (int32_t)(t2 - t0);
-        const int32_t pr = (int32_t)(e.y >> 3);
+        const int32_t pr = (int32_t)(e >> 8);
         const int f = pr < l1 ? 0 : 1;
         const int32_t fbr = f ? l1 : 0, fer = f ? l2 : l1;
         const int64_t p = t0 + pr;
@@ -379,7 +362,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 const int Lk = 4 - i;
-                const bool want = valid && ((e.y >> i) & 1u) && pr + Lk <= fer;
+                const bool want = valid && ((e >> i) & 1u) && pr + Lk <= fer;
                 key[i] = ((uint64_t)Lk << 32) | (h8 & ((1ull << (8 * Lk)) - 1));
                 slot[i] = fk_ht_slot(key[i], FT.ht_mask);
                 hs[i] = want ? FT.ht4[slot[i]] : make_uint4(~0u, ~0u, 0u, 0u);

@@ -46,7 +46,7 @@ def _parse():
     ap.add_argument('--hits', choices=('root', 'all', 'none'), default='root',
                     help='N > 1: hit records exchanged every step over libkwmatch\'s RCCL communicator '
                          '(root = to rank 0, the writer; all = all-gather; none = counts only)')
-    ap.add_argument('--traffic-json', default=os.path.join(REPO, 'profiles', 'traffic_r02.json'),
+    ap.add_argument('--traffic-json', default=None,
                     help='per-launch HBM bytes from the rocprofv3 PMC passes (profiles/pmc_traffic.py)')
     ap.add_argument('--workload', choices=('match', 'kb50k', 'dedup'), default='match',
                     help='match = BASELINE.json metric (config 2/3); kb50k = ~50k-pattern synthetic KB '
@@ -248,7 +248,7 @@ def main():
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
-            'traffic': (pmc_traffic(args.traffic_json, 'kw_filter_kernel', n_local, args.seed)
+            'traffic': (pmc_traffic(args.traffic_json or TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=n_local, seed=args.seed)
                         if args.workload == 'match' else None),
             'algorithmic_bytes_per_launch': local_bytes,
             'kernel': 'kw::kw_filter_kernel', 'kernel_ms_avg': round(scan_avg, 4),
@@ -327,7 +327,9 @@ def bench_dedup(args):
                    'dropped_no_html': counts[0], 'dropped_filter': counts[2], 'duplicates': counts[3],
                    'parallelism': 'replicas only (one independent keep-first per GPU)' if world > 1 else 'single GPU'},
         'roofline': {'bound': 'hbm', 'achieved': round(transform_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(transform_gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'frac': round(transform_gbs / HBM_PEAK_GBS, 4),
+                     'traffic': pmc_traffic(args.traffic_json or TRAFFIC_DEDUP, 'dd_transform_kernel', rows_per_gpu=n,
+                                            seed=args.seed),
                      'algorithmic_bytes_per_launch': rows.n_bytes, 'kernel': 'dd::dd_transform_kernel',
                      'kernel_ms_avg': kms['transform_hash'], 'kernels_ms_avg': kms},
         'cpu_baseline': cpu,
@@ -356,15 +358,22 @@ def cpu_baseline_dedup(rows, n_sample: int):
                       f'(yahoo_links_selenium.py:63-79), one process, {secs:.2f} s', 'kept': int(len(df))}
 
 
-def pmc_traffic(path: str, kernel: str, docs: int, seed: int):
+TRAFFIC_KW = os.path.join(REPO, 'profiles', 'traffic_r02.json')
+TRAFFIC_DEDUP = os.path.join(REPO, 'profiles', 'traffic_dedup_r02.json')
+
+
+def pmc_traffic(path: str, kernel: str, **workload):
     """HBM bytes per launch of `kernel` measured by the PMC passes of the same
-    workload (FETCH_SIZE x2 + WRITE_SIZE, see profiles/pmc_traffic.py), or None."""
+    workload (every given key equal; FETCH_SIZE x2 + WRITE_SIZE, see
+    profiles/pmc_traffic.py), or None."""
+    if not path or path == 'none':
+        return None
     try:
         j = json.load(open(path))
     except (OSError, ValueError):
         return None
     w = j.get('workload', {})
-    if str(w.get('docs_per_gpu')) != str(docs) or str(w.get('seed')) != str(seed):
+    if any(str(w.get(k)) != str(v) for k, v in workload.items()):
         return None
     for k, v in j.get('kernels', {}).items():
         if kernel in k:
