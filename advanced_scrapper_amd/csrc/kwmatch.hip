@@ -560,7 +560,11 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
             if ((int)m > prev_m) return fail(KW_EINVAL, "kw_compile: fuzzy patterns must be sorted by length, longest first");
             prev_m = (int)m;
             if (m > (uint32_t)MAXM)
-                return fail(KW_EUNSUPPORTED, "kw_compile: fuzzy name longer than 64 code points (rapidfuzz long-needle path is not restated)");
+                return fail(KW_EUNSUPPORTED,
+                            "kw_compile: fuzzy name '" + std::string((const char *)s, bl) + "' (pattern " + std::to_string(i) +
+                                ") is longer than 64 code points: rapidfuzz's partial_ratio switches to a matching-blocks "
+                                "heuristic for needles over 64 whose score is not the window-family maximum restated "
+                                "here, and rapidfuzz is absent from this image, so no result for it could be checked");
             if (bl == 1) return fail(KW_EUNSUPPORTED, "kw_compile: one-byte fuzzy names are not supported");
             if (m == 0) empty_pat = i;
         } else {

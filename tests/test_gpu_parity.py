@@ -410,3 +410,19 @@ def test_field_over_8mib_is_a_stated_limit():
     m = GpuMatcher(compile_kb(processed))
     with pytest.raises(_native.KwError, match='longer than 8388607 bytes'):
         m.match_strings(['x' * (9 << 20)], ['t'])
+
+
+def test_fuzzy_name_over_64_code_points_is_rejected_with_the_reason():
+    """Fuzzy names over 64 code points: rapidfuzz scores such needles with a heuristic this build does not
+    restate, so kw_compile refuses the KB and says why, naming the name."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    long_name = 'Acme Consolidated Holdings of North American Widget Manufacturers Inc'   # 69 code points
+    processed = {'ACM': {'aliases': {'ACME': (None, None), long_name: (None, None)}}}
+    with pytest.raises(_native.KwError, match='matching-blocks heuristic') as ei:
+        GpuMatcher(compile_kb(processed))
+    assert long_name in str(ei.value)
