@@ -1389,7 +1389,6 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
     const int64_t t = gw / G;
     const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
-    (void)T;
     uint32_t *win = lvwin_all + threadIdx.x * LV_WIN;
     uint16_t *jobs = jobs_all + wib * WAVE * LV_MAXJ;
     uint32_t *okf = okf_all + wib * WAVE;
@@ -1452,16 +1451,10 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
             const uint32_t jnwj = (uint32_t)__shfl((int)nwj, l, WAVE);
             const uint32_t jpre = (uint32_t)__shfl((int)pre, l, WAVE);
             const uint32_t jpmin = (uint32_t)__shfl((int)(uint32_t)pmin, l, WAVE);
+            const uint32_t jP = (uint32_t)__shfl((int)P, l, WAVE);
             const uint32_t fbl = (uint32_t)__shfl((int)(uint32_t)fb, l, WAVE);
             const uint32_t fbh = (uint32_t)__shfl((int)(uint32_t)((uint64_t)fb >> 32), l, WAVE);
             const int64_t jfb = (int64_t)(((uint64_t)fbh << 32) | fbl);
-            uint64_t JW[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const uint32_t x0 = (uint32_t)__shfl((int)(uint32_t)NW[w], l, WAVE);
-                const uint32_t x1 = (uint32_t)__shfl((int)(uint32_t)(NW[w] >> 32), l, WAVE);
-                JW[w] = ((uint64_t)x1 << 32) | x0;
-            }
             if (!jv) continue;
             // job kind: full window at pmin + j, prefix text[:w] (w < m), suffix text[i:] (reversed)
             const bool full = j < jnwj;
@@ -1477,16 +1470,30 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
             }
             const uint32_t d0 = (uint32_t)(jfb + start - A);
             const uint64_t needle = low_mask(jm);
+            // the name's match vectors from the compiled table (bit i = name[i] == c), eight text bytes'
+            // loads in flight at a time
+            const uint64_t *pmr = T.pm_ascii + (size_t)jP * 128;
             uint64_t V = ~0ull;
             bool ok = false;
-            for (uint32_t s2 = 0; s2 < len; ++s2) {
-                const uint32_t bi = d0 + (rev ? len - 1 - s2 : s2);
-                const uint32_t c = (win[bi >> 2] >> (8 * (bi & 3))) & 0xFFu;
-                uint64_t M = lv_match(JW, c, needle);
-                if (rev) M = __builtin_bitreverse64(M) >> (64 - jm);   // bit i = name[m - 1 - i] == c
-                const uint64_t U = V & M;
-                V = (V + U) | (V - U);
-                if (!full && passes((uint32_t)__popcll(~V & needle), jm, s2 + 1)) { ok = true; break; }
+            for (uint32_t s0 = 0; s0 < len && !ok; s0 += 8) {
+                uint64_t Mb[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t s2 = s0 + (uint32_t)u;
+                    const uint32_t bi = d0 + (rev ? len - 1 - s2 : s2);
+                    const uint32_t c = s2 < len ? (win[bi >> 2] >> (8 * (bi & 3))) & 0xFFu : 0x80u;
+                    Mb[u] = c < 0x80u ? pmr[c] : 0ull;   // (ASCII names never match a non-ASCII byte)
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t s2 = s0 + (uint32_t)u;
+                    if (s2 >= len) break;
+                    uint64_t M = Mb[u];
+                    if (rev) M = __builtin_bitreverse64(M) >> (64 - jm);   // bit i = name[m - 1 - i] == c
+                    const uint64_t U = V & M;
+                    V = (V + U) | (V - U);
+                    if (!full && passes((uint32_t)__popcll(~V & needle), jm, s2 + 1)) { ok = true; break; }
+                }
             }
             if (full) ok = 20u * (jm - (uint32_t)__popcll(~V & needle)) < jm;
             ++nwin;
