@@ -36,9 +36,9 @@ EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_l
 # KW_URL_* row codes (include/kwdedup.h)
 KW_URL_NO_HTML, KW_URL_KEPT, KW_URL_FILTERED, KW_URL_DUPLICATE = 0, 1, 2, 3
 KW_DEDUP_NORMALIZE = 1
-KW_N_STATS = 18
+KW_N_STATS = 20
 KW_COMM_ID_BYTES = 128
-KW_ROUTE_SCAN, KW_ROUTE_RESOLVE, KW_ROUTE_GENERIC = 0, 1, 2
+KW_ROUTE_SCAN, KW_ROUTE_RESOLVE, KW_ROUTE_GENERIC, KW_ROUTE_TRANSCODE = 0, 1, 2, 3
 
 
 class KwError(RuntimeError):

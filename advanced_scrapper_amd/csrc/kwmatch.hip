@@ -33,9 +33,10 @@ struct ScratchCaps {
     uint32_t defer_cap = 0, rx_cap = 0;
     uint32_t vcap = 0, ecap = 0, scap = 0, xcap = 0;   // per scan wave task regions
     uint64_t dsize = 0;                    // decided-set slots (power of two)
+    uint64_t tx_cap = 0;                   // bytes of the transcoded view of non-ASCII documents
     bool covers(const ScratchCaps &o) const
     {
-        return nk >= o.nk && nr >= o.nr && ng >= o.ng && ns >= o.ns && cand_cap >= o.cand_cap &&
+        return tx_cap >= o.tx_cap && nk >= o.nk && nr >= o.nr && ng >= o.ng && ns >= o.ns && cand_cap >= o.cand_cap &&
                item_cap >= o.item_cap && out_cap >= o.out_cap && gi_cap >= o.gi_cap && gc_cap >= o.gc_cap &&
                hdr_cap >= o.hdr_cap && defer_cap >= o.defer_cap && rx_cap >= o.rx_cap && vcap >= o.vcap &&
                ecap >= o.ecap && scap >= o.scap && xcap >= o.xcap && dsize >= o.dsize;
@@ -49,6 +50,7 @@ struct ScratchCaps {
         hdr_cap = std::max(hdr_cap, o.hdr_cap); defer_cap = std::max(defer_cap, o.defer_cap);
         rx_cap = std::max(rx_cap, o.rx_cap); vcap = std::max(vcap, o.vcap); ecap = std::max(ecap, o.ecap);
         scap = std::max(scap, o.scap); xcap = std::max(xcap, o.xcap); dsize = std::max(dsize, o.dsize);
+        tx_cap = std::max(tx_cap, o.tx_cap);
     }
 };
 
@@ -103,6 +105,8 @@ struct kw_handle {
     int n_anchor_fast = 0;
     unsigned long long fstats[16] = {0};
     hipEvent_t evr = nullptr, evg = nullptr;
+    unsigned long long tx_need = 0;    // transcoded-view bytes the last scan wanted (the next one's capacity)
+    hipEvent_t evx = nullptr;          // after the transcoding kernel (side stream)
 };
 
 static thread_local std::string g_err;
@@ -217,7 +221,8 @@ size_t rarest4(const QStats &Q, const uint8_t *s, size_t lo, size_t hi, size_t m
 }
 
 int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_bytes, const int64_t *pat_off,
-               const std::vector<std::vector<uint32_t>> &cps, const std::vector<uint32_t> &pat_info,
+               const std::vector<std::vector<uint32_t>> &cps, const std::vector<std::vector<uint32_t>> &tcps,
+               const std::vector<uint32_t> &pat_info,
                const std::vector<int4> &atoms, const std::vector<uint32_t> &rxo, std::string &err)
 {
     struct Use { uint32_t pat, i0, i1; };
@@ -244,6 +249,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         const uint32_t m = (uint32_t)cps[i].size();
         const bool fuzzy = pat_info[i] & PI_FUZZY;
         for (uint32_t c : cps[i]) B.sig[i] |= 1ull << (c & 63);
+        for (uint32_t c : tcps[i]) B.sig[i] |= 1ull << (c & 63);   // (the transcoded view's bytes too)
         // whole-name use (U or FULL): anchor at the rarest 4-byte window (offset <= 255)
         auto span_use = [&](uint32_t kind, size_t sb, size_t se, uint32_t pcp, uint32_t pcl) {
             const size_t len = se - sb;
@@ -297,11 +303,18 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
             if (m >= EDGE_MIN_M && m <= EDGE_MAX_M) {
                 for (uint32_t del = 0; del < m; ++del) {
                     if (del > 0 && cps[i][del] == cps[i][del - 1]) continue;   // same variant as del-1
-                    uint64_t hh = 0;
-                    for (uint32_t j = 0; j < m; ++j)
-                        if (j != del) hh = hh * SUB_B + cps[i][j];
-                    const uint64_t key = (hh + (uint64_t)(m - 1) * 0x9E3779B97F4A7C15ull) | 1ull;
-                    B.edge[key].push_back(((uint32_t)i << 5) | del);
+                    // keyed by the code points (resolve kernel) and, for non-ASCII names, by the transcoded
+                    // view's bytes (epilogue); every lookup compares the candidate exactly
+                    for (int view = 0; view < 2; ++view) {
+                        const auto &cv = view ? tcps[i] : cps[i];
+                        if (view && cv == cps[i]) break;
+                        uint64_t hh = 0;
+                        for (uint32_t j = 0; j < m; ++j)
+                            if (j != del) hh = hh * SUB_B + cv[j];
+                        const uint64_t key = (hh + (uint64_t)(m - 1) * 0x9E3779B97F4A7C15ull) | 1ull;
+                        auto &ev = B.edge[key];
+                        if (ev.empty() || ev.back() != (((uint32_t)i << 5) | del)) ev.push_back(((uint32_t)i << 5) | del);
+                    }
                     // prefilter keys: first / last eight UTF-8 bytes of the variant (>= 10 code points)
                     std::string v;
                     v.append((const char *)s, utf8_offset(cps[i], del));
@@ -697,6 +710,60 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     if (kl_anchor.empty()) kl_anchor.push_back(0);
 
     // ---- bit-parallel match vectors (needle = name)
+    // ---- the epilogue's transcoded view of non-ASCII documents: the non-ASCII code points of the fuzzy names,
+    // most frequent first, get the one-byte markers 0x81..0xFF; a name with a code point beyond them, or with
+    // quantified regex atoms and a non-ASCII code point, is PI_TXUNSAFE (its documents go to the resolve kernel)
+    std::vector<uint32_t> tx_key(256, 0xFFFFFFFFu), tx_val(256, 0x80u), tx_inv(128, 0xFFFFFFFFu);
+    std::vector<std::vector<uint32_t>> tcps(n_pat);
+    std::vector<uint32_t> pat_tcps;
+    int tx_unsafe_short = 0, tx_unsafe_edge = 0;
+    {
+        std::map<uint32_t, uint64_t> freq;
+        for (int i = f_first; i < n_pat; ++i)
+            for (uint32_t c : cps[i])
+                if (c >= 0x80) ++freq[c];
+        std::vector<std::pair<uint64_t, uint32_t>> order;
+        for (auto &kv : freq) order.emplace_back(kv.second, kv.first);
+        std::sort(order.begin(), order.end(), [](const auto &a, const auto &b) {
+            return a.first != b.first ? a.first > b.first : a.second < b.second;
+        });
+        size_t nmark = 127;
+        if (const char *e = getenv("KW_TEST_TX_MARKERS")) nmark = std::min<size_t>(127, (size_t)std::max(0, atoi(e)));
+        std::unordered_map<uint32_t, uint32_t> mk;
+        for (size_t k = 0; k < order.size() && k < nmark; ++k) {
+            const uint32_t cp = order[k].second, v = 0x81u + (uint32_t)k;
+            mk[cp] = v;
+            tx_inv[v - 0x80u] = cp;
+            uint32_t slot = (cp * 0x9E3779B1u) >> 24;
+            while (tx_key[slot] != 0xFFFFFFFFu) slot = (slot + 1) & 255u;
+            tx_key[slot] = cp;
+            tx_val[slot] = v;
+        }
+        for (int i = 0; i < n_pat; ++i) {
+            bool unmapped = false;
+            tcps[i].reserve(cps[i].size());
+            for (uint32_t c : cps[i]) {
+                if (c < 0x80) { tcps[i].push_back(c); continue; }
+                auto it = mk.find(c);
+                unmapped |= it == mk.end();
+                tcps[i].push_back(it == mk.end() ? 0x80u : it->second);
+            }
+            pat_tcps.insert(pat_tcps.end(), tcps[i].begin(), tcps[i].end());
+            if (!(pat_info[i] & PI_FUZZY)) continue;
+            bool quantified = false;
+            for (uint32_t a = rxo[i]; a < rxo[i + 1]; ++a) quantified |= !(atoms[a].z == 1 && atoms[a].w == 1);
+            quantified |= rxo[i + 1] - rxo[i] > 64;
+            const bool nonascii = !(pat_info[i] & PI_ASCII);
+            if (unmapped || (nonascii && quantified)) {
+                pat_info[i] |= PI_TXUNSAFE;
+                tx_unsafe_short = 1;
+                const uint32_t m = (uint32_t)cps[i].size();
+                if (m >= EDGE_MIN_M && m <= EDGE_MAX_M) tx_unsafe_edge = 1;
+            }
+        }
+        if (pat_tcps.empty()) pat_tcps.push_back(0);
+    }
+
     std::vector<uint64_t> pm_ascii((size_t)std::max(n_pat, 1) * 128, 0);
     std::vector<uint32_t> pm_ext_off(n_pat + 1, 0), pm_ext_cp;
     std::vector<uint64_t> pm_ext_mask;
@@ -720,13 +787,18 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     std::unordered_map<uint64_t, std::vector<uint32_t>> subs;
     for (int i = f_first; i < n_pat; ++i) {
         const auto &c = cps[i];
-        for (size_t s0 = 0; s0 < c.size(); ++s0) {
-            uint64_t hh = 0;
-            for (size_t l = 1; l <= (size_t)SHORT_EXACT_MAX && s0 + l <= c.size(); ++l) {
-                hh = hh * SUB_B + c[s0 + l - 1];
-                uint64_t key = (hh + (uint64_t)l * 0x9E3779B97F4A7C15ull) | 1ull;
-                auto &v = subs[key];
-                if (v.empty() || v.back() != (uint32_t)i) v.push_back((uint32_t)i);
+        // keyed by code points and, for non-ASCII names, by the transcoded view's bytes (exact compare follows)
+        for (int view = 0; view < 2; ++view) {
+            const auto &cv = view ? tcps[i] : c;
+            if (view && cv == c) break;
+            for (size_t s0 = 0; s0 < cv.size(); ++s0) {
+                uint64_t hh = 0;
+                for (size_t l = 1; l <= (size_t)SHORT_EXACT_MAX && s0 + l <= cv.size(); ++l) {
+                    hh = hh * SUB_B + cv[s0 + l - 1];
+                    uint64_t key = (hh + (uint64_t)l * 0x9E3779B97F4A7C15ull) | 1ull;
+                    auto &v = subs[key];
+                    if (v.empty() || v.back() != (uint32_t)i) v.push_back((uint32_t)i);
+                }
             }
         }
     }
@@ -771,7 +843,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     FastBuild FB;
     {
         std::string ferr;
-        int frc = build_fast(FB, Q, n_pat, pat_bytes, pat_off, cps, pat_info, atoms, rxo, ferr);
+        int frc = build_fast(FB, Q, n_pat, pat_bytes, pat_off, cps, tcps, pat_info, atoms, rxo, ferr);
         if (frc) return fail(frc, ferr);
     }
     if (const char *dump = getenv("KW_DUMP_ANCHORS")) {
@@ -815,7 +887,8 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_rxl = push_array(blob, FB.rxf_len), f_rxeo = push_array(blob, FB.rxf_ext_off),
            f_rxec = push_array(blob, FB.rxf_ext_cp), f_rxem = push_array(blob, FB.rxf_ext_mask),
            f_ht4 = push_array(blob, FB.ht4), f_arec = push_array(blob, FB.arec), f_urec = push_array(blob, FB.urec),
-           f_urec2 = push_array(blob, FB.urec2);
+           f_urec2 = push_array(blob, FB.urec2), f_tcps = push_array(blob, pat_tcps), f_txk = push_array(blob, tx_key),
+           f_txv = push_array(blob, tx_val), f_txi = push_array(blob, tx_inv);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -912,6 +985,12 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.rxf_ext_mask = (const uint64_t *)(B + f_rxem);
     F.f_first = f_first;
     F.empty_pat = empty_pat;
+    F.pat_tcps = (const uint32_t *)(B + f_tcps);
+    F.tx_key = (const uint32_t *)(B + f_txk);
+    F.tx_val = (const uint32_t *)(B + f_txv);
+    F.tx_inv = (const uint32_t *)(B + f_txi);
+    F.tx_unsafe_short = tx_unsafe_short;
+    F.tx_unsafe_edge = tx_unsafe_edge;
     h->n_anchor_fast = (int)FB.as_len.size();
 
     hipDeviceProp_t prop;
@@ -936,6 +1015,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     HIPCHK(h, hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking));
     HIPCHK(h, hipEventCreateWithFlags(&h->eve, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->evq, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->evx, hipEventDisableTiming));
     HIPCHK(h, hipEventCreate(&h->evs0));
     HIPCHK(h, hipEventCreate(&h->evs1));
     HIPCHK(h, hipEventCreate(&h->evt));
@@ -972,7 +1052,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
                    nw * per_out + (size_t)c.ns * c.item_cap * 8 + (size_t)c.hdr_cap * 8 + (size_t)c.defer_cap * 8 +
                    (size_t)c.ns * c.cand_cap * 4 + (size_t)c.ns * 4 + (size_t)c.hdr_cap * 12 + 4 * 256 +
                    (size_t)c.nr * c.rx_cap * 16 + (size_t)c.nk * per_tasks + (size_t)c.nk * 16 + c.dsize * 8 +
-                   32 * 256;
+                   (size_t)c.tx_cap + 64 + (size_t)c.hdr_cap * 16 + (size_t)c.defer_cap * 4 + 35 * 256;
     HIPCHK(h, hipMalloc(&h->d_scratch, total));
     uint8_t *p = (uint8_t *)h->d_scratch;
     auto carve = [&](size_t bytes) { uint8_t *r = p; p += (bytes + 255) & ~(size_t)255; return r; };
@@ -993,6 +1073,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.hdr = (uint2 *)carve((size_t)c.hdr_cap * 8);
     h->FS.defer_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
     h->FS.big_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
+    h->FS.res_list = (uint32_t *)carve((size_t)c.defer_cap * 4);
     h->FS.rx_tasks = (uint4 *)carve((size_t)c.nr * c.rx_cap * 16);
     h->FS.rx_cap = c.rx_cap;
     h->FS.vq = (uint4 *)carve((size_t)c.nk * c.vcap * 16);
@@ -1010,6 +1091,9 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.xcnt = tcnt + 3 * (size_t)c.nk;
     h->FS.dset = (unsigned long long *)carve(c.dsize * 8);
     h->FS.dmask = c.dsize - 1;
+    h->FS.vrec = (uint4 *)carve((size_t)c.hdr_cap * 16);
+    h->FS.tarena = (uint8_t *)carve((size_t)c.tx_cap + 64);
+    h->FS.tx_cap = c.tx_cap;
     size_t small = 1024 + nw * 4 + 256 + (nw + 1) * 8 + 256;
     HIPCHK(h, hipMalloc(&h->d_small, small));
     uint8_t *q = (uint8_t *)h->d_small;
@@ -1021,7 +1105,9 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.cmax = (uint32_t *)(q + 48);                  // 2 x u32
     h->S.gmax = (uint32_t *)(q + 56);                   // 2 x u32
     h->S.stats = (unsigned long long *)(q + 64);        // 3 x u64 (generic)
-    h->FS.stats = (unsigned long long *)(q + 128);      // 32 x u64 (fast path; 13.. developer counters)
+    h->FS.stats = (unsigned long long *)(q + 128);      // 32 x u64 (fast path; 21.. developer counters)
+    h->FS.tx_used = (unsigned long long *)(q + 384);    // transcoded-view bytes handed out
+    h->FS.res_cnt = (uint32_t *)(q + 392);              // documents left to the resolve kernel
     uint32_t *cnts = (uint32_t *)(q + 1024);
     h->out_cnt_all = cnts;
     h->FS.kout_cnt = cnts;
@@ -1056,6 +1142,9 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
 static int launch_scan(kw_handle *h)
 {
     hipStream_t st = h->stream;
+    // KW_SERIAL=1 (profiling aid): every kernel on the main stream, so kernel traces show isolated durations
+    static const bool serial = getenv("KW_SERIAL") != nullptr;
+    hipStream_t side = serial ? st : h->side, side2 = serial ? st : h->side2;
     const int64_t n_docs = h->n_docs;
     // split scan: filter regions (one wave each, resident at once), probe waves = filter regions,
     // epilogue waves = task regions
@@ -1106,10 +1195,14 @@ static int launch_scan(kw_handle *h)
     w.dsize = 4096;
     while (w.dsize < (uint64_t)std::max<int64_t>(n_docs, 1) * 16) w.dsize <<= 1;
     if (const char *e = getenv("KW_TEST_DSET_SIZE")) w.dsize = std::max<uint64_t>(2, (uint64_t)atoll(e));
+    // transcoded view: 768 B per document (~25 % of 2 KB articles non-ASCII), or what the last scan wanted
+    w.tx_cap = std::max<uint64_t>((uint64_t)64 << 20, (uint64_t)std::max<int64_t>(n_docs, 1) * 768);
+    w.tx_cap = std::max<uint64_t>(w.tx_cap, h->tx_need);
+    if (const char *e = getenv("KW_TEST_TX_CAP")) w.tx_cap = (uint64_t)std::max<long long>(16, atoll(e));
     int rc = ensure_scratch(h, w);
     if (rc) return rc;
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
-    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 384, st));
+    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 400, st));   // status .. stats, tx_used, res_cnt
     HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
@@ -1122,23 +1215,18 @@ static int launch_scan(kw_handle *h)
         hipLaunchKernelGGL(kw_filter_kernel, dim3(nsb), dim3(FS_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
                            h->FS);
     HIPCHK(h, hipEventRecord(h->evf, st));
+    // the transcoded view of the documents with a non-ASCII field (the filter flagged them) on the side
+    // stream, beside the probe; the epilogue waits for it
+    HIPCHK(h, hipStreamWaitEvent(side, h->evf, 0));
+    if (n_docs > 0)
+        hipLaunchKernelGGL(kw_tx_kernel, dim3(std::max(1, (int)std::min<int64_t>((n_docs + TX_BLOCK - 1) / TX_BLOCK, (int64_t)h->cus * 8))),
+                           dim3(TX_BLOCK), 0, side, h->FT, h->arena, h->doc_off, n_docs, h->FS);
+    HIPCHK(h, hipEventRecord(h->evx, side));
     if (n_docs > 0)
         hipLaunchKernelGGL(kw_probe_kernel, dim3((n_regions + PK_WAVES - 1) / PK_WAVES), dim3(PK_BLOCK), 0, st, h->FT,
                            h->T, h->arena, h->doc_off, n_regions, h->FS);
     HIPCHK(h, hipEventRecord(h->evp, st));
-    // the documents with a non-ASCII field: the resolve kernel on the side stream, beside the epilogue and
-    // the task kernels (disjoint documents, disjoint result regions); joined before the generic kernel
-    HIPCHK(h, hipStreamWaitEvent(h->side, h->evp, 0));
-    HIPCHK(h, hipEventRecord(h->evs0, h->side));
-    if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, h->side, h->FT, h->T, h->arena, h->doc_off,
-                           n_docs, h->FS, h->S);
-        // its documents with more items than its LDS holds: one wave each, wave w in resolve wave w's regions
-        hipLaunchKernelGGL(kw_resolve_big_kernel, dim3(std::min(nrb * RK_WAVES, h->cus * 4)), dim3(WAVE), 0, h->side,
-                           h->FT, h->T, h->arena, h->doc_off, h->FS, h->S);
-        HIPCHK(h, hipGetLastError());
-    }
-    HIPCHK(h, hipEventRecord(h->evs1, h->side));
+    HIPCHK(h, hipStreamWaitEvent(st, h->evx, 0));
     if (n_docs > 0) {
         hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
                            h->FS, h->S);
@@ -1146,6 +1234,19 @@ static int launch_scan(kw_handle *h)
     }
     h->ns = n_regions;
     HIPCHK(h, hipEventRecord(h->ev1, st));
+    // the non-ASCII documents the epilogue's transcoded view left (DH_RESOLVE): the resolve kernel on the side
+    // stream, beside the task kernels (disjoint documents, disjoint result regions); joined before the generic kernel
+    HIPCHK(h, hipStreamWaitEvent(side, h->ev1, 0));
+    HIPCHK(h, hipEventRecord(h->evs0, side));
+    if (n_docs > 0) {
+        hipLaunchKernelGGL(kw_resolve_kernel, dim3(nrb), dim3(RK_BLOCK), 0, side, h->FT, h->T, h->arena, h->doc_off,
+                           n_docs, h->FS, h->S);
+        // its documents with more items than its LDS holds: one wave each, wave w in resolve wave w's regions
+        hipLaunchKernelGGL(kw_resolve_big_kernel, dim3(std::min(nrb * RK_WAVES, h->cus * 4)), dim3(WAVE), 0, side,
+                           h->FT, h->T, h->arena, h->doc_off, h->FS, h->S);
+        HIPCHK(h, hipGetLastError());
+    }
+    HIPCHK(h, hipEventRecord(h->evs1, side));
     if (n_docs > 0) {
         // flat resolve tasks: verify -> short -> regex (regex decisions of the first two queue up);
         // G[k] waves share each epilogue wave's task region
@@ -1160,9 +1261,9 @@ static int launch_scan(kw_handle *h)
         // verify and short-field tasks are independent (both only append decisions): side by side; the
         // regex tasks they (and the epilogue) queued run after both
         HIPCHK(h, hipEventRecord(h->eve, st));
-        HIPCHK(h, hipStreamWaitEvent(h->side2, h->eve, 0));
-        task(kw_short_kernel, G[2], h->side2);
-        HIPCHK(h, hipEventRecord(h->evq, h->side2));
+        HIPCHK(h, hipStreamWaitEvent(side2, h->eve, 0));
+        task(kw_short_kernel, G[2], side2);
+        HIPCHK(h, hipEventRecord(h->evq, side2));
         task(kw_verify_kernel, G[0], st);
         HIPCHK(h, hipStreamWaitEvent(st, h->evq, 0));
         task(kw_rx_task_kernel, G[3], st);
@@ -1291,6 +1392,11 @@ static int finish(kw_handle *h)
         h->stats[3] = fst[3];
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
         h->stats[17] = (unsigned long long)h->rescans;
+        {   // the transcoded view: documents it took / left to the resolve kernel; the next scan's capacity
+            unsigned long long used = 0;
+            HIPCHK(h, hipMemcpy(&used, h->FS.tx_used, sizeof(used), hipMemcpyDeviceToHost));
+            if (used > h->caps.tx_cap && !getenv("KW_TEST_TX_CAP")) h->tx_need = used + used / 8;
+        }
         if (getenv("KW_DUMP_TIMING")) {   // FK_TIMING builds: resolve-kernel cycles summed over waves
             fprintf(stderr, "KW_TIMING resolve decode %llu edge %llu items %llu short %llu regex %llu all %llu\n", fst[21],
                     fst[22], fst[23], fst[24], fst[25], fst[26]);
@@ -1376,7 +1482,10 @@ extern "C" int kw_doc_routes(kw_handle *h, uint8_t *routes, int64_t n)
     if (n > 0) HIPCHK(h, hipMemcpy(hdr.data(), h->FS.hdr, (size_t)n * sizeof(uint2), hipMemcpyDeviceToHost));
     for (int64_t d = 0; d < n; ++d) {
         const uint32_t y = hdr[d].y;
-        routes[d] = (y & DH_DEFER) ? KW_ROUTE_GENERIC : (y & (DH_NA0 | DH_NA1)) ? KW_ROUTE_RESOLVE : KW_ROUTE_SCAN;
+        routes[d] = (y & DH_DEFER)                ? KW_ROUTE_GENERIC
+                    : (y & DH_TX)                 ? KW_ROUTE_TRANSCODE
+                    : (y & (DH_NA0 | DH_NA1))     ? KW_ROUTE_RESOLVE
+                                                  : KW_ROUTE_SCAN;
     }
     return KW_OK;
 }
@@ -1408,6 +1517,7 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->side2) (void)hipStreamDestroy(h->side2);
     if (h->eve) (void)hipEventDestroy(h->eve);
     if (h->evq) (void)hipEventDestroy(h->evq);
+    if (h->evx) (void)hipEventDestroy(h->evx);
     if (h->evp) (void)hipEventDestroy(h->evp);
     delete h;
     return KW_OK;

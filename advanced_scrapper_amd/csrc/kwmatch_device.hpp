@@ -43,6 +43,8 @@ constexpr uint32_t PI_LITERAL = 2u;      // F: re.finditer(name) == literal sear
 constexpr uint32_t PI_WORD_FIRST = 4u;   // U: first code point is a \b word char
 constexpr uint32_t PI_WORD_LAST = 8u;    // U: last code point is a \b word char
 constexpr uint32_t PI_ASCII = 16u;       // every code point < 128 (bytes = code points)
+constexpr uint32_t PI_TXUNSAFE = 32u;    // F: the transcoded view cannot decide it (a code point without a
+                                         // marker, or quantified regex atoms over non-ASCII code points)
 // m (code points) in bits [15:8], byte length in bits [31:16]
 __host__ __device__ inline uint32_t pi_m(uint32_t pi) { return (pi >> 8) & 0xFF; }
 __host__ __device__ inline uint32_t pi_blen(uint32_t pi) { return pi >> 16; }

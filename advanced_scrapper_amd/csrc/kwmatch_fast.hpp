@@ -71,6 +71,8 @@ constexpr uint32_t DH_EDGE1 = 1u << 19;
 constexpr uint32_t DH_NA0 = 1u << 20;           // field 0 has non-ASCII bytes
 constexpr uint32_t DH_NA1 = 1u << 21;
 constexpr uint32_t DH_DEFER = 1u << 22;         // sent to the generic kernel by the scan
+constexpr uint32_t DH_TX = 1u << 23;            // finished by the epilogue on its transcoded view (hdr)
+constexpr uint32_t DH_RESOLVE = 1u << 24;       // non-ASCII document left to the resolve kernel (dflags)
 static_assert(FK_ITEMS0 < 1024 && FK_ITEMS1 < 128, "item counts must fit the document header");
 
 struct FastTables {
@@ -128,6 +130,14 @@ struct FastTables {
     const uint32_t *rxf_ext_off;   // [r + 1] non-ASCII literal atoms
     const uint32_t *rxf_ext_cp;
     const uint64_t *rxf_ext_mask;
+    // transcoded view of non-ASCII documents (one byte per code point: ASCII as is, the other code points of
+    // the fuzzy names as markers 0x81..0xFF, every other code point 0x80)
+    const uint32_t *pat_tcps;   // per pattern (pat_cp_off): code points with the non-ASCII ones as markers
+    const uint32_t *tx_key;     // [256] non-ASCII code point -> tx_val (open addressing, ~0 = empty)
+    const uint32_t *tx_val;
+    const uint32_t *tx_inv;     // [128] marker - 0x80 -> code point (~0 for 0x80: no name holds it)
+    int tx_unsafe_short;        // a name the view cannot decide (PI_TXUNSAFE) may decide a short field
+    int tx_unsafe_edge;         // ... or an edge window
 };
 
 struct FastScratch {
@@ -166,6 +176,13 @@ struct FastScratch {
     uint2 *ncnt;                // per document: items of field 0 / field 1 (the probe adds them up)
     uint32_t *dflags;           // per document: DH_NA0 / DH_NA1 (the filter ORs them in) and DH_DEFER (probe)
     uint32_t *cmax;             // [2] largest candidate / item count a region needed (rescan sizing)
+    // the epilogue's transcoded view of non-ASCII documents
+    uint8_t *tarena;            // tx_cap bytes, bump-allocated per document (tx_used)
+    unsigned long long tx_cap;
+    unsigned long long *tx_used;
+    uint4 *vrec;                // per document: {text start lo, hi | transcoded << 31, text / title code points}
+    uint32_t *res_list;         // documents the epilogue left to the resolve kernel (DH_RESOLVE; defer_cap)
+    uint32_t *res_cnt;
 };
 
 // host + device hashes of the LDS tables

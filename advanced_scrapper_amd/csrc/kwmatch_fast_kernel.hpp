@@ -534,7 +534,7 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
             const int c_cnt = (int)(s_hi + L - 1 - s_lo);
             uint64_t D = 0;
             const uint8_t *t = txt + (s_lo - tb);
-            if (F.ascii) {
+            if (F.ascii && !F.tx) {
 #pragma unroll 8
                 for (int k = 0; k < c_cnt; ++k) {
                     D = ((D << 1) | 1ull) & tab[t[k] & 0x7Fu];
@@ -546,8 +546,8 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
                     uint64_t B;
                     if (b < 128) {
                         B = tab[b];
-                    } else {
-                        const uint32_t c = F.cps[s_lo + k];
+                    } else {   // (transcoded view: the marker's code point; 0x80 is none of the names')
+                        const uint32_t c = F.tx ? FT.tx_inv[b & 0x7Fu] : F.cps[s_lo + k];
                         B = anym;
                         for (uint32_t e = eb; e < ee; ++e)
                             if (FT.rxf_ext_cp[e] == c) B |= FT.rxf_ext_mask[e];
@@ -645,7 +645,8 @@ __device__ __forceinline__ void fk_regex_enqueue(const DevScratch &GS, const Fie
 // the field are the haystacks (exact-substring table for n <= 10, signatures + LCS above).
 // on_regex(P) receives the decided regex-class names (their positions need the regex search).
 template <class RxFn>
-__device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O,
+__device__ void fk_short_field(const FastTables &FT, const uint32_t *__restrict__ pcps, const DevScratch &GS,
+                               const FieldCtx &F, OutCtx &O,
                                unsigned long long &nver, unsigned long long &nwin, RxFn on_regex)
 {
     const int lane = lane_id();
@@ -680,7 +681,7 @@ __device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const
                 P = FT.sub_pat[b + idx];
                 const uint32_t m = pi_m(FT.pat_info[P]);
                 rk = FT.pat_rxk[P];
-                const uint32_t *nmp = FT.pat_cps + FT.pat_cp_off[P];
+                const uint32_t *nmp = pcps + FT.pat_cp_off[P];
                 for (uint32_t p = 0; p + n <= m && !hit; ++p) {
                     bool eq = true;
 #pragma unroll
@@ -731,7 +732,7 @@ __device__ void fk_short_field(const FastTables &FT, const DevScratch &GS, const
             const uint32_t m = pi_m(FT.pat_info[P]);
             bool exact = false;
             ++nver;
-            const uint32_t nmr = (lane < (int)m) ? FT.pat_cps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
+            const uint32_t nmr = (lane < (int)m) ? pcps[FT.pat_cp_off[P] + lane] : 0xFFFFFFFDu;
             if (!fk_short_decide(fc, n, nmr, m, &exact, nwin)) continue;
             if (FT.pat_rxk[P] == RXK_REGEX) on_regex(P);
             else emit_hits(O, GS, lane == 0, F.doc, P, exact ? 0u : KW_NOPOS, F.field);
@@ -892,7 +893,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     FK_TACC(tacc[2], tr2);
     // ---- short field: the field is the needle, the longer names are the haystacks
     FK_T0(tr3);
-    if (is_short) fk_short_field(FT, GS, F, O, nver, nwin, [&](uint32_t P) { fk_regex_enqueue(GS, F, P, RQ); });
+    if (is_short) fk_short_field(FT, FT.pat_cps, GS, F, O, nver, nwin, [&](uint32_t P) { fk_regex_enqueue(GS, F, P, RQ); });
     FK_TACC(tacc[3], tr3);
     return 0;
 }
@@ -1150,7 +1151,7 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                 // the name's code points, all loads in flight together; the window is in wb
                 uint32_t nmv[EDGE_MAX_M];
 #pragma unroll
-                for (int k = 0; k < (int)EDGE_MAX_M; ++k) nmv[k] = (uint32_t)k <= L ? FT.pat_cps[co + k] : 0u;
+                for (int k = 0; k < (int)EDGE_MAX_M; ++k) nmv[k] = (uint32_t)k <= L ? FT.pat_tcps[co + k] : 0u;
                 bool eq = true;
 #pragma unroll
                 for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j) {
@@ -1176,13 +1177,17 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
 
 // ---------------------------------------------------------------- kernel: the tasks of the flat resolve
 // Task wave t works the task regions of scan wave t: verify, edge, short, then regex tasks.
-__device__ __forceinline__ void fk_field_ctx(FieldCtx &F, const uint8_t *arena, const int64_t *off, uint32_t doc,
+// field of an epilogue document through its view record (the arena, or the transcoded view of a document
+// with a non-ASCII field: one byte per code point)
+__device__ __forceinline__ void fk_field_ctx(FieldCtx &F, const uint8_t *arena, const FastScratch &S, uint32_t doc,
                                              uint32_t field)
 {
-    F.arena = arena;
-    F.fb = off[2 * (int64_t)doc + field];
-    F.fe = off[2 * (int64_t)doc + field + 1];
-    F.n = (uint32_t)(F.fe - F.fb);
+    const uint4 v = S.vrec[doc];
+    F.tx = (v.y >> 31) != 0;
+    F.arena = F.tx ? S.tarena : arena;
+    F.fb = (int64_t)(((uint64_t)(v.y & 0x7FFFFFFFu) << 32) | v.x) + (field ? (int64_t)v.z : 0);
+    F.n = field ? v.w : v.z;
+    F.fe = F.fb + F.n;
     F.ascii = true;
     F.cps = nullptr;
     F.blkcnt = nullptr;
@@ -1408,10 +1413,14 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
         const bool lanewise = todo && (pi & PI_ASCII) != 0;
         int64_t fb = 0;
         uint32_t n = 0;
+        bool tx = false;
         if (todo) {
-            fb = off[2 * (int64_t)doc + field];
-            n = (uint32_t)(off[2 * (int64_t)doc + field + 1] - fb);
+            const uint4 v = S.vrec[doc];
+            tx = (v.y >> 31) != 0;
+            fb = (int64_t)(((uint64_t)(v.y & 0x7FFFFFFFu) << 32) | v.x) + (field ? (int64_t)v.z : 0);
+            n = field ? v.w : v.z;
         }
+        const uint8_t *la = tx ? S.tarena : arena;
         const uint32_t q = tk.z, o = tk.w & 0xFFu, pl = (tk.w >> 8) & 0xFFu;
         uint64_t NW[8];
         {
@@ -1430,7 +1439,7 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
         uint32_t nwj = 0, pre = 0, cj = 0;
         if (lanewise) {
             ++nver;
-            nwj = lv_band(arena, fb, n, NW, m, (int64_t)q - (int64_t)o, kfull(m), win, pmin);
+            nwj = lv_band(la, fb, n, NW, m, (int64_t)q - (int64_t)o, kfull(m), win, pmin);
             pre = q + pl + 1 <= m ? 1u : 0u;
             cj = nwj + pre + (q + m > n ? 1u : 0u);
         }
@@ -1455,6 +1464,7 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
             const uint32_t fbl = (uint32_t)__shfl((int)(uint32_t)fb, l, WAVE);
             const uint32_t fbh = (uint32_t)__shfl((int)(uint32_t)((uint64_t)fb >> 32), l, WAVE);
             const int64_t jfb = (int64_t)(((uint64_t)fbh << 32) | fbl);
+            const uint8_t *ja = __shfl((int)tx, l, WAVE) ? S.tarena : arena;
             if (!jv) continue;
             // job kind: full window at pmin + j, prefix text[:w] (w < m), suffix text[i:] (reversed)
             const bool full = j < jnwj;
@@ -1466,7 +1476,7 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
                 const int64_t ad = A + 4 * w;
-                win[w] = (ad + 4 > jfb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+                win[w] = (ad + 4 > jfb && ad < fe) ? *(const uint32_t *)(ja + ad) : 0u;
             }
             const uint32_t d0 = (uint32_t)(jfb + start - A);
             const uint64_t needle = low_mask(jm);
@@ -1507,11 +1517,11 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
             const int l = __builtin_ctzll(wm);
             wm &= wm - 1;
             FieldCtx F;
-            fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readlane((int)doc, l),
+            fk_field_ctx(F, arena, S, (uint32_t)__builtin_amdgcn_readlane((int)doc, l),
                          (uint32_t)__builtin_amdgcn_readlane((int)field, l));
             const uint32_t lP = (uint32_t)__builtin_amdgcn_readlane((int)P, l);
             const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
-            const uint32_t nm = (lane < (int)lm) ? FT.pat_cps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
+            const uint32_t nm = (lane < (int)lm) ? FT.pat_tcps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
             const uint32_t lw = (uint32_t)__builtin_amdgcn_readlane((int)tk.w, l);
             const uint32_t lq = (uint32_t)__builtin_amdgcn_readlane((int)tk.z, l);
             ++nver_w;
@@ -1642,7 +1652,7 @@ __device__ __forceinline__ void fk_short_run(const FastTables &FT, const DevScra
         slow &= slow - 1;
         const uint32_t lP = (uint32_t)__builtin_amdgcn_readlane((int)P, l);
         const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)m, l);
-        const uint32_t nmr = (lane < (int)lm) ? FT.pat_cps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
+        const uint32_t nmr = (lane < (int)lm) ? FT.pat_tcps[FT.pat_cp_off[lP] + lane] : 0xFFFFFFFDu;
         bool exact = false;
         const bool dec = fk_short_decide(fc, n, nmr, lm, &exact, nwin_w);
         if (lane == l) {
@@ -1664,28 +1674,35 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
     const int lane = lane_id();
     const uint32_t n = F.n;
     if (n <= (uint32_t)SHORT_EXACT_MAX) {
-        fk_short_field(FT, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
+        fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
         return;
     }
-    const uint64_t needle = low_mask(n);
-    uint64_t FW[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        uint64_t x = 0;
-        if (8 * w < (int)n) x = load8(F.arena, F.fb + 8 * w);
-        const int rem = (int)n - 8 * w;
-        if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
-        FW[w] = x;
-    }
-    // the field's match vectors for every ASCII byte, and its signature
-    const uint64_t m0 = lv_match(FW, (uint32_t)lane, needle), m1 = lv_match(FW, (uint32_t)lane + 64, needle);
-    wave_sync();
-    pm[lane] = m0;
-    pm[lane + 64] = m1;
-    uint64_t fsig = (m0 ? 1ull << lane : 0ull) | (m1 ? 1ull << lane : 0ull);   // bit c & 63
+    // the field's signature first (bit c & 63 of every byte): most fields have no candidate name at all
+    const uint32_t fc = (lane < (int)n) ? (uint32_t)F.arena[F.fb + lane] : 0xFFFFFFFCu;
+    uint64_t fsig = (lane < (int)n) ? 1ull << (fc & 63u) : 0ull;
 #pragma unroll
     for (int d = 1; d < WAVE; d <<= 1) fsig |= __shfl_xor(fsig, d, WAVE);
-    const uint32_t fc = (lane < (int)n) ? (uint32_t)F.arena[F.fb + lane] : 0xFFFFFFFCu;
+    bool have_pm = false;
+    auto run = [&](uint32_t nc) {
+        if (!have_pm) {   // the field's match vectors for every ASCII byte (LDS pm), built for the first candidates
+            const uint64_t needle = low_mask(n);
+            uint64_t FW[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                uint64_t x = 0;
+                if (8 * w < (int)n) x = load8(F.arena, F.fb + 8 * w);
+                const int rem = (int)n - 8 * w;
+                if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
+                FW[w] = x;
+            }
+            const uint64_t m0 = lv_match(FW, (uint32_t)lane, needle), m1 = lv_match(FW, (uint32_t)lane + 64, needle);
+            pm[lane] = m0;
+            pm[lane + 64] = m1;
+            have_pm = true;
+            wave_sync();
+        }
+        fk_short_run(FT, GS, F, O, X, pm, names, cand, nc, fc, nver, nwin, nwin_w);
+    };
     wave_sync();
     const uint32_t allow = (2 * n - 1) / 20;
     const uint32_t count = (uint32_t)FT.f_count_ge[n];
@@ -1705,7 +1722,7 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
             const uint64_t cm = __ballot(cnd);
             if (!cm) continue;
             if (nc + (uint32_t)__popcll(cm) > (uint32_t)WAVE) {
-                fk_short_run(FT, GS, F, O, X, pm, names, cand, nc, fc, nver, nwin, nwin_w);
+                run(nc);
                 nc = 0;
             }
             if (cnd) cand[nc + mbcnt(cm)] = (uint32_t)FT.f_first + c0 + (uint32_t)lane;
@@ -1713,7 +1730,7 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
             wave_sync();
         }
     }
-    if (nc) fk_short_run(FT, GS, F, O, X, pm, names, cand, nc, fc, nver, nwin, nwin_w);
+    if (nc) run(nc);
 }
 
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
@@ -1742,12 +1759,12 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
     const uint4 *sq = S.sq + (size_t)t * S.scap;
     for (uint32_t k = sub; k < ns; k += (uint32_t)G) {
         const uint4 tk = sq[k];
-        fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
+        fk_field_ctx(F, arena, S, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
         if (FK_SHORT_LANES)
             fk_short_lanes(FT, GS, F, O, X, pm, names, cand, nver, nwin, nver_w, nwin_w);
         else
-            fk_short_field(FT, GS, F, O, nver_w, nwin_w,
+            fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w,
                            [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
     }
     task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
@@ -1776,7 +1793,7 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, Dev
     for (uint32_t k = sub; k < nx; k += (uint32_t)G) {
         const uint4 tk = xq[k];
         const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
-        fk_field_ctx(F, arena, off, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
+        fk_field_ctx(F, arena, S, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
         fk_regex_now(FT, T, GS, F, O, y >> 1, rxtab, txt, nrx, nrx_bt, nrx_rounds);
     }
     task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
@@ -1920,7 +1937,7 @@ __device__ __forceinline__ void rk_wave_tail(const FastTables &FT, const DevTabl
         v += __shfl_xor(v, dd, WAVE);
         w += __shfl_xor(w, dd, WAVE);
     }
-    if (lane == 0) {
+    if (lane == 0 && (C.nres | C.ndefer)) {   // (a wave without documents adds nothing: no same-address atomics)
         atomicAdd(&S.stats[2], w / WAVE);
         atomicAdd(&S.stats[3], v / WAVE);
         atomicAdd(&S.stats[4], (unsigned long long)C.ndefer);
@@ -1968,15 +1985,16 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0};   // FK_TIMING: decode, edge, items, short, regex, all
     FK_T0(tall0);
 
-    for (int64_t c0 = wave * WAVE; c0 < n_docs; c0 += n_waves * WAVE) {
-        // lane = document: this kernel owns the documents with a non-ASCII field (the epilogue kernel the
-        // others); it runs beside the epilogue and task kernels, right after the probe
-        const int64_t dl = c0 + lane;
+    const int64_t n_list = (int64_t)min(*S.res_cnt, S.defer_cap);
+    for (int64_t c0 = wave * WAVE; c0 < n_list; c0 += n_waves * WAVE) {
+        // lane = document: this kernel owns the documents the epilogue left to it (res_list, DH_RESOLVE: a
+        // non-ASCII field its transcoded view cannot take); it runs beside the task kernels, after the epilogue
+        const int64_t dl = c0 + lane < n_list ? (int64_t)S.res_list[c0 + lane] : n_docs;
         uint2 hl = make_uint2(0u, 0u);
         bool dfr = false, dfr_items = false;
         {
             const uint32_t fl = dl < n_docs ? S.dflags[dl] : 0u;
-            if (fl & (DH_NA0 | DH_NA1)) {
+            if (fl & DH_RESOLVE) {   // (the epilogue's non-ASCII documents its transcoded view cannot take)
                 const uint2 nc = S.ncnt[dl];
                 const uint32_t ibeg = S.hdr[dl].x;
                 const int64_t t0 = off[2 * dl], t1 = off[2 * dl + 1], t2 = off[2 * dl + 2];
@@ -2030,7 +2048,7 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
         while (todo) {
             const int l = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const int64_t d = c0 + l;
+            const int64_t d = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dl, l);
             const uint32_t hx = (uint32_t)__shfl((int)hl.x, l, WAVE);
             const uint32_t hy = (uint32_t)__shfl((int)hl.y, l, WAVE);
             rk_resolve_doc<FK_ITEMS_MAX>(FT, T, GS, S, arena, off, d, hx, hy & 1023u, (hy >> DH_N1_SHIFT) & 127u, hy,

@@ -119,6 +119,7 @@ struct FieldCtx {
     const uint32_t *cps;    // decoded code points (non-ASCII fields)
     const uint32_t *blkcnt; // cumulative lead-byte counts per 64 B block
     uint32_t doc, field;
+    bool tx = false;        // the epilogue's transcoded view (ascii: one byte per code point, markers >= 0x80)
 };
 
 __device__ __forceinline__ uint32_t fcp(const FieldCtx &F, uint32_t i)

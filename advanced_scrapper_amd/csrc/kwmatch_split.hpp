@@ -44,8 +44,11 @@ constexpr int PK_BLOCK = PK_WAVES * WAVE;
 #define PK_POOL_CFG 1024
 #endif
 constexpr int PK_POOL = PK_POOL_CFG;     // items one batch of 64 candidates may stage (more: their documents defer)
+#ifndef FK_TX
+#define FK_TX 1     // 0: every document with a non-ASCII field goes to the resolve kernel
+#endif
 #ifndef EK_MINW
-#define EK_MINW 5   // 96 VGPRs, no spill: 5 waves per SIMD (measured 9.10 vs 9.35 ms per step)
+#define EK_MINW 4   // 128 VGPRs, no spill (5 waves per SIMD spills 96 B per lane: epilogue 2.08 vs 1.98 ms)
 #endif
 #ifndef PK_MINW
 #define PK_MINW 1
@@ -545,6 +548,276 @@ __device__ __forceinline__ uint32_t fk_edge_flags(const FastTables &FT, const Fa
     return ((em & 3ull) ? DH_EDGE0 : 0u) | ((em & 12ull) ? DH_EDGE1 : 0u);
 }
 
+// fk_edge_flags with the keys already loaded (lanes 0..3: epi_prefetch)
+__device__ __forceinline__ uint32_t fk_edge_flags_key(const FastTables &FT, const FastDoc &D, uint64_t k)
+{
+    const int lane = lane_id();
+    const int f = lane >> 1;
+    const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+    bool e = false;
+    if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+        const uint32_t idx = fk_edge_index(k);
+        e = (((lane & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u;
+    }
+    const uint64_t em = __ballot(e);
+    return ((em & 3ull) ? DH_EDGE0 : 0u) | ((em & 12ull) ? DH_EDGE1 : 0u);
+}
+
+// ---------------------------------------------------------------- transcoded view of non-ASCII documents
+// A document with a non-ASCII field is rewritten to one byte per code point (ASCII as is, the non-ASCII code
+// points of the fuzzy names as their markers 0x81..0xFF, any other code point 0x80) in S.tarena by
+// kw_tx_kernel (side stream, beside the probe); the epilogue turns its items' byte positions into code point
+// positions and finishes it exactly like an all-ASCII document: every comparison the epilogue and the task
+// kernels make is then code point against code point (names through pat_tcps, positions are code point
+// indices as re.finditer reports them).  Documents the view cannot decide (an item of a PI_TXUNSAFE name,
+// more items than the epilogue holds, a non-ASCII field over FK_CP_CAP bytes, no room left) go to the resolve
+// kernel (DH_RESOLVE).
+//
+// Per transcoded document, one tarena allocation (16-byte aligned): the text's then the title's code point
+// bytes (tx_bytes), then per non-ASCII field the code points before each 16-byte chunk of the field's arena
+// bytes (u16, chunks counted from fb & ~15); vrec[d] = {start lo, start hi | 1 << 31, text cps, title cps}
+// (vrec[d].y = ~0: not transcoded).
+#ifndef TX_NOSTORE   // profiling aid: 1 = the view's body stores are skipped (wrong results, store cost measured)
+#define TX_NOSTORE 0
+#endif
+constexpr int TX_WAVES = 4;
+constexpr int TX_BLOCK = TX_WAVES * WAVE;
+constexpr uint32_t TX_NONE = 0xFFFFFFFFu;
+constexpr unsigned long long TX_SLAB = 16384;   // bytes of tarena a transcoding wave takes at a time
+
+__device__ __forceinline__ uint64_t tx_bytes(int64_t l0, int64_t l1)
+{
+    return ((uint64_t)(l0 + l1) + 16ull + 15ull) & ~15ull;   // (+16: unaligned reads past the end)
+}
+__device__ __forceinline__ uint32_t tx_nchunks(int64_t fb, int64_t fe) { return (uint32_t)((fe - (fb & ~(int64_t)15) + 15) >> 4) + 1u; }
+
+__device__ __forceinline__ uint32_t tx_marker(const FastTables &FT, uint32_t cp)
+{
+    uint32_t s = (cp * 0x9E3779B1u) >> 24;
+    for (int k = 0; k < 256; ++k) {
+        const uint32_t kk = FT.tx_key[s];
+        if (kk == cp) return FT.tx_val[s];
+        if (kk == 0xFFFFFFFFu) break;
+        s = (s + 1) & 255u;
+    }
+    return 0x80u;
+}
+
+// Field bytes [fb, fe) of the arena -> out[o0, o0 + n) (one byte per code point; out 16-byte aligned); chunk
+// (may be null) [k] = code points of the field before its 16-byte chunk k.  stg: the wave's 1040-byte LDS
+// staging buffer (each 1 KiB block's output leaves with 16-byte stores).  Returns n.  Whole wave.
+__device__ uint32_t tx_field(const FastTables &FT, const uint8_t *__restrict__ a, int64_t fb, int64_t fe,
+                             uint8_t *__restrict__ out, uint32_t o0, uint16_t *__restrict__ chunk, uint8_t *stg)
+{
+    const int lane = lane_id();
+    const int64_t base = fb & ~(int64_t)15;
+    uint32_t count = 0;
+    for (int64_t blk = base; blk < fe; blk += 1024) {
+        const int64_t lp = blk + 16 * (int64_t)lane;
+        uint32_t W[5];
+        if (lp < fe) {
+            const uint4 v = *(const uint4 *)(a + lp);
+            W[0] = v.x; W[1] = v.y; W[2] = v.z; W[3] = v.w;
+        } else {
+            W[0] = W[1] = W[2] = W[3] = 0;
+        }
+        W[4] = (uint32_t)__shfl_down((int)W[0], 1, WAVE);
+        if (lane == WAVE - 1) W[4] = (blk + 1024 < fe) ? *(const uint32_t *)(a + blk + 1024) : 0u;
+        const int64_t r0 = fb - lp, r2 = fe - lp;
+        const int jlo = r0 <= 0 ? 0 : (r0 >= 16 ? 16 : (int)r0);
+        const int jhi = r2 <= 0 ? 0 : (r2 >= 16 ? 16 : (int)r2);
+        const uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
+        uint32_t lead = 0, high = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t b = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            lead |= (uint32_t)((b & 0xC0u) != 0x80u) << j;
+            high |= (uint32_t)(b >= 0x80u) << j;
+        }
+        lead &= valid;
+        high &= valid;
+        int total;
+        const int ex = wave_excl_scan(__popc(lead), &total);
+        if (chunk && lp < fe) chunk[(lp - base) >> 4] = (uint16_t)(count + (uint32_t)ex);
+        // the block's output, staged: lanes without a multi-byte character copy their bytes
+        wave_sync();
+        uint32_t k = (uint32_t)ex;
+        if (high == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if ((lead >> j) & 1u) stg[k++] = (uint8_t)(W[j >> 2] >> (8 * (j & 3)));
+        } else {
+            uint32_t lm = lead;
+            while (lm) {
+                const int j = __ffs(lm) - 1;
+                lm &= lm - 1;
+                const uint32_t b0 = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                uint32_t c = b0;
+                if (b0 >= 0x80u) {
+                    const uint32_t n = (b0 >= 0xF0u) ? 4u : (b0 >= 0xE0u) ? 3u : 2u;
+                    c = b0 & (0x7Fu >> n);
+                    for (uint32_t q = 1; q < n; ++q) {
+                        const int jj = j + (int)q;
+                        const uint32_t bk = (lp + jj < fe) ? ((W[jj >> 2] >> (8 * (jj & 3))) & 0xFFu) : 0x80u;
+                        c = (c << 6) | (bk & 0x3Fu);
+                    }
+                    c = tx_marker(FT, c);
+                }
+                stg[k++] = (uint8_t)c;
+            }
+        }
+        wave_sync();
+        // out[count, count + total): 16-byte stores for the aligned body, byte stores at the two ends
+        const uint32_t g0 = o0 + count, g1 = g0 + (uint32_t)total;
+        const uint32_t a0 = (g0 + 15u) & ~15u, a1 = g1 & ~15u;
+        if (a0 < a1) {
+            if ((uint32_t)lane < a0 - g0) out[g0 + lane] = stg[lane];
+            if ((uint32_t)lane < g1 - a1) out[a1 + lane] = stg[a1 - g0 + lane];
+            for (uint32_t q = a0 + 16u * (uint32_t)lane; q < a1; q += 16u * WAVE) {
+                const uint32_t so = q - g0;
+                uint32_t w[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    w[i] = (uint32_t)stg[so + 4 * i] | ((uint32_t)stg[so + 4 * i + 1] << 8) |
+                           ((uint32_t)stg[so + 4 * i + 2] << 16) | ((uint32_t)stg[so + 4 * i + 3] << 24);
+                if (!TX_NOSTORE) *(uint4 *)(out + q) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        } else {
+            for (uint32_t q = g0 + (uint32_t)lane; q < g1; q += WAVE) out[q] = stg[q - g0];
+        }
+        count += (uint32_t)total;
+    }
+    wave_sync();
+    return count;
+}
+
+// Transcode the documents with a non-ASCII field (the filter's dflags) into the view.  One wave takes 64
+// documents at a time (lane = document), then their non-ASCII ones in turn.
+__global__ __launch_bounds__(TX_BLOCK) void kw_tx_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+                                                         const int64_t *__restrict__ off, int64_t n_docs, FastScratch S)
+{
+    __shared__ uint32_t stg_all[TX_WAVES * (1040 / 4)];
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t wave = (int64_t)blockIdx.x * TX_WAVES + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * TX_WAVES;
+    uint8_t *stg = (uint8_t *)(stg_all + wib * (1040 / 4));
+    // the view's space: the wave takes TX_SLAB-byte slabs of tarena (one atomic each, not one per document)
+    unsigned long long slab = 0, slab_end = 0;
+    for (int64_t c0 = wave * WAVE; c0 < n_docs; c0 += n_waves * WAVE) {
+        const int64_t dl = c0 + lane;
+        const uint32_t fl = dl < n_docs ? S.dflags[dl] : 0u;
+        const bool na = (fl & (DH_NA0 | DH_NA1)) != 0;
+        // every lane's offsets at once (lane = document)
+        const int64_t lt0 = na ? off[2 * dl] : 0, lt1 = na ? off[2 * dl + 1] : 0, lt2 = na ? off[2 * dl + 2] : 0;
+        uint64_t todo = __ballot(na);
+        while (todo) {
+            const int l = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t d = c0 + l;
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fl, l);
+            const int64_t t0 = rdlane64(lt0, l), t1 = rdlane64(lt1, l), t2 = rdlane64(lt2, l);
+            const int64_t l0 = t1 - t0, l1 = t2 - t1;
+            bool ok = !(f & DH_DEFER) && l0 <= MAX_FIELD_BYTES && l1 <= MAX_FIELD_BYTES &&
+                      !((f & DH_NA0) && l0 > FK_CP_CAP) && !((f & DH_NA1) && l1 > FK_CP_CAP);
+            const uint64_t nb = tx_bytes(l0, l1);
+            const uint32_t nc0 = (f & DH_NA0) ? tx_nchunks(t0, t1) : 0u, nc1 = (f & DH_NA1) ? tx_nchunks(t1, t2) : 0u;
+            const unsigned long long need = nb + ((2ull * (nc0 + nc1) + 15ull) & ~15ull);
+            unsigned long long tb = 0;
+            if (ok) {
+                if (slab + need > slab_end) {
+                    const unsigned long long take = need > TX_SLAB ? need : TX_SLAB;
+                    unsigned long long b0 = 0;
+                    if (lane == 0) b0 = atomicAdd(S.tx_used, take);
+                    b0 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b0 >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b0);
+                    slab = b0;
+                    slab_end = b0 + take;
+                }
+                tb = slab;
+                slab += need;
+                ok = tb + need <= S.tx_cap;
+            }
+            if (!ok) {
+                if (lane == 0) S.vrec[d] = make_uint4(0u, TX_NONE, 0u, 0u);
+                continue;
+            }
+            uint8_t *out = S.tarena + tb;
+            uint16_t *ch = (uint16_t *)(S.tarena + tb + nb);
+            const uint32_t n0 = tx_field(FT, arena, t0, t1, out, 0u, (f & DH_NA0) ? ch : nullptr, stg);
+            const uint32_t n1 = tx_field(FT, arena, t1, t2, out, n0, (f & DH_NA1) ? ch + nc0 : nullptr, stg);
+            if (lane == 0) S.vrec[d] = make_uint4((uint32_t)tb, (uint32_t)(tb >> 32) | 0x80000000u, n0, n1);
+        }
+    }
+}
+
+// code point position of field byte bpos (field [fb, ...) of the arena; chunk from tx_field)
+__device__ __forceinline__ uint32_t tx_pos(const uint8_t *__restrict__ a, int64_t fb, const uint16_t *chunk,
+                                           uint32_t bpos)
+{
+    const int64_t base = fb & ~(int64_t)15, p = fb + bpos;
+    const int64_t k = (p - base) >> 4, cs = base + 16 * k;
+    const uint4 v = *(const uint4 *)(a + cs);
+    const uint32_t W[4] = {v.x, v.y, v.z, v.w};
+    const int jlo = fb > cs ? (int)(fb - cs) : 0, jhi = (int)(p - cs);
+    uint32_t c = chunk[k];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        c += (j >= jlo && j < jhi && (b & 0xC0u) != 0x80u) ? 1u : 0u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ uint64_t it_with_pos(uint64_t it, uint32_t pos)
+{
+    return (it & ~((uint64_t)IT_POS_MASK << IT_POS_SHIFT)) | ((uint64_t)pos << IT_POS_SHIFT);
+}
+
+// Finish a transcoded document (V = its vrec) in the epilogue.  D0: the document in the arena, flags: its
+// dflags | edge flags (of the arena bytes).  Returns false, before anything is emitted, when the resolve
+// kernel must take it; otherwise *done = the epilogue's result (false: the generic kernel).
+__device__ bool epi_tx_doc(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D0, uint4 V,
+                           uint32_t ibeg, uint32_t n0, uint32_t n1, uint32_t flags, uint64_t *items, int64_t wave,
+                           OutCtx &O, TaskCounts &TC, bool *done)
+{
+    const int lane = lane_id();
+    if (V.y == TX_NONE || (flags & DH_DEFER) || n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1) return false;
+    if (FT.tx_unsafe_edge && (((flags & DH_NA0) && (flags & DH_EDGE0)) || ((flags & DH_NA1) && (flags & DH_EDGE1))))
+        return false;
+    const uint32_t c0 = V.z, c1 = V.w;
+    // a short non-ASCII field meets every name at least as long: one the view cannot decide may be among them
+    if (FT.tx_unsafe_short && (((flags & DH_NA0) && c0 <= (uint32_t)MAXM) || ((flags & DH_NA1) && c1 <= (uint32_t)MAXM)))
+        return false;
+    const int64_t tb = (int64_t)(((uint64_t)(V.y & 0x7FFFFFFFu) << 32) | V.x);
+    const uint64_t nb = tx_bytes(D0.t1 - D0.t0, D0.t2 - D0.t1);
+    const uint16_t *ch0 = (const uint16_t *)(S.tarena + tb + nb);
+    const uint16_t *ch1 = ch0 + ((flags & DH_NA0) ? tx_nchunks(D0.t0, D0.t1) : 0u);
+    // the items at code point positions; a name the view cannot decide sends the document to the resolve kernel
+    const uint64_t *src = S.items + ibeg;
+    bool unsafe = false;
+    for (uint32_t i = (uint32_t)lane; i < n0 + n1; i += WAVE) {
+        uint64_t it = src[i];
+        const bool t = i < n0;
+        unsafe |= (FT.pat_info[it_pat(it)] & PI_TXUNSAFE) != 0;
+        if (flags & (t ? DH_NA0 : DH_NA1))
+            it = it_with_pos(it, tx_pos(D0.arena, t ? D0.t0 : D0.t1, t ? ch0 : ch1, it_pos(it)));
+        items[t ? i : FK_ITEMS0 + (i - n0)] = it;
+    }
+    if (__ballot(unsafe)) return false;
+    wave_sync();
+    FastDoc D;
+    D.arena = S.tarena;
+    D.t0 = tb;
+    D.t1 = D.t0 + c0;
+    D.t2 = D.t1 + c1;
+    D.doc = D0.doc;
+    D.l1 = (int32_t)c0;
+    D.l2 = (int32_t)(c0 + c1);
+    *done = fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+    return true;
+}
+
 // ---------------------------------------------------------------- big all-ASCII documents
 // An all-ASCII document with more items than one epilogue wave's LDS holds (FK_ITEMS0 / FK_ITEMS1; a
 // 50k-name KB has pieces that many names share), up to FK_BIG0 / FK_BIG1: finished by the same epilogue
@@ -599,10 +872,42 @@ uint32_t epi_big_doc(const FastTables &FT, const FastScratch &S, const DevScratc
     } else {
         // (the header's counts saturate: informational only past the resolve kernel)
         h.y = min(n0, 1023u) | (min(n1, 127u) << DH_N1_SHIFT) | flags;
+        if (lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
     }
     if (lane == 0) S.hdr[d] = h;
     wave_sync();
     return done ? 0u : 1u;
+}
+
+// the epilogue's per-document loads: lanes 0..2 the offsets, lane 3 the header, lane 4 the item counts,
+// lane 5 the flags (y)
+__device__ __forceinline__ void epi_meta(const FastScratch &S, const int64_t *__restrict__ off, int64_t d, int64_t &ov,
+                                         uint2 &hv)
+{
+    const int lane = lane_id();
+    ov = lane < 3 ? off[2 * d + lane] : 0;
+    hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) : make_uint2(0u, 0u)));
+}
+
+// the loads that depend on epi_meta's: lanes 0..3 the edge keys (first / last eight bytes of each field),
+// lanes < n0 + n1 the document's first 64 items (all-ASCII documents the epilogue will finish only)
+__device__ __forceinline__ void epi_prefetch(const uint8_t *__restrict__ arena, const FastScratch &S, int64_t ov,
+                                             uint2 hv, uint64_t &ek, uint64_t &itp)
+{
+    const int lane = lane_id();
+    const int64_t t0 = rdlane64(ov, 0), t1 = rdlane64(ov, 1), t2 = rdlane64(ov, 2);
+    const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5);
+    if (fl & (DH_NA0 | DH_NA1 | DH_DEFER)) return;
+    if (t1 - t0 > MAX_FIELD_BYTES || t2 - t1 > MAX_FIELD_BYTES) return;
+    const int f = lane >> 1;
+    const int64_t fb = f ? t1 : t0, fe = f ? t2 : t1;
+    if (lane < 4 && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+        const int64_t a = (lane & 1) ? fe - 8 : fb;
+        ek = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
+    }
+    const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4) + (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+    if ((uint32_t)lane < n) itp = S.items[ibeg + (uint32_t)lane];
 }
 
 // ---------------------------------------------------------------- kernel 3: per-document epilogue
@@ -621,18 +926,28 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
     const int64_t wave = (int64_t)blockIdx.x * EK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * EK_WAVES;
     uint64_t *items = items_all + wib * (FK_ITEMS0 + FK_ITEMS1);
-    uint32_t ndefer = 0, ndef_items = 0;
+    uint32_t ndefer = 0, ndef_items = 0, ntx = 0, nres = 0;
     OutCtx O;
     O.shared = nullptr;
     O.out = S.kout + (size_t)wave * S.out_cap;
     O.cap = S.out_cap;
     O.n = 0;
     TaskCounts TC = {0u, 0u, 0u, 0u};
+    // Software pipeline over the wave's documents: the next document's offsets / header / counts / flags
+    // are in flight while the current one is processed, and its edge keys and first 64 items are loaded
+    // right after, so a document starts with only the edge-bitmap and name-table round trips ahead of it.
+    int64_t ov = 0;
+    uint2 hv = make_uint2(0u, 0u);
+    uint64_t ek = 0, itp = 0;
+    if (wave < n_docs) {
+        epi_meta(S, off, wave, ov, hv);
+        epi_prefetch(arena, S, ov, hv, ek, itp);
+    }
     for (int64_t d = wave; d < n_docs; d += n_waves) {
-        // lanes 0..2: offsets, lane 3: header, lane 4: item counts, lane 5: flags (y)
-        const int64_t ov = lane < 3 ? off[2 * d + lane] : 0;
-        const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) :
-                                                                        make_uint2(0u, 0u)));
+        const int64_t dn = d + n_waves;
+        int64_t ovn = 0;
+        uint2 hvn = make_uint2(0u, 0u);
+        if (dn < n_docs) epi_meta(S, off, dn, ovn, hvn);
         FastDoc D;
         D.arena = arena;
         D.t0 = rdlane64(ov, 0);
@@ -643,56 +958,102 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         D.l2 = (int32_t)(D.t2 - D.t0);
         const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
         uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5);
-        if (flags & (DH_NA0 | DH_NA1)) continue;   // the resolve kernel's document
-        const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
-        const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
-        flags |= fk_edge_flags(FT, D);
-        bool defer = (flags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
-        if (defer && lane == 0) atomicAdd(&S.stats[15], 1ull);   // (rare: counted where they happen)
-        if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) {
-            // more items than this kernel's LDS holds: the big-document epilogue, beyond its caps the generic kernel
-            uint32_t bi = 0xFFFFFFFFu;
-            if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG1) {
-                if (lane == 0) bi = atomicAdd(&blk_n, 1u);
-                bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+        if (flags & (DH_NA0 | DH_NA1)) {
+            // a non-ASCII field: the transcoded view, or the resolve kernel
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
+            const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+            const uint32_t fl = flags | fk_edge_flags(FT, D);
+            bool done = false;
+            if (FK_TX && epi_tx_doc(FT, S, GS, D, S.vrec[d], ibeg, n0, n1, fl, items, wave, O, TC, &done)) {
+                ++ntx;
+                uint2 h;
+                h.x = ibeg;
+                if (!done) {
+                    ++ndefer;
+                    ++ndef_items;
+                    h.y = DH_DEFER;
+                    if (lane == 0) {
+                        atomicAdd(&S.stats[13], 1ull);
+                        const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                        if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
+                        else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+                    }
+                } else {
+                    h.y = n0 | (n1 << DH_N1_SHIFT) | (fl & ~DH_DEFER) | DH_TX;   // (vrec: kw_tx_kernel's)
+                }
+                if (lane == 0) S.hdr[d] = h;
+            } else {
+                ++nres;
+                if (lane == 0) {
+                    S.dflags[d] = flags | DH_RESOLVE;
+                    const uint32_t i = atomicAdd(S.res_cnt, 1u);
+                    if (i < S.defer_cap) S.res_list[i] = (uint32_t)d;
+                }
             }
-            if (bi < (uint32_t)EK_BIGQ) {
-                if (lane == 0) blk_docs[bi] = (uint32_t)d;
-                continue;
-            }
-            defer = true;
-            ++ndef_items;
-            if (lane == 0) atomicAdd(&S.stats[14], 1ull);
-        }
-        flags &= ~DH_DEFER;
-        bool done = false;
-        if (!defer && !(flags & (DH_NA0 | DH_NA1))) {
-            const uint64_t *src = S.items + ibeg;
-            for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) items[i] = src[i];
-            for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
             wave_sync();
-            done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
-            if (!done) {
-                defer = true;
-                ++ndef_items;
-                if (lane == 0) atomicAdd(&S.stats[13], 1ull);
-            }
-        }
-        uint2 h;
-        h.x = ibeg;
-        if (defer) {
-            ++ndefer;
-            h.y = DH_DEFER;
-            if (lane == 0) {
-                const uint32_t i = atomicAdd(S.defer_cnt, 1u);
-                if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
-                else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
-            }
         } else {
-            h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
+            const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+            flags |= fk_edge_flags_key(FT, D, ek);
+            bool defer = (flags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
+            if (defer && lane == 0) atomicAdd(&S.stats[15], 1ull);   // (rare: counted where they happen)
+            bool queued = false;
+            if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) {
+                // more items than this kernel's LDS holds: the big-document epilogue, beyond its caps the generic kernel
+                uint32_t bi = 0xFFFFFFFFu;
+                if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG1) {
+                    if (lane == 0) bi = atomicAdd(&blk_n, 1u);
+                    bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+                }
+                if (bi < (uint32_t)EK_BIGQ) {
+                    if (lane == 0) blk_docs[bi] = (uint32_t)d;
+                    queued = true;
+                } else {
+                    defer = true;
+                    ++ndef_items;
+                    if (lane == 0) atomicAdd(&S.stats[14], 1ull);
+                }
+            }
+            if (!queued) {
+                flags &= ~DH_DEFER;
+                if (!defer) {
+                    // the first 64 items came with the prefetch (text items first, then the title's)
+                    if ((uint32_t)lane < n0 + n1) items[(uint32_t)lane < n0 ? lane : FK_ITEMS0 + lane - (int)n0] = itp;
+                    const uint64_t *src = S.items + ibeg;
+                    for (uint32_t i = (uint32_t)lane + WAVE; i < n0; i += WAVE) items[i] = src[i];
+                    for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE)
+                        if (n0 + i >= (uint32_t)WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
+                    wave_sync();
+                    const bool done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+                    if (!done) {
+                        defer = true;
+                        ++ndef_items;
+                        if (lane == 0) atomicAdd(&S.stats[13], 1ull);
+                    }
+                }
+                uint2 h;
+                h.x = ibeg;
+                if (defer) {
+                    ++ndefer;
+                    h.y = DH_DEFER;
+                    if (lane == 0) {
+                        const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                        if (i < S.defer_cap) S.defer_list[i] = (uint32_t)d;
+                        else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+                    }
+                } else {
+                    h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
+                    if (lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
+                }
+                if (lane == 0) S.hdr[d] = h;
+                wave_sync();
+            }
         }
-        if (lane == 0) S.hdr[d] = h;
-        wave_sync();
+        ek = 0;
+        itp = 0;
+        if (dn < n_docs) epi_prefetch(arena, S, ovn, hvn, ek, itp);
+        ov = ovn;
+        hv = hvn;
     }
     // the workgroup's big documents: wave 0 with the whole workgroup's LDS as one 4096 + 512-item buffer
     __syncthreads();
@@ -715,6 +1076,8 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         }
         atomicAdd(&S.stats[4], (unsigned long long)ndefer);
         atomicAdd(&S.stats[5], (unsigned long long)ndef_items);
+        if (ntx) atomicAdd(&S.stats[18], (unsigned long long)ntx);
+        if (nres) atomicAdd(&S.stats[19], (unsigned long long)nres);
     }
 }
 

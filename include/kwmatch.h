@@ -118,8 +118,10 @@ int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void
  * beyond the probe's pool, a field beyond 8 MiB); [16] all-ASCII documents
  * finished by the big-document epilogue (more than 512 / 64 items); [17] times
  * the batch was scanned again after a device buffer grew (0 once the buffers
- * fit the workload: growth persists across kw_scan calls). */
-#define KW_N_STATS 18
+ * fit the workload: growth persists across kw_scan calls); documents with a
+ * non-ASCII field that [18] the epilogue finished on their transcoded view (one
+ * byte per code point) or [19] it left to the resolve kernel. */
+#define KW_N_STATS 20
 int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
 /* Device times (ms) of the last kw_scan, from HIP events on the scan's stream
@@ -138,11 +140,14 @@ int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 
 /* Which kernel finished each document of the last scan (after kw_hits):
  * routes[d] = KW_ROUTE_SCAN (the scan kernel's epilogue and its task kernels),
- * KW_ROUTE_RESOLVE (the resolve kernel: non-ASCII fields) or KW_ROUTE_GENERIC
- * (deferred to the generic kernel: capacity limits).  For tests and tuning. */
+ * KW_ROUTE_TRANSCODE (a non-ASCII field: the epilogue on the document's
+ * transcoded view, then the task kernels), KW_ROUTE_RESOLVE (the resolve
+ * kernel: non-ASCII fields the view cannot take) or KW_ROUTE_GENERIC (deferred
+ * to the generic kernel: capacity limits).  For tests and tuning. */
 #define KW_ROUTE_SCAN 0
 #define KW_ROUTE_RESOLVE 1
 #define KW_ROUTE_GENERIC 2
+#define KW_ROUTE_TRANSCODE 3
 int kw_doc_routes(kw_handle *h, uint8_t *routes, int64_t n);
 
 const char *kw_last_error(kw_handle *h);

@@ -339,6 +339,81 @@ def test_nonascii_wildcard_and_regex_names_vs_oracle():
     assert not bad, f"GPU differs from the oracle on non-ASCII wildcard docs {bad[:20]}"
 
 
+def _transcode_docs(ckb):
+    """Documents built around the KB's non-ASCII fuzzy names, for the epilogue's transcoded view: exact
+    occurrences, one-edit near misses (ASCII edits and the non-ASCII code point itself), edge windows (the
+    name cut at the field start / end), short non-ASCII titles (the name, a part, a one-deletion variant, a
+    <= 10 code point substring) and non-ASCII characters without markers sprinkled around them."""
+    rng = random.Random(53)
+    na = [n for n, c in zip(ckb.names, ckb.classes) if c == 'F' and any(ord(ch) > 127 for ch in n)]
+    assert na
+    words = ['market', 'shares', 'rose', 'the', 'company', 'said', 'on', 'Monday', 'analysts', 'quarter']
+    other = ['中', '😀', 'Ω', 'ж', '€', '—', 'ß']
+    texts, titles = [], []
+    for i in range(240):
+        n = na[i % len(na)]
+        k = rng.randrange(len(n))
+        edit = rng.choice(['exact', 'del', 'ins', 'del_na', 'swap_na'])
+        v = n
+        if edit == 'del':
+            v = n[:k] + n[k + 1:]
+        elif edit == 'ins':
+            v = n[:k] + rng.choice('xyz') + n[k:]
+        elif edit == 'del_na':
+            v = ''.join(ch for ch in n if ord(ch) < 128)
+        elif edit == 'swap_na':
+            v = ''.join(rng.choice(other) if ord(ch) > 127 else ch for ch in n)
+        filler = lambda: ' '.join(rng.choice(words + other) for _ in range(rng.randrange(5, 60)))
+        shape = rng.choice(['mid', 'start', 'end', 'both'])
+        if shape == 'mid':
+            t = f"{filler()} {v} {filler()}"
+        elif shape == 'start':
+            t = f"{v[rng.randrange(1, 3):]} {filler()}"
+        elif shape == 'end':
+            t = f"{filler()} {v[:-rng.randrange(1, 3)]}"
+        else:
+            t = f"{v} {filler()} {v}"
+        while len(t.encode()) <= 300:
+            t = rng.choice(words) + ' ' + t
+        texts.append(t)
+        j = rng.randrange(len(n))
+        titles.append(rng.choice([n, v, n[:j] + n[j + 1:], n[max(0, j - 6):j + 4], f"{n} {rng.choice(other)}",
+                                  f"{rng.choice(other)} news", 'plain title']))
+    return texts, titles
+
+
+@pytest.mark.parametrize('mode', ['view', 'no_markers', 'no_room'])
+def test_transcoded_view_vs_oracle(golden, monkeypatch, mode):
+    """Non-ASCII documents on the epilogue's transcoded view (one byte per code point; the fuzzy names'
+    non-ASCII code points as markers), and on the resolve kernel when the view cannot take them: names
+    without markers (KW_TEST_TX_MARKERS=0: every non-ASCII name is PI_TXUNSAFE) or no room in the view."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    if mode == 'no_markers':
+        monkeypatch.setenv('KW_TEST_TX_MARKERS', '0')
+    elif mode == 'no_room':
+        monkeypatch.setenv('KW_TEST_TX_CAP', '16')
+    processed = golden.kb_processed()
+    m = GpuMatcher(compile_kb(processed))
+    texts, titles = _transcode_docs(m.ckb)
+    got = _gpu_maps(m, texts, titles)
+    routes = m.doc_routes(len(texts))
+    bad = _compare(processed, texts, titles, got)
+    assert not bad, f"{mode}: GPU differs from the oracle on transcoded-view docs {bad[:20]}"
+    n_tx = int((routes == _native.KW_ROUTE_TRANSCODE).sum())
+    n_res = int((routes == _native.KW_ROUTE_RESOLVE).sum())
+    if mode == 'view':
+        assert n_tx > len(texts) // 2, (n_tx, n_res)
+    elif mode == 'no_room':
+        assert n_tx == 0 and n_res > 0, (n_tx, n_res)
+    else:
+        assert n_res > 0, (n_tx, n_res)
+
+
 @pytest.mark.parametrize('case', ['invalid_regex', 'bad_date', 'int_dates'])
 def test_dropin_error_paths_gpu(golden, tmp_path, monkeypatch, case):
     """process_chunk on the GPU writes exactly the rows the reference wrote before raising, and raises the

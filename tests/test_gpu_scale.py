@@ -1,11 +1,12 @@
 """Parity at bench scale: the bench's own config-2 corpus (1M synthetic ~2 KB articles, bench.py's seed).
 
-* a seeded sample of the corpus, a seeded sample of the documents the resolve
-  kernel finished (non-ASCII fields), every document the generic kernel
+* a seeded sample of the corpus, seeded samples of the documents with a
+  non-ASCII field (those the epilogue finished on their transcoded view and
+  those the resolve kernel finished), every document the generic kernel
   finished (capacity deferrals), and the documents closest to the capacity
   boundaries (the most hit records, the longest fields) are checked against
   the CPU oracle, field by field, positions included (the oracle takes ~60 ms
-  per article, so the 120k resolve-route documents are sampled, not all run);
+  per article, so the 120k non-ASCII documents are sampled, not all run);
 * config 3's sharding logic with the real kernels: the corpus is scanned as
   2-, 4- and 8-way contiguous byte-balanced shards one after another on this
   GPU, each shard's records are rebased to global document ids by
@@ -58,9 +59,12 @@ def test_bench_corpus_vs_oracle(bench_scan):
     rng = np.random.default_rng(SEED)
     pick = set(rng.choice(N_DOCS, 2000, replace=False).tolist())
     resolve = np.flatnonzero(routes == _native.KW_ROUTE_RESOLVE)
+    transcode = np.flatnonzero(routes == _native.KW_ROUTE_TRANSCODE)
     generic = np.flatnonzero(routes == _native.KW_ROUTE_GENERIC)
-    assert len(resolve) > 0
-    pick |= set(rng.choice(resolve, min(1500, len(resolve)), replace=False).tolist())
+    assert len(transcode) > 0
+    pick |= set(rng.choice(transcode, min(1200, len(transcode)), replace=False).tolist())
+    if len(resolve):
+        pick |= set(rng.choice(resolve, min(600, len(resolve)), replace=False).tolist())
     pick |= set(generic.tolist())
     per_doc = np.bincount(rec['doc'].astype(np.int64), minlength=N_DOCS)
     pick |= set(np.argsort(-per_doc, kind='stable')[:250].tolist())
@@ -90,7 +94,8 @@ def test_bench_corpus_vs_oracle(bench_scan):
                        if got_t.get(n) != want_t[k].get(n)},
                       {n: (got_i.get(n), want_i[k].get(n)) for n in set(got_i) | set(want_i[k])
                        if got_i.get(n) != want_i[k].get(n)})
-    print(f'checked {len(docs)} docs ({len(resolve)} resolve-route, {len(generic)} generic-route in the corpus)')
+    print(f'checked {len(docs)} docs ({len(transcode)} transcode-route, {len(resolve)} resolve-route, '
+          f'{len(generic)} generic-route in the corpus)')
     assert not bad, f'{len(bad)} of {len(docs)} documents differ from the oracle: {bad[:20]}'
 
 
