@@ -206,6 +206,9 @@ struct FastBuild {
     std::vector<int32_t> rxf_idx;
     std::vector<uint64_t> rxf_pm, rxf_any, rxf_ext_mask;
     std::vector<uint32_t> rxf_len, rxf_ext_off, rxf_ext_cp;
+    std::vector<uint8_t> rx_bytes;                  // RXM program strings (after the names in the device bytes)
+    std::vector<uint32_t> use_rxs, rxl;             // per use: RXM string offset (~0: none); per pattern: RXM length
+    std::vector<uint64_t> use_wild;                 // per use: wildcard positions of an RXM string
 };
 
 // rarest 4-byte window inside bytes [lo, hi) (hi - lo >= 4); returns its start
@@ -225,7 +228,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
                const std::vector<uint32_t> &pat_info,
                const std::vector<int4> &atoms, const std::vector<uint32_t> &rxo, std::string &err)
 {
-    struct Use { uint32_t pat, i0, i1; };
+    struct Use { uint32_t pat, i0, i1; uint32_t rxs = 0xFFFFFFFFu; uint64_t wild = 0; };   // rxs: RXM string offset
     std::unordered_map<std::string, uint32_t> aid;
     std::vector<std::string> astr;
     std::vector<std::vector<Use>> auses;
@@ -241,6 +244,9 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     B.edge_pre.assign(FK_EDGE_WORDS, 0);
     B.edge_suf.assign(FK_EDGE_WORDS, 0);
     B.boff.assign(std::max(n_pat, 1), 0);
+    B.rxl.assign(std::max(n_pat, 1), 0);
+    struct RxmTodo { uint32_t pat, L; uint64_t wild; std::string rs; };
+    std::vector<RxmTodo> rxm_todo;   // quantifier-free ASCII regex programs: RXM uses once every anchor is known
     B.sig.assign(std::max(n_pat, 1), 0);
     for (int i = 0; i < n_pat; ++i) {
         const uint8_t *s = pat_bytes + pat_off[i];
@@ -295,6 +301,20 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
                 B.rxf_any.push_back(any);
                 B.rxf_ext_off.push_back((uint32_t)B.rxf_ext_cp.size());
                 for (auto &e : ext) { B.rxf_ext_cp.push_back(e.first); B.rxf_ext_mask.push_back(e.second); }
+                // an RXM use: the program as a byte string with '.' wildcards (ASCII atoms only), anchored at
+                // its rarest 4-byte window of literals; the probe's RXM items are then exactly the program's
+                // matches in an ASCII field (re.finditer positions without a search over the field)
+                const uint32_t L = rxo[i + 1] - rxo[i];
+                bool ascii_prog = true;
+                std::string rs(L, '\0');
+                uint64_t wild = 0;
+                for (uint32_t a = rxo[i]; a < rxo[i + 1]; ++a) {
+                    const uint32_t k = a - rxo[i];
+                    if (atoms[a].x == KW_RX_ANY) { wild |= 1ull << k; continue; }
+                    if ((uint32_t)atoms[a].y >= 128u || atoms[a].y == 0) ascii_prog = false;
+                    rs[k] = (char)atoms[a].y;
+                }
+                if (ascii_prog) rxm_todo.push_back({(uint32_t)i, L, wild, rs});
             }
         }
         // m <= 20: interior windows must be exact (FULL); the one-deletion edge
@@ -374,6 +394,35 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
             a = b;
         }
     }
+    // ---- RXM uses: anchored at a window of literals whose first four bytes already key another anchor (the
+    // filters pass nothing new; the probe checks one more use there), the rarest such window
+    {
+        std::unordered_map<uint32_t, int> pre4;
+        for (const auto &st : astr)
+            if (st.size() >= 4) pre4[*(const uint32_t *)st.data()] = 1;
+        for (const auto &t : rxm_todo) {
+            size_t best = SIZE_MAX;
+            uint32_t bc = 0xFFFFFFFFu;
+            for (size_t w = 0; w + 4 <= t.L && w <= 255; ++w) {
+                if ((t.wild >> w) & 0xFull) continue;
+                if (!pre4.count(*(const uint32_t *)(t.rs.data() + w))) continue;
+                const uint32_t c = Q.count((const uint8_t *)t.rs.data() + w);
+                if (c < bc) { bc = c; best = w; }
+            }
+            if (best == SIZE_MAX) continue;   // (its positions come from the regex tasks' search)
+            size_t al = 4;
+            while (al < 8 && best + al < t.L && !((t.wild >> (best + al)) & 1ull)) ++al;
+            Use u;
+            u.pat = t.pat;
+            u.i0 = FU_RXM | ((uint32_t)best << 8);
+            u.i1 = t.L;
+            u.rxs = (uint32_t)B.rx_bytes.size();
+            u.wild = t.wild;
+            B.rx_bytes.insert(B.rx_bytes.end(), t.rs.begin(), t.rs.end());
+            B.rxl[t.pat] = t.L;
+            add(t.rs.substr(best, al), u);
+        }
+    }
     // ---- anchors, uses
     const uint32_t na = (uint32_t)astr.size();
     for (uint32_t a = 0; a < na; ++a) {
@@ -384,7 +433,13 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         B.as_len.push_back((uint32_t)st.size());
         B.as_use_begin.push_back((uint32_t)B.use_pat.size());
         B.as_use_cnt.push_back((uint32_t)auses[a].size());
-        for (auto &u : auses[a]) { B.use_pat.push_back(u.pat); B.use_info0.push_back(u.i0); B.use_info1.push_back(u.i1); }
+        for (auto &u : auses[a]) {
+            B.use_pat.push_back(u.pat);
+            B.use_info0.push_back(u.i0);
+            B.use_info1.push_back(u.i1);
+            B.use_rxs.push_back(u.rxs);
+            B.use_wild.push_back(u.wild);
+        }
     }
     if (B.use_pat.size() > IT_USE_MASK) { err = "kw_compile: more than 2^19 anchor uses"; return KW_EUNSUPPORTED; }
     // ---- LDS filter, bigram table, gate, global hash table
@@ -476,8 +531,12 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         B.arec.push_back(B.as_use_begin[a]);
         B.arec.push_back((B.as_use_cnt[a] << 8) | B.as_len[a]);
     }
+    const uint32_t rx_base = (uint32_t)(n_pat ? pat_off[n_pat] : 0) + 16;   // RXM strings follow the names (+16 pad)
     for (size_t u = 0; u < B.use_pat.size(); ++u) {
-        const uint32_t sb = B.boff[B.use_pat[u]] + (B.use_info0[u] >> 16), sl = B.use_info1[u] & 0xFFFF;
+        const bool rxm = B.use_rxs[u] != 0xFFFFFFFFu;
+        const uint32_t sb = rxm ? rx_base + B.use_rxs[u] : B.boff[B.use_pat[u]] + (B.use_info0[u] >> 16);
+        const uint32_t sl = B.use_info1[u] & 0xFFFF;
+        const uint8_t *sp = rxm ? B.rx_bytes.data() + B.use_rxs[u] : pat_bytes + sb;
         B.urec.push_back(B.use_info0[u]);
         B.urec.push_back(B.use_info1[u]);
         B.urec.push_back(B.use_pat[u]);
@@ -485,8 +544,8 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         // first and last (up to) 8 bytes of the span: spans of <= 16 bytes need no other compare
         uint64_t hd = 0, tl = 0;
         const uint32_t hl = sl < 8 ? sl : 8;
-        for (uint32_t k = 0; k < hl; ++k) hd |= (uint64_t)pat_bytes[sb + k] << (8 * k);
-        for (uint32_t k = 0; k < hl; ++k) tl |= (uint64_t)pat_bytes[sb + sl - hl + k] << (8 * k);
+        for (uint32_t k = 0; k < hl; ++k) hd |= (uint64_t)sp[k] << (8 * k);
+        for (uint32_t k = 0; k < hl; ++k) tl |= (uint64_t)sp[sl - hl + k] << (8 * k);
         B.urec2.push_back((uint32_t)hd);
         B.urec2.push_back((uint32_t)(hd >> 32));
         B.urec2.push_back((uint32_t)tl);
@@ -517,6 +576,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     if (B.rxf_ext_cp.empty()) { B.rxf_ext_cp.push_back(0); B.rxf_ext_mask.push_back(0); }
     if (B.as_head.empty()) { B.as_head.push_back(0); B.as_len.push_back(0); B.as_use_begin.push_back(0); B.as_use_cnt.push_back(0); }
     if (B.use_pat.empty()) { B.use_pat.push_back(0); B.use_info0.push_back(0); B.use_info1.push_back(0); }
+    if (B.use_wild.empty()) { B.use_wild.push_back(0); B.use_rxs.push_back(0xFFFFFFFFu); }
     return KW_OK;
 }
 
@@ -860,6 +920,8 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     }
     std::vector<uint8_t> all_bytes(pat_bytes, pat_bytes + (n_pat ? pat_off[n_pat] : 0));
     all_bytes.resize(all_bytes.size() + 16, 0);
+    all_bytes.insert(all_bytes.end(), FB.rx_bytes.begin(), FB.rx_bytes.end());   // RXM strings (build_fast's rx_base)
+    all_bytes.resize(all_bytes.size() + 16, 0);
 
     // ---- one device blob
     std::vector<uint8_t> blob;
@@ -888,7 +950,8 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_rxec = push_array(blob, FB.rxf_ext_cp), f_rxem = push_array(blob, FB.rxf_ext_mask),
            f_ht4 = push_array(blob, FB.ht4), f_arec = push_array(blob, FB.arec), f_urec = push_array(blob, FB.urec),
            f_urec2 = push_array(blob, FB.urec2), f_tcps = push_array(blob, pat_tcps), f_txk = push_array(blob, tx_key),
-           f_txv = push_array(blob, tx_val), f_txi = push_array(blob, tx_inv);
+           f_txv = push_array(blob, tx_val), f_txi = push_array(blob, tx_inv),
+           f_uw = push_array(blob, FB.use_wild), f_prxl = push_array(blob, FB.rxl);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -990,6 +1053,8 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.tx_val = (const uint32_t *)(B + f_txv);
     F.tx_inv = (const uint32_t *)(B + f_txi);
     F.tx_unsafe_short = tx_unsafe_short;
+    F.use_wild = (const uint64_t *)(B + f_uw);
+    F.pat_rxl = (const uint32_t *)(B + f_prxl);
     F.tx_unsafe_edge = tx_unsafe_edge;
     h->n_anchor_fast = (int)FB.as_len.size();
 

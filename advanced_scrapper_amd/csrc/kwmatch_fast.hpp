@@ -54,7 +54,10 @@ constexpr int FK_L2_WORDS = 1 << (FK_L2_BITS - 5);
 constexpr int FK_T3_WORDS = 1 << (FK_T3_BITS - 5);
 constexpr int FK_EDGE_WORDS = 1 << (FK_EDGE_BITS - 5);
 
-enum FastUseKind : uint32_t { FU_UPPER = 0, FU_FULL = 1, FU_PIECE = 2, FU_EDGE = 3 };
+// item kinds (2 bits).  3 is FU_RXM in the probe's items (a match of a quantifier-free regex name's program,
+// '.' wildcards; ASCII fields) and FU_EDGE in the resolve kernel's lists, where an edge item's use is
+// IT_USE_MASK (an RXM item's is a real use).
+enum FastUseKind : uint32_t { FU_UPPER = 0, FU_FULL = 1, FU_PIECE = 2, FU_EDGE = 3, FU_RXM = 3 };
 
 // how re.finditer(name) finds positions: literal search or the regex engine
 enum RxKind : uint32_t { RXK_LITERAL = 0, RXK_REGEX = 1 };
@@ -138,6 +141,8 @@ struct FastTables {
     const uint32_t *tx_inv;     // [128] marker - 0x80 -> code point (~0 for 0x80: no name holds it)
     int tx_unsafe_short;        // a name the view cannot decide (PI_TXUNSAFE) may decide a short field
     int tx_unsafe_edge;         // ... or an edge window
+    const uint64_t *use_wild;   // per use: wildcard positions of an RXM program string
+    const uint32_t *pat_rxl;    // per pattern: its RXM program length (0: no RXM use; positions by the rx tasks)
 };
 
 struct FastScratch {

@@ -460,7 +460,7 @@ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint64_t *items,
             if (!eq) continue;
             const uint32_t idx = atomicAdd(icnt_f, 1u);
             if (idx < ICAP)
-                items[idx] = ((uint64_t)P << IT_PAT_SHIFT) | ((uint64_t)FU_EDGE << IT_KIND_SHIFT);
+                items[idx] = ((uint64_t)P << IT_PAT_SHIFT) | ((uint64_t)FU_EDGE << IT_KIND_SHIFT) | (uint64_t)IT_USE_MASK;
             else
                 atomicOr(dflag, 1u);
             ++added;
@@ -818,7 +818,8 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
         // the short path owns fuzzy names at least as long as the field
         const bool live = valid && !(fuzzy && m >= F.n);
-        const uint64_t fullm = __ballot(live && (kind == FU_FULL || kind == FU_EDGE));
+        // (kind 3 is an edge item here only with use IT_USE_MASK; the probe's RXM items never decide)
+        const uint64_t fullm = __ballot(live && (kind == FU_FULL || (kind == FU_EDGE && use == IT_USE_MASK)));
         const bool decided_full = (fullm & gmask) != 0;
         // ---- verification of pieces of undecided fuzzy names (wave-serial over such items)
         const bool vpiece = live && fuzzy && !decided_full && kind == FU_PIECE;
@@ -1008,6 +1009,8 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
         F.field = f;
         const uint32_t N = f ? n1 : n0;
         uint64_t *its = items + (f ? f1off : 0);
+        // (RXM items are exact regex matches in an ASCII field only; a transcoded field's regex names are searched)
+        const bool rxm_ok = !(flags & (f ? DH_NA1 : DH_NA0));
         if (F.n <= (uint32_t)MAXM) task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
         if (N == 0) continue;
         for (uint32_t bs = 0; bs < N;) {
@@ -1030,8 +1033,12 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             // the name's info, regex class and (pieces) use record: all lanes' loads in flight at once
             const uint32_t pi = valid ? FT.pat_info[pat] : 0u;
             const uint32_t rxk = valid ? FT.pat_rxk[pat] : 0u;
+            const uint32_t rxl = valid ? FT.pat_rxl[pat] : 0u;
             const uint32_t uinfo = (valid && kind == FU_PIECE) ? FT.use_info1[use] : 0u;
             const uint32_t m = pi_m(pi);
+            // a regex name with an RXM use: its positions are its RXM items (matches of rxl code points)
+            const bool rxi = rxk == RXK_REGEX && rxl != 0u && rxm_ok;
+            const uint32_t mlen = rxi ? rxl : m;
             const bool fuzzy = (pi & PI_FUZZY) != 0;
             const uint32_t prev_pat = (uint32_t)__shfl_up((int)pat, 1, WAVE);
             const bool head = valid && (lane == 0 || prev_pat != pat);
@@ -1065,15 +1072,17 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                 last_key = key;
                 task_push(vq, S.vcap, TC.v, make_uint4(D.doc, (P << 1) | f, q, o | (pl << 8)));
             }
-            // positions: uppercase names and exact occurrences of decided literal fuzzy names
+            // positions: uppercase names, exact occurrences of decided literal fuzzy names, RXM matches of
+            // decided regex names
             const bool relevant = live && ((!fuzzy && kind == FU_UPPER) ||
-                                           (fuzzy && decided && rxk == RXK_LITERAL && kind == FU_FULL));
+                                           (fuzzy && decided && ((rxk == RXK_LITERAL && kind == FU_FULL) ||
+                                                                 (rxi && kind == FU_RXM))));
             const uint32_t cpos = bpos;
             const uint64_t relm = __ballot(relevant);
             const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
             const int pr = prevrel ? 63 - __builtin_clzll(prevrel) : -1;
             const uint32_t pcpos = (uint32_t)__shfl((int)cpos, pr < 0 ? lane : pr, WAVE);
-            const bool overlap = relevant && pr >= 0 && cpos < pcpos + m;
+            const bool overlap = relevant && pr >= 0 && cpos < pcpos + mlen;
             uint64_t keep = relm;
             if (__ballot(overlap)) {
                 keep = 0;
@@ -1085,17 +1094,18 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                     mm2 &= mm2 - 1;
                     const int hh = __shfl(gs, l, WAVE);
                     const uint32_t st = (uint32_t)__shfl((int)cpos, l, WAVE);
-                    const uint32_t len = (uint32_t)__shfl((int)m, l, WAVE);
+                    const uint32_t len = (uint32_t)__shfl((int)mlen, l, WAVE);
                     if (hh != cur_head) { cur_head = hh; keep |= 1ull << l; last_end = st + len; continue; }
                     if (st >= last_end) { keep |= 1ull << l; last_end = st + len; }
                 }
             }
             emit_hits(O, GS, (keep >> lane) & 1ull, F.doc, pat, cpos, F.field);
             // exactly decided fuzzy names: an edge window (11 <= m <= 20) may decide them again -> the set;
-            // regex-class ones get their re.finditer search
+            // regex-class ones get their re.finditer search unless their RXM items gave the positions
             const bool dec_head = head && live && fuzzy && decided;
             if (dec_head && m >= EDGE_MIN_M && m <= EDGE_MAX_M) (void)dset_insert(S, dset_key(D.doc, pat, f));
-            const bool xrx = dec_head && rxk == RXK_REGEX;
+            emit_hits(O, GS, dec_head && rxi && (keep & gmask) == 0, F.doc, pat, KW_NOPOS, F.field);
+            const bool xrx = dec_head && rxk == RXK_REGEX && !rxi;
             const uint64_t xm = __ballot(xrx);
             if (xm) {
                 const uint32_t xi = TC.x + mbcnt(xm);
@@ -1770,6 +1780,49 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
     task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
 }
 
+// re.finditer positions of a decided regex name P with an RXM use (program length L) in an ASCII field: the
+// leftmost non-overlapping of the field's RXM items of P (the probe's exact matches of the program).  Returns
+// false, having emitted nothing, when P has more than 64 of them (the field search takes it).
+__device__ bool fk_rx_items(const FastScratch &S, const DevScratch &GS, const FieldCtx &F, OutCtx &O, uint32_t P,
+                            uint32_t L)
+{
+    const int lane = lane_id();
+    const uint2 h = S.hdr[F.doc], nc = S.ncnt[F.doc];
+    const uint32_t b = h.x + (F.field ? nc.x : 0u), n = F.field ? nc.y : nc.x;
+    uint64_t key = ~0ull;   // (position, lane slot) of this lane's match
+    uint32_t k = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        const uint64_t it = i < n ? S.items[b + i] : 0ull;
+        const bool mine = i < n && it_pat(it) == P && it_kind(it) == FU_RXM && it_use(it) != IT_USE_MASK;
+        const uint64_t bm = __ballot(mine);
+        const uint32_t c = (uint32_t)__popcll(bm);
+        if (k + c > (uint32_t)WAVE) return false;
+        // gather this round's matches into lanes k .. k + c
+        const uint32_t pos = it_pos(it);
+        uint64_t rest = bm;
+        for (uint32_t q = 0; q < c; ++q) {
+            const int l = __builtin_ctzll(rest);
+            rest &= rest - 1;
+            const uint32_t pq = (uint32_t)__shfl((int)pos, l, WAVE);
+            if ((uint32_t)lane == k + q) key = pq;
+        }
+        k += c;
+    }
+    key = wave_sort_reg(key);
+    // greedy leftmost non-overlapping selection (matches are L code points long)
+    uint64_t keep = 0;
+    uint32_t last_end = 0;
+    for (uint32_t q = 0; q < k; ++q) {
+        const uint32_t pq = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, (int)q);
+        if (q == 0 || pq >= last_end) { keep |= 1ull << q; last_end = pq + L; }
+    }
+    const bool kq = (keep >> lane) & 1ull;
+    emit_hits(O, GS, kq, F.doc, P, (uint32_t)key, F.field);
+    emit_hits(O, GS, k == 0 && lane == 0, F.doc, P, KW_NOPOS, F.field);
+    return true;
+}
+
 // Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.
 __global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                               const int64_t *__restrict__ off, int n_regions, int G,
@@ -1794,7 +1847,10 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, Dev
         const uint4 tk = xq[k];
         const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
         fk_field_ctx(F, arena, S, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
-        fk_regex_now(FT, T, GS, F, O, y >> 1, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+        const uint32_t P = y >> 1, L = FT.pat_rxl[P];
+        // a name with an RXM use in an ASCII field: the probe's RXM items are its matches, no search
+        if (L && !(S.dflags[F.doc] & (F.field ? DH_NA1 : DH_NA0)) && fk_rx_items(S, GS, F, O, P, L)) continue;
+        fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
     }
     task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
 }

@@ -304,6 +304,24 @@ __global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables
     }
 }
 
+// An RXM use's program string (L <= 64 bytes, '.' atoms as wildcard bits wm) against the text at s0: every
+// literal byte equal, every wildcard byte other than '\n' (re's '.'; non-ASCII fields never use these items).
+__device__ __forceinline__ bool rxm_match(const uint8_t *__restrict__ a, int64_t s0, const uint8_t *__restrict__ prog,
+                                          uint32_t L, uint64_t wm)
+{
+    for (uint32_t k = 0; k < L; k += 8) {
+        const uint64_t t = load8(a, s0 + k), p = load8(prog, k);
+        const uint32_t nb = L - k < 8 ? L - k : 8;
+        const uint64_t valid = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+        uint64_t wb = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wb |= ((wm >> (k + j)) & 1ull) ? (0xFFull << (8 * j)) : 0ull;
+        wb &= valid;
+        if (((t ^ p) & valid & ~wb) != 0 || (zb64(t ^ 0x0A0A0A0A0A0A0A0Aull) & wb) != 0) return false;
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- kernel 2: the anchor probe
 __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int32_t n_regions,
@@ -457,9 +475,14 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
                 const uint32_t nextb = hasn ? (uint32_t)arena[s0 + sblen] : 0u;
                 const uint32_t hl = sblen < 8 ? sblen : 8;
                 const uint64_t hm = hl >= 8 ? ~0ull : ((1ull << (8 * hl)) - 1);
-                if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) break;
-                if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) break;
-                if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) break;
+                if (kind == FU_RXM) {
+                    // a regex program's match: literal bytes equal, '.' wildcards any byte but '\n'
+                    if (!rxm_match(arena, s0, FT.pat_bytes + ur.w, sblen, FT.use_wild[u])) break;
+                } else {
+                    if ((th ^ ((uint64_t)u2.x | ((uint64_t)u2.y << 32))) & hm) break;
+                    if (sblen > 8 && tt != ((uint64_t)u2.z | ((uint64_t)u2.w << 32))) break;
+                    if (sblen > 16 && !span_equal(arena, s0 + 8, FT.pat_bytes + ur.w + 8, sblen - 16)) break;
+                }
                 if (kind == FU_UPPER) {
                     const bool wf = (pi & PI_WORD_FIRST) != 0, wl = (pi & PI_WORD_LAST) != 0;
                     bool wp = false;
