@@ -52,6 +52,10 @@ def _parse():
                     help='match = BASELINE.json metric (config 2/3); kb50k = ~50k-pattern synthetic KB '
                          '(config 4); dedup = CDX URL dedup (config 5)')
     ap.add_argument('--rows-per-gpu', type=int, default=500_000_000, help='dedup: CDX rows per GPU (config 5)')
+    ap.add_argument('--inflight', type=int, choices=(1, 2), default=1,
+                    help='scans in flight per GPU: 2 = two libkwmatch handles on two streams, step i + 1 is '
+                         'launched before step i\'s hits are read (its filter overlaps step i\'s latency-bound '
+                         'epilogue and task kernels); 1 = one scan at a time')
     return ap.parse_args()
 
 
@@ -123,7 +127,10 @@ def main():
     t_gen = time.perf_counter() - t_gen
     # anchor statistics from an independent sample (different seed, not the timed documents)
     bg_corpus = synth.generate(2000, names, kinds, seed=args.seed + 7777, doc_base=0)
-    m = GpuMatcher(ckb, local, background_sample(bg_corpus.texts() + bg_corpus.titles()))
+    bgs = background_sample(bg_corpus.texts() + bg_corpus.titles())
+    m = GpuMatcher(ckb, local, bgs)
+    # --inflight 2: a second handle (its own scratch and streams) so two complete scans overlap
+    ms = [m] + [GpuMatcher(ckb, local, bgs) for _ in range(args.inflight - 1)]
     t_up = time.perf_counter()
     d_arena, d_off = m.upload(corpus.arena, corpus.off)
     torch.cuda.synchronize()
@@ -133,16 +140,21 @@ def main():
     # N > 1: the hit records of step i move over libkwmatch's RCCL communicator on a stream of their own
     # while step i + 1 scans (double-buffered staging copies; the counts exchange is the step's rendezvous)
     comm = dist.KwComm(rank, world, local) if world > 1 else None
-    compute = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.inflight - 1)]
     comm_stream = torch.cuda.Stream(dev) if comm is not None else None
     stage = [None, None]
     copied = [torch.cuda.Event(), torch.cuda.Event()]
     sent = [None, None]
     last = {'gathered': None, 'counts': None}
 
-    def step(i):
-        m.scan(d_arena, d_off, n_local, compute)
-        n = m.n_hits()                                   # waits for the scan, reads the count
+    def launch(i):
+        k = i % len(ms)
+        ms[k].scan(d_arena, d_off, n_local, streams[k])
+
+    def collect(i):
+        k = i % len(ms)
+        mk, compute = ms[k], streams[k]
+        n = mk.n_hits()                                  # waits for that scan, reads the count
         if comm is None:
             return [n]
         b = i & 1
@@ -150,7 +162,7 @@ def main():
             compute.wait_event(sent[b])                  # the exchange that read this staging buffer is done
         if stage[b] is None or stage[b].shape[0] < max(n, 1):
             stage[b] = torch.empty((max(n + n // 4, 1), 4), dtype=torch.int32, device=dev)
-        m.hits_copy_into(stage[b], compute)
+        mk.hits_copy_into(stage[b], compute)
         copied[b].record(compute)
         if args.hits == 'none':
             return comm.allgather_counts(n, comm_stream)
@@ -169,15 +181,33 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    for i in range(args.warmup):
-        step(i)
+    def run(n_steps, times=None):
+        # step i + 1 is launched before step i's hits are read: with two handles their kernels overlap
+        out = None
+        if len(ms) == 1:
+            for i in range(n_steps):
+                launch(i)
+                out = collect(i)
+                if times is not None:
+                    times.append(m.kernel_times())
+            return out
+        for i in range(n_steps):
+            launch(i)
+            if i >= 1:
+                out = collect(i - 1)
+                if times is not None:
+                    times.append(ms[(i - 1) % len(ms)].kernel_times())
+        if n_steps:
+            out = collect(n_steps - 1)
+            if times is not None:
+                times.append(ms[(n_steps - 1) % len(ms)].kernel_times())
+        return out
+
+    run(args.warmup)
     sync_all()
     ktimes = []
     t0 = time.perf_counter()
-    counts = None
-    for i in range(args.steps):
-        counts = step(i)
-        ktimes.append(m.kernel_times())
+    counts = run(args.steps, ktimes)
     sync_all()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -244,6 +274,7 @@ def main():
             'hits_digest': digest,
             'parallelism': (f'dp{world} (contiguous document shards; per step: {exch}, overlapped with the '
                             f'next scan)' if world > 1 else 'dp1'),
+            'scans_in_flight': args.inflight,
         },
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
