@@ -193,7 +193,8 @@ struct FastScratch {
 // host + device hashes of the LDS tables
 __host__ __device__ __forceinline__ uint32_t fk_word(uint32_t key4)
 {
-    // bits 19..31 of the product of bytes 0..2 (the high half would hardly depend on byte 0)
+    // bits 19..31 of the product of bytes 0..2 (the high half would hardly depend on byte 0: a v_mul_hi
+    // word hash passed 14x the positions)
     return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;
 }
 __host__ __device__ __forceinline__ uint32_t fk_bit(uint32_t key4)

@@ -31,6 +31,11 @@
 #endif
 #define FK_T0(v) const unsigned long long v = FK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
 #define FK_TACC(acc, v) do { if (FK_TIMING) acc += __builtin_amdgcn_s_memtime() - (v); } while (0)
+#ifndef EK_TIMING   // developer aid: per-phase cycle counters of the epilogue kernel (KW_DUMP_TIMING, stats 21..31)
+#define EK_TIMING 0
+#endif
+#define EK_T0(v) const unsigned long long v = EK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
+#define EK_TACC(acc, v) do { if (EK_TIMING) (acc) += __builtin_amdgcn_s_memtime() - (v); } while (0)
 
 #ifndef FK_SCHED   // 1: pin the stage-1 LDS reads into groups of eight (sched_group_barrier; measured ~1 % faster)
 #define FK_SCHED 1
@@ -958,7 +963,7 @@ __device__ __forceinline__ bool dset_insert_wave(const FastScratch &S, uint32_t 
 // append one record to a wave's task region (cnt is wave-uniform; lane 0 writes)
 __device__ __forceinline__ void task_push(uint4 *region, uint32_t cap, uint32_t &cnt, uint4 rec)
 {
-    if (cnt < cap && lane_id() == 0) region[cnt] = rec;
+    if (!XSTORE_OFF && cnt < cap && lane_id() == 0) region[cnt] = rec;
     ++cnt;
 }
 
@@ -981,10 +986,13 @@ __device__ __forceinline__ bool fk_long_run(const uint64_t *a, uint32_t n)
 template <uint32_t F1OFF = FK_ITEMS0>
 __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D,
                                  uint64_t *items, uint32_t n0, uint32_t n1, uint32_t flags, int64_t wave, OutCtx &O,
-                                 TaskCounts &TC)
+                                 TaskCounts &TC, unsigned long long *ekt = nullptr)
 {
     constexpr uint32_t f1off = F1OFF;
     const int lane = lane_id();
+    unsigned long long ekt_dummy[8];
+    if (!ekt) ekt = ekt_dummy;
+    EK_T0(te0);
     // the fields' items sorted first: the deferral test precedes every emission
     if (n0 > (uint32_t)WAVE) {
         wave_sort_lds(items, n0);
@@ -996,6 +1004,7 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
     }
     uint4 *vq = S.vq + (size_t)wave * S.vcap;
     uint4 *sq = S.sq + (size_t)wave * S.scap, *xq = S.xq + (size_t)wave * S.xcap;
+    EK_TACC(ekt[0], te0);
     for (uint32_t f = 0; f < 2; ++f) {
         FieldCtx F;
         F.arena = D.arena;
@@ -1022,9 +1031,12 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                 if (be == bs) be = bs + WAVE;   // (cannot happen: fk_long_run deferred such documents)
             }
             const uint32_t NB = be - bs;
+            EK_T0(te1);
             uint64_t it = (lane < (int)NB) ? its[bs + lane] : ~0ull;
             it = wave_sort_few(it, NB, its + bs);
             bs = be;
+            EK_TACC(ekt[1], te1);
+            EK_T0(te2);
             const bool valid = lane < (int)NB;
             const uint32_t pat = valid ? it_pat(it) : 0xFFFFFu;
             const uint32_t kind = it_kind(it);
@@ -1051,6 +1063,8 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             // the short path owns fuzzy names at least as long as the field
             const bool live = valid && !(fuzzy && m >= F.n);
             const uint64_t fullm = __ballot(live && kind == FU_FULL);
+            EK_TACC(ekt[2], te2);
+            EK_T0(te3);
             const bool decided = (fullm & gmask) != 0;
             // pieces of undecided fuzzy names -> verify tasks (one per alignment base)
             const bool vpiece = live && fuzzy && !decided && kind == FU_PIECE;
@@ -1112,8 +1126,10 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
                 if (xrx && xi < S.xcap) xq[xi] = make_uint4(D.doc, (pat << 1) | f, 0u, 0u);
                 TC.x += (uint32_t)__popcll(xm);
             }
+            EK_TACC(ekt[3], te3);
         }
     }
+    EK_T0(te4);
     // ---- one-deletion edge windows of the 11..20-code-point names, both fields at once:
     // lane 20 f + 10 side + (L - 10) hashes the first (side 0) or last (side 1) L bytes of field f
     if ((FK_EPI_EDGE & 1) && (flags & (DH_EDGE0 | DH_EDGE1)) && (FK_EPI_EDGE & 2)) {
@@ -1182,6 +1198,7 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
             TC.e += (uint32_t)__popcll(__ballot(hit));   // edge items found (statistics)
         }
     }
+    EK_TACC(ekt[4], te4);
     return true;
 }
 

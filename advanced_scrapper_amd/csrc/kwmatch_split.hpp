@@ -175,7 +175,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                     const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
                     fw[jj] = lds_word_at(filt, fk_word_byte(key));
                     bm[jj] = fk_b2_mul(key);
-                    bw[jj] = b2[(bm[jj] >> 5) & (FK_B2_WORDS - 1)];
+                    bw[jj] = lds_word_at(b2, (bm[jj] >> 3) & (4u * FK_B2_WORDS - 4u));   // word (bm >> 5), as bytes
                 }
                 if (FK_SCHED) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
@@ -966,7 +966,10 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         epi_meta(S, off, wave, ov, hv);
         epi_prefetch(arena, S, ov, hv, ek, itp);
     }
+    unsigned long long ekt[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    EK_T0(tk0);
     for (int64_t d = wave; d < n_docs; d += n_waves) {
+        EK_T0(td0);
         const int64_t dn = d + n_waves;
         int64_t ovn = 0;
         uint2 hvn = make_uint2(0u, 0u);
@@ -1017,7 +1020,10 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         } else {
             const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
             const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
+            EK_TACC(ekt[5], td0);
+            EK_T0(td1);
             flags |= fk_edge_flags_key(FT, D, ek);
+            EK_TACC(ekt[6], td1);
             bool defer = (flags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
             if (defer && lane == 0) atomicAdd(&S.stats[15], 1ull);   // (rare: counted where they happen)
             bool queued = false;
@@ -1047,7 +1053,9 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
                     for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE)
                         if (n0 + i >= (uint32_t)WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
                     wave_sync();
-                    const bool done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+                    EK_T0(td2);
+                    const bool done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC, ekt);
+                    EK_TACC(ekt[7], td2);
                     if (!done) {
                         defer = true;
                         ++ndef_items;
@@ -1066,18 +1074,24 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
                     }
                 } else {
                     h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
-                    if (lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
+                    if (!XSTORE_OFF && lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
                 }
-                if (lane == 0) S.hdr[d] = h;
+                if (!XSTORE_OFF && lane == 0) S.hdr[d] = h;
                 wave_sync();
             }
         }
+        EK_T0(td3);
         ek = 0;
         itp = 0;
         if (dn < n_docs) epi_prefetch(arena, S, ovn, hvn, ek, itp);
         ov = ovn;
         hv = hvn;
+        EK_TACC(ekt[8], td3);
+        EK_TACC(ekt[9], td0);
     }
+    EK_TACC(ekt[10], tk0);
+    if (EK_TIMING && lane == 0)
+        for (int i = 0; i < 11; ++i) atomicAdd(&S.stats[21 + i], ekt[i]);
     // the workgroup's big documents: wave 0 with the whole workgroup's LDS as one 4096 + 512-item buffer
     __syncthreads();
     const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
