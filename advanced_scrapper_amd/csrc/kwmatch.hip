@@ -1293,8 +1293,14 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipEventRecord(h->evp, st));
     HIPCHK(h, hipStreamWaitEvent(st, h->evx, 0));
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
-                           h->FS, h->S);
+        // the group epilogue (lane = item across 32 documents); KW_EPI_FLAT=0: one wave per document
+        static const bool flat = !getenv("KW_EPI_FLAT") || atoi(getenv("KW_EPI_FLAT")) != 0;
+        if (flat)
+            hipLaunchKernelGGL(kw_epi_flat_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off,
+                               n_docs, h->FS, h->S);
+        else
+            hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
+                               h->FS, h->S);
         HIPCHK(h, hipGetLastError());
     }
     h->ns = n_regions;

@@ -605,6 +605,25 @@ __device__ __forceinline__ uint64_t wave_sort_few(uint64_t x, uint32_t n, uint64
     return lane < (int)n ? buf[lane] : ~0ull;
 }
 
+// wave_sort_reg with a 32-bit payload per key
+__device__ __forceinline__ uint64_t wave_sort_reg_kv(uint64_t x, uint32_t &v)
+{
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= WAVE; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t y = __shfl_xor(x, j, WAVE);
+            const uint32_t w = (uint32_t)__shfl_xor((int)v, j, WAVE);
+            const bool take_min = ((lane & j) == 0) == ((lane & k) == 0);
+            const bool take_y = take_min ? y < x : x < y;
+            x = take_y ? y : x;
+            v = take_y ? w : v;
+        }
+    }
+    return x;
+}
+
 // sort n <= FK_ITEMS_MAX u64 keys in this wave's LDS buffer (bitonic over the next power of two; pads with ~0)
 __device__ void wave_sort_lds(uint64_t *a, uint32_t n)
 {
@@ -979,6 +998,82 @@ __device__ __forceinline__ bool fk_long_run(const uint64_t *a, uint32_t n)
     return __ballot(r) != 0;
 }
 
+// One-deletion edge windows of a document's 11..20-code-point names (flags: its edge prefilter bits), after its
+// items were decided (the decided set then holds every name an exact occurrence decided).
+__device__ __forceinline__ void fk_epi_edge(const FastTables &FT, const FastScratch &S, const DevScratch &GS,
+                                            const FastDoc &D, uint32_t flags, OutCtx &O, TaskCounts &TC, uint4 *xq)
+{
+    const int lane = lane_id();
+    // ---- one-deletion edge windows of the 11..20-code-point names, both fields at once:
+    // lane 20 f + 10 side + (L - 10) hashes the first (side 0) or last (side 1) L bytes of field f
+    if ((FK_EPI_EDGE & 1) && (flags & (DH_EDGE0 | DH_EDGE1)) && (FK_EPI_EDGE & 2)) {
+        const int f = lane >= 20 ? 1 : 0;
+        const int sidx = lane - 20 * f;
+        const uint32_t L = (EDGE_MIN_M - 1) + (uint32_t)(sidx % 10);
+        const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
+        const bool act = lane < 40 && (flags & (f ? DH_EDGE1 : DH_EDGE0)) && fe - fb >= (int64_t)L + 2;
+        const int64_t w0 = sidx >= 10 ? fe - (int64_t)L : fb;
+        uint64_t hh = 0;
+        uint32_t wb[5] = {0u, 0u, 0u, 0u, 0u};   // the window's first 20 bytes
+        if (act) {
+            const int64_t a0 = w0 & ~(int64_t)3;
+            const uint32_t sh = (uint32_t)(w0 & 3);
+            uint32_t dw[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dw[i] = *(const uint32_t *)(D.arena + a0 + 4 * i);   // the arena is padded
+#pragma unroll
+            for (int i = 0; i < 5; ++i) wb[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+#pragma unroll
+            for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j)
+                if ((uint32_t)j < L) hh = hh * SUB_B + ((wb[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        }
+        uint32_t ecur = 0, eend = 0;
+        if (act) {
+            const uint64_t key = (hh + (uint64_t)L * 0x9E3779B97F4A7C15ull) | 1ull;
+            uint32_t slot = (uint32_t)(key >> 32) & FT.edge_mask;
+            for (;;) {
+                const uint64_t kk = FT.edge_key[slot];
+                if (kk == key) { ecur = FT.edge_begin[slot]; eend = ecur + FT.edge_cnt[slot]; break; }
+                if (kk == 0) break;
+                slot = (slot + 1) & FT.edge_mask;
+            }
+        }
+        // one matching variant per lane per round (a lane rarely has two)
+        while (__ballot(ecur < eend)) {
+            uint32_t P = 0;
+            bool hit = false;
+            while (ecur < eend && !hit) {
+                const uint32_t ent = FT.edge_ent[ecur++];
+                P = ent >> 5;
+                const uint32_t del = ent & 31u;
+                const uint32_t pi = FT.pat_info[P], co = FT.pat_cp_off[P];
+                if (pi_m(pi) != L + 1) continue;
+                // the name's code points, all loads in flight together; the window is in wb
+                uint32_t nmv[EDGE_MAX_M];
+#pragma unroll
+                for (int k = 0; k < (int)EDGE_MAX_M; ++k) nmv[k] = (uint32_t)k <= L ? FT.pat_tcps[co + k] : 0u;
+                bool eq = true;
+#pragma unroll
+                for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j) {
+                    const uint32_t want = (uint32_t)j < del ? nmv[j] : nmv[j + 1];
+                    if ((uint32_t)j < L) eq = eq && ((wb[j >> 2] >> (8 * (j & 3))) & 0xFFu) == want;
+                }
+                hit = eq;
+            }
+            const bool first = hit && dset_insert(S, dset_key(D.doc, P, (uint32_t)f));
+            const bool rx = first && FT.pat_rxk[P] == RXK_REGEX;
+            emit_hits(O, GS, first && !rx, D.doc, P, KW_NOPOS, (uint32_t)f);
+            const uint64_t xm = __ballot(rx);
+            if (xm) {
+                const uint32_t xi = TC.x + mbcnt(xm);
+                if (rx && xi < S.xcap) xq[xi] = make_uint4(D.doc, (P << 1) | (uint32_t)f, 0u, 0u);
+                TC.x += (uint32_t)__popcll(xm);
+            }
+            TC.e += (uint32_t)__popcll(__ballot(hit));   // edge items found (statistics)
+        }
+    }
+}
+
 // Finish an all-ASCII document in the scan kernel.  items: the wave's LDS item lists (field 0 at 0,
 // field 1 at f1off; each buffer holds the next power of two of its count), n0 / n1 items.  Returns
 // false, before anything is emitted, when a name has more than 64 items in a field (the generic kernel
@@ -1130,74 +1225,7 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
         }
     }
     EK_T0(te4);
-    // ---- one-deletion edge windows of the 11..20-code-point names, both fields at once:
-    // lane 20 f + 10 side + (L - 10) hashes the first (side 0) or last (side 1) L bytes of field f
-    if ((FK_EPI_EDGE & 1) && (flags & (DH_EDGE0 | DH_EDGE1)) && (FK_EPI_EDGE & 2)) {
-        const int f = lane >= 20 ? 1 : 0;
-        const int sidx = lane - 20 * f;
-        const uint32_t L = (EDGE_MIN_M - 1) + (uint32_t)(sidx % 10);
-        const int64_t fb = f ? D.t1 : D.t0, fe = f ? D.t2 : D.t1;
-        const bool act = lane < 40 && (flags & (f ? DH_EDGE1 : DH_EDGE0)) && fe - fb >= (int64_t)L + 2;
-        const int64_t w0 = sidx >= 10 ? fe - (int64_t)L : fb;
-        uint64_t hh = 0;
-        uint32_t wb[5] = {0u, 0u, 0u, 0u, 0u};   // the window's first 20 bytes
-        if (act) {
-            const int64_t a0 = w0 & ~(int64_t)3;
-            const uint32_t sh = (uint32_t)(w0 & 3);
-            uint32_t dw[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) dw[i] = *(const uint32_t *)(D.arena + a0 + 4 * i);   // the arena is padded
-#pragma unroll
-            for (int i = 0; i < 5; ++i) wb[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
-#pragma unroll
-            for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j)
-                if ((uint32_t)j < L) hh = hh * SUB_B + ((wb[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-        }
-        uint32_t ecur = 0, eend = 0;
-        if (act) {
-            const uint64_t key = (hh + (uint64_t)L * 0x9E3779B97F4A7C15ull) | 1ull;
-            uint32_t slot = (uint32_t)(key >> 32) & FT.edge_mask;
-            for (;;) {
-                const uint64_t kk = FT.edge_key[slot];
-                if (kk == key) { ecur = FT.edge_begin[slot]; eend = ecur + FT.edge_cnt[slot]; break; }
-                if (kk == 0) break;
-                slot = (slot + 1) & FT.edge_mask;
-            }
-        }
-        // one matching variant per lane per round (a lane rarely has two)
-        while (__ballot(ecur < eend)) {
-            uint32_t P = 0;
-            bool hit = false;
-            while (ecur < eend && !hit) {
-                const uint32_t ent = FT.edge_ent[ecur++];
-                P = ent >> 5;
-                const uint32_t del = ent & 31u;
-                const uint32_t pi = FT.pat_info[P], co = FT.pat_cp_off[P];
-                if (pi_m(pi) != L + 1) continue;
-                // the name's code points, all loads in flight together; the window is in wb
-                uint32_t nmv[EDGE_MAX_M];
-#pragma unroll
-                for (int k = 0; k < (int)EDGE_MAX_M; ++k) nmv[k] = (uint32_t)k <= L ? FT.pat_tcps[co + k] : 0u;
-                bool eq = true;
-#pragma unroll
-                for (int j = 0; j < (int)EDGE_MAX_M - 1; ++j) {
-                    const uint32_t want = (uint32_t)j < del ? nmv[j] : nmv[j + 1];
-                    if ((uint32_t)j < L) eq = eq && ((wb[j >> 2] >> (8 * (j & 3))) & 0xFFu) == want;
-                }
-                hit = eq;
-            }
-            const bool first = hit && dset_insert(S, dset_key(D.doc, P, (uint32_t)f));
-            const bool rx = first && FT.pat_rxk[P] == RXK_REGEX;
-            emit_hits(O, GS, first && !rx, D.doc, P, KW_NOPOS, (uint32_t)f);
-            const uint64_t xm = __ballot(rx);
-            if (xm) {
-                const uint32_t xi = TC.x + mbcnt(xm);
-                if (rx && xi < S.xcap) xq[xi] = make_uint4(D.doc, (P << 1) | (uint32_t)f, 0u, 0u);
-                TC.x += (uint32_t)__popcll(xm);
-            }
-            TC.e += (uint32_t)__popcll(__ballot(hit));   // edge items found (statistics)
-        }
-    }
+    fk_epi_edge(FT, S, GS, D, flags, O, TC, xq);
     EK_TACC(ekt[4], te4);
     return true;
 }

@@ -1119,4 +1119,336 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
 }
 
 
+
+// ---------------------------------------------------------------- kernel 3b: the epilogue over groups of documents
+// The same decisions as kw_epi_kernel, but a wave takes a filter group (32 consecutive documents) at a time
+// and works the items of its plain documents (all-ASCII, not deferred, <= 64 items per field) 64 at a time
+// across documents: lane = item, a batch is a run of whole (document, field) segments, sorted by (segment,
+// name, position), the name groups are (segment, name) runs.  Document-level work (edge prefilter, short-field
+// tasks, headers, view records) is lane = document.  Edge windows of flagged documents and the other
+// documents (non-ASCII, big, deferred) take the per-document code after the batches.
+__device__ __forceinline__ uint32_t ep_n(const uint32_t (&v)[2], uint32_t f) { return f ? v[1] : v[0]; }
+
+__global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+                                                               const int64_t *__restrict__ off, int64_t n_docs,
+                                                               FastScratch S, DevScratch GS)
+{
+    __shared__ uint64_t items_all[EK_WAVES * (FK_ITEMS0 + FK_ITEMS1)];
+    __shared__ uint32_t blk_docs[EK_BIGQ];
+    __shared__ uint32_t blk_n;
+    if (threadIdx.x == 0) blk_n = 0;
+    __syncthreads();
+    const int lane = lane_id();
+    const int wib = threadIdx.x / WAVE;
+    const int64_t wave = (int64_t)blockIdx.x * EK_WAVES + wib;
+    const int64_t n_waves = (int64_t)gridDim.x * EK_WAVES;
+    uint64_t *items = items_all + wib * (FK_ITEMS0 + FK_ITEMS1);
+    uint32_t ndefer = 0, ndef_items = 0, ntx = 0, nres = 0;
+    OutCtx O;
+    O.shared = nullptr;
+    O.out = S.kout + (size_t)wave * S.out_cap;
+    O.cap = S.out_cap;
+    O.n = 0;
+    TaskCounts TC = {0u, 0u, 0u, 0u};
+    uint4 *vq = S.vq + (size_t)wave * S.vcap;
+    uint4 *sq = S.sq + (size_t)wave * S.scap, *xq = S.xq + (size_t)wave * S.xcap;
+    const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
+    for (int64_t g = wave; g < n_groups; g += n_waves) {
+        const int64_t d0 = g * FG_DOCS;
+        const int nd = (int)(n_docs - d0 < FG_DOCS ? n_docs - d0 : FG_DOCS);
+        // ---- lane = document: offsets, header, counts, flags, the edge prefilter
+        const bool act = lane < nd;
+        const int64_t d = d0 + (act ? lane : 0);
+        const int64_t t0 = act ? off[2 * d] : 0, t1 = act ? off[2 * d + 1] : 0, t2 = act ? off[2 * d + 2] : 0;
+        const uint2 hd = act ? S.hdr[d] : make_uint2(0u, 0u);
+        const uint2 nc = act ? S.ncnt[d] : make_uint2(0u, 0u);
+        const uint32_t fl = act ? S.dflags[d] : 0u;
+        uint32_t ef = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int f = k >> 1;
+            const int64_t fb = f ? t1 : t0, fe = f ? t2 : t1;
+            if (act && fe - fb >= (int64_t)EDGE_MIN_M + 1) {
+                const int64_t a = (k & 1) ? fe - 8 : fb;
+                const uint64_t key8 = (uint64_t)ld_u32_unaligned(arena, a) | ((uint64_t)ld_u32_unaligned(arena, a + 4) << 32);
+                const uint32_t idx = fk_edge_index(key8);
+                if ((((k & 1) ? FT.edge_suf : FT.edge_pre)[idx >> 5] >> (idx & 31u)) & 1u) ef |= f ? DH_EDGE1 : DH_EDGE0;
+            }
+        }
+        const uint32_t flags = fl | ef;
+        const int64_t l0 = t1 - t0, l1 = t2 - t1;
+        const bool flat = act && !(fl & (DH_NA0 | DH_NA1 | DH_DEFER)) && l0 <= MAX_FIELD_BYTES &&
+                          l1 <= MAX_FIELD_BYTES && nc.x <= (uint32_t)WAVE && nc.y <= (uint32_t)WAVE;
+        const uint64_t flatm = __ballot(flat);
+        // ---- lane = segment s = 2 * document + field of the plain documents: size, first item, batch offset
+        const int sd = lane >> 1, sf = lane & 1;
+        const uint32_t s_n0 = (uint32_t)__shfl((int)nc.x, sd, WAVE), s_n1 = (uint32_t)__shfl((int)nc.y, sd, WAVE);
+        const uint32_t s_beg = (uint32_t)__shfl((int)hd.x, sd, WAVE);
+        const bool s_flat = (flatm >> sd) & 1ull;
+        const uint32_t sz = s_flat ? (sf ? s_n1 : s_n0) : 0u;
+        const uint32_t st = s_beg + (sf ? s_n0 : 0u);
+        int stot;
+        const uint32_t soff = (uint32_t)wave_excl_scan((int)sz, &stot);
+        const uint32_t s_l0 = (uint32_t)__shfl((int)(uint32_t)l0, sd, WAVE), s_l1 = (uint32_t)__shfl((int)(uint32_t)l1, sd, WAVE);
+        const uint32_t s_len = sf ? s_l1 : s_l0;   // the segment's field bytes (= code points: ASCII)
+        // ---- batches of whole segments, <= 64 items each
+        for (uint32_t base = 0; base < (uint32_t)stot;) {
+            // the segments that fit: soff + sz - base <= 64 (soff ascending)
+            const uint64_t fit = __ballot(soff >= base && soff + sz - base <= (uint32_t)WAVE);
+            const int last = 63 - __builtin_clzll(fit);
+            const uint32_t bend = (uint32_t)__shfl((int)(soff + sz), last, WAVE);
+            const uint32_t cnt = bend - base;
+            // lane = item: its segment (the last one starting at or before it), the item
+            int sg = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int c = sg + step;
+                const uint32_t oc = (uint32_t)__shfl((int)soff, c & 63, WAVE);
+                if (c < WAVE && oc <= base + (uint32_t)lane) sg = c;
+            }
+            const bool valid = (uint32_t)lane < cnt;
+            const uint32_t sgo = (uint32_t)__shfl((int)soff, sg, WAVE), sgs = (uint32_t)__shfl((int)st, sg, WAVE);
+            const uint64_t it0 = valid ? S.items[sgs + (base + (uint32_t)lane - sgo)] : 0ull;
+            base = bend;
+            // sort by (segment, name, position, kind); the use rides along
+            uint32_t use = it_use(it0);
+            const uint64_t key0 = valid ? (((uint64_t)sg << 58) | ((it0 >> 19) << 13)) : ~0ull;   // (it >> 19: name,
+            const uint64_t key = wave_sort_reg_kv(key0, use);                                      //  position, kind)
+            const uint32_t seg = (uint32_t)(key >> 58);
+            const uint32_t pat = valid ? (uint32_t)((key >> 38) & 0xFFFFFu) : 0xFFFFFu;
+            const uint32_t bpos = (uint32_t)((key >> 15) & IT_POS_MASK);
+            const uint32_t kind = (uint32_t)((key >> 13) & 3u);
+            const uint32_t f = seg & 1u;
+            const uint32_t doc = (uint32_t)(d0 + (seg >> 1));
+            const uint32_t nf = (uint32_t)__shfl((int)s_len, (int)seg & 63, WAVE);
+            const uint32_t pi = valid ? FT.pat_info[pat] : 0u;
+            const uint32_t rxk = valid ? FT.pat_rxk[pat] : 0u;
+            const uint32_t rxl = valid ? FT.pat_rxl[pat] : 0u;
+            const uint32_t uinfo = (valid && kind == FU_PIECE) ? FT.use_info1[use] : 0u;
+            const uint32_t m = pi_m(pi);
+            const bool rxi = rxk == RXK_REGEX && rxl != 0u;   // (plain documents: every field is ASCII)
+            const uint32_t mlen = rxi ? rxl : m;
+            const bool fuzzy = (pi & PI_FUZZY) != 0;
+            const uint64_t gkey = key >> 38;   // (segment, name)
+            const uint64_t prev_g = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(gkey >> 32), 1, WAVE) << 32) |
+                                    (uint32_t)__shfl_up((int)(uint32_t)gkey, 1, WAVE);
+            const bool head = valid && (lane == 0 || prev_g != gkey);
+            const uint64_t heads = __ballot(head);
+            const uint64_t below = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+            const int gs = 63 - __builtin_clzll((heads & below) | 1ull);
+            const uint64_t after = heads & ~below;
+            const int ge = after ? __builtin_ctzll(after) : (int)cnt;
+            const uint64_t gmask = (ge >= 64 ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gs) - 1);
+            const bool live = valid && !(fuzzy && m >= nf);
+            const uint64_t fullm = __ballot(live && kind == FU_FULL);
+            const bool decided = (fullm & gmask) != 0;
+            // pieces of undecided fuzzy names -> verify tasks, one per (group, alignment base): a piece lane is
+            // pushed unless the previous piece lane of its group had the same base
+            const bool vpiece = live && fuzzy && !decided && kind == FU_PIECE;
+            const uint32_t o = (uinfo >> 16) & 0xFFu, pl = uinfo >> 24;
+            const int64_t wkey = vpiece ? piece_window_key(bpos, o, pl, m, nf) : -1;
+            const uint64_t vm = __ballot(vpiece);
+            const uint64_t pv = vm & ((1ull << lane) - 1);
+            const int pvl = pv ? 63 - __builtin_clzll(pv) : lane;
+            const int pgs = __shfl(gs, pvl, WAVE);
+            const uint32_t pk_lo = (uint32_t)__shfl((int)(uint32_t)wkey, pvl, WAVE);
+            const uint32_t pk_hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)wkey >> 32), pvl, WAVE);
+            const int64_t pkey = (int64_t)(((uint64_t)pk_hi << 32) | pk_lo);
+            const bool vpush = vpiece && !(pv && pgs == gs && pkey == wkey);
+            const uint64_t vpm = __ballot(vpush);
+            if (vpm) {
+                const uint32_t vi = TC.v + mbcnt(vpm);
+                if (vpush && vi < S.vcap) vq[vi] = make_uint4(doc, (pat << 1) | f, bpos, o | (pl << 8));
+                TC.v += (uint32_t)__popcll(vpm);
+            }
+            // positions: uppercase names, exact occurrences of decided literal fuzzy names, RXM matches of decided
+            // regex names (leftmost non-overlapping per group)
+            const bool relevant = live && ((!fuzzy && kind == FU_UPPER) ||
+                                           (fuzzy && decided && ((rxk == RXK_LITERAL && kind == FU_FULL) ||
+                                                                 (rxi && kind == FU_RXM && use != IT_USE_MASK))));
+            const uint64_t relm = __ballot(relevant);
+            const uint64_t prevrel = relm & gmask & ((1ull << lane) - 1);
+            const int pr = prevrel ? 63 - __builtin_clzll(prevrel) : -1;
+            const uint32_t pcpos = (uint32_t)__shfl((int)bpos, pr < 0 ? lane : pr, WAVE);
+            const bool overlap = relevant && pr >= 0 && bpos < pcpos + mlen;
+            uint64_t keep = relm;
+            if (__ballot(overlap)) {
+                keep = 0;
+                uint64_t mm2 = relm;
+                int cur_head = -1;
+                uint32_t last_end = 0;
+                while (mm2) {
+                    const int l = __builtin_ctzll(mm2);
+                    mm2 &= mm2 - 1;
+                    const int hh = __shfl(gs, l, WAVE);
+                    const uint32_t stp = (uint32_t)__shfl((int)bpos, l, WAVE);
+                    const uint32_t len = (uint32_t)__shfl((int)mlen, l, WAVE);
+                    if (hh != cur_head) { cur_head = hh; keep |= 1ull << l; last_end = stp + len; continue; }
+                    if (stp >= last_end) { keep |= 1ull << l; last_end = stp + len; }
+                }
+            }
+            emit_hits(O, GS, (keep >> lane) & 1ull, doc, pat, bpos, f);
+            const bool dec_head = head && live && fuzzy && decided;
+            if (dec_head && m >= EDGE_MIN_M && m <= EDGE_MAX_M) (void)dset_insert(S, dset_key(doc, pat, f));
+            emit_hits(O, GS, dec_head && rxi && (keep & gmask) == 0, doc, pat, KW_NOPOS, f);
+            const bool xrx = dec_head && rxk == RXK_REGEX && !rxi;
+            const uint64_t xm = __ballot(xrx);
+            if (xm) {
+                const uint32_t xi = TC.x + mbcnt(xm);
+                if (xrx && xi < S.xcap) xq[xi] = make_uint4(doc, (pat << 1) | f, 0u, 0u);
+                TC.x += (uint32_t)__popcll(xm);
+            }
+        }
+        // ---- lane = document: short-field tasks, headers, view records of the plain documents
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            const bool sh = flat && (f ? l1 : l0) <= (int64_t)MAXM;
+            const uint64_t shm = __ballot(sh);
+            if (shm) {
+                const uint32_t si = TC.s + mbcnt(shm);
+                if (sh && si < S.scap) sq[si] = make_uint4((uint32_t)d, (uint32_t)f, 0u, 0u);
+                TC.s += (uint32_t)__popcll(shm);
+            }
+        }
+        // edge windows of the flagged plain documents (after all their items: the decided set is complete)
+        uint64_t edm = __ballot(flat && (ef & (DH_EDGE0 | DH_EDGE1)));
+        while (edm) {
+            const int l = __builtin_ctzll(edm);
+            edm &= edm - 1;
+            FastDoc D;
+            D.arena = arena;
+            D.t0 = rdlane64(t0, l);
+            D.t1 = rdlane64(t1, l);
+            D.t2 = rdlane64(t2, l);
+            D.doc = (uint32_t)(d0 + l);
+            D.l1 = (int32_t)(D.t1 - D.t0);
+            D.l2 = (int32_t)(D.t2 - D.t0);
+            fk_epi_edge(FT, S, GS, D, (uint32_t)__builtin_amdgcn_readlane((int)flags, l), O, TC, xq);
+        }
+        if (flat) {
+            S.hdr[d] = make_uint2(hd.x, nc.x | (nc.y << DH_N1_SHIFT) | flags);
+            S.vrec[d] = make_uint4((uint32_t)t0, (uint32_t)((uint64_t)t0 >> 32), (uint32_t)l0, (uint32_t)l1);
+        }
+        // ---- the other documents, one at a time (kw_epi_kernel's per-document code)
+        uint64_t slow = __ballot(act && !flat);
+        while (slow) {
+            const int l = __builtin_ctzll(slow);
+            slow &= slow - 1;
+            const int64_t dd = d0 + l;
+            FastDoc D;
+            D.arena = arena;
+            D.t0 = rdlane64(t0, l);
+            D.t1 = rdlane64(t1, l);
+            D.t2 = rdlane64(t2, l);
+            D.doc = (uint32_t)dd;
+            D.l1 = (int32_t)(D.t1 - D.t0);
+            D.l2 = (int32_t)(D.t2 - D.t0);
+            const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hd.x, l);
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nc.x, l);
+            const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)nc.y, l);
+            const uint32_t dfl = (uint32_t)__builtin_amdgcn_readlane((int)fl, l);
+            const uint32_t dflags = (uint32_t)__builtin_amdgcn_readlane((int)flags, l);
+            if (dfl & (DH_NA0 | DH_NA1)) {
+                bool done = false;
+                if (FK_TX && epi_tx_doc(FT, S, GS, D, S.vrec[dd], ibeg, n0, n1, dflags, items, wave, O, TC, &done)) {
+                    ++ntx;
+                    uint2 h;
+                    h.x = ibeg;
+                    if (!done) {
+                        ++ndefer;
+                        ++ndef_items;
+                        h.y = DH_DEFER;
+                        if (lane == 0) {
+                            atomicAdd(&S.stats[13], 1ull);
+                            const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                            if (i < S.defer_cap) S.defer_list[i] = (uint32_t)dd;
+                            else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+                        }
+                    } else {
+                        h.y = n0 | (n1 << DH_N1_SHIFT) | (dflags & ~DH_DEFER) | DH_TX;   // (vrec: kw_tx_kernel's)
+                    }
+                    if (lane == 0) S.hdr[dd] = h;
+                } else {
+                    ++nres;
+                    if (lane == 0) {
+                        S.dflags[dd] = dfl | DH_RESOLVE;
+                        const uint32_t i = atomicAdd(S.res_cnt, 1u);
+                        if (i < S.defer_cap) S.res_list[i] = (uint32_t)dd;
+                    }
+                }
+                wave_sync();
+                continue;
+            }
+            bool defer = (dflags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
+            if (defer && lane == 0) atomicAdd(&S.stats[15], 1ull);
+            if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) {
+                uint32_t bi = 0xFFFFFFFFu;
+                if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG1) {
+                    if (lane == 0) bi = atomicAdd(&blk_n, 1u);
+                    bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+                }
+                if (bi < (uint32_t)EK_BIGQ) {
+                    if (lane == 0) blk_docs[bi] = (uint32_t)dd;
+                    continue;
+                }
+                defer = true;
+                ++ndef_items;
+                if (lane == 0) atomicAdd(&S.stats[14], 1ull);
+            }
+            const uint32_t fl2 = dflags & ~DH_DEFER;
+            if (!defer) {
+                const uint64_t *src = S.items + ibeg;
+                for (uint32_t i = (uint32_t)lane; i < n0; i += WAVE) items[i] = src[i];
+                for (uint32_t i = (uint32_t)lane; i < n1; i += WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
+                wave_sync();
+                if (!fk_scan_epilogue(FT, S, GS, D, items, n0, n1, fl2, wave, O, TC)) {
+                    defer = true;
+                    ++ndef_items;
+                    if (lane == 0) atomicAdd(&S.stats[13], 1ull);
+                }
+            }
+            uint2 h;
+            h.x = ibeg;
+            if (defer) {
+                ++ndefer;
+                h.y = DH_DEFER;
+                if (lane == 0) {
+                    const uint32_t i = atomicAdd(S.defer_cnt, 1u);
+                    if (i < S.defer_cap) S.defer_list[i] = (uint32_t)dd;
+                    else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
+                }
+            } else {
+                h.y = n0 | (n1 << DH_N1_SHIFT) | fl2;
+                if (lane == 0) S.vrec[dd] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
+            }
+            if (lane == 0) S.hdr[dd] = h;
+            wave_sync();
+        }
+    }
+    // the workgroup's big documents: wave 0 with the whole workgroup's LDS as one 4096 + 512-item buffer
+    __syncthreads();
+    const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
+    if (wib == 0 && nb) {
+        for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC);
+        if (lane == 0) atomicAdd(&S.stats[16], (unsigned long long)nb);
+    }
+    if (lane == 0) {
+        S.kout_cnt[wave] = O.n;
+        S.vcnt[wave] = TC.v;
+        if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);
+        S.scnt[wave] = TC.s;
+        S.xcnt[wave] = TC.x;
+        if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
+            atomicOr(&S.status[0], ST_TASK_OVERFLOW);
+            atomicMax(&S.tmax[0], TC.v);
+            atomicMax(&S.tmax[2], TC.s);
+            atomicMax(&S.tmax[3], TC.x);
+        }
+        atomicAdd(&S.stats[4], (unsigned long long)ndefer);
+        atomicAdd(&S.stats[5], (unsigned long long)ndef_items);
+        if (ntx) atomicAdd(&S.stats[18], (unsigned long long)ntx);
+        if (nres) atomicAdd(&S.stats[19], (unsigned long long)nres);
+    }
+}
+
 }  // namespace kw
