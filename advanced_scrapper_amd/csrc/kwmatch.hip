@@ -776,6 +776,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     std::vector<uint32_t> tx_key(256, 0xFFFFFFFFu), tx_val(256, 0x80u), tx_inv(128, 0xFFFFFFFFu);
     std::vector<std::vector<uint32_t>> tcps(n_pat);
     std::vector<uint32_t> pat_tcps;
+    std::vector<uint8_t> pat_tbytes;
     int tx_unsafe_short = 0, tx_unsafe_edge = 0;
     {
         std::map<uint32_t, uint64_t> freq;
@@ -822,6 +823,8 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
             }
         }
         if (pat_tcps.empty()) pat_tcps.push_back(0);
+        pat_tbytes.assign(pat_tcps.begin(), pat_tcps.end());   // (every value < 256)
+        pat_tbytes.resize(pat_tbytes.size() + 72, 0);          // (unaligned 4-byte reads past a name)
     }
 
     std::vector<uint64_t> pm_ascii((size_t)std::max(n_pat, 1) * 128, 0);
@@ -856,8 +859,9 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
                 for (size_t l = 1; l <= (size_t)SHORT_EXACT_MAX && s0 + l <= cv.size(); ++l) {
                     hh = hh * SUB_B + cv[s0 + l - 1];
                     uint64_t key = (hh + (uint64_t)l * 0x9E3779B97F4A7C15ull) | 1ull;
+                    // entry: pattern | first offset of the substring << 20 (one compare verifies the hash)
                     auto &v = subs[key];
-                    if (v.empty() || v.back() != (uint32_t)i) v.push_back((uint32_t)i);
+                    if (v.empty() || (v.back() & 0xFFFFFu) != (uint32_t)i) v.push_back((uint32_t)i | ((uint32_t)s0 << 20));
                 }
             }
         }
@@ -950,7 +954,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_rxec = push_array(blob, FB.rxf_ext_cp), f_rxem = push_array(blob, FB.rxf_ext_mask),
            f_ht4 = push_array(blob, FB.ht4), f_arec = push_array(blob, FB.arec), f_urec = push_array(blob, FB.urec),
            f_urec2 = push_array(blob, FB.urec2), f_tcps = push_array(blob, pat_tcps), f_txk = push_array(blob, tx_key),
-           f_txv = push_array(blob, tx_val), f_txi = push_array(blob, tx_inv),
+           f_txv = push_array(blob, tx_val), f_txi = push_array(blob, tx_inv), f_tb = push_array(blob, pat_tbytes),
            f_uw = push_array(blob, FB.use_wild), f_prxl = push_array(blob, FB.rxl);
 
     HIPCHK(h, hipSetDevice(device));
@@ -1049,6 +1053,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.f_first = f_first;
     F.empty_pat = empty_pat;
     F.pat_tcps = (const uint32_t *)(B + f_tcps);
+    F.pat_tbytes = (const uint8_t *)(B + f_tb);
     F.tx_key = (const uint32_t *)(B + f_txk);
     F.tx_val = (const uint32_t *)(B + f_txv);
     F.tx_inv = (const uint32_t *)(B + f_txi);

@@ -136,6 +136,7 @@ struct FastTables {
     // transcoded view of non-ASCII documents (one byte per code point: ASCII as is, the other code points of
     // the fuzzy names as markers 0x81..0xFF, every other code point 0x80)
     const uint32_t *pat_tcps;   // per pattern (pat_cp_off): code points with the non-ASCII ones as markers
+    const uint8_t *pat_tbytes;  // the same, one byte each (names on lanes: short fields, verify)
     const uint32_t *tx_key;     // [256] non-ASCII code point -> tx_val (open addressing, ~0 = empty)
     const uint32_t *tx_val;
     const uint32_t *tx_inv;     // [128] marker - 0x80 -> code point (~0 for 0x80: no name holds it)

@@ -18,6 +18,12 @@
 #define FK_STAGE 3
 #endif
 // profiling builds: task phases to skip (1 verify, 2 edge, 4 short, 8 regex)
+#ifndef SHORT_COUNT
+#define SHORT_COUNT 0
+#endif
+#ifndef SHORT_SKIP   // profiling aid: 1 = skip short fields of <= SHORT_EXACT_MAX, 2 = the longer ones (wrong results)
+#define SHORT_SKIP 0
+#endif
 #ifndef TK_SKIP
 #define TK_SKIP 0
 #endif
@@ -702,10 +708,19 @@ __device__ void fk_short_field(const FastTables &FT, const uint32_t *__restrict_
             bool hit = false, exact = false;
             uint32_t P = 0, rk = 0;
             if (idx < cnt) {
-                P = FT.sub_pat[b + idx];
+                const uint32_t e = FT.sub_pat[b + idx];
+                P = e & 0xFFFFFu;
                 const uint32_t m = pi_m(FT.pat_info[P]);
                 rk = FT.pat_rxk[P];
                 const uint32_t *nmp = pcps + FT.pat_cp_off[P];
+                {   // the substring's recorded offset first (loads in flight together), every offset on a collision
+                    const uint32_t p0 = e >> 20;
+                    bool eq = p0 + n <= m;
+#pragma unroll
+                    for (int j = 0; j < SHORT_EXACT_MAX; ++j)
+                        if ((uint32_t)j < n) eq = eq && nmp[p0 + j] == fch[j];
+                    hit = eq;
+                }
                 for (uint32_t p = 0; p + n <= m && !hit; ++p) {
                     bool eq = true;
 #pragma unroll
@@ -998,6 +1013,25 @@ __device__ __forceinline__ bool fk_long_run(const uint64_t *a, uint32_t n)
     return __ballot(r) != 0;
 }
 
+// Whether a short field (<= MAXM code points, one byte each: ASCII or the transcoded view) needs the short
+// kernel: fields of <= SHORT_EXACT_MAX always; longer ones only if some name at least as long passes the
+// short kernel's signature test (popcount(field signature & ~name signature) <= (2n - 1) / 20), checked here
+// when those names are at most 64.  Whole wave.
+__device__ __forceinline__ bool fk_short_has_cand(const FastTables &FT, const FieldCtx &F)
+{
+    const int lane = lane_id();
+    const uint32_t n = F.n;
+    if (n <= (uint32_t)SHORT_EXACT_MAX) return true;
+    const uint32_t cnt = (uint32_t)FT.f_count_ge[n];
+    if (cnt > (uint32_t)WAVE) return true;
+    uint64_t fsig = (lane < (int)n) ? 1ull << (F.arena[F.fb + lane] & 63u) : 0ull;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) fsig |= __shfl_xor(fsig, d, WAVE);
+    const uint32_t allow = (2 * n - 1) / 20;
+    const bool c = lane < (int)cnt && (uint32_t)__popcll(fsig & ~FT.pat_sig[FT.f_first + lane]) <= allow;
+    return __ballot(c) != 0;
+}
+
 // One-deletion edge windows of a document's 11..20-code-point names (flags: its edge prefilter bits), after its
 // items were decided (the decided set then holds every name an exact occurrence decided).
 __device__ __forceinline__ void fk_epi_edge(const FastTables &FT, const FastScratch &S, const DevScratch &GS,
@@ -1115,7 +1149,10 @@ __device__ bool fk_scan_epilogue(const FastTables &FT, const FastScratch &S, con
         uint64_t *its = items + (f ? f1off : 0);
         // (RXM items are exact regex matches in an ASCII field only; a transcoded field's regex names are searched)
         const bool rxm_ok = !(flags & (f ? DH_NA1 : DH_NA0));
-        if (F.n <= (uint32_t)MAXM) task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
+        if (F.n <= (uint32_t)MAXM && fk_short_has_cand(FT, F)) {
+            if (SHORT_COUNT && lane == 0) atomicAdd(&S.stats[27 + (flags & (DH_NA0 | DH_NA1) ? 1 : 0)], 1ull);
+            task_push(sq, S.scap, TC.s, make_uint4(D.doc, f, 0u, 0u));
+        }
         if (N == 0) continue;
         for (uint32_t bs = 0; bs < N;) {
             uint32_t be = N;
@@ -1614,8 +1651,10 @@ __device__ __forceinline__ void fk_short_run(const FastTables &FT, const DevScra
     const uint32_t P = has ? cand[lane] : 0u;
     const uint32_t pi = has ? FT.pat_info[P] : 0u;
     const uint32_t m = pi_m(pi);
-    const bool lanes_ok = has && (pi & PI_ASCII) != 0 && m <= (uint32_t)SL_NAME;
-    const int64_t boff = lanes_ok ? FT.pat_boff[P] : 0;
+    // every name on lanes: its code points as one byte each (ASCII, or the transcoded view's markers), the
+    // field's match vectors cover all 256 byte values
+    const bool lanes_ok = has && m <= (uint32_t)SL_NAME;
+    const int64_t boff = lanes_ok ? (int64_t)FT.pat_cp_off[P] : 0;
     nver += has ? 1u : 0u;
     // stage the names: 16 dwords per candidate
     for (uint32_t i0 = 0; i0 < nc * (SL_NAME / 4); i0 += WAVE) {
@@ -1626,7 +1665,7 @@ __device__ __forceinline__ void fk_short_run(const FastTables &FT, const DevScra
         const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)boff >> 32), k & 63, WAVE);
         const int32_t km = __shfl((int)m, k & 63, WAVE);
         if (idx < nc * (SL_NAME / 4) && 4 * w < (uint32_t)km)
-            ((uint32_t *)names)[idx] = ld_u32_unaligned(FT.pat_bytes, (int64_t)(((uint64_t)bhi << 32) | blo) + 4 * w);
+            ((uint32_t *)names)[idx] = ld_u32_unaligned(FT.pat_tbytes, (int64_t)(((uint64_t)bhi << 32) | blo) + 4 * w);
     }
     // jobs per candidate: m - n + 1 full windows, the prefixes, the suffixes, the swapped run (m == n)
     const uint32_t nj = lanes_ok ? (m - n + 3 + (m == n ? 1u : 0u)) : 0u;
@@ -1729,9 +1768,11 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
     const int lane = lane_id();
     const uint32_t n = F.n;
     if (n <= (uint32_t)SHORT_EXACT_MAX) {
-        fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
+        if (!(SHORT_SKIP & 1))
+            fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
         return;
     }
+    if (SHORT_SKIP & 2) return;
     // the field's signature first (bit c & 63 of every byte): most fields have no candidate name at all
     const uint32_t fc = (lane < (int)n) ? (uint32_t)F.arena[F.fb + lane] : 0xFFFFFFFCu;
     uint64_t fsig = (lane < (int)n) ? 1ull << (fc & 63u) : 0ull;
@@ -1750,9 +1791,8 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
                 if (rem < 8) x &= rem <= 0 ? 0ull : ((1ull << (8 * rem)) - 1);
                 FW[w] = x;
             }
-            const uint64_t m0 = lv_match(FW, (uint32_t)lane, needle), m1 = lv_match(FW, (uint32_t)lane + 64, needle);
-            pm[lane] = m0;
-            pm[lane + 64] = m1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pm[lane + 64 * q] = lv_match(FW, (uint32_t)lane + 64u * q, needle);
             have_pm = true;
             wave_sync();
         }
@@ -1786,6 +1826,7 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
         }
     }
     if (nc) run(nc);
+    if (SHORT_COUNT && lane == 0 && have_pm) atomicAdd(&GS.stats[2], 1000000000ull);   // (debug: fields with candidates)
 }
 
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
@@ -1800,10 +1841,10 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
     const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     (void)T;
-    __shared__ uint64_t pm_all[RK_WAVES * 128];
+    __shared__ uint64_t pm_all[RK_WAVES * 256];
     __shared__ uint32_t names_all[RK_WAVES * WAVE * SL_NAME / 4];
     __shared__ uint32_t cand_all[RK_WAVES * WAVE];
-    uint64_t *pm = pm_all + wib * 128;
+    uint64_t *pm = pm_all + wib * 256;
     uint8_t *names = (uint8_t *)(names_all + wib * WAVE * SL_NAME / 4);
     uint32_t *cand = cand_all + wib * WAVE;
     OutCtx O = tout_region(S, t);
@@ -1817,7 +1858,13 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
         fk_field_ctx(F, arena, S, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x),
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y));
         if (FK_SHORT_LANES)
+        {
+            if (SHORT_COUNT && lane == 0) {   // developer aid: short tasks by length class (stats 21..24)
+                atomicAdd(&S.stats[21 + (F.n <= (uint32_t)SHORT_EXACT_MAX ? 0 : F.n < 40u ? 1 : 2)], 1ull);
+                atomicAdd(&S.stats[24], (unsigned long long)FT.f_count_ge[F.n]);
+            }
             fk_short_lanes(FT, GS, F, O, X, pm, names, cand, nver, nwin, nver_w, nwin_w);
+        }
         else
             fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w,
                            [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });

@@ -546,9 +546,16 @@ __device__ void short_path(const DevTables &T, const DevScratch &S, const FieldC
             bool hit = false, exact = false;
             uint32_t P = 0;
             if (idx < cnt) {
-                P = T.sub_pat[b + idx];
+                const uint32_t e = T.sub_pat[b + idx];
+                P = e & 0xFFFFFu;
                 uint32_t m = pi_m(T.pat_info[P]);
                 const uint32_t *nm = T.pat_cps + T.pat_cp_off[P];
+                {   // the substring's recorded offset first, every offset if the hash collided
+                    const uint32_t p = e >> 20;
+                    bool eq = p + n <= m;
+                    for (uint32_t j = 0; j < n && eq; ++j) eq = nm[p + j] == fcp(F, j);
+                    hit = eq;
+                }
                 for (uint32_t p = 0; p + n <= m && !hit; ++p) {
                     bool eq = true;
                     for (uint32_t j = 0; j < n; ++j)

@@ -1299,11 +1299,36 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
                 TC.x += (uint32_t)__popcll(xm);
             }
         }
-        // ---- lane = document: short-field tasks, headers, view records of the plain documents
+        // ---- lane = document: short-field tasks, headers, view records of the plain documents.  A short field
+        // of more than SHORT_EXACT_MAX bytes whose names at least as long are few (titles: <= 12 of the S&P500
+        // KB's) first takes the short kernel's signature test here: without a candidate name it needs no task.
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-            const bool sh = flat && (f ? l1 : l0) <= (int64_t)MAXM;
+            const int64_t lf = f ? l1 : l0;
+            bool sh = flat && lf <= (int64_t)MAXM;
+            if (sh && lf > (int64_t)SHORT_EXACT_MAX) {
+                const uint32_t n = (uint32_t)lf, cnt = (uint32_t)FT.f_count_ge[n];
+                if (cnt <= (uint32_t)WAVE) {
+                    const int64_t fb = f ? t1 : t0, a0 = fb & ~(int64_t)3;
+                    const uint32_t sh0 = (uint32_t)(fb - a0);
+                    uint64_t fsig = 0;
+                    for (uint32_t w = 0; 4 * w < n + sh0; ++w) {
+                        const uint32_t x = *(const uint32_t *)(arena + a0 + 4 * w);   // (the arena is padded)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t p = 4 * w + (uint32_t)k;
+                            if (p >= sh0 && p < n + sh0) fsig |= 1ull << ((x >> (8 * k)) & 63u);
+                        }
+                    }
+                    const uint32_t allow = (2 * n - 1) / 20;
+                    bool cand = false;
+                    for (uint32_t c = 0; c < cnt && !cand; ++c)
+                        cand = (uint32_t)__popcll(fsig & ~FT.pat_sig[FT.f_first + c]) <= allow;
+                    sh = cand;
+                }
+            }
             const uint64_t shm = __ballot(sh);
+            if (SHORT_COUNT && lane == 0 && shm) atomicAdd(&S.stats[25 + f], (unsigned long long)__popcll(shm));
             if (shm) {
                 const uint32_t si = TC.s + mbcnt(shm);
                 if (sh && si < S.scap) sq[si] = make_uint4((uint32_t)d, (uint32_t)f, 0u, 0u);
