@@ -194,7 +194,7 @@ struct FastBuild {
     uint32_t gate_lo[4] = {0, 0, 0, 0}, gate_hi[4] = {0, 0, 0, 0};
     int n_gate = 0;
     int has_t3 = 0;
-    std::vector<uint64_t> ht_key, as_head, sig;
+    std::vector<uint64_t> ht_key, as_head, sig, bsig;
     std::vector<uint32_t> ht_begin, ht_cnt, kl, as_len, as_use_begin, as_use_cnt, use_pat, use_info0, use_info1,
         rxk, boff;
     uint32_t ht_mask = 0;
@@ -248,6 +248,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     struct RxmTodo { uint32_t pat, L; uint64_t wild; std::string rs; };
     std::vector<RxmTodo> rxm_todo;   // quantifier-free ASCII regex programs: RXM uses once every anchor is known
     B.sig.assign(std::max(n_pat, 1), 0);
+    B.bsig.assign(2 * (size_t)std::max(n_pat, 1), 0);
     for (int i = 0; i < n_pat; ++i) {
         const uint8_t *s = pat_bytes + pat_off[i];
         const size_t bl = (size_t)(pat_off[i + 1] - pat_off[i]);
@@ -256,6 +257,10 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         const bool fuzzy = pat_info[i] & PI_FUZZY;
         for (uint32_t c : cps[i]) B.sig[i] |= 1ull << (c & 63);
         for (uint32_t c : tcps[i]) B.sig[i] |= 1ull << (c & 63);   // (the transcoded view's bytes too)
+        for (size_t j = 0; j + 1 < tcps[i].size(); ++j) {
+            const uint32_t h = fk_bg_bit(tcps[i][j], tcps[i][j + 1]);
+            B.bsig[2 * (size_t)i + (h >> 6)] |= 1ull << (h & 63);
+        }
         // whole-name use (U or FULL): anchor at the rarest 4-byte window (offset <= 255)
         auto span_use = [&](uint32_t kind, size_t sb, size_t se, uint32_t pcp, uint32_t pcl) {
             const size_t len = se - sb;
@@ -946,7 +951,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_asub = push_array(blob, FB.as_use_begin), f_asuc = push_array(blob, FB.as_use_cnt),
            f_up = push_array(blob, FB.use_pat), f_ui0 = push_array(blob, FB.use_info0),
            f_ui1 = push_array(blob, FB.use_info1), f_rxk = push_array(blob, FB.rxk), f_boff = push_array(blob, FB.boff),
-           f_pb = push_array(blob, all_bytes), f_sig = push_array(blob, FB.sig),
+           f_pb = push_array(blob, all_bytes), f_sig = push_array(blob, FB.sig), f_bsig = push_array(blob, FB.bsig),
            f_ek = push_array(blob, FB.edge_key), f_eb = push_array(blob, FB.edge_begin),
            f_ec = push_array(blob, FB.edge_cnt), f_ee = push_array(blob, FB.edge_ent),
            f_rxi = push_array(blob, FB.rxf_idx), f_rxp = push_array(blob, FB.rxf_pm), f_rxa = push_array(blob, FB.rxf_any),
@@ -1027,6 +1032,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.pat_cp_off = T.pat_cp_off;
     F.pat_cps = T.pat_cps;
     F.pat_sig = (const uint64_t *)(B + f_sig);
+    F.pat_bsig = (const uint64_t *)(B + f_bsig);
     F.f_count_ge = T.f_count_ge;
     F.sub_key = T.sub_key;
     F.sub_begin = T.sub_begin;
@@ -1081,8 +1087,15 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     bpc = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_epi_kernel, EK_BLOCK, 0));
     h->epi_blocks_per_cu = bpc > 0 ? bpc : 1;
-    HIPCHK(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-    HIPCHK(h, hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking));
+    {
+        // KW_SIDE_PRIO=1|2: the side stream (transcoding beside the probe) or
+        // side2 (short fields beside verify) at the greatest priority
+        const char *e = getenv("KW_SIDE_PRIO");
+        int sp = e ? atoi(e) : 0, lo = 0, hi = 0;
+        HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, (sp & 1) ? hi : lo));
+        HIPCHK(h, hipStreamCreateWithPriority(&h->side2, hipStreamNonBlocking, (sp & 2) ? hi : lo));
+    }
     HIPCHK(h, hipEventCreateWithFlags(&h->eve, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->evq, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->evx, hipEventDisableTiming));

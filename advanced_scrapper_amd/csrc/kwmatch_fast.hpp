@@ -107,6 +107,7 @@ struct FastTables {
     const uint32_t *pat_cp_off;
     const uint32_t *pat_cps;
     const uint64_t *pat_sig;    // char-set signature (bit c & 63)
+    const uint64_t *pat_bsig;   // bigram-set signature of the one-byte code points, 128 bits (fk_bg_bit)
     const int32_t *f_count_ge;
     const uint64_t *sub_key;
     const uint32_t *sub_begin;
@@ -221,6 +222,11 @@ __host__ __device__ __forceinline__ uint32_t fk_t3_index(uint32_t key4)
 __host__ __device__ __forceinline__ uint32_t fk_edge_index(uint64_t key8)
 {
     return (uint32_t)((key8 * 0x9E3779B97F4A7C15ull) >> (64 - FK_EDGE_BITS));
+}
+// bigram signature bit (0..127) of two one-byte code points (the short kernel's second filter)
+__host__ __device__ __forceinline__ uint32_t fk_bg_bit(uint32_t a, uint32_t b)
+{
+    return ((((a & 0xFFu) << 8) | (b & 0xFFu)) * 40503u >> 9) & 127u;
 }
 __host__ __device__ __forceinline__ uint32_t fk_b2_index(uint32_t key2)
 {

@@ -18,6 +18,15 @@
 #define FK_STAGE 3
 #endif
 // profiling builds: task phases to skip (1 verify, 2 edge, 4 short, 8 regex)
+#ifndef EPI_SHORT_PREF   // the group epilogue's signature test of short fields before their tasks
+#define EPI_SHORT_PREF 1
+#endif
+#ifndef SHORT_TB   // short kernel: every name on lanes (one-byte code points, 256-entry match vectors)
+#define SHORT_TB 1
+#endif
+#ifndef SHORT_BG   // short kernel: the bigram-signature filter after the character signature
+#define SHORT_BG 1
+#endif
 #ifndef SHORT_COUNT
 #define SHORT_COUNT 0
 #endif
@@ -1653,8 +1662,8 @@ __device__ __forceinline__ void fk_short_run(const FastTables &FT, const DevScra
     const uint32_t m = pi_m(pi);
     // every name on lanes: its code points as one byte each (ASCII, or the transcoded view's markers), the
     // field's match vectors cover all 256 byte values
-    const bool lanes_ok = has && m <= (uint32_t)SL_NAME;
-    const int64_t boff = lanes_ok ? (int64_t)FT.pat_cp_off[P] : 0;
+    const bool lanes_ok = has && (SHORT_TB || (pi & PI_ASCII) != 0) && m <= (uint32_t)SL_NAME;
+    const int64_t boff = lanes_ok ? (SHORT_TB ? (int64_t)FT.pat_cp_off[P] : FT.pat_boff[P]) : 0;
     nver += has ? 1u : 0u;
     // stage the names: 16 dwords per candidate
     for (uint32_t i0 = 0; i0 < nc * (SL_NAME / 4); i0 += WAVE) {
@@ -1665,7 +1674,7 @@ __device__ __forceinline__ void fk_short_run(const FastTables &FT, const DevScra
         const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)boff >> 32), k & 63, WAVE);
         const int32_t km = __shfl((int)m, k & 63, WAVE);
         if (idx < nc * (SL_NAME / 4) && 4 * w < (uint32_t)km)
-            ((uint32_t *)names)[idx] = ld_u32_unaligned(FT.pat_tbytes, (int64_t)(((uint64_t)bhi << 32) | blo) + 4 * w);
+            ((uint32_t *)names)[idx] = ld_u32_unaligned(SHORT_TB ? FT.pat_tbytes : FT.pat_bytes, (int64_t)(((uint64_t)bhi << 32) | blo) + 4 * w);
     }
     // jobs per candidate: m - n + 1 full windows, the prefixes, the suffixes, the swapped run (m == n)
     const uint32_t nj = lanes_ok ? (m - n + 3 + (m == n ? 1u : 0u)) : 0u;
@@ -1776,8 +1785,23 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
     // the field's signature first (bit c & 63 of every byte): most fields have no candidate name at all
     const uint32_t fc = (lane < (int)n) ? (uint32_t)F.arena[F.fb + lane] : 0xFFFFFFFCu;
     uint64_t fsig = (lane < (int)n) ? 1ull << (fc & 63u) : 0ull;
+    // and its bigram signature: a window alignment within partial_ratio's bound d <= allow keeps all but
+    // 2d of the field's bigram positions in the name (3d when the name is the needle, m == n), so a name
+    // missing more than 3 * allow of the field's bigram bits has no window
+    uint64_t fb0 = 0, fb1 = 0;
+    {
+        const uint32_t nx = (uint32_t)__shfl((int)fc, (lane + 1) & (WAVE - 1), WAVE);
+        if (SHORT_BG && lane + 1 < (int)n) {
+            const uint32_t h = fk_bg_bit(fc, nx);
+            (h & 64u ? fb1 : fb0) = 1ull << (h & 63u);
+        }
+    }
 #pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) fsig |= __shfl_xor(fsig, d, WAVE);
+    for (int d = 1; d < WAVE; d <<= 1) {
+        fsig |= __shfl_xor(fsig, d, WAVE);
+        fb0 |= __shfl_xor(fb0, d, WAVE);
+        fb1 |= __shfl_xor(fb1, d, WAVE);
+    }
     bool have_pm = false;
     auto run = [&](uint32_t nc) {
         if (!have_pm) {   // the field's match vectors for every ASCII byte (LDS pm), built for the first candidates
@@ -1792,7 +1816,7 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
                 FW[w] = x;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) pm[lane + 64 * q] = lv_match(FW, (uint32_t)lane + 64u * q, needle);
+            for (int q = 0; q < (SHORT_TB ? 4 : 2); ++q) pm[lane + 64 * q] = lv_match(FW, (uint32_t)lane + 64u * q, needle);
             have_pm = true;
             wave_sync();
         }
@@ -1805,15 +1829,18 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
     constexpr int SIG_U = 8;
     for (uint32_t c00 = 0; c00 < count; c00 += SIG_U * WAVE) {
         uint64_t nsig[SIG_U];
+        ulonglong2 nbs[SIG_U];
 #pragma unroll
         for (int u = 0; u < SIG_U; ++u) {
             const uint32_t idx = c00 + (uint32_t)(u * WAVE + lane);
             nsig[u] = idx < count ? FT.pat_sig[FT.f_first + idx] : ~0ull;
+            nbs[u] = (SHORT_BG && idx < count) ? ((const ulonglong2 *)FT.pat_bsig)[FT.f_first + idx] : make_ulonglong2(~0ull, ~0ull);
         }
 #pragma unroll
         for (int u = 0; u < SIG_U; ++u) {
             const uint32_t c0 = c00 + (uint32_t)(u * WAVE);
-            const bool cnd = c0 + (uint32_t)lane < count && (uint32_t)__popcll(fsig & ~nsig[u]) <= allow;
+            const bool cnd = c0 + (uint32_t)lane < count && (uint32_t)__popcll(fsig & ~nsig[u]) <= allow &&
+                             (uint32_t)(__popcll(fb0 & ~nbs[u].x) + __popcll(fb1 & ~nbs[u].y)) <= 3 * allow;
             const uint64_t cm = __ballot(cnd);
             if (!cm) continue;
             if (nc + (uint32_t)__popcll(cm) > (uint32_t)WAVE) {
@@ -1841,10 +1868,10 @@ __global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTa
     const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
     (void)T;
-    __shared__ uint64_t pm_all[RK_WAVES * 256];
+    __shared__ uint64_t pm_all[RK_WAVES * (SHORT_TB ? 256 : 128)];
     __shared__ uint32_t names_all[RK_WAVES * WAVE * SL_NAME / 4];
     __shared__ uint32_t cand_all[RK_WAVES * WAVE];
-    uint64_t *pm = pm_all + wib * 256;
+    uint64_t *pm = pm_all + wib * (SHORT_TB ? 256 : 128);
     uint8_t *names = (uint8_t *)(names_all + wib * WAVE * SL_NAME / 4);
     uint32_t *cand = cand_all + wib * WAVE;
     OutCtx O = tout_region(S, t);

@@ -1306,7 +1306,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         for (int f = 0; f < 2; ++f) {
             const int64_t lf = f ? l1 : l0;
             bool sh = flat && lf <= (int64_t)MAXM;
-            if (sh && lf > (int64_t)SHORT_EXACT_MAX) {
+            if (EPI_SHORT_PREF && sh && lf > (int64_t)SHORT_EXACT_MAX) {
                 const uint32_t n = (uint32_t)lf, cnt = (uint32_t)FT.f_count_ge[n];
                 if (cnt <= (uint32_t)WAVE) {
                     const int64_t fb = f ? t1 : t0, a0 = fb & ~(int64_t)3;
