@@ -27,6 +27,12 @@
 #ifndef SHORT_BG   // short kernel: the bigram-signature filter after the character signature
 #define SHORT_BG 1
 #endif
+#ifndef VK_MODE   // profiling aid (wrong results): verify kernel without 1 its LCS jobs, 2 band tests, 4 wave-serial names
+#define VK_MODE 0
+#endif
+#ifndef VK_U   // verify jobs: name match-vector loads in flight
+#define VK_U 8
+#endif
 #ifndef SHORT_COUNT
 #define SHORT_COUNT 0
 #endif
@@ -1511,7 +1517,7 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
         const bool todo = valid && !dset_contains(S, dset_key(doc, P, field));
         const uint32_t pi = todo ? FT.pat_info[P] : 0u;
         const uint32_t m = pi_m(pi);
-        const bool lanewise = todo && (pi & PI_ASCII) != 0;
+        const bool lanewise = !(VK_MODE & 2) && todo && (pi & PI_ASCII) != 0;
         int64_t fb = 0;
         uint32_t n = 0;
         bool tx = false;
@@ -1543,6 +1549,7 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
             nwj = lv_band(la, fb, n, NW, m, (int64_t)q - (int64_t)o, kfull(m), win, pmin);
             pre = q + pl + 1 <= m ? 1u : 0u;
             cj = nwj + pre + (q + m > n ? 1u : 0u);
+            if (VK_MODE & 1) cj = 0;
         }
         int J = 0;
         const int ex = wave_excl_scan((int)cj, &J);
@@ -1586,17 +1593,17 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
             const uint64_t *pmr = T.pm_ascii + (size_t)jP * 128;
             uint64_t V = ~0ull;
             bool ok = false;
-            for (uint32_t s0 = 0; s0 < len && !ok; s0 += 8) {
-                uint64_t Mb[8];
+            for (uint32_t s0 = 0; s0 < len && !ok; s0 += VK_U) {
+                uint64_t Mb[VK_U];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < VK_U; ++u) {
                     const uint32_t s2 = s0 + (uint32_t)u;
                     const uint32_t bi = d0 + (rev ? len - 1 - s2 : s2);
                     const uint32_t c = s2 < len ? (win[bi >> 2] >> (8 * (bi & 3))) & 0xFFu : 0x80u;
                     Mb[u] = c < 0x80u ? pmr[c] : 0ull;   // (ASCII names never match a non-ASCII byte)
                 }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < VK_U; ++u) {
                     const uint32_t s2 = s0 + (uint32_t)u;
                     if (s2 >= len) break;
                     uint64_t M = Mb[u];
@@ -1613,7 +1620,7 @@ __global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, D
         wave_sync();
         bool pass = lanewise && okf[lane] != 0;
         // names lanes cannot take (non-ASCII code points), wave-serially
-        uint64_t wm = __ballot(todo && !lanewise);
+        uint64_t wm = __ballot(!(VK_MODE & 6) && todo && !lanewise);
         while (wm) {
             const int l = __builtin_ctzll(wm);
             wm &= wm - 1;
