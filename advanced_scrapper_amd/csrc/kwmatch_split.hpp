@@ -614,12 +614,13 @@ __device__ __forceinline__ uint64_t tx_bytes(int64_t l0, int64_t l1)
 }
 __device__ __forceinline__ uint32_t tx_nchunks(int64_t fb, int64_t fe) { return (uint32_t)((fe - (fb & ~(int64_t)15) + 15) >> 4) + 1u; }
 
-__device__ __forceinline__ uint32_t tx_marker(const FastTables &FT, uint32_t cp)
+// the marker of code point cp (txk / txv: the 256-entry marker table, staged in LDS)
+__device__ __forceinline__ uint32_t tx_marker(const uint32_t *txk, const uint32_t *txv, uint32_t cp)
 {
     uint32_t s = (cp * 0x9E3779B1u) >> 24;
     for (int k = 0; k < 256; ++k) {
-        const uint32_t kk = FT.tx_key[s];
-        if (kk == cp) return FT.tx_val[s];
+        const uint32_t kk = txk[s];
+        if (kk == cp) return txv[s];
         if (kk == 0xFFFFFFFFu) break;
         s = (s + 1) & 255u;
     }
@@ -629,23 +630,30 @@ __device__ __forceinline__ uint32_t tx_marker(const FastTables &FT, uint32_t cp)
 // Field bytes [fb, fe) of the arena -> out[o0, o0 + n) (one byte per code point; out 16-byte aligned); chunk
 // (may be null) [k] = code points of the field before its 16-byte chunk k.  stg: the wave's 1040-byte LDS
 // staging buffer (each 1 KiB block's output leaves with 16-byte stores).  Returns n.  Whole wave.
-__device__ uint32_t tx_field(const FastTables &FT, const uint8_t *__restrict__ a, int64_t fb, int64_t fe,
+__device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uint8_t *__restrict__ a, int64_t fb, int64_t fe,
                              uint8_t *__restrict__ out, uint32_t o0, uint16_t *__restrict__ chunk, uint8_t *stg)
 {
     const int lane = lane_id();
     const int64_t base = fb & ~(int64_t)15;
     uint32_t count = 0;
+    // the next block's loads are issued before this block's work
+    auto ld = [&](int64_t b, uint4 &v, uint32_t &w4) {
+        const int64_t p = b + 16 * (int64_t)lane;
+        v = p < fe ? *(const uint4 *)(a + p) : make_uint4(0u, 0u, 0u, 0u);
+        w4 = (lane == WAVE - 1 && b + 1024 < fe) ? *(const uint32_t *)(a + b + 1024) : 0u;
+    };
+    uint4 vn;
+    uint32_t wn;
+    ld(base, vn, wn);
     for (int64_t blk = base; blk < fe; blk += 1024) {
         const int64_t lp = blk + 16 * (int64_t)lane;
+        const uint4 v = vn;
+        const uint32_t w4 = wn;
+        if (blk + 1024 < fe) ld(blk + 1024, vn, wn);
         uint32_t W[5];
-        if (lp < fe) {
-            const uint4 v = *(const uint4 *)(a + lp);
-            W[0] = v.x; W[1] = v.y; W[2] = v.z; W[3] = v.w;
-        } else {
-            W[0] = W[1] = W[2] = W[3] = 0;
-        }
+        W[0] = v.x; W[1] = v.y; W[2] = v.z; W[3] = v.w;
         W[4] = (uint32_t)__shfl_down((int)W[0], 1, WAVE);
-        if (lane == WAVE - 1) W[4] = (blk + 1024 < fe) ? *(const uint32_t *)(a + blk + 1024) : 0u;
+        if (lane == WAVE - 1) W[4] = w4;
         const int64_t r0 = fb - lp, r2 = fe - lp;
         const int jlo = r0 <= 0 ? 0 : (r0 >= 16 ? 16 : (int)r0);
         const int jhi = r2 <= 0 ? 0 : (r2 >= 16 ? 16 : (int)r2);
@@ -684,7 +692,7 @@ __device__ uint32_t tx_field(const FastTables &FT, const uint8_t *__restrict__ a
                         const uint32_t bk = (lp + jj < fe) ? ((W[jj >> 2] >> (8 * (jj & 3))) & 0xFFu) : 0x80u;
                         c = (c << 6) | (bk & 0x3Fu);
                     }
-                    c = tx_marker(FT, c);
+                    c = tx_marker(txk, txv, c);
                 }
                 stg[k++] = (uint8_t)c;
             }
@@ -720,6 +728,12 @@ __global__ __launch_bounds__(TX_BLOCK) void kw_tx_kernel(FastTables FT, const ui
                                                          const int64_t *__restrict__ off, int64_t n_docs, FastScratch S)
 {
     __shared__ uint32_t stg_all[TX_WAVES * (1040 / 4)];
+    __shared__ uint32_t txk[256], txv[256];
+    for (int i = threadIdx.x; i < 256; i += TX_BLOCK) {
+        txk[i] = FT.tx_key[i];
+        txv[i] = FT.tx_val[i];
+    }
+    __syncthreads();
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t wave = (int64_t)blockIdx.x * TX_WAVES + wib;
@@ -767,8 +781,8 @@ __global__ __launch_bounds__(TX_BLOCK) void kw_tx_kernel(FastTables FT, const ui
             }
             uint8_t *out = S.tarena + tb;
             uint16_t *ch = (uint16_t *)(S.tarena + tb + nb);
-            const uint32_t n0 = tx_field(FT, arena, t0, t1, out, 0u, (f & DH_NA0) ? ch : nullptr, stg);
-            const uint32_t n1 = tx_field(FT, arena, t1, t2, out, n0, (f & DH_NA1) ? ch + nc0 : nullptr, stg);
+            const uint32_t n0 = tx_field(txk, txv, arena, t0, t1, out, 0u, (f & DH_NA0) ? ch : nullptr, stg);
+            const uint32_t n1 = tx_field(txk, txv, arena, t1, t2, out, n0, (f & DH_NA1) ? ch + nc0 : nullptr, stg);
             if (lane == 0) S.vrec[d] = make_uint4((uint32_t)tb, (uint32_t)(tb >> 32) | 0x80000000u, n0, n1);
         }
     }
