@@ -33,6 +33,16 @@
 #ifndef VK_U   // verify jobs: name match-vector loads in flight
 #define VK_U 8
 #endif
+// task kernels' minimum waves per SIMD (register budget: 4 -> 128 VGPRs, 5 -> 102, 6 -> 84, 8 -> 64)
+#ifndef VK_MINW
+#define VK_MINW 4
+#endif
+#ifndef SK_MINW
+#define SK_MINW 1
+#endif
+#ifndef RX_MINW
+#define RX_MINW 1
+#endif
 #ifndef SHORT_COUNT
 #define SHORT_COUNT 0
 #endif
@@ -1488,7 +1498,7 @@ constexpr int LV_MAXJ = 16;   // window jobs per verify task: <= 2 kfull(64) + 1
 // Verify tasks.  Lanes take 64 tasks at a time: band test per lane, then the surviving windows
 // (full windows, prefixes, suffixes) of all 64 tasks as one flat job list, 64 jobs a round, each
 // job's text staged in its lane's LDS window.  Names with non-ASCII code points wave-serially.
-__global__ __launch_bounds__(RK_BLOCK, 4) void kw_verify_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                              const int64_t *__restrict__ off, int n_regions, int G,
                                                              FastScratch S, DevScratch GS)
 {
@@ -1864,7 +1874,7 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
 }
 
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
-__global__ __launch_bounds__(RK_BLOCK) void kw_short_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(RK_BLOCK, SK_MINW) void kw_short_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                             const int64_t *__restrict__ off, int n_regions, int G,
                                                             FastScratch S, DevScratch GS)
 {
@@ -1950,7 +1960,7 @@ __device__ bool fk_rx_items(const FastScratch &S, const DevScratch &GS, const Fi
 }
 
 // Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.
-__global__ __launch_bounds__(RK_BLOCK) void kw_rx_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                               const int64_t *__restrict__ off, int n_regions, int G,
                                                               FastScratch S, DevScratch GS)
 {

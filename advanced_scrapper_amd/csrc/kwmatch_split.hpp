@@ -41,7 +41,7 @@ constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
 constexpr int PK_BLOCK = PK_WAVES * WAVE;
 #ifndef PK_POOL_CFG
-#define PK_POOL_CFG 1024
+#define PK_POOL_CFG 768   // (with PK_MINW 5: 5 probe waves per SIMD; 1024 / 4: 6.15 vs 5.97 ms per step)
 #endif
 constexpr int PK_POOL = PK_POOL_CFG;     // items one batch of 64 candidates may stage (more: their documents defer)
 #ifndef FK_TX
@@ -51,7 +51,7 @@ constexpr int PK_POOL = PK_POOL_CFG;     // items one batch of 64 candidates may
 #define EK_MINW 4   // 128 VGPRs, no spill (5 waves per SIMD spills 96 B per lane: epilogue 2.08 vs 1.98 ms)
 #endif
 #ifndef PK_MINW
-#define PK_MINW 1
+#define PK_MINW 5   // <= 102 VGPRs: the probe and the transcoding kernel beside it share the CUs better
 #endif
 constexpr int EK_WAVES = 8;              // waves per epilogue workgroup
 constexpr int EK_BIGQ = 64;              // big documents one epilogue workgroup finishes itself (more: generic)
@@ -603,6 +603,9 @@ __device__ __forceinline__ uint32_t fk_edge_flags_key(const FastTables &FT, cons
 #ifndef TX_NOSTORE   // profiling aid: 1 = the view's body stores are skipped (wrong results, store cost measured)
 #define TX_NOSTORE 0
 #endif
+#ifndef TX_MINW
+#define TX_MINW 8   // 64 VGPRs (a 56-byte spill): 0.57 vs 0.60 ms isolated
+#endif
 constexpr int TX_WAVES = 4;
 constexpr int TX_BLOCK = TX_WAVES * WAVE;
 constexpr uint32_t TX_NONE = 0xFFFFFFFFu;
@@ -724,7 +727,7 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
 
 // Transcode the documents with a non-ASCII field (the filter's dflags) into the view.  One wave takes 64
 // documents at a time (lane = document), then their non-ASCII ones in turn.
-__global__ __launch_bounds__(TX_BLOCK) void kw_tx_kernel(FastTables FT, const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(TX_BLOCK, TX_MINW) void kw_tx_kernel(FastTables FT, const uint8_t *__restrict__ arena,
                                                          const int64_t *__restrict__ off, int64_t n_docs, FastScratch S)
 {
     __shared__ uint32_t stg_all[TX_WAVES * (1040 / 4)];
