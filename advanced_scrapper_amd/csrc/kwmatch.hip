@@ -1241,6 +1241,7 @@ static int launch_scan(kw_handle *h)
     if (const char *e = getenv("KW_RESOLVE_MUL")) rmul = std::max(1, atoi(e));
     int nrb = (int)std::min<int64_t>((n_docs + (int64_t)RK_WAVES * WAVE - 1) / ((int64_t)RK_WAVES * WAVE),
                                      (int64_t)h->cus * h->resolve_blocks_per_cu * rmul);
+    if (const char *e = getenv("KW_RESOLVE_BLOCKS")) nrb = std::min(nrb, std::max(1, atoi(e)));
     if (nrb < 1) nrb = 1;
     // generic kernel: 4 blocks per CU (one resident, 1 wave / SIMD at 256 VGPRs): the deferred documents'
     // costs vary by orders of magnitude, later blocks take the work of the slow ones
