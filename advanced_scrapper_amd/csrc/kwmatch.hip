@@ -1301,9 +1301,10 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipEventRecord(h->evf, st));
     // the transcoded view of the documents with a non-ASCII field (the filter flagged them) on the side
     // stream, beside the probe; the epilogue waits for it
+    static const int tx_bpc = getenv("KW_TX_BLOCKS_PER_CU") ? std::max(1, atoi(getenv("KW_TX_BLOCKS_PER_CU"))) : 8;
     HIPCHK(h, hipStreamWaitEvent(side, h->evf, 0));
     if (n_docs > 0)
-        hipLaunchKernelGGL(kw_tx_kernel, dim3(std::max(1, (int)std::min<int64_t>((n_docs + TX_BLOCK - 1) / TX_BLOCK, (int64_t)h->cus * 8))),
+        hipLaunchKernelGGL(kw_tx_kernel, dim3(std::max(1, (int)std::min<int64_t>((n_docs + TX_BLOCK - 1) / TX_BLOCK, (int64_t)h->cus * tx_bpc))),
                            dim3(TX_BLOCK), 0, side, h->FT, h->arena, h->doc_off, n_docs, h->FS);
     HIPCHK(h, hipEventRecord(h->evx, side));
     if (n_docs > 0)
