@@ -1870,7 +1870,6 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
         }
     }
     if (nc) run(nc);
-    if (SHORT_COUNT && lane == 0 && have_pm) atomicAdd(&GS.stats[2], 1000000000ull);   // (debug: fields with candidates)
 }
 
 // Short fields: the field is the needle, the fuzzy names at least as long as the field the haystacks.
