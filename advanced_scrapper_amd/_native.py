@@ -13,7 +13,19 @@ import os
 import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib')
-LIB_PATH = os.environ.get('KW_LIB') or os.path.join(LIB_DIR, 'libkwmatch.so')   # KW_LIB: profiling variants
+DEFAULT_LIB = os.path.join(LIB_DIR, 'libkwmatch.so')
+LIB_PATH = DEFAULT_LIB
+
+
+def _lib_path() -> str:
+    """The default in-tree library; ``KW_LIB`` (a tuning variant of build.build_kwmatch_variant) only when
+    ``bench.py --lib-variant`` asked for it (``KW_LIB_VARIANT_OK=1``): nothing else may swap the library."""
+    alt = os.environ.get('KW_LIB')
+    if not alt or os.path.abspath(alt) == DEFAULT_LIB:
+        return DEFAULT_LIB
+    if os.environ.get('KW_LIB_VARIANT_OK') != '1':
+        raise RuntimeError(f"KW_LIB={alt}: only bench.py --lib-variant loads a non-default libkwmatch")
+    return os.path.abspath(alt)
 
 KW_OK = 0
 KW_EINVAL = -1
@@ -52,9 +64,10 @@ _LIB = None
 
 def lib() -> ctypes.CDLL:
     """Load libkwmatch.so (raises if it was not built)."""
-    global _LIB
+    global _LIB, LIB_PATH
     if _LIB is not None:
         return _LIB
+    LIB_PATH = _lib_path()
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(LIB_PATH)
@@ -104,6 +117,17 @@ def lib() -> ctypes.CDLL:
     L.kw_destroy.restype = ctypes.c_int
     _LIB = L
     return L
+
+
+def lib_identity() -> dict:
+    """Which libkwmatch this process loaded: path (relative to the package), sha256, default or variant."""
+    import hashlib
+    lib()
+    with open(LIB_PATH, 'rb') as fh:
+        digest = hashlib.sha256(fh.read()).hexdigest()
+    return {'path': os.path.relpath(LIB_PATH, os.path.dirname(LIB_DIR)), 'sha256': digest,
+            'default': LIB_PATH == DEFAULT_LIB,
+            'env': {k: v for k, v in sorted(os.environ.items()) if k.startswith('KW_')}}
 
 
 def check(rc: int, handle=None) -> None:

@@ -47,22 +47,10 @@ def _kw_sources():
     return srcs
 
 
-def build_kwmatch_stage(stage: int, force: bool = False) -> str:
-    """Profiling variant of the fast kernel truncated after stage `stage`
-    (0 = filter, 1 = + anchor probe, 2 = + resolve without LCS); bench only."""
-    os.makedirs(LIB, exist_ok=True)
-    out = os.path.join(LIB, f'libkwmatch_stage{stage}.so')
-    srcs = _kw_sources()
-    if force or _stale(out, srcs):
-        units = [s for s in srcs if s.endswith('.hip')]
-        _run([HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-shared', '-fPIC', f'-DFK_STAGE={stage}',
-              '-o', out] + units + ['-ldl'])
-    return out
-
-
 def build_kwmatch_variant(tag: str, defines, force: bool = False) -> str:
-    """Profiling / tuning variant ``lib/libkwmatch_<tag>.so`` built with extra -D defines (entries
-    starting with '-' are passed as compiler flags); bench only."""
+    """Tuning variant ``lib/libkwmatch_<tag>.so`` built with extra -D defines of the documented tuning knobs
+    (waves per SIMD, grids, pool sizes; entries starting with '-' are passed as compiler flags).  Only
+    ``bench.py --lib-variant`` loads one (``_native`` refuses ``KW_LIB`` otherwise); results are the same."""
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, f'libkwmatch_{tag}.so')
     srcs = _kw_sources()
@@ -108,6 +96,3 @@ def build_all(force: bool = False):
 
 if __name__ == '__main__':
     build_all(force='--force' in sys.argv)
-    if '--stages' in sys.argv:
-        for st in (0, 1, 2):
-            build_kwmatch_stage(st, force='--force' in sys.argv)

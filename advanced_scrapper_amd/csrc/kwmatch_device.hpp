@@ -38,9 +38,6 @@ constexpr int64_t MAX_FIELD_BYTES = (int64_t)IT_POS_MASK;
 enum UseKind : uint32_t { USE_UPPER = 0, USE_FULL = 1, USE_PIECE = 2 };
 
 // pat_info bits
-#ifndef XSTORE_OFF   // profiling aid: 1 = hit records and task records are not stored (wrong results)
-#define XSTORE_OFF 0
-#endif
 constexpr uint32_t PI_FUZZY = 1u;        // class F (else U)
 constexpr uint32_t PI_LITERAL = 2u;      // F: re.finditer(name) == literal search
 constexpr uint32_t PI_WORD_FIRST = 4u;   // U: first code point is a \b word char

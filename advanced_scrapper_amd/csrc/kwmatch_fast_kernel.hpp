@@ -13,11 +13,6 @@
 #include "kwmatch_fast.hpp"
 #include "kwmatch_kernels.hpp"
 
-// profiling builds: 0 = filter only, 1 = + anchor probe, 2 = + resolve w/o LCS, 3 = full
-#ifndef FK_STAGE
-#define FK_STAGE 3
-#endif
-// profiling builds: task phases to skip (1 verify, 2 edge, 4 short, 8 regex)
 #ifndef EPI_SHORT_PREF   // the group epilogue's signature test of short fields before their tasks
 #define EPI_SHORT_PREF 1
 #endif
@@ -26,9 +21,6 @@
 #endif
 #ifndef SHORT_BG   // short kernel: the bigram-signature filter after the character signature
 #define SHORT_BG 1
-#endif
-#ifndef VK_MODE   // profiling aid (wrong results): verify kernel without 1 its LCS jobs, 2 band tests, 4 wave-serial names
-#define VK_MODE 0
 #endif
 #ifndef VK_U   // verify jobs: name match-vector loads in flight
 #define VK_U 8
@@ -45,16 +37,6 @@
 #endif
 #ifndef SHORT_COUNT
 #define SHORT_COUNT 0
-#endif
-#ifndef SHORT_SKIP   // profiling aid: 1 = skip short fields of <= SHORT_EXACT_MAX, 2 = the longer ones (wrong results)
-#define SHORT_SKIP 0
-#endif
-#ifndef TK_SKIP
-#define TK_SKIP 0
-#endif
-// profiling builds: stage-2 filter and ring without the anchor-table probe
-#ifndef FK_NOPROBE
-#define FK_NOPROBE 0
 #endif
 // waves per SIMD the resolve kernel is compiled for (register budget)
 #ifndef FK_TIMING   // developer aid: per-phase cycle counters of the resolve kernel (KW_DUMP_TIMING)
@@ -86,11 +68,6 @@
 
 #ifndef RK_OCC
 #define RK_OCC 4
-#endif
-// profiling builds: bit 0 skips the short-field path, bit 1 the edge windows, bit 2 the items,
-// bit 3 the regex positions
-#ifndef RK_SKIP
-#define RK_SKIP 0
 #endif
 
 namespace kw {
@@ -316,7 +293,6 @@ __device__ __forceinline__ uint32_t fk_staged_v(uint32_t ta, uint32_t tb, int id
 __device__ bool fk_verify_piece(const FieldCtx &F, uint32_t nm, uint32_t m, uint32_t q, uint32_t o, uint32_t pl,
                                 unsigned long long &nwin)
 {
-    if (FK_STAGE < 3) return false;
     const int lane = lane_id();
     const uint32_t n = F.n;
     const uint64_t needle = low_mask(m);
@@ -376,7 +352,6 @@ __device__ bool fk_short_decide(uint32_t fc, uint32_t n, uint32_t nmr, uint32_t 
                                 unsigned long long &nwin)
 {
     *exact = false;
-    if (FK_STAGE < 3) return false;
     const int lane = lane_id();
     const uint64_t needle = low_mask(n);
     uint64_t Vf = ~0ull;
@@ -830,9 +805,9 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
     }
     FK_TACC(tacc[0], tr0);
     FK_T0(tr1);
-    const bool is_short = !(RK_SKIP & 1) && F.n <= (uint32_t)MAXM;
+    const bool is_short = F.n <= (uint32_t)MAXM;
     // ---- one-deletion edge windows of the 11..20-code-point names (prefiltered by the scan)
-    if (!(RK_SKIP & 2) && edge && F.n >= EDGE_MIN_M + 1) {
+    if (edge && F.n >= EDGE_MIN_M + 1) {
         uint32_t added = fk_edge_items<ICAP>(FT, F, items_lds, icnt_f, dflag);
         added = (uint32_t)wave_sum((int)added);
         if (added) {
@@ -850,7 +825,7 @@ __device__ int fk_resolve_field(const FastTables &FT, const DevTables &T, const 
         // more than one register tile: sort in LDS, then take pattern-aligned batches of <= 64 items
         wave_sort_lds(items_lds, N);
     }
-    for (uint32_t bs = 0; !(RK_SKIP & 4) && bs < N;) {
+    for (uint32_t bs = 0; bs < N;) {
         uint32_t be = N;
         if (N > (uint32_t)WAVE) {
             be = bs + WAVE < N ? bs + WAVE : N;
@@ -1022,7 +997,7 @@ __device__ __forceinline__ bool dset_insert_wave(const FastScratch &S, uint32_t 
 // append one record to a wave's task region (cnt is wave-uniform; lane 0 writes)
 __device__ __forceinline__ void task_push(uint4 *region, uint32_t cap, uint32_t &cnt, uint4 rec)
 {
-    if (!XSTORE_OFF && cnt < cap && lane_id() == 0) region[cnt] = rec;
+    if (cnt < cap && lane_id() == 0) region[cnt] = rec;
     ++cnt;
 }
 
@@ -1322,9 +1297,8 @@ __device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTabl
     ++nrx;
     nrx_bt += r < 0;
     nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-    const uint32_t cnt = (RK_SKIP & 8) ? 1u
-                         : (r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, txt)
-                                   : rx_positions(T, GS, F, O, P));
+    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, txt)
+                                : rx_positions(T, GS, F, O, P);
     if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
 }
 
@@ -1517,7 +1491,7 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
     OutCtx O = tout_region(S, t);
     XPush X = xq_region(S, t);
     unsigned long long nver = 0, nwin = 0, nver_w = 0, nwin_w = 0;
-    const uint32_t nv = (TK_SKIP & 1) ? 0u : min(S.vcnt[t], S.vcap);
+    const uint32_t nv = min(S.vcnt[t], S.vcap);
     const uint4 *vq = S.vq + (size_t)t * S.vcap;
     for (uint32_t k0 = sub * WAVE; k0 < nv; k0 += (uint32_t)G * WAVE) {
         const uint32_t kk = k0 + (uint32_t)lane;
@@ -1527,7 +1501,7 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
         const bool todo = valid && !dset_contains(S, dset_key(doc, P, field));
         const uint32_t pi = todo ? FT.pat_info[P] : 0u;
         const uint32_t m = pi_m(pi);
-        const bool lanewise = !(VK_MODE & 2) && todo && (pi & PI_ASCII) != 0;
+        const bool lanewise = todo && (pi & PI_ASCII) != 0;
         int64_t fb = 0;
         uint32_t n = 0;
         bool tx = false;
@@ -1559,7 +1533,6 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
             nwj = lv_band(la, fb, n, NW, m, (int64_t)q - (int64_t)o, kfull(m), win, pmin);
             pre = q + pl + 1 <= m ? 1u : 0u;
             cj = nwj + pre + (q + m > n ? 1u : 0u);
-            if (VK_MODE & 1) cj = 0;
         }
         int J = 0;
         const int ex = wave_excl_scan((int)cj, &J);
@@ -1630,7 +1603,7 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
         wave_sync();
         bool pass = lanewise && okf[lane] != 0;
         // names lanes cannot take (non-ASCII code points), wave-serially
-        uint64_t wm = __ballot(!(VK_MODE & 6) && todo && !lanewise);
+        uint64_t wm = __ballot(todo && !lanewise);
         while (wm) {
             const int l = __builtin_ctzll(wm);
             wm &= wm - 1;
@@ -1794,11 +1767,9 @@ __device__ void fk_short_lanes(const FastTables &FT, const DevScratch &GS, const
     const int lane = lane_id();
     const uint32_t n = F.n;
     if (n <= (uint32_t)SHORT_EXACT_MAX) {
-        if (!(SHORT_SKIP & 1))
-            fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
+        fk_short_field(FT, FT.pat_tcps, GS, F, O, nver_w, nwin_w, [&](uint32_t P) { xq_push(X, lane == 0, F.doc, P, F.field); });
         return;
     }
-    if (SHORT_SKIP & 2) return;
     // the field's signature first (bit c & 63 of every byte): most fields have no candidate name at all
     const uint32_t fc = (lane < (int)n) ? (uint32_t)F.arena[F.fb + lane] : 0xFFFFFFFCu;
     uint64_t fsig = (lane < (int)n) ? 1ull << (fc & 63u) : 0ull;
@@ -1894,7 +1865,7 @@ __global__ __launch_bounds__(RK_BLOCK, SK_MINW) void kw_short_kernel(FastTables 
     XPush X = xq_region(S, t);
     unsigned long long nver = 0, nwin = 0, nver_w = 0, nwin_w = 0;
     FieldCtx F;
-    const uint32_t ns = (TK_SKIP & 4) ? 0u : min(S.scnt[t], S.scap);
+    const uint32_t ns = min(S.scnt[t], S.scap);
     const uint4 *sq = S.sq + (size_t)t * S.scap;
     for (uint32_t k = sub; k < ns; k += (uint32_t)G) {
         const uint4 tk = sq[k];
@@ -1965,7 +1936,6 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
 {
     __shared__ uint64_t rxtab_all[RK_WAVES * 128];
     __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
-    const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
     const int64_t t = gw / G;
@@ -1976,7 +1946,7 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
     OutCtx O = tout_region(S, t);
     unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
     FieldCtx F;
-    const uint32_t nx = (TK_SKIP & 8) ? 0u : min(S.xcnt[t], S.xcap);
+    const uint32_t nx = min(S.xcnt[t], S.xcap);
     const uint4 *xq = S.xq + (size_t)t * S.xcap;
     for (uint32_t k = sub; k < nx; k += (uint32_t)G) {
         const uint4 tk = xq[k];
@@ -2049,14 +2019,12 @@ __device__ __forceinline__ void rk_resolve_doc(const FastTables &FT, const DevTa
         const bool na = (hy & (f ? DH_NA1 : DH_NA0)) != 0;
         const bool edge = (hy & (f ? DH_EDGE1 : DH_EDGE0)) != 0;
         int rs = 0;
-        if (FK_STAGE >= 2) {
-            if constexpr (RK_NOINLINE)
-                rs = fk_resolve_field_call<ICAP>(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps, blkcnt, rxtab, RQ, na,
-                                                 edge, C.nver, C.nwin, C.nedge, tacc);
-            else
-                rs = fk_resolve_field<ICAP>(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps, blkcnt, rxtab, RQ, na, edge,
-                                            C.nver, C.nwin, C.nedge, tacc);
-        }
+        if constexpr (RK_NOINLINE)
+            rs = fk_resolve_field_call<ICAP>(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps, blkcnt, rxtab, RQ, na,
+                                             edge, C.nver, C.nwin, C.nedge, tacc);
+        else
+            rs = fk_resolve_field<ICAP>(FT, T, GS, F, O, items, &icnt[0], &icnt[1], cps, blkcnt, rxtab, RQ, na, edge,
+                                        C.nver, C.nwin, C.nedge, tacc);
         if (rs) {
             defer = true;
             if (rs == 1) ++C.ndef_cp;
@@ -2113,8 +2081,8 @@ __device__ __forceinline__ void rk_wave_tail(const FastTables &FT, const DevTabl
         ++C.nrx;
         C.nrx_bt += r < 0;
         C.nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-        const uint32_t cnt = (RK_SKIP & 8) ? 1u : (r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, RQ.txt)
-                                                         : ((RK_SKIP & 16) ? 1u : rx_positions(T, GS, F, O, P)));
+        const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, RQ.txt)
+                                    : rx_positions(T, GS, F, O, P);
         if (cnt == 0) emit_hits(O, GS, lane == 0, d, P, KW_NOPOS, F.field);
     }
     FK_TACC(tacc[4], trx0);

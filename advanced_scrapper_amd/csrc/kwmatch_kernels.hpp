@@ -164,7 +164,7 @@ __device__ __forceinline__ void emit_hits(OutCtx &O, const DevScratch &S, bool e
             h.pattern = pat;
             h.pos = pos;
             h.field = field;
-            if (!XSTORE_OFF) O.out[idx] = h;
+            O.out[idx] = h;
         } else {
             atomicOr(&S.status[0], ST_OUT_OVERFLOW);
         }

@@ -600,9 +600,6 @@ __device__ __forceinline__ uint32_t fk_edge_flags_key(const FastTables &FT, cons
 // bytes (tx_bytes), then per non-ASCII field the code points before each 16-byte chunk of the field's arena
 // bytes (u16, chunks counted from fb & ~15); vrec[d] = {start lo, start hi | 1 << 31, text cps, title cps}
 // (vrec[d].y = ~0: not transcoded).
-#ifndef TX_NOSTORE   // profiling aid: 1 = the view's body stores are skipped (wrong results, store cost measured)
-#define TX_NOSTORE 0
-#endif
 #ifndef TX_MINW
 #define TX_MINW 8   // 64 VGPRs (a 56-byte spill): 0.57 vs 0.60 ms isolated
 #endif
@@ -714,7 +711,7 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
                 for (int i = 0; i < 4; ++i)
                     w[i] = (uint32_t)stg[so + 4 * i] | ((uint32_t)stg[so + 4 * i + 1] << 8) |
                            ((uint32_t)stg[so + 4 * i + 2] << 16) | ((uint32_t)stg[so + 4 * i + 3] << 24);
-                if (!TX_NOSTORE) *(uint4 *)(out + q) = make_uint4(w[0], w[1], w[2], w[3]);
+                *(uint4 *)(out + q) = make_uint4(w[0], w[1], w[2], w[3]);
             }
         } else {
             for (uint32_t q = g0 + (uint32_t)lane; q < g1; q += WAVE) out[q] = stg[q - g0];
@@ -1071,7 +1068,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
                         if (n0 + i >= (uint32_t)WAVE) items[FK_ITEMS0 + i] = src[n0 + i];
                     wave_sync();
                     EK_T0(td2);
-                    const bool done = FK_STAGE < 2 || fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC, ekt);
+                    const bool done = fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC, ekt);
                     EK_TACC(ekt[7], td2);
                     if (!done) {
                         defer = true;
@@ -1091,9 +1088,9 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
                     }
                 } else {
                     h.y = n0 | (n1 << DH_N1_SHIFT) | flags;
-                    if (!XSTORE_OFF && lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
+                    if (lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
                 }
-                if (!XSTORE_OFF && lane == 0) S.hdr[d] = h;
+                if (lane == 0) S.hdr[d] = h;
                 wave_sync();
             }
         }

@@ -42,7 +42,11 @@ def _parse():
     ap.add_argument('--cpu-sample', type=int, default=10000,
                     help='docs of the same corpus timed on the CPU port of the reference loop (0 = skip)')
     ap.add_argument('--cpu-procs', type=int, default=0,
-                    help='CPU port processes (0 = the host share: min(16, os.cpu_count()))')
+                    help='CPU port processes (0 = the CPUs this process may use: affinity, capped by the cgroup '
+                         'CPU quota; the reference uses Pool(cpu_count()))')
+    ap.add_argument('--lib-variant', default=None,
+                    help='time lib/libkwmatch_<TAG>.so (a tuning build, advanced_scrapper_amd/build.py) instead of '
+                         'the default library; the line names the library and its sha256 either way')
     ap.add_argument('--hits', choices=('root', 'all', 'none'), default='root',
                     help='N > 1: hit records exchanged every step over libkwmatch\'s RCCL communicator '
                          '(root = to rank 0, the writer; all = all-gather; none = counts only)')
@@ -95,8 +99,26 @@ def hits_digest(hits) -> str:
     return f'{int(x.sum().item()) & 0xFFFFFFFFFFFFFFFF:016x}'
 
 
+def host_cpus() -> dict:
+    """CPUs this process may use: os.cpu_count(), the affinity mask, the cgroup v2 CPU quota (cpu.max) and
+    the usable count = min(affinity, quota)."""
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, p = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return {'os_cpu_count': os.cpu_count(), 'affinity': n_aff, 'cgroup_quota': quota,
+            'usable': min(n_aff, quota) if quota else n_aff}
+
+
 def main():
     args = _parse()
+    if args.lib_variant:
+        os.environ['KW_LIB'] = os.path.join(REPO, 'advanced_scrapper_amd', 'lib', f'libkwmatch_{args.lib_variant}.so')
+        os.environ['KW_LIB_VARIANT_OK'] = '1'
     rc = _launch_ranks(args)
     if rc >= 0:
         sys.exit(rc)
@@ -104,7 +126,7 @@ def main():
         return bench_dedup(args)
 
     import torch
-    from advanced_scrapper_amd import dist, synth
+    from advanced_scrapper_amd import _native, dist, synth
     from advanced_scrapper_amd.kb import compile_kb
     from advanced_scrapper_amd.matcher import GpuMatcher, background_sample
     from tests import golden_data
@@ -288,9 +310,10 @@ def main():
         },
         'cpu_baseline': cpu,
         'scan_stats': st,
+        'library': _native.lib_identity(),
         'host': {'generate_s': round(t_gen, 2), 'h2d_s': round(t_up, 3),
                  'h2d_GBps_pcie_inclusive': round(local_bytes / t_up / 1e9, 2) if t_up > 0 else None,
-                 'os_cpu_count': os.cpu_count()},
+                 **host_cpus()},
     }
     print(json.dumps(out), flush=True)
 
@@ -302,7 +325,7 @@ def bench_dedup(args):
     hash, table insert, rep compare, dense kept rows.  value = (URL bytes + 8 B
     per offset) of all ranks / step time."""
     import torch
-    from advanced_scrapper_amd import dist, synth
+    from advanced_scrapper_amd import _native, dist, synth
     from advanced_scrapper_amd.cdx_dedup import GpuUrlDedup
     rank, world, local = dist.init('nccl')
     torch.cuda.set_device(local)
@@ -364,6 +387,7 @@ def bench_dedup(args):
                      'algorithmic_bytes_per_launch': rows.n_bytes, 'kernel': 'dd::dd_transform_kernel',
                      'kernel_ms_avg': kms['transform_hash'], 'kernels_ms_avg': kms},
         'cpu_baseline': cpu,
+        'library': _native.lib_identity(),
         'host': {'generate_s': round(t_gen, 2)},
     }
     print(json.dumps(out), flush=True)
@@ -416,8 +440,8 @@ def cpu_baseline(processed, corpus, n_sample: int, procs: int):
     """Time the CPU port of the reference loop (oracle/cpu_port.py) on the first n_sample documents of the
     same corpus, in the reference's pool shape; procs = the host share (min(16, os.cpu_count()))."""
     from oracle import cpu_port
-    ncpu = os.cpu_count() or 1
-    procs = procs or min(16, ncpu)
+    hc = host_cpus()
+    procs = procs or hc['usable']
     n = min(n_sample, corpus.n_docs)
     rows = []
     nbytes = 0
@@ -431,10 +455,11 @@ def cpu_baseline(processed, corpus, n_sample: int, procs: int):
             'sample': f'first {done} docs of the same corpus ({nbytes} bytes): the reference loop '
                       f'(match_keywords.py:148-192: per name occurrence period check, re, partial_ratio '
                       f'decisions by the oracle C restatement, per-hit pandas appends) in its pool shape '
-                      f'(:230-238), {procs} processes on a host with os.cpu_count() = {ncpu} (16 = the '
-                      f'GPU box CPU share), {secs:.2f} s wall',
+                      f'(:230-238), {procs} processes = the CPUs this process may use (affinity '
+                      f'{hc["affinity"]}, cgroup quota {hc["cgroup_quota"]}; os.cpu_count() = {hc["os_cpu_count"]}), '
+                      f'{secs:.2f} s wall',
             'docs_per_s': round(done / secs, 2), 'docs_per_s_per_core': round(done / secs / procs, 3),
-            'host_cpu_count': ncpu}
+            'host_cpus': hc}
 
 
 if __name__ == '__main__':

@@ -127,6 +127,9 @@ def name_class(name: str) -> str:
 
 
 def upper_positions(name: str, s: str) -> List[int]:
+    # the pattern is the escaped literal between two \b: no match without the literal as a substring
+    if name not in s:
+        return []
     return [m.start() for m in re.finditer(r'\b' + re.escape(name) + r'\b', s)]
 
 

@@ -203,20 +203,41 @@ static inline int passes(int lcs, int l1, int lw)
     return 20 * (lensum - 2 * lcs) < lensum;
 }
 
-static int find_exact(const uint32_t *nd, int l1, const uint32_t *hy, int l2)
+/* Occurrence lists of the haystack's ASCII code points (built once per text
+ * by pr_decide_many): head[c] = first position of c, nxt[p] = next position
+ * holding hy[p], -1 at the end.  NULL = scan every position. */
+typedef struct {
+    const int32_t *nxt;
+    int32_t head[128];
+} occ_t;
+
+/* the occurrences of pat in hy, one at a time: q = the previous one or -1;
+ * returns the next one or -1 */
+static inline int next_occ(const occ_t *ix, const uint32_t *pat, int len, const uint32_t *hy, int l2, int q)
 {
-    if (l1 == 0) return 1;
-    for (int p = 0; p + l1 <= l2; ++p) {
-        if (hy[p] != nd[0]) continue;
-        if (memcmp(hy + p, nd, sizeof(uint32_t) * (size_t)l1) == 0) return 1;
+    if (ix && pat[0] < 128) {
+        q = (q < 0) ? ix->head[pat[0]] : ix->nxt[q];
+        for (; q >= 0 && q + len <= l2; q = ix->nxt[q])
+            if (memcmp(hy + q, pat, sizeof(uint32_t) * (size_t)len) == 0) return q;
+        return -1;
     }
-    return 0;
+    for (++q; q + len <= l2; ++q) {
+        if (hy[q] != pat[0]) continue;
+        if (memcmp(hy + q, pat, sizeof(uint32_t) * (size_t)len) == 0) return q;
+    }
+    return -1;
 }
 
-static int decide_dir(const uint32_t *nd, int l1, const uint32_t *hy, int l2)
+static int find_exact(const uint32_t *nd, int l1, const uint32_t *hy, int l2, const occ_t *ix)
+{
+    if (l1 == 0) return 1;
+    return next_occ(ix, nd, l1, hy, l2, -1) >= 0;
+}
+
+static int decide_dir(const uint32_t *nd, int l1, const uint32_t *hy, int l2, const occ_t *ix)
 {
     /* exact full window => score 100 */
-    if (find_exact(nd, l1, hy, l2)) return 1;
+    if (find_exact(nd, l1, hy, l2, ix)) return 1;
     /* l1 <= 10: a full window needs LCS > 0.95*l1, i.e. LCS == l1 (exact), and
        an edge window |W| < l1 needs 21|W| > 19*l1 + 40j, impossible for l1 <= 10;
        so nothing but an exact occurrence can pass (checked against the brute
@@ -225,51 +246,35 @@ static int decide_dir(const uint32_t *nd, int l1, const uint32_t *hy, int l2)
     pm_t pm;
     pm_build(&pm, nd, l1);
     uint64_t mask = (l1 == 64) ? ~0ull : ((1ull << l1) - 1);
-    /* full windows, pruned by the sliding character-histogram bound
-       LCS <= sum_c min(cnt_needle[c], cnt_window[c]) */
-    if (l1 <= l2) {
-        /* map needle chars to ids 1..k, everything else to 0 */
-        int cnt_n[65] = {0}, cnt_w[65] = {0};
-        uint32_t ids_cp[64];
-        int nid = 0;
-        int nid_of_pos[64];
-        for (int i = 0; i < l1; ++i) {
-            int k = 0;
-            for (; k < nid; ++k) if (ids_cp[k] == nd[i]) break;
-            if (k == nid) ids_cp[nid++] = nd[i];
-            nid_of_pos[i] = k + 1;
-            cnt_n[k + 1]++;
-        }
-        (void)nid_of_pos;
-        int *hid = (int *)malloc(sizeof(int) * (size_t)l2);
-        int ascii_id[128];
-        for (int c = 0; c < 128; ++c) ascii_id[c] = 0;
-        for (int k = 0; k < nid; ++k) if (ids_cp[k] < 128) ascii_id[ids_cp[k]] = k + 1;
-        for (int j = 0; j < l2; ++j) {
-            if (hy[j] < 128) { hid[j] = ascii_id[hy[j]]; continue; }
-            int k = 0;
-            for (; k < nid; ++k) if (ids_cp[k] == hy[j]) break;
-            hid[j] = (k < nid) ? k + 1 : 0;
-        }
-        int common = 0;
-        for (int j = 0; j < l1; ++j) {
-            int c = hid[j];
-            if (c && cnt_w[c] < cnt_n[c]) common++;
-            cnt_w[c]++;
-        }
-        for (int p = 0; p + l1 <= l2; ++p) {
-            if (p > 0) {
-                int cout = hid[p - 1];
-                cnt_w[cout]--;
-                if (cout && cnt_w[cout] < cnt_n[cout]) common--;
-                int cin = hid[p + l1 - 1];
-                if (cin && cnt_w[cin] < cnt_n[cin]) common++;
-                cnt_w[cin]++;
+    /* full windows: a full window passes iff 20*2*(l1-LCS) < 2*l1, i.e.
+       20*(l1-LCS) < l1; for l1 <= 20 that forces LCS == l1, an exact
+       occurrence, which find_exact has already ruled out.  Longer needles:
+       pigeonhole coverage.  A passing full window has d = 2*(l1-LCS) indel
+       operations with 20*d < 2*l1; cut the needle into dmax+1 pieces and one
+       of them has no operation inside, i.e. occurs verbatim inside the
+       window.  Only windows containing a piece occurrence take the LCS. */
+    if (l1 <= l2 && l1 > 20) {
+        int dmax = 2 * ((l1 - 1) / 20);
+        int npiece = dmax + 1, nwin = l2 - l1 + 1;
+        int *cov = (int *)calloc((size_t)nwin + 1, sizeof(int));
+        for (int k = 0; k < npiece; ++k) {
+            int a = k * l1 / npiece, b = (k + 1) * l1 / npiece, len = b - a;
+            for (int q = next_occ(ix, nd + a, len, hy, l2, -1); q >= 0; q = next_occ(ix, nd + a, len, hy, l2, q)) {
+                int lo = q + len - l1, hi = q;          /* windows p with p <= q, q+len <= p+l1 */
+                if (lo < 0) lo = 0;
+                if (hi > nwin - 1) hi = nwin - 1;
+                if (lo > hi) continue;
+                cov[lo]++;
+                cov[hi + 1]--;
             }
-            if (!passes(common, l1, l1)) continue;
-            if (passes(lcs_bp(&pm, hy + p, l1), l1, l1)) { free(hid); return 1; }
         }
-        free(hid);
+        int covered = 0, found = 0;
+        for (int p = 0; p < nwin && !found; ++p) {
+            covered += cov[p];
+            if (covered && passes(lcs_bp(&pm, hy + p, l1), l1, l1)) found = 1;
+        }
+        free(cov);
+        if (found) return 1;
     }
     /* prefixes */
     {
@@ -299,16 +304,23 @@ static int decide_dir(const uint32_t *nd, int l1, const uint32_t *hy, int l2)
 }
 
 /* 1 iff partial_ratio(s1, s2) > 95 */
-int pr_decide(const uint32_t *s1, int n1, const uint32_t *s2, int n2)
+static int decide_ix(const uint32_t *s1, int n1, const uint32_t *s2, int n2, const occ_t *ix1)
 {
     if (n1 == 0 || n2 == 0) return n1 == n2;
     const uint32_t *nd = s1, *hy = s2;
+    const occ_t *ix = NULL;               /* ix1 indexes s1: usable only while s1 is the haystack */
     int l1 = n1, l2 = n2;
-    if (l1 > l2) { nd = s2; hy = s1; l1 = n2; l2 = n1; }
+    if (l1 > l2) { nd = s2; hy = s1; l1 = n2; l2 = n1; ix = ix1; }
     if (l1 > 64) return pr_score_brute(s1, n1, s2, n2) > 95.0;
-    if (decide_dir(nd, l1, hy, l2)) return 1;
-    if (l1 == l2) return decide_dir(hy, l2, nd, l1);
+    if (decide_dir(nd, l1, hy, l2, ix)) return 1;
+    if (l1 == l2) return decide_dir(hy, l2, nd, l1, NULL);
     return 0;
+}
+
+/* 1 iff partial_ratio(s1, s2) > 95 */
+int pr_decide(const uint32_t *s1, int n1, const uint32_t *s2, int n2)
+{
+    return decide_ix(s1, n1, s2, n2, NULL);
 }
 
 /* Batched decision: one text against many names (the per-article inner loop
@@ -317,9 +329,18 @@ int pr_decide(const uint32_t *s1, int n1, const uint32_t *s2, int n2)
 void pr_decide_many(const uint32_t *text, int n, const uint32_t *names, const int64_t *name_off,
                     int n_names, uint8_t *out)
 {
+    occ_t ix;
+    int32_t *nxt = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    for (int c = 0; c < 128; ++c) ix.head[c] = -1;
+    for (int p = n - 1; p >= 0; --p) {
+        nxt[p] = -1;
+        if (text[p] < 128) { nxt[p] = ix.head[text[p]]; ix.head[text[p]] = p; }
+    }
+    ix.nxt = nxt;
     for (int i = 0; i < n_names; ++i) {
         const uint32_t *nm = names + name_off[i];
         int m = (int)(name_off[i + 1] - name_off[i]);
-        out[i] = (uint8_t)pr_decide(text, n, nm, m);
+        out[i] = (uint8_t)decide_ix(text, n, nm, m, &ix);
     }
+    free(nxt);
 }

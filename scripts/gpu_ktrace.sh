@@ -5,6 +5,6 @@ export TMPDIR=/tmp
 out=$1; shift
 mkdir -p gpurun_out
 for tag in "$@"; do
-  if [ "$tag" = default ]; then unset KW_LIB; else export KW_LIB=$PWD/advanced_scrapper_amd/lib/libkwmatch_$tag.so; fi
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$out/$tag -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/${out}_$tag.log 2>&1 || exit $?
+  if [ "$tag" = default ]; then V=""; else V="--lib-variant $tag"; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$out/$tag -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 $V > gpurun_out/${out}_$tag.log 2>&1 || exit $?
 done

@@ -6,5 +6,5 @@ mkdir -p gpurun_out
 export KW_DUMP_TIMING=1
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-sample 0 $BENCH_ARGS > gpurun_out/var_default.log 2>&1 || exit $?
 for tag in "$@"; do
-  KW_LIB=$PWD/advanced_scrapper_amd/lib/libkwmatch_$tag.so timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-sample 0 $BENCH_ARGS > gpurun_out/var_$tag.log 2>&1 || exit $?
+  timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-sample 0 --lib-variant $tag $BENCH_ARGS > gpurun_out/var_$tag.log 2>&1 || exit $?
 done

@@ -1,0 +1,126 @@
+"""Pin the WHOLE config-2 bench corpus: per-document oracle digests (tests/golden/c2_digests.npz).
+
+The bench corpus is bench.py's: 1M synthetic ~2 KB articles (csrc/synth.c,
+seed 20250905, documents 0..999 999) against the reference KB
+(tests/golden/kb_processed.json.gz).  For every document the CPU oracle
+(oracle/kwmatch_oracle.py, match_keywords.py:155-180 per field) gives
+``name -> positions`` for the text and the title; those become kw_scan-shaped
+records ``(doc, pattern, pos, field)`` (tests/corpus_digest.py) and the
+document's digest is the wrapping sum of bench.hits_digest's record mix.  The
+sum over all documents is the bench line's ``hits_digest``.
+
+Runs in the build container on CPU (a spawn pool, ~5 ms of oracle per
+article), never on GPU minutes:
+
+    python tests/golden/make_c2_digests.py [--procs 7] [--docs 1000000]
+
+Output: c2_digests.npz (digest uint64[n], count uint16[n]) + c2_digests.json
+(seed, n_docs, corpus fingerprint, total digest, total records).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+SEED = 20250905
+BLOCK = 2000
+_W = {}
+
+
+def _init():
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from oracle import kwmatch_oracle as orc
+    from tests import golden_data
+    processed = golden_data.kb_processed()
+    ckb = compile_kb(processed)
+    _W['names'] = synth.injectable_names(ckb)
+    _W['pid'] = {n: i for i, n in enumerate(ckb.names)}
+    _W['oracle'] = orc.Oracle(processed)
+
+
+def _field(s):
+    import re
+    from oracle import kwmatch_oracle as orc
+    O = _W['oracle']
+    out = {}
+    for n in O.upper:
+        pos = orc.upper_positions(n, s)
+        if pos:
+            out[n] = pos
+    for n, hit in zip(O.fuzzy, O.fset.decide(s)):
+        if hit:
+            try:
+                out[n] = orc.regex_positions(n, s)
+            except re.error:
+                out[n] = []
+    return out
+
+
+def _block(lo_hi):
+    from advanced_scrapper_amd import synth
+    from tests import corpus_digest as cd
+    lo, hi = lo_hi
+    names, kinds = _W['names']
+    c = synth.generate(hi - lo, names, kinds, seed=SEED, doc_base=lo)
+    rows = []
+    for i in range(hi - lo):
+        rows += cd.oracle_records(lo + i, [_field(c.text(i)), _field(c.title(i))], _W['pid'])
+    a = np.asarray(rows, dtype=np.uint32).reshape(-1, 4)
+    rec = np.ascontiguousarray(a).view(np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'),
+                                                   ('field', '<u4')])).reshape(-1)
+    dig, cnt = cd.per_doc(rec, hi - lo, lo)
+    return lo, dig, cnt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--procs', type=int, default=7)
+    ap.add_argument('--docs', type=int, default=1_000_000)
+    ap.add_argument('--out', default=os.path.join(HERE, 'c2_digests'))
+    args = ap.parse_args()
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from tests import corpus_digest as cd
+    from tests import golden_data
+    n = args.docs
+    ckb = compile_kb(golden_data.kb_processed())
+    names, kinds = synth.injectable_names(ckb)
+    corpus = synth.generate(n, names, kinds, seed=SEED, doc_base=0)
+    fp = cd.corpus_fingerprint(corpus)
+    n_bytes = corpus.n_bytes
+    del corpus
+    dig = np.zeros(n, np.uint64)
+    cnt = np.zeros(n, np.int64)
+    blocks = [(lo, min(lo + BLOCK, n)) for lo in range(0, n, BLOCK)]
+    t0 = time.time()
+    ctx = mp.get_context('spawn')
+    with ctx.Pool(args.procs, initializer=_init) as pool:
+        for k, (lo, d, c) in enumerate(pool.imap_unordered(_block, blocks)):
+            dig[lo:lo + len(d)] = d
+            cnt[lo:lo + len(c)] = c
+            if k % 25 == 0:
+                print(f'{k + 1}/{len(blocks)} blocks, {time.time() - t0:.0f} s', flush=True)
+    assert cnt.max() < 65536
+    np.savez_compressed(args.out + '.npz', digest=dig, count=cnt.astype(np.uint16))
+    meta = {'generator': 'tests/golden/make_c2_digests.py (CPU oracle, oracle/kwmatch_oracle.py)',
+            'seed': SEED, 'n_docs': n, 'corpus_bytes': n_bytes, 'corpus_fingerprint': fp,
+            'kb': 'tests/golden/kb_processed.json.gz', 'total_records': int(cnt.sum()),
+            'hits_digest': cd.total(dig), 'oracle_seconds': round(time.time() - t0, 1), 'procs': args.procs}
+    with open(args.out + '.json', 'w') as fh:
+        json.dump(meta, fh, indent=1)
+    print(json.dumps(meta, indent=1))
+
+
+if __name__ == '__main__':
+    main()

@@ -1,5 +1,9 @@
 """Parity at bench scale: the bench's own config-2 corpus (1M synthetic ~2 KB articles, bench.py's seed).
 
+* every document: per-document digests of the GPU's hit records against the
+  CPU oracle's, computed once for the whole corpus in the build container
+  (tests/golden/make_c2_digests.py -> c2_digests.npz), and the bench line's
+  hits_digest against the oracle's total;
 * a seeded sample of the corpus, seeded samples of the documents with a
   non-ASCII field (those the epilogue finished on their transcoded view and
   those the resolve kernel finished), every document the generic kernel
@@ -97,6 +101,39 @@ def test_bench_corpus_vs_oracle(bench_scan):
     print(f'checked {len(docs)} docs ({len(transcode)} transcode-route, {len(resolve)} resolve-route, '
           f'{len(generic)} generic-route in the corpus)')
     assert not bad, f'{len(bad)} of {len(docs)} documents differ from the oracle: {bad[:20]}'
+
+
+def test_whole_corpus_vs_oracle_digests(bench_scan):
+    """EVERY document of the 1M config-2 corpus: the GPU's per-document record digest equals the CPU
+    oracle's (tests/golden/c2_digests.npz, made in the build container by make_c2_digests.py), and so does
+    the bench line's hits_digest."""
+    import json
+    import os
+    import bench
+    from tests import corpus_digest as cd
+    from tests.golden_data import HERE
+    b = bench_scan
+    meta = json.load(open(os.path.join(HERE, 'c2_digests.json')))
+    z = np.load(os.path.join(HERE, 'c2_digests.npz'))
+    assert meta['n_docs'] == N_DOCS and meta['seed'] == SEED
+    assert cd.corpus_fingerprint(b['corpus']) == meta['corpus_fingerprint'], 'the generator no longer makes the pinned corpus'
+    dig, cnt = cd.per_doc(b['rec'], N_DOCS)
+    bad = np.flatnonzero((dig != z['digest']) | (cnt != z['count'].astype(np.int64)))
+    if len(bad):
+        from advanced_scrapper_amd.matcher import group_hits
+        sel = b['rec'][np.isin(b['rec']['doc'], bad[:3].astype(np.uint32))]
+        g = group_hits(sel)
+        names = b['ckb'].names
+        want = oracle_pool.field_results(b['processed'], [s for d in bad[:3] for s in
+                                                          (b['corpus'].text(int(d)), b['corpus'].title(int(d)))], 3)
+        for k, d in enumerate(bad[:3].tolist()):
+            for f in (0, 1):
+                got = {names[p]: v for p, v in g.get(d, {}).get(f, {}).items()}
+                w = want[2 * k + f]
+                print('doc', d, 'field', f, {n: (got.get(n), w.get(n)) for n in set(got) | set(w) if got.get(n) != w.get(n)})
+    assert not len(bad), f'{len(bad)} of {N_DOCS} documents differ from the oracle; first: {bad[:20].tolist()}'
+    assert int(cnt.sum()) == meta['total_records']
+    assert cd.total(dig) == meta['hits_digest'] == bench.hits_digest(b['hits'])
 
 
 def test_sharded_scans_equal_one_shot(bench_scan):

@@ -44,6 +44,39 @@ def test_partial_ratio_brute_fast_decide_agree(seed):
         assert orc.partial_ratio_score(a, b) == orc.partial_ratio_score(b, a)
 
 
+@pytest.mark.parametrize('seed', [3, 4])
+def test_long_needles_decide_many_equals_brute(seed):
+    """Names of 21..64 code points (the pigeonhole-covered full windows) inside longer texts with up to 6
+    indels, through pr_decide_many (the per-text occurrence index) and pr_decide, against the brute-force
+    window-family score."""
+    rng = random.Random(seed)
+    alpha = 'abcdeé ,.AB'
+    for _ in range(60):
+        names = []
+        for _k in range(8):
+            names.append(''.join(rng.choice(alpha) for _ in range(rng.randint(21, 64))))
+        text = ''.join(rng.choice(alpha) for _ in range(rng.randint(60, 260)))
+        for nm in rng.sample(names, 3):
+            piece = list(nm)
+            for _k in range(rng.randint(0, 6)):
+                if rng.random() < 0.5:
+                    del piece[rng.randrange(len(piece))]
+                else:
+                    piece.insert(rng.randint(0, len(piece)), rng.choice(alpha))
+            cut = rng.randint(0, len(text))
+            if rng.random() < 0.2:
+                cut = rng.choice((0, len(text)))
+                piece = piece[rng.randint(0, 5):] if cut == 0 else piece[:len(piece) - rng.randint(0, 5)]
+            text = text[:cut] + ''.join(piece) + text[cut:]
+        if rng.random() < 0.2:
+            text = text[:rng.randint(20, 64)]        # texts shorter than some names swap roles
+        many = orc.NameSet(names).decide(text)
+        for nm, got in zip(names, many):
+            want = orc.partial_ratio_score(text, nm, brute=True) > 95
+            assert bool(got) == want, (text, nm)
+            assert orc.partial_ratio_gt95(text, nm) == want, (text, nm)
+
+
 def test_partial_ratio_known_properties():
     assert orc.partial_ratio_score('', '') == 100.0
     assert orc.partial_ratio_score('abc', '') == 0.0
