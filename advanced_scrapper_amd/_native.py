@@ -40,8 +40,8 @@ HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('fiel
 # every symbol include/kwmatch.h and include/kwdedup.h declare
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
            'kw_last_kernel_times', 'kw_doc_routes', 'kw_last_error', 'kw_destroy',
-           'kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_comm_last_error',
-           'kw_comm_destroy',
+           'kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_exchange_plan',
+           'kw_comm_last_error', 'kw_comm_destroy',
            'kw_dedup_create', 'kw_dedup_run', 'kw_dedup_counts', 'kw_dedup_kept_size', 'kw_dedup_kept_copy',
            'kw_dedup_last_ms', 'kw_dedup_last_error', 'kw_dedup_destroy', 'dedup_urls')
 
@@ -51,6 +51,7 @@ KW_DEDUP_NORMALIZE = 1
 KW_N_STATS = 20
 KW_COMM_ID_BYTES = 128
 KW_ROUTE_SCAN, KW_ROUTE_RESOLVE, KW_ROUTE_GENERIC, KW_ROUTE_TRANSCODE = 0, 1, 2, 3
+KW_PLAN_SEND, KW_PLAN_RECV = 1, 2
 
 
 class KwError(RuntimeError):
@@ -107,6 +108,8 @@ def lib() -> ctypes.CDLL:
     L.kw_allgather_counts.argtypes = [vp, i64, vp, vp]
     L.kw_allgather_hits.argtypes = [vp, vp, i64, i64, i32, vp, i64, ctypes.POINTER(i64), vp, vp]
     L.kw_comm_destroy.argtypes = [vp]
+    L.kw_exchange_plan.argtypes = [i32, i32, i32, vp, vp, vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.kw_exchange_plan.restype = ctypes.c_int
     for f in ('kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_comm_destroy'):
         getattr(L, f).restype = ctypes.c_int
     L.kw_comm_last_error.argtypes = [vp]
@@ -128,6 +131,18 @@ def lib_identity() -> dict:
     return {'path': os.path.relpath(LIB_PATH, os.path.dirname(LIB_DIR)), 'sha256': digest,
             'default': LIB_PATH == DEFAULT_LIB,
             'env': {k: v for k, v in sorted(os.environ.items()) if k.startswith('KW_')}}
+
+
+def exchange_plan(nranks: int, rank: int, root: int, counts):
+    """kw_exchange_plan (pure host): (recv_off[nranks + 1], ops[nranks], n_total, n_recv) of `rank`."""
+    cnt = np.ascontiguousarray(counts, dtype=np.int64)
+    off = np.zeros(nranks + 1, dtype=np.int64)
+    ops = np.zeros(nranks, dtype=np.int32)
+    tot, nrecv = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib().kw_exchange_plan(nranks, rank, root, ptr(cnt), ptr(off), ptr(ops), ctypes.byref(tot), ctypes.byref(nrecv))
+    if rc != KW_OK:
+        raise KwError(rc, 'kw_exchange_plan: bad arguments')
+    return off, ops, int(tot.value), int(nrecv.value)
 
 
 def check(rc: int, handle=None) -> None:

@@ -157,6 +157,32 @@ extern "C" int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, v
     return gather_counts(c, count, counts, (hipStream_t)stream);
 }
 
+extern "C" int kw_exchange_plan(int32_t nranks, int32_t rank, int32_t root, const int64_t *counts, int64_t *recv_off,
+                                int32_t *ops, int64_t *n_total, int64_t *n_recv)
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks || root >= nranks || !counts || !recv_off || !ops || !n_total ||
+        !n_recv)
+        return KW_EINVAL;
+    recv_off[0] = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (counts[r] < 0) return KW_EINVAL;
+        recv_off[r + 1] = recv_off[r] + counts[r];
+    }
+    *n_total = recv_off[nranks];
+    const bool receive = root < 0 || root == rank;
+    *n_recv = receive ? recv_off[nranks] : 0;
+    // point-to-point over the xGMI mesh: every (sender, receiver) pair moves exactly the sender's records;
+    // nothing moves to a rank that does not receive, nor from a rank without records
+    for (int p = 0; p < nranks; ++p) {
+        ops[p] = 0;
+        if (p == rank) continue;
+        const bool p_receives = root < 0 || root == p;
+        if (p_receives && counts[rank] > 0) ops[p] |= KW_PLAN_SEND;
+        if (receive && counts[p] > 0) ops[p] |= KW_PLAN_RECV;
+    }
+    return KW_OK;
+}
+
 extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
                                  kw_hit *d_out, int64_t cap, int64_t *n_total, int64_t *counts, void *stream)
 {
@@ -169,9 +195,13 @@ extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, i
     rc = gather_counts(c, n, cnt.data(), st);
     if (rc) return rc;
     std::vector<int64_t> pre(c->nranks + 1, 0);
-    for (int r = 0; r < c->nranks; ++r) pre[r + 1] = pre[r] + cnt[r];
+    std::vector<int32_t> ops(c->nranks, 0);
+    int64_t n_recv = 0;
+    if (kw_exchange_plan(c->nranks, c->rank, root, cnt.data(), pre.data(), ops.data(), n_total, &n_recv) != KW_OK) {
+        c->err = "kw_allgather_hits: bad exchange plan";
+        return KW_EINVAL;
+    }
     if (counts) memcpy(counts, cnt.data(), sizeof(int64_t) * c->nranks);
-    *n_total = pre[c->nranks];
     const bool receive = root < 0 || root == c->rank;
     if (receive && pre[c->nranks] > cap) { c->err = "kw_allgather_hits: destination too small"; return KW_EINVAL; }
     if (receive && pre[c->nranks] > 0 && !d_out) { c->err = "kw_allgather_hits: null destination"; return KW_EINVAL; }
@@ -198,10 +228,8 @@ extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, i
     // point-to-point over the xGMI mesh: every (sender, receiver) pair moves exactly its records
     NCHK(c, g_rccl.GroupStart());
     for (int p = 0; p < c->nranks; ++p) {
-        if (p == c->rank) continue;
-        const bool p_receives = root < 0 || root == p;
-        if (p_receives && n > 0) NCHK(c, g_rccl.Send(mine, (size_t)n * 4, nccl_uint32, p, c->comm, st));
-        if (receive && cnt[p] > 0) NCHK(c, g_rccl.Recv(d_out + pre[p], (size_t)cnt[p] * 4, nccl_uint32, p, c->comm, st));
+        if (ops[p] & KW_PLAN_SEND) NCHK(c, g_rccl.Send(mine, (size_t)n * 4, nccl_uint32, p, c->comm, st));
+        if (ops[p] & KW_PLAN_RECV) NCHK(c, g_rccl.Recv(d_out + pre[p], (size_t)cnt[p] * 4, nccl_uint32, p, c->comm, st));
     }
     NCHK(c, g_rccl.GroupEnd());
     return KW_OK;

@@ -190,9 +190,8 @@ struct QStats {
 };
 
 struct FastBuild {
-    std::vector<uint32_t> filt, l2, t3, b2, edge_pre, edge_suf;
-    uint32_t gate_lo[4] = {0, 0, 0, 0}, gate_hi[4] = {0, 0, 0, 0};
-    int n_gate = 0;
+    std::vector<uint32_t> mid, p2, l2, t3, b2, edge_pre, edge_suf;
+    int has_short = 0;
     int has_t3 = 0;
     std::vector<uint64_t> ht_key, as_head, sig, bsig;
     std::vector<uint32_t> ht_begin, ht_cnt, kl, as_len, as_use_begin, as_use_cnt, use_pat, use_info0, use_info1,
@@ -447,61 +446,39 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         }
     }
     if (B.use_pat.size() > IT_USE_MASK) { err = "kw_compile: more than 2^19 anchor uses"; return KW_EUNSUPPORTED; }
-    // ---- LDS filter, bigram table, gate, global hash table
-    B.filt.assign(FK_FILT_WORDS, 0);
+    // ---- LDS filters (stage 1: mid entries + exact pair table; stage 2: l2 / t3 / b2), global hash table
+    B.mid.assign(2 * (size_t)FK_MID_ENTRIES, 0);
+    B.p2.assign(FK_P2_WORDS, 0);
     B.l2.assign(FK_L2_WORDS, 0);
     B.t3.assign(FK_T3_WORDS, 0);
     B.b2.assign(FK_B2_WORDS, 0);
     std::unordered_map<uint64_t, std::vector<uint32_t>> keys;
-    std::vector<uint8_t> gate_bytes;
-    bool gate_high = false;
     for (uint32_t a = 0; a < na; ++a) {
         const std::string &st = astr[a];
         const uint8_t *p = (const uint8_t *)st.data();
         if (st.size() >= 4) {
             const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-            B.filt[fk_word(k4)] |= 1u << fk_bit(k4);
+            // start at an even position E: entry of bytes 1..3, low word; at E + 1: entry of bytes 0..2, high word
+            B.mid[2 * (size_t)fk_mid_entry(k4 >> 8)] |= 1u << fk_fold0(p[0], p[1]);
+            B.mid[2 * (size_t)fk_mid_entry(k4) + 1] |= 1u << fk_fold(p[3]);
             B.l2[fk_l2_index(k4) >> 5] |= 1u << (fk_l2_index(k4) & 31);
             keys[(4ull << 32) | k4].push_back(a);
-        } else if (st.size() == 3) {
-            const uint32_t k3 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-            B.filt[fk_word(k3)] = 0xFFFFFFFFu;
-            B.t3[fk_t3_index(k3) >> 5] |= 1u << (fk_t3_index(k3) & 31);
-            B.has_t3 = 1;
-            keys[(3ull << 32) | k3].push_back(a);
-        } else if (st.size() == 2) {
+        } else if (st.size() >= 2) {
             const uint32_t k2 = (uint32_t)p[0] | ((uint32_t)p[1] << 8);
-            const uint32_t x = fk_b2_index(k2);
-            B.b2[x >> 5] |= 1u << (x & 31);
-            keys[(2ull << 32) | k2].push_back(a);
-            gate_bytes.push_back(p[0]);
-            gate_high |= p[0] >= 0x80;
+            B.p2[fk_b2_index(k2) >> 5] |= 1u << (fk_b2_index(k2) & 31);
+            B.has_short = 1;
+            if (st.size() == 3) {
+                const uint32_t k3 = k2 | ((uint32_t)p[2] << 16);
+                B.t3[fk_t3_index(k3) >> 5] |= 1u << (fk_t3_index(k3) & 31);
+                B.has_t3 = 1;
+                keys[(3ull << 32) | k3].push_back(a);
+            } else {
+                B.b2[fk_b2h_index(k2) >> 5] |= 1u << (fk_b2h_index(k2) & 31);
+                keys[(2ull << 32) | k2].push_back(a);
+            }
         } else {
             err = "kw_compile: one-byte anchor";
             return KW_EUNSUPPORTED;
-        }
-    }
-    if (!gate_bytes.empty()) {
-        if (gate_high) {
-            B.n_gate = -1;
-        } else {
-            std::sort(gate_bytes.begin(), gate_bytes.end());
-            gate_bytes.erase(std::unique(gate_bytes.begin(), gate_bytes.end()), gate_bytes.end());
-            std::vector<std::pair<uint32_t, uint32_t>> rg;
-            for (uint8_t g : gate_bytes) {
-                if (!rg.empty() && rg.back().second + 1 >= g) rg.back().second = g;
-                else rg.emplace_back(g, g);
-            }
-            while (rg.size() > 4) {   // merge the two closest ranges (a superset gate is still exact)
-                size_t bi = 0;
-                uint32_t bg = 0xFFFFFFFFu;
-                for (size_t r = 0; r + 1 < rg.size(); ++r)
-                    if (rg[r + 1].first - rg[r].second < bg) { bg = rg[r + 1].first - rg[r].second; bi = r; }
-                rg[bi].second = rg[bi + 1].second;
-                rg.erase(rg.begin() + bi + 1);
-            }
-            B.n_gate = (int)rg.size();
-            for (size_t r = 0; r < rg.size(); ++r) { B.gate_lo[r] = rg[r].first; B.gate_hi[r] = rg[r].second; }
         }
     }
     uint32_t hs = 1024;
@@ -944,7 +921,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            o_rxa = push_array(blob, atoms), o_wb = push_array(blob, wb), o_fc = push_array(blob, f_count_ge),
            o_sk = push_array(blob, sub_key), o_sb = push_array(blob, sub_begin), o_sc = push_array(blob, sub_cnt),
            o_sp = push_array(blob, sub_pat);
-    size_t f_filt = push_array(blob, FB.filt), f_b2 = push_array(blob, FB.b2), f_l2 = push_array(blob, FB.l2),
+    size_t f_mid = push_array(blob, FB.mid), f_p2 = push_array(blob, FB.p2), f_b2 = push_array(blob, FB.b2), f_l2 = push_array(blob, FB.l2),
            f_t3 = push_array(blob, FB.t3), f_epre = push_array(blob, FB.edge_pre), f_esuf = push_array(blob, FB.edge_suf), f_htk = push_array(blob, FB.ht_key),
            f_htb = push_array(blob, FB.ht_begin), f_htc = push_array(blob, FB.ht_cnt), f_kl = push_array(blob, FB.kl),
            f_ash = push_array(blob, FB.as_head), f_asl = push_array(blob, FB.as_len),
@@ -1004,15 +981,15 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     T.empty_pat = empty_pat;
 
     FastTables &F = h->FT;
-    F.filt = (const uint32_t *)(B + f_filt);
+    F.mid = (const uint2 *)(B + f_mid);
+    F.p2 = (const uint32_t *)(B + f_p2);
     F.b2 = (const uint32_t *)(B + f_b2);
     F.l2 = (const uint32_t *)(B + f_l2);
     F.t3 = (const uint32_t *)(B + f_t3);
     F.edge_pre = (const uint32_t *)(B + f_epre);
     F.edge_suf = (const uint32_t *)(B + f_esuf);
     F.has_t3 = FB.has_t3;
-    for (int r = 0; r < 4; ++r) { F.gate_lo[r] = FB.gate_lo[r]; F.gate_hi[r] = FB.gate_hi[r]; }
-    F.n_gate = FB.n_gate;
+    F.has_short = FB.has_short;
     F.ht_key = (const uint64_t *)(B + f_htk);
     F.ht_begin = (const uint32_t *)(B + f_htb);
     F.ht_cnt = (const uint32_t *)(B + f_htc);

@@ -19,23 +19,29 @@
 // over its field after the decision (rx_positions).
 // Any anchor choice is correct; only the speed depends on the statistics.
 //
-// Filters (all in LDS).  Stage 1, every byte position: 4-byte key -> one bit
-// of a 2^18-bit table, word = hash(b0,b1,b2), bit = mix(b3); a 3-byte anchor
-// fills its whole word.  2-byte anchors: a byte-class gate + an exact 64K-bit
-// bigram table.  Stage 2, compacted survivors only: an independent hash of
-// the 4-byte key (2^17 bits) or of the 3-byte key (2^16 bits) must hit before
-// the global anchor hash table is probed.  Field edges: the first / last four
-// bytes of a field are tested against the prefix / suffix keys of the
-// one-deletion variants (2 x 2^15 bits); only flagged fields run the edge check.
+// Filters (all in LDS).  Stage 1 looks at every EVEN byte position E and
+// decides for the two starts E and E+1 at once: one 64-bit "mid" entry chosen
+// by the three bytes E+1..E+3 holds two 32-bit families, bit fold(b[E]) of
+// the low word for an anchor (>= 4 bytes) starting at E and bit fold(b[E+4])
+// of the high word for one starting at E+1 (an anchor's first four bytes set
+// one bit in each family).  Anchors of 2-3 bytes: their first two bytes in an
+// exact 64K-bit pair table, tested for the pairs (E, E+1) and (E+1, E+2).
+// Stage 2, compacted survivors only: an independent hash of the 4-byte key
+// (2^17 bits), of the 3-byte key (2^14 bits) or of the 2-byte key (2^14 bits)
+// must hit before the global anchor hash table is probed.  Field edges: the
+// first / last four bytes of a field are tested against the prefix / suffix
+// keys of the one-deletion variants (2 x 2^15 bits); only flagged fields run
+// the edge check.
 #pragma once
 #include "kwmatch_device.hpp"
 
 namespace kw {
 
-constexpr int FK_FILT_WORDS = 8192;             // stage 1: 2^18 bits = 32 KB
+constexpr int FK_MID_ENTRIES = 4096;            // stage 1: 4096 x 64 bits = 32 KB
+constexpr int FK_P2_WORDS = 2048;               // stage 1, 2-3 byte anchors: exact pair table, 8 KB
 constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
-constexpr int FK_T3_BITS = 16;                  // stage 2, 3-byte keys: 8 KB
-constexpr int FK_B2_WORDS = 2048;               // exact bigram table: 8 KB
+constexpr int FK_T3_BITS = 14;                  // stage 2, 3-byte keys: 2 KB
+constexpr int FK_B2_BITS = 14;                  // stage 2, 2-byte keys: 2 KB
 constexpr int FK_EDGE_BITS = 20;                // edge prefix / suffix 8-byte keys: 2 x 128 KB (global, L2)
 constexpr int FK_ITEMS0 = 512;                  // items of field 0 (text) on the fast path (power of 2: LDS sort)
 constexpr int FK_ITEMS1 = 64;                   // items of field 1 (title)
@@ -52,6 +58,7 @@ constexpr uint32_t FK_MUL4 = 0x27D4EB2Fu;
 
 constexpr int FK_L2_WORDS = 1 << (FK_L2_BITS - 5);
 constexpr int FK_T3_WORDS = 1 << (FK_T3_BITS - 5);
+constexpr int FK_B2_WORDS = 1 << (FK_B2_BITS - 5);
 constexpr int FK_EDGE_WORDS = 1 << (FK_EDGE_BITS - 5);
 
 // item kinds (2 bits).  3 is FU_RXM in the probe's items (a match of a quantifier-free regex name's program,
@@ -79,14 +86,14 @@ constexpr uint32_t DH_RESOLVE = 1u << 24;       // non-ASCII document left to th
 static_assert(FK_ITEMS0 < 1024 && FK_ITEMS1 < 128, "item counts must fit the document header");
 
 struct FastTables {
-    const uint32_t *filt;       // FK_FILT_WORDS
+    const uint2 *mid;           // FK_MID_ENTRIES: {start at E: bit fk_fold0, start at E+1: bit fk_fold(b[E+4])}
+    const uint32_t *p2;         // FK_P2_WORDS: first two bytes of the 2-3 byte anchors (exact)
     const uint32_t *l2;         // FK_L2_WORDS
     const uint32_t *t3;         // FK_T3_WORDS
     const uint32_t *b2;         // FK_B2_WORDS
     const uint32_t *edge_pre;   // FK_EDGE_WORDS
     const uint32_t *edge_suf;   // FK_EDGE_WORDS
-    uint32_t gate_lo[4], gate_hi[4];   // byte ranges gating the 2-byte path
-    int n_gate;                 // 0 = no 2-byte anchors, -1 = test every position
+    int has_short;              // any 2- or 3-byte anchor
     int has_t3;                 // any 3-byte anchor
     const uint64_t *ht_key;     // (len << 32) | key bytes; ~0 = empty
     const uint32_t *ht_begin;
@@ -193,23 +200,19 @@ struct FastScratch {
 };
 
 // host + device hashes of the LDS tables
-__host__ __device__ __forceinline__ uint32_t fk_word(uint32_t key4)
+// stage-1 mid entry of three bytes (low 24 bits of k3): bits 20..31 of the 24-bit product (the high half of a
+// v_mul_hi would hardly depend on the low byte)
+__host__ __device__ __forceinline__ uint32_t fk_mid_entry(uint32_t k3) { return ((k3 & 0xFFFFFFu) * FK_MUL1) >> 20; }
+// a byte folded to 5 bits: b + (b >> 5) keeps upper and lower case apart
+__host__ __device__ __forceinline__ uint32_t fk_fold(uint32_t b) { return (b + (b >> 5)) & 31u; }
+// the start-at-E family's bit: the device adds the byte and the dword shifted right by 8 * jj + 5, whose low
+// five bits also carry the next byte's bits 0..1 (v_add_u32 with a byte select; v_bfe_u32 reads 5 bits)
+__host__ __device__ __forceinline__ uint32_t fk_fold0(uint32_t b0, uint32_t b1)
 {
-    // bits 19..31 of the product of bytes 0..2 (the high half would hardly depend on byte 0: a v_mul_hi
-    // word hash passed 14x the positions)
-    return ((key4 & 0xFFFFFFu) * FK_MUL1) >> 19;
+    return (b0 + (b0 >> 5) + ((b1 & 3u) << 3)) & 31u;
 }
-__host__ __device__ __forceinline__ uint32_t fk_bit(uint32_t key4)
-{
-    return ((key4 >> 24) + (key4 >> 29)) & 31u;   // byte 3 folded to 5 bits (v_lshr_add_u32)
-}
-// device: the stage-1 word's LDS byte offset (= 4 * fk_word) and a bit offset whose low 5 bits are fk_bit
-// (v_bfe_u32 reads only those)
-__device__ __forceinline__ uint32_t fk_word_byte(uint32_t key4)
-{
-    return (__umul24(key4, FK_MUL1) >> 17) & (4u * FK_FILT_WORDS - 4u);
-}
-__device__ __forceinline__ uint32_t fk_bit_raw(uint32_t key4) { return (key4 >> 24) + (key4 >> 29); }
+// device: the mid entry's LDS byte offset (= 8 * fk_mid_entry)
+__device__ __forceinline__ uint32_t fk_mid_byte(uint32_t k3) { return (__umul24(k3, FK_MUL1) >> 17) & (8u * FK_MID_ENTRIES - 8u); }
 __device__ __forceinline__ uint32_t lds_word_at(const uint32_t *t, uint32_t byte_off)
 {
     return *(const uint32_t *)((const uint8_t *)t + byte_off);
@@ -230,8 +233,9 @@ __host__ __device__ __forceinline__ uint32_t fk_bg_bit(uint32_t a, uint32_t b)
 }
 __host__ __device__ __forceinline__ uint32_t fk_b2_index(uint32_t key2)
 {
-    return ((key2 & 0xFFFFu) * 40503u) & 0xFFFFu;     // bijection on 16 bits (odd multiplier)
+    return ((key2 & 0xFFFFu) * 40503u) & 0xFFFFu;     // bijection on 16 bits (odd multiplier): the exact pair table
 }
+__host__ __device__ __forceinline__ uint32_t fk_b2h_index(uint32_t key2) { return fk_b2_index(key2) >> (16 - FK_B2_BITS); }
 __host__ __device__ __forceinline__ uint32_t fk_ht_slot(uint64_t k, uint32_t mask)
 {
     uint64_t x = k * 0x9E3779B97F4A7C15ull;

@@ -50,13 +50,7 @@
 #define EK_T0(v) const unsigned long long v = EK_TIMING ? __builtin_amdgcn_s_memtime() : 0ull
 #define EK_TACC(acc, v) do { if (EK_TIMING) (acc) += __builtin_amdgcn_s_memtime() - (v); } while (0)
 
-#ifndef FK_SCHED   // 1: pin the stage-1 LDS reads into groups of eight (sched_group_barrier; measured ~1 % faster)
-#define FK_SCHED 1
-#endif
 
-#ifndef FK_GATE_ALL   // 1: look up the bigram table at every position; 0: only behind the byte-class gate
-#define FK_GATE_ALL 1
-#endif
 
 #ifndef FK_EPI_EDGE   // developer aid: 3 = edge windows in the epilogue; 1 = code present, never run; 0 = absent
 #define FK_EPI_EDGE 3
@@ -98,16 +92,6 @@ __device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t *__restrict__
     const uint32_t x1 = *(const uint32_t *)(a + a0 + 4);
     const uint32_t x2 = *(const uint32_t *)(a + a0 + 8);
     return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s) << 32);
-}
-
-// the 4-byte key at position j (0..15) of a lane's 16-byte chunk W[0..4]
-__device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], int j)
-{
-    uint32_t a = W[0], b = W[1];
-    if (j >= 4) { a = W[1]; b = W[2]; }
-    if (j >= 8) { a = W[2]; b = W[3]; }
-    if (j >= 12) { a = W[3]; b = W[4]; }
-    return __builtin_amdgcn_alignbyte(b, a, j & 3);
 }
 
 // a 64-bit value of lane l, l varying per lane

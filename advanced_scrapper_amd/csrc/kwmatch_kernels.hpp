@@ -68,6 +68,21 @@ __device__ __forceinline__ int wave_excl_scan(int v, int *total)
     return x - v;
 }
 
+// the same exclusive scan with DPP row shifts and row broadcasts (no LDS traffic, no bpermute latency chain);
+// total = the wave's sum
+__device__ __forceinline__ int wave_excl_scan_dpp(int v, int *total)
+{
+    int x = v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    *total = __builtin_amdgcn_readlane(x, WAVE - 1);
+    return x - v;
+}
+
 __device__ __forceinline__ int wave_sum(int v)
 {
 #pragma unroll

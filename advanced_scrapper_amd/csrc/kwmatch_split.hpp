@@ -60,13 +60,15 @@ constexpr int EK_BLOCK = EK_WAVES * WAVE;
 constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range; 5 bits of a candidate)
 
 struct __attribute__((aligned(16))) FilterLds {
-    uint32_t filt[FK_FILT_WORDS];
+    uint2 mid[FK_MID_ENTRIES];
+    uint32_t p2[FK_P2_WORDS];
     uint32_t l2[FK_L2_WORDS];
     uint32_t t3[FK_T3_WORDS];
     uint32_t b2[FK_B2_WORDS];
+    uint32_t tile[FS_WAVES][4 * WAVE + 4];    // the tile's bytes (+ the word after it) for stage 2's keys
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
-    uint2 stg[FS_WAVES][WAVE];                // stage-2 positions of one round (key, lane << 4 | j | flags)
+    uint32_t stg[FS_WAVES][WAVE];             // stage-2 starts of one round (lane << 4 | j | flags)
 };
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
@@ -81,24 +83,72 @@ __device__ __forceinline__ uint32_t fg_doc(const uint32_t *dstart, uint32_t nd, 
     return lo;
 }
 
-// bigram-table bit index: the low 16 bits of a 24-bit product equal fk_b2_index's (key2 * 40503) & 0xFFFF
-__device__ __forceinline__ uint32_t fk_b2_mul(uint32_t key) { return __umul24(key, 40503u); }
+// pair-table bit index: the low 16 bits of a 24-bit product equal fk_b2_index's (key2 * 40503) & 0xFFFF.  As
+// inline asm: left to itself the compiler sees that only the low 16 bits are used and emits a quarter-rate
+// v_mul_lo_u32 (twice: once for the word, once for the bit)
+__device__ __forceinline__ uint32_t fk_b2_mul(uint32_t key)
+{
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(40503u), "v"(key));
+    return r;
+}
+
+// Stage 1 of one lane's 16 bytes W[0..3] (+ W[4], the next lane's first word): bit j of `hit` = an anchor of
+// >= 4 bytes may start at position j, bit j of `gate` = a 2-3 byte anchor may (its first two bytes are an
+// exact pair).  Only even positions E are looked up; each decides the starts E and E + 1.
+template <bool SHORT>
+__device__ __forceinline__ void fk_stage1(const FilterLds &L, const uint32_t (&W)[5], uint32_t &hit, uint32_t &gate)
+{
+    uint2 mw[8];
+    uint32_t pw[16], pm[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int j = 2 * e, q = j >> 2, jj = j & 3;
+        const uint32_t km = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj + 1);   // bytes j+1 .. j+4
+        mw[e] = *(const uint2 *)((const uint8_t *)L.mid + fk_mid_byte(km));
+        if (SHORT) {
+            const uint32_t k0 = jj ? (W[q] >> 16) : W[q];                           // bytes j, j+1
+            pm[2 * e] = fk_b2_mul(k0);
+            pm[2 * e + 1] = fk_b2_mul(km);
+            pw[2 * e] = lds_word_at(L.p2, (pm[2 * e] >> 3) & (4u * FK_P2_WORDS - 4u));
+            pw[2 * e + 1] = lds_word_at(L.p2, (pm[2 * e + 1] >> 3) & (4u * FK_P2_WORDS - 4u));
+        }
+    }
+    uint32_t h = 0, g = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int j = 2 * e, q = j >> 2, jj = j & 3;
+        const uint32_t km = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj + 1);
+        const uint32_t o0 = __builtin_amdgcn_ubfe(W[q], 8 * jj, 8) + (W[q] >> (8 * jj + 5));   // fk_fold0
+        const uint32_t o1 = (km >> 24) + (km >> 29);                                           // fk_fold(b[j+4])
+        h |= __builtin_amdgcn_ubfe(mw[e].x, o0, 1) << j;
+        h |= __builtin_amdgcn_ubfe(mw[e].y, o1, 1) << (j + 1);
+        if (SHORT) {
+            g |= __builtin_amdgcn_ubfe(pw[2 * e], pm[2 * e], 1) << j;
+            g |= __builtin_amdgcn_ubfe(pw[2 * e + 1], pm[2 * e + 1], 1) << (j + 1);
+        }
+    }
+    hit = h;
+    gate = g;
+}
 
 // ---------------------------------------------------------------- kernel 1: the filters
 // A wave takes groups of FG_DOCS consecutive documents and streams each group's bytes as one flat range
-// (1 KiB tiles, 16 bytes per lane, the next tile's loads in flight): no per-document tile shapes or
+// (1 KiB tiles, 16 bytes per lane, the next tiles' loads in flight): no per-document tile shapes or
 // set-up.  Keys that run over a field or document end are kept (a superset): the probe checks every
 // anchor against its field.  Non-ASCII bytes mark their field in dflags (rare: an LDS lookup of the
 // document, one atomic per field).
+template <bool SHORT>
 __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds &L, const uint8_t *__restrict__ arena,
                                                  const int64_t *__restrict__ off, int64_t n_docs, const FastScratch &S,
                                                  int64_t wave, int64_t n_waves, int wib, uint32_t &ncand, uint32_t &ncand2,
                                                  uint32_t &ccur)
 {
     const int lane = lane_id();
-    const uint32_t *filt = L.filt, *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
+    const uint32_t *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
-    uint2 *stg = L.stg[wib];
+    uint32_t *stg = L.stg[wib];
+    uint32_t *tbuf = L.tile[wib];
     uint32_t *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const bool has_t3 = FT.has_t3 != 0;
@@ -158,44 +208,28 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 while (hb) {   // one atomic per (document, field) the lane's non-ASCII bytes fall in
                     const uint32_t r = rel + (uint32_t)(__ffs(hb) - 1);
                     const uint32_t k = fg_doc(dstart, (uint32_t)nd, r);
-                    const uint32_t tb = dtitle[k];
-                    const bool title = r >= tb;
+                    const uint32_t tb2 = dtitle[k];
+                    const bool title = r >= tb2;
                     atomicOr(&S.dflags[d0 + k], title ? DH_NA1 : DH_NA0);
-                    const uint32_t fend = title ? dstart[k + 1] : tb;   // group-relative end of that field
+                    const uint32_t fend = title ? dstart[k + 1] : tb2;   // group-relative end of that field
                     const int64_t skip = (int64_t)fend - (lp - gb);
                     hb &= skip >= 16 ? 0u : ~((1u << (uint32_t)skip) - 1u);
                 }
             }
-            uint32_t hit = 0, gate = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t fw[4], bw[4], bm[4];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
-                    fw[jj] = lds_word_at(filt, fk_word_byte(key));
-                    bm[jj] = fk_b2_mul(key);
-                    bw[jj] = lds_word_at(b2, (bm[jj] >> 3) & (4u * FK_B2_WORDS - 4u));   // word (bm >> 5), as bytes
-                }
-                if (FK_SCHED) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int j = 4 * q + jj;
-                    const uint32_t key = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj);
-                    hit |= __builtin_amdgcn_ubfe(fw[jj], fk_bit_raw(key), 1) << j;
-                    gate |= __builtin_amdgcn_ubfe(bw[jj], bm[jj], 1) << j;
-                }
-            }
+            uint32_t hit, gate;
+            fk_stage1<SHORT>(L, W, hit, gate);
             hit &= valid;
             gate &= valid;
             ncand += (uint32_t)__popc(hit);
-            // stage 2 over the wave: the tile's stage-1 and bigram-gate positions compacted into 64-entry
-            // rounds (lane = position; usually one round), both LDS lookups at once, then the survivors
-            // ("candidates") ranked by ballot and written with their document
+            // stage 2 over the wave: the tile's stage-1 starts compacted into 64-entry rounds (lane = start;
+            // usually one round), their keys read back from the tile staged in LDS, the stage-2 lookups,
+            // then the survivors ("candidates") ranked by ballot and written with their document
             const uint32_t sm = hit | gate;
             int ts;
-            const int sx = wave_excl_scan(__popc(sm), &ts);
+            const int sx = wave_excl_scan_dpp(__popc(sm), &ts);
             if (ts == 0) return;
+            *(uint4 *)(tbuf + 4 * lane) = v;
+            if (lane == WAVE - 1) tbuf[4 * WAVE] = w4;
             {
                 const int64_t r0 = tb - gb;
                 const uint32_t rt = r0 > 0 ? (uint32_t)r0 : 0u;
@@ -212,24 +246,27 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                         hm &= hm - 1;
                         if (rk >= c0 + WAVE) break;
                         if (rk >= c0)
-                            stg[rk - c0] = make_uint2(fk_key_at(W, j), ((uint32_t)lane << 4) | (uint32_t)j |
-                                                                    (((hit >> j) & 1u) << 10) | (((gate >> j) & 1u) << 11));
+                            stg[rk - c0] = ((uint32_t)lane << 4) | (uint32_t)j | (((hit >> j) & 1u) << 10) |
+                                           (((gate >> j) & 1u) << 11);
                         ++rk;
                     }
                 }
                 wave_sync();
                 const bool act = c0 + lane < ts;
-                const uint2 e = act ? stg[lane] : make_uint2(0u, 0u);
+                const uint32_t e = act ? stg[lane] : 0u;
+                const uint32_t ob = e & 1023u;   // byte of the start in the staged tile
+                const uint32_t key = __builtin_amdgcn_alignbyte(tbuf[(ob >> 2) + 1], tbuf[ob >> 2], ob & 3u);
                 wave_sync();
-                const bool h1 = (e.y >> 10) & 1u;
-                const uint32_t b4 = lds_bit(l2, fk_l2_index(e.x)) ? 1u : 0u;
-                const uint32_t b3 = (has_t3 && lds_bit(t3, fk_t3_index(e.x))) ? 2u : 0u;
-                const uint32_t fl = (h1 ? (b4 | b3) : 0u) | (((e.y >> 11) & 1u) << 2);
+                const bool h1 = (e >> 10) & 1u, g1 = (e >> 11) & 1u;
+                const uint32_t b4 = (h1 && lds_bit(l2, fk_l2_index(key))) ? 1u : 0u;
+                const uint32_t b3 = (g1 && has_t3 && lds_bit(t3, fk_t3_index(key))) ? 2u : 0u;
+                const uint32_t bb = (g1 && lds_bit(b2, fk_b2h_index(key))) ? 4u : 0u;
+                const uint32_t fl = b4 | b3 | bb;
                 const bool pass = act && fl != 0u;
                 uint32_t k = kdoc, pd = 0;
                 bool keep = pass;
                 if (pass) {
-                    const uint32_t r = rtile + 16u * ((e.y >> 4) & 63u) + (e.y & 15u);
+                    const uint32_t r = rtile + ob;
                     while (dstart[k + 1] <= r) ++k;
                     pd = r - dstart[k];
                     keep = pd < (1u << 24);   // (a longer document has a field over 8 MiB: the generic kernel's)
@@ -277,7 +314,12 @@ __global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables
                                                              FastScratch S)
 {
     __shared__ FilterLds L;
-    for (int i = threadIdx.x; i < FK_FILT_WORDS; i += FS_BLOCK) L.filt[i] = FT.filt[i];
+    {
+        const uint4 *src = (const uint4 *)FT.mid;
+        uint4 *dst = (uint4 *)L.mid;
+        for (int i = threadIdx.x; i < FK_MID_ENTRIES / 2; i += FS_BLOCK) dst[i] = src[i];
+    }
+    for (int i = threadIdx.x; i < FK_P2_WORDS; i += FS_BLOCK) L.p2[i] = FT.p2[i];
     for (int i = threadIdx.x; i < FK_L2_WORDS; i += FS_BLOCK) L.l2[i] = FT.l2[i];
     for (int i = threadIdx.x; i < FK_T3_WORDS; i += FS_BLOCK) L.t3[i] = FT.t3[i];
     for (int i = threadIdx.x; i < FK_B2_WORDS; i += FS_BLOCK) L.b2[i] = FT.b2[i];
@@ -287,7 +329,10 @@ __global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables
     const int64_t wave = (int64_t)blockIdx.x * FS_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * FS_WAVES;
     uint32_t ncand = 0, ncand2 = 0, ccur = 0;
-    fk_filter_groups(FT, L, arena, off, n_docs, S, wave, n_waves, wib, ncand, ncand2, ccur);
+    if (FT.has_short)
+        fk_filter_groups<true>(FT, L, arena, off, n_docs, S, wave, n_waves, wib, ncand, ncand2, ccur);
+    else
+        fk_filter_groups<false>(FT, L, arena, off, n_docs, S, wave, n_waves, wib, ncand, ncand2, ccur);
     if (lane == 0) {
         S.ccnt[wave] = ccur;
         if (ccur > S.cand_cap) {

@@ -190,6 +190,23 @@ int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, void *stream
 int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root, kw_hit *d_out,
                       int64_t cap, int64_t *n_total, int64_t *counts, void *stream);
 
+/* The exchange plan kw_allgather_hits runs, as a pure host function (no GPU,
+ * no RCCL; tests check it against a gloo execution): given every rank's
+ * record count counts[nranks] and the root (< 0: all ranks receive), rank
+ * `rank`'s part of the plan:
+ *   recv_off[nranks + 1]  where each rank's records land in a receiver's
+ *                         output (the prefix sums: rank order = document order)
+ *   ops[nranks]           per peer p: KW_PLAN_SEND (this rank sends its records
+ *                         to p), KW_PLAN_RECV (it receives cnt[p] records of p
+ *                         at recv_off[p]); 0 for itself and idle pairs
+ *   *n_total              all records; *n_recv: records this rank ends with
+ *                         (n_total on a receiver, else 0)
+ * Returns KW_EINVAL on bad arguments (rank/root out of range, a negative count). */
+#define KW_PLAN_SEND 1
+#define KW_PLAN_RECV 2
+int kw_exchange_plan(int32_t nranks, int32_t rank, int32_t root, const int64_t *counts, int64_t *recv_off,
+                     int32_t *ops, int64_t *n_total, int64_t *n_recv);
+
 const char *kw_comm_last_error(kw_comm *c);
 int kw_comm_destroy(kw_comm *c);
 

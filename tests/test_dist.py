@@ -189,3 +189,77 @@ def test_main_single_rank_equals_reference_outputs(tmp_path, monkeypatch):
     assert sorted(os.listdir(out)) == sorted(want)
     for fn in want:
         assert (out / fn).read_bytes() == want[fn], fn
+
+
+def _plan_worker(rank, world, port, q):
+    """Execute libkwmatch's exchange plan (kw_exchange_plan, the send/recv pairs kw_allgather_hits issues
+    over RCCL) with gloo point-to-point calls, for every root, and report what each rank received."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from advanced_scrapper_amd import _native
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    out = {}
+    for trial in range(3):
+        counts = [((r * 7 + trial * 3) % 5) * (r + 1) for r in range(world)]     # ragged, some ranks empty
+        mine = torch.tensor([[trial, r, k, world] for r in [rank] for k in range(counts[rank])],
+                            dtype=torch.int32).reshape(-1, 4)
+        for root in (-1, 0, world - 1, world // 2):
+            off, ops, total, nrecv = _native.exchange_plan(world, rank, root, counts)
+            recv = torch.full((nrecv, 4), -1, dtype=torch.int32)
+            if nrecv:
+                recv[off[rank]:off[rank + 1]] = mine
+            reqs = []
+            for p in range(world):
+                if ops[p] & _native.KW_PLAN_SEND:
+                    reqs.append(dist.isend(mine.contiguous(), p, tag=trial * 100 + root + 10))
+                if ops[p] & _native.KW_PLAN_RECV:
+                    buf = torch.empty((counts[p], 4), dtype=torch.int32)
+                    reqs.append((dist.irecv(buf, p, tag=trial * 100 + root + 10), buf, p))
+            for r in reqs:
+                if isinstance(r, tuple):
+                    r[0].wait()
+                    recv[off[r[2]]:off[r[2] + 1]] = r[1]
+                else:
+                    r.wait()
+            out[(trial, root)] = (total, recv.numpy().tolist())
+            dist.barrier()
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exchange_plan_gloo_matches_concatenation():
+    """kw_exchange_plan, run with gloo send/recv for world sizes 2-8 and roots -1 (all), 0, the last and a
+    middle rank: every receiver ends with every rank's records in rank order, non-receivers with nothing,
+    and no send lacks its receive (a mismatch would hang and fail the timeout)."""
+    for world in (2, 3, 5, 8):
+        ctx = mp.get_context('spawn')
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_plan_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = dict(q.get(timeout=300) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        for trial in range(3):
+            counts = [((r * 7 + trial * 3) % 5) * (r + 1) for r in range(world)]
+            want = [[trial, r, k, world] for r in range(world) for k in range(counts[r])]
+            for root in (-1, 0, world - 1, world // 2):
+                for rank in range(world):
+                    total, got = res[rank][(trial, root)]
+                    assert total == len(want)
+                    if root < 0 or root == rank:
+                        assert got == want, (world, trial, root, rank)
+                    else:
+                        assert got == [], (world, trial, root, rank)
+
+
+def test_exchange_plan_rejects_bad_arguments():
+    import pytest
+    from advanced_scrapper_amd import _native
+    for args in ((0, 0, -1, [1]), (2, 2, -1, [1, 1]), (2, 0, 2, [1, 1]), (2, 0, -1, [1, -1])):
+        with pytest.raises(_native.KwError):
+            _native.exchange_plan(*args)

@@ -160,3 +160,38 @@ def test_sharded_scans_equal_one_shot(bench_scan):
             assert bench.hits_digest(torch.cat(parts)) == digest, world
     finally:
         comm.close()
+
+
+def test_c2_slice_drop_in_csv_bytes_equal_reference(tmp_path, monkeypatch, golden):
+    """The drop-in's main path (native CSV ingest, GPU matching, egress, the final sort) over the first 20 000
+    documents of the config-2 corpus as one reference chunk writes per-ticker files whose bytes equal those
+    the REFERENCE's own process_chunk + sort_matched_csv wrote in the build container
+    (tests/golden/make_c2_slice.py -> c2_slice.json: sha256 and size of every file)."""
+    import hashlib
+    import json
+    import os
+    import time
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import match_keywords as mk
+    from tests.golden.make_c2_slice import slice_csv_bytes
+    from tests.golden_data import HERE
+    meta = json.load(open(os.path.join(HERE, 'c2_slice.json')))
+    data = slice_csv_bytes(meta['rows'])
+    assert hashlib.sha256(data).hexdigest() == meta['csv_sha256'], 'the generator no longer makes the pinned CSV'
+    (tmp_path / 'articles.csv').write_bytes(data)
+    monkeypatch.setenv('TZ', 'UTC')
+    time.tzset()
+    monkeypatch.chdir(tmp_path)
+    processed = golden.kb_processed()
+    monkeypatch.setattr(mk, 'read_and_process_json_files', lambda _d: processed)
+    args = mk._parse(['--info-dir', 'unused', '--articles', str(tmp_path / 'articles.csv'),
+                      '--chunksize', str(meta['chunksize'])])
+    assert mk.run(args, 0, 1, None, None) == 0
+    out = tmp_path / 'yahoo_ticker_matched_articles'
+    got = {fn: (out / fn).read_bytes() for fn in os.listdir(out)}
+    assert sorted(got) == sorted(meta['files'])
+    bad = [fn for fn, w in meta['files'].items()
+           if len(got[fn]) != w['bytes'] or hashlib.sha256(got[fn]).hexdigest() != w['sha256']]
+    assert not bad, f'{len(bad)} of {len(got)} files differ from the reference: {bad[:10]}'
