@@ -199,3 +199,54 @@ int64_t kwcsv_pack(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, 
     }
     return a;
 }
+
+/*
+ * Record boundaries only (the --gpus N ingest: every rank finds a chunk's records, then tokenizes just its
+ * own byte-balanced share with kwcsv_parse).  The same record split as kwcsv_parse: blank lines skipped,
+ * '"' quoting with doubled quotes, "\n" / "\r\n" / "\r" ends.  starts[r] = the first byte of record r
+ * (r < rows), starts[rows] = the position after the last record (= kwcsv_parse's *pos_out).  Returns the
+ * records found (at most max_rows; 0 at the end of the input), -2 for a record kwcsv_parse would not
+ * reproduce (a character after a closing quote, an unterminated quote), -3 for a field count other than
+ * ncols.
+ */
+int64_t kwcsv_records(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_rows, int32_t ncols, int64_t *starts)
+{
+    int64_t p = pos, rows = 0;
+    while (rows < max_rows) {
+        for (;;) {
+            int64_t k = p;
+            while (k < len && (buf[k] == ' ' || buf[k] == '\t')) ++k;
+            if (k < len && (buf[k] == '\n' || buf[k] == '\r')) { p = k + 1; continue; }
+            if (k >= len) p = k;
+            break;
+        }
+        if (p >= len) break;
+        starts[rows] = p;
+        int32_t f = 0;
+        for (;;) {
+            if (p < len && buf[p] == '"') {
+                ++p;
+                for (;;) {
+                    const uint8_t *q = p < len ? (const uint8_t *)memchr(buf + p, '"', (size_t)(len - p)) : NULL;
+                    if (!q) return -2;
+                    p = (int64_t)(q - buf) + 1;
+                    if (p < len && buf[p] == '"') { ++p; continue; }
+                    break;
+                }
+                if (p < len && buf[p] != ',' && buf[p] != '\n' && buf[p] != '\r') return -2;
+            } else {
+                while (p < len && buf[p] != ',' && buf[p] != '\n' && buf[p] != '\r') ++p;
+            }
+            if (f >= ncols) return -3;
+            ++f;
+            if (p < len && buf[p] == ',') { ++p; continue; }
+            if (p < len && buf[p] == '\r') ++p;
+            if (p < len && buf[p] == '\n' && buf[p - 1] != '\n') ++p;
+            break;
+        }
+        if (f != ncols) return -3;
+        ++rows;
+    }
+    starts[rows] = p;
+    return rows;
+}

@@ -87,6 +87,9 @@ class KwComm:
         return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, 'cuda_stream') else (stream or 0))
 
     def allgather_counts(self, count: int, stream=None) -> List[int]:
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self.device)
         out = np.zeros(self.world, dtype=np.int64)
         self._n.check_comm(self._n.lib().kw_allgather_counts(self.h, int(count), self._n.ptr(out), self._sp(stream)),
                            self.h)
@@ -95,9 +98,12 @@ class KwComm:
     def gather_hits(self, hits, doc_base: int, root: int = -1, stream=None):
         """Exchange [n, 4] int32 device records (doc ids local to the rank's shard).  Returns
         (records of every rank in document order with global doc ids -- on receiving ranks, else
-        None -- and the per-rank counts).  Asynchronous on ``stream`` after the counts exchange."""
+        None -- and the per-rank counts).  Asynchronous on ``stream`` after the counts exchange; the
+        default is torch's current stream of the device, the stream the records were produced on."""
         import ctypes
         import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
         n = int(hits.shape[0])
         counts = self.allgather_counts(n, stream)
         total = sum(counts)
@@ -122,7 +128,30 @@ class Exchange:
 
     def __init__(self, rank: int, world: int, device, backend: str):
         self.rank, self.world, self.backend = rank, world, backend
+        self.device = device
         self.comm = KwComm(rank, world, device) if backend == 'nccl' and world > 1 else None
+
+    def _dev(self):
+        import torch
+        return torch.device('cuda', self.device if self.device is not None else torch.cuda.current_device()) \
+            if self.backend == 'nccl' else torch.device('cpu')
+
+    def allreduce_min(self, values) -> np.ndarray:
+        """Element-wise MIN of a small int64 vector over the ranks (the sharded reader's chunk decisions,
+        the first failing row of a chunk)."""
+        import torch
+        import torch.distributed as td
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        if self.world == 1:
+            return v.copy()
+        t = torch.from_numpy(v.copy()).to(self._dev())
+        td.all_reduce(t, op=td.ReduceOp.MIN)
+        return t.cpu().numpy()
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as td
+            td.barrier()
 
     def gather(self, hits, doc_base: int):
         """Records of every rank with batch-global doc ids, in document order, on rank 0 (None elsewhere)."""

@@ -42,6 +42,8 @@ def _lib():
         L.kwcsv_pack.argtypes = [P, P, P, i64, i32, i32, i32, P, i64, P]
         L.kwcsv_utf8_ok.restype = i32
         L.kwcsv_utf8_ok.argtypes = [P, P, P, i64, i32, i32]
+        L.kwcsv_records.restype = i64
+        L.kwcsv_records.argtypes = [P, i64, i64, i64, i32, P]
         _LIB = L
     return _LIB
 
@@ -128,12 +130,9 @@ class NativeChunk:
 
 def _split_header(buf: bytes):
     """Header fields and the byte position after the header record (simple unquoted or quoted names)."""
-    end = len(buf)
-    for i, ch in enumerate(buf):
-        if ch in (10, 13):
-            end = i
-            break
-    head = buf[:end].decode('utf-8')
+    ends = [k for k in (buf.find(b'\n'), buf.find(b'\r')) if k >= 0]
+    end = min(ends) if ends else len(buf)
+    head = bytes(buf[:end]).decode('utf-8')
     pos = end
     if buf[pos:pos + 2] == b'\r\n':
         pos += 2
@@ -144,62 +143,171 @@ def _split_header(buf: bytes):
     return names, head, pos
 
 
+def _map(path: str):
+    """The file's bytes, memory-mapped read-only (ranks of one node share the page cache; nothing is copied)."""
+    import mmap
+    with open(path, 'rb') as fh:
+        if os.fstat(fh.fileno()).st_size == 0:
+            return b''
+        return mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+
+
 def read_chunks(path: str, chunksize: int) -> Iterator[Union[NativeChunk, pd.DataFrame]]:
     """Chunks of the article CSV: :class:`NativeChunk` where the fast path equals pandas, else the
     ``DataFrame`` pandas parses from the same rows (see the module doc)."""
-    with open(path, 'rb') as fh:
-        data = fh.read()
-    yield from read_chunks_bytes(data, chunksize)
+    yield from read_chunks_bytes(_map(path), chunksize, path)
 
 
-def read_chunks_bytes(data: bytes, chunksize: int) -> Iterator[Union[NativeChunk, pd.DataFrame]]:
+def _pandas_rows(data, pos: int, end: int, index0: int) -> pd.DataFrame:
+    """pandas on exactly the records in data[pos:end) (dtype inference is per chunk): the header + these bytes."""
+    frame = pd.read_csv(io.BytesIO(bytes(data[:_header_end(data)]) + bytes(data[pos:end])))
+    frame.index = pd.RangeIndex(index0, index0 + len(frame))
+    return frame
+
+
+def _pandas_rest(data, pos: int, chunksize: int, index0: int):
+    """A record the tokenizer does not reproduce: pandas takes the rest of the file, chunk by chunk."""
+    tail = bytes(data[:_header_end(data)]) + bytes(data[pos:])
+    for frame in pd.read_csv(io.BytesIO(tail), chunksize=chunksize):
+        frame.index = pd.RangeIndex(index0, index0 + len(frame))
+        index0 += len(frame)
+        yield frame
+
+
+def _header_ok(names) -> bool:
+    return len(names) > 0 and len(set(names)) == len(names) and all(n in names for n in NEEDED)
+
+
+def _tokenize(data, buf: np.ndarray, pos: int, end: int, rows: int, ncols: int):
+    """kwcsv_parse of exactly `rows` records in buf[pos:end) -> (Cells, position after them) or None."""
+    na_buf, na_off, n_na = _na_table()
+    out = np.empty(end - pos + 16, dtype=np.uint8)     # a record's cells take at most its bytes
+    coff = np.empty(rows * ncols + 1, dtype=np.int64)
+    cfl = np.empty(max(rows * ncols, 1), dtype=np.uint8)
+    newpos = ctypes.c_int64(pos)
+    got = _lib().kwcsv_parse(_p(buf), len(buf), pos, rows, ncols, _p(na_buf), _p(na_off), n_na, _p(out),
+                             len(out), _p(coff), _p(cfl), ctypes.byref(newpos), None)
+    if got != rows:
+        return None
+    return Cells(out, coff[:rows * ncols + 1], cfl[:rows * ncols], int(rows), ncols), newpos.value
+
+
+def _native_flags(cells: Cells, need_idx) -> np.ndarray:
+    """Per needed column: [no text witness among these rows, invalid UTF-8 among them] (0 / 1)."""
+    L = _lib()
+    n, nc = cells.nrows, cells.ncols
+    fl = cells.flags.reshape(n, nc) if n else np.zeros((0, nc), np.uint8)
+    out = np.zeros(2 * len(need_idx), dtype=np.int64)
+    for k, c in enumerate(need_idx):
+        out[2 * k] = 0 if (n and (fl[:, c] & TEXT).any()) else 1
+        out[2 * k + 1] = 0 if L.kwcsv_utf8_ok(_p(cells.buf), _p(cells.off), _p(cells.flags), n, nc, c) else 1
+    return out
+
+
+def read_chunks_bytes(data, chunksize: int, path: Optional[str] = None) -> Iterator[Union[NativeChunk, pd.DataFrame]]:
     names, head, pos = _split_header(data)
     ncols = len(names)
-    if ncols == 0 or len(set(names)) != ncols or any(n not in names for n in NEEDED):
-        yield from pd.read_csv(io.BytesIO(data), chunksize=chunksize)
+    if not _header_ok(names):
+        yield from pd.read_csv(io.BytesIO(bytes(data)) if path is None else path, chunksize=chunksize)
         return
     need_idx = [names.index(n) for n in NEEDED]
-    na_buf, na_off, n_na = _na_table()
     buf = np.frombuffer(data, dtype=np.uint8)
     L = _lib()
     index0 = 0
-    rest_pandas = False
-    while pos < len(data) and not rest_pandas:
-        # a chunk's cells take at most its bytes
-        cap = min(len(data) - pos, 1 << 62) + 16
-        out = np.empty(cap, dtype=np.uint8)
-        coff = np.empty(chunksize * ncols + 1, dtype=np.int64)
-        cfl = np.empty(chunksize * ncols, dtype=np.uint8)
-        newpos = ctypes.c_int64(pos)
-        # bound the scan: at most the bytes of chunksize records (unknown), so parse all that remains
-        rows = L.kwcsv_parse(_p(buf), len(data), pos, chunksize, ncols, _p(na_buf), _p(na_off), n_na, _p(out), cap,
-                             _p(coff), _p(cfl), ctypes.byref(newpos), None)
+    starts = np.empty(chunksize + 1, dtype=np.int64)
+    while pos < len(data):
+        rows = L.kwcsv_records(_p(buf), len(buf), pos, chunksize, ncols, _p(starts))
         if rows == 0:
             break
         if rows < 0:
-            rest_pandas = True
-            break
-        flags = cfl[:rows * ncols].reshape(rows, ncols)
-        ok = all(bool((flags[:, c] & TEXT).any()) for c in need_idx)
-        cells = Cells(out, coff[:rows * ncols + 1], cfl[:rows * ncols], int(rows), ncols)
-        if ok:
-            ok = all(L.kwcsv_utf8_ok(_p(out), _p(coff), _p(cfl), rows, ncols, c) for c in need_idx)
-        if ok:
+            yield from _pandas_rest(data, pos, chunksize, index0)
+            return
+        end = int(starts[rows])
+        tok = _tokenize(data, buf, pos, end, int(rows), ncols)
+        if tok is None:
+            yield from _pandas_rest(data, pos, chunksize, index0)
+            return
+        cells, newpos = tok
+        if not _native_flags(cells, need_idx).any():
             yield NativeChunk(cells, names, index0)
         else:
-            # pandas on exactly these rows (dtype inference is per chunk): the header + this chunk's bytes
-            frame = pd.read_csv(io.BytesIO(data[:_header_end(data)] + data[pos:newpos.value]))
-            frame.index = pd.RangeIndex(index0, index0 + len(frame))
-            yield frame
+            yield _pandas_rows(data, pos, newpos, index0)
         index0 += int(rows)
-        pos = newpos.value
-    if rest_pandas:
-        # a record the tokenizer does not reproduce: pandas takes the rest of the file, chunk by chunk
-        tail = data[:_header_end(data)] + data[pos:]
-        for frame in pd.read_csv(io.BytesIO(tail), chunksize=chunksize):
-            frame.index = pd.RangeIndex(index0, index0 + len(frame))
-            index0 += len(frame)
-            yield frame
+        pos = newpos
+
+
+class ShardChunk(NativeChunk):
+    """This rank's byte-balanced share [lo, hi) of one chunk's rows (``--gpus N``): its cells only; the chunk
+    has ``chunk_rows`` rows starting at file row ``chunk_index0``."""
+
+    def __init__(self, cells: Cells, columns, chunk_index0: int, lo: int, hi: int, chunk_rows: int):
+        super().__init__(cells, columns, chunk_index0 + lo)
+        self.chunk_index0, self.lo, self.hi, self.chunk_rows = chunk_index0, lo, hi, chunk_rows
+
+
+def balanced_cuts(starts: np.ndarray, world: int):
+    """Contiguous row ranges of ~equal record bytes (starts = rows + 1 record start offsets)."""
+    n = len(starts) - 1
+    total = float(starts[-1] - starts[0])
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(starts[1:], starts[0] + total * r / world, side='left')) + 1)
+    cuts.append(n)
+    cuts = [min(max(c, 0), n) for c in cuts]
+    for i in range(1, len(cuts)):
+        cuts[i] = max(cuts[i], cuts[i - 1])
+    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+
+
+def read_chunks_sharded(path: str, chunksize: int, rank: int, world: int, allreduce_min
+                        ) -> Iterator[Union[ShardChunk, pd.DataFrame]]:
+    """The ``--gpus N`` reader: every rank memory-maps the file and finds each chunk's record boundaries
+    (kwcsv_records, no cell copies), then tokenizes only its own byte-balanced share of the chunk's
+    records.  Whether the chunk equals pandas' (a text witness in each needed column, valid UTF-8) is
+    decided over the whole chunk by ``allreduce_min`` (an element-wise MIN of small int64 vectors over the
+    ranks).  Every rank gets the same sequence: a :class:`ShardChunk` (its rows) per native chunk, the
+    whole chunk as pandas' DataFrame otherwise."""
+    data = _map(path)
+    names, head, pos = _split_header(data)
+    ncols = len(names)
+    if not _header_ok(names):
+        yield from pd.read_csv(path, chunksize=chunksize)
+        return
+    need_idx = [names.index(n) for n in NEEDED]
+    buf = np.frombuffer(data, dtype=np.uint8)
+    L = _lib()
+    index0 = 0
+    starts = np.empty(chunksize + 1, dtype=np.int64)
+    while pos < len(data):
+        rows = L.kwcsv_records(_p(buf), len(buf), pos, chunksize, ncols, _p(starts))
+        if rows == 0:
+            break
+        if rows < 0:
+            yield from _pandas_rest(data, pos, chunksize, index0)
+            return
+        rows = int(rows)
+        end = int(starts[rows])
+        lo, hi = balanced_cuts(starts[:rows + 1], world)[rank]
+        if hi > lo:
+            tok = _tokenize(data, buf, int(starts[lo]), int(starts[hi]), hi - lo, ncols)
+        else:   # no rows on this rank: nothing to witness, nothing invalid
+            tok = (Cells(np.zeros(16, np.uint8), np.zeros(1, np.int64), np.zeros(1, np.uint8), 0, ncols), end)
+        local = np.zeros(2 * len(need_idx) + 1, dtype=np.int64)
+        if tok is None:
+            local[-1] = 1
+        else:
+            local[:-1] = _native_flags(tok[0], need_idx)
+        # witness: some rank has one (MIN of "no witness" = 0); UTF-8 and tokenizing: every rank is fine
+        # (MIN of the negated flags, i.e. MAX of the failures, through -x)
+        red = allreduce_min(np.concatenate([local[0:-1:2], -local[1:-1:2], -local[-1:]]))
+        k = len(need_idx)
+        native = not red[:k].any() and not (red[k:] < 0).any()
+        if native:
+            yield ShardChunk(tok[0], names, index0, lo, hi, rows)
+        else:
+            yield _pandas_rows(data, pos, end, index0)
+        index0 += rows
+        pos = end
 
 
 def _header_end(data: bytes) -> int:

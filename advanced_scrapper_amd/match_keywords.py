@@ -32,7 +32,7 @@ import pandas as pd
 from dateutil import parser
 
 from . import egress, ingest
-from .ingest import NativeChunk
+from .ingest import NativeChunk, ShardChunk
 from .dates import parse_date
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
@@ -79,7 +79,7 @@ def _chunk_rows(chunk, results, dates):
     """Output rows of a matched chunk grouped by ticker, from ``ticker_matches`` dicts (see :func:`_cell_rows`)."""
     cells = [(i, t, json.dumps(m['text']), json.dumps(m['title'])) for i, tm in enumerate(results)
              for t, m in tm.items()]
-    return _cell_rows(chunk, cells, dates)
+    return _cell_rows(chunk, cells, dates)[:2]
 
 
 def _cell_rows(chunk, cells, dates):
@@ -94,10 +94,11 @@ def _cell_rows(chunk, cells, dates):
     own call runs).  A chunk without an object column (``iloc`` would upcast its ints to floats) takes the
     ``iloc`` path.  When a row's ``time_unix`` raises (the reference raises in that article's first
     ``append_to_csv``, :131-132), the rows of the articles before it are kept and the exception returned.
+    The third value is the failing row's index (``None`` if no row raises).
     """
     rows_by_ticker: Dict[str, list] = {}
     if not cells:
-        return rows_by_ticker, None
+        return rows_by_ticker, None, None
     if isinstance(chunk, NativeChunk):
         # the native tokenizer's chunk (all six columns object-typed): only matched rows are decoded
         last, stamp, tail, raw = -1, None, None, None
@@ -107,11 +108,11 @@ def _cell_rows(chunk, cells, dates):
                 try:
                     stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
                 except Exception as exc:   # noqa: BLE001
-                    return rows_by_ticker, exc
+                    return rows_by_ticker, exc, i
                 tail = tuple(chunk.value(i, c) for c in ('title', 'url', 'source', 'source_url', 'article_text'))
                 last = i
             rows_by_ticker.setdefault(ticker, []).append((stamp, raw, tj, tt) + tail)
-        return rows_by_ticker, None
+        return rows_by_ticker, None, None
     if not any(dt == object for dt in chunk.dtypes):
         last, stamp, row = -1, None, None
         for i, ticker, tj, tt in cells:
@@ -119,11 +120,11 @@ def _cell_rows(chunk, cells, dates):
             try:
                 stamp = int(parser.parse(row['date_time']).timestamp())
             except Exception as exc:   # noqa: BLE001 - the reference's own exception, re-raised by the caller
-                return rows_by_ticker, exc
+                return rows_by_ticker, exc, i
             rows_by_ticker.setdefault(ticker, []).append(
                 (stamp, row['date_time'], tj, tt, row['title'], row['url'], row['source'], row['source_url'],
                  row['article_text']))
-        return rows_by_ticker, None
+        return rows_by_ticker, None, None
     cols = {c: chunk[c].tolist() for c in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')}
     last, stamp, tail = -1, None, None
     for i, ticker, tj, tt in cells:
@@ -132,12 +133,12 @@ def _cell_rows(chunk, cells, dates):
             try:
                 stamp = int((dates[i] if isinstance(raw, str) else parser.parse(raw)).timestamp())
             except Exception as exc:   # noqa: BLE001
-                return rows_by_ticker, exc
+                return rows_by_ticker, exc, i
             tail = (cols['title'][i], cols['url'][i], cols['source'][i], cols['source_url'][i],
                     cols['article_text'][i])
             last = i
         rows_by_ticker.setdefault(ticker, []).append((stamp, raw, tj, tt) + tail)
-    return rows_by_ticker, None
+    return rows_by_ticker, None, None
 
 
 # --------------------------------------------------------------------- matcher cache
@@ -238,23 +239,35 @@ def _match_hits(chunk, processed_data, matcher: Optional[GpuMatcher] = None):
     return hits, error, dates, matcher
 
 
-def _write_hits(source_name, chunk, matcher, hits, dates, error):
-    """Append the rows of a matched chunk and raise the first of its errors in the reference's row order:
-    a row whose output cells raise, an article whose assembly raises, then the date parse error (the
-    rows of the articles before the failing one are written first, as the reference's loop does)."""
+def _hit_rows(chunk, matcher, hits, dates, error):
+    """The output rows of a matched chunk grouped by ticker, up to its first failing article, with that
+    article's exception and row (``None, None`` if none fails).  In the reference's row order a row fails
+    when its ``date_time`` does not parse (:152, row ``len(dates)``), its assembly raises (``re.error``,
+    :178) or its output cells raise (:131); the rows of the articles before it are written."""
     cells = assemble_json_rows(matcher.ckb, hits, dates) if hits is not None else None
-    err_rows = None
+    asm_row = None
     if cells is None:
         results, err_asm = _results(matcher, hits, dates)
-        by_ticker, err_rows = _chunk_rows(chunk, results, dates)
+        if err_asm is not None:
+            asm_row = len(results)
+        cells = [(i, t, json.dumps(m['text']), json.dumps(m['title'])) for i, tm in enumerate(results)
+                 for t, m in tm.items()]
     else:
         err_asm = None
-        by_ticker, err_rows = _cell_rows(chunk, cells, dates)
+    by_ticker, err_rows, row = _cell_rows(chunk, cells, dates)
+    for exc, r in ((err_rows, row), (err_asm, asm_row), (error, len(dates))):
+        if exc is not None:
+            return by_ticker, exc, r
+    return by_ticker, None, None
+
+
+def _write_hits(source_name, chunk, matcher, hits, dates, error):
+    """Append the rows of a matched chunk, then raise its first error (see :func:`_hit_rows`)."""
+    by_ticker, exc, _row = _hit_rows(chunk, matcher, hits, dates, error)
     for ticker, rows in by_ticker.items():
         _append_rows(source_name, ticker, rows)
-    for exc in (err_rows, err_asm, error):
-        if exc is not None:
-            raise exc
+    if exc is not None:
+        raise exc
 
 
 def _write_chunk(source_name, chunk, processed_data, matcher: Optional[GpuMatcher] = None):
@@ -331,6 +344,40 @@ def _write_native(source_name, chunk: NativeChunk, processed_data, matcher, exch
         _write_hits(source_name, chunk, matcher, hits, dates, error)
     elif error is not None:
         raise error
+    return matcher
+
+
+class ShardError(RuntimeError):
+    """Raised on the ranks of ``--gpus N`` that did not hold the failing row of a chunk (its rank raises
+    the reference's own exception)."""
+
+
+def _write_shard(source_name, chunk: ShardChunk, processed_data, matcher, exchange):
+    """``--gpus N`` with sharded host work: this rank parses the dates, packs and uploads the arena, scans,
+    builds the JSON cells and the output rows of ITS byte-balanced share of the chunk only
+    (ingest.read_chunks_sharded).  The chunk's first failing row is agreed on by a MIN all-reduce, and the
+    ranks append their rows in rank order (= article order: shares are contiguous) up to it, one rank at a
+    time, so every per-ticker file receives the rows in the order the reference's loop appends them."""
+    dates, error = _dates(chunk.column_list('date_time'))
+    n_ok = len(dates)
+    hits = None
+    if n_ok:
+        arena, off = chunk.arena()
+        d_arena, d_off = matcher.upload(arena, off[:2 * n_ok + 1])
+        matcher.scan(d_arena, d_off, n_ok)
+        hits = matcher.fetch()
+    by_ticker, exc, row = _hit_rows(chunk, matcher, hits, dates, error)
+    never = np.iinfo(np.int64).max
+    first = int(exchange.allreduce_min([chunk.lo + row if exc is not None else never])[0])
+    for r in range(exchange.world):
+        if r == exchange.rank and chunk.lo <= first:
+            for ticker, rows in by_ticker.items():
+                _append_rows(source_name, ticker, rows)
+        exchange.barrier()
+    if first != never:
+        if exc is not None and chunk.lo + row == first:
+            raise exc
+        raise ShardError(f'process_chunk stopped at row {chunk.chunk_index0 + first} of the articles (on another rank)')
     return matcher
 
 
@@ -460,6 +507,12 @@ def run(args, rank: int, world: int, device, backend, matcher=None):
     if world > 1:
         from .dist import Exchange
         exchange = Exchange(rank, world, device, backend)
+        os.makedirs(out_dir, exist_ok=True)
+        exchange.barrier()
+        try:
+            return _run_sharded(args, processed, exchange, device, out_dir, matcher)
+        finally:
+            exchange.close()
     try:
         # the native tokenizer (ingest.py), chunk by chunk, with pandas' own chunks where it cannot be exact
         for chunk in ingest.read_chunks(args.articles, args.chunksize):
@@ -477,12 +530,37 @@ def run(args, rank: int, world: int, device, backend, matcher=None):
     finally:
         if exchange is not None:
             exchange.close()
-    if rank != 0:
-        return 0
     print("All matched CSV files have been processed.")
     for name in os.listdir(out_dir):
         sort_matched_csv(f"{out_dir}/{name}")
     print("All matched CSV files have been sorted by date and time.")
+    return 0
+
+
+def _run_sharded(args, processed, exchange, device, out_dir, matcher=None):
+    """``--gpus N``: every rank reads its byte-balanced share of each chunk (ingest.read_chunks_sharded),
+    matches and writes it (rank order per chunk); then the ranks sort disjoint sets of the output files.
+    A chunk pandas must parse (the native tokenizer cannot prove its dtypes) is parsed whole by every rank,
+    matched in shares and written by rank 0."""
+    rank, world = exchange.rank, exchange.world
+    for chunk in ingest.read_chunks_sharded(args.articles, args.chunksize, rank, world, exchange.allreduce_min):
+        if isinstance(chunk, ShardChunk):
+            if matcher is None:
+                matcher = get_matcher(processed, device, _native_sample(chunk))
+            matcher = _write_shard(args.source, chunk, processed, matcher, exchange)
+            continue
+        if matcher is None:
+            matcher = get_matcher(processed, device, [field_str(v) for v in chunk['article_text'].tolist()])
+        matcher = _write_chunk_sharded(args.source, chunk, processed, matcher, exchange)
+        exchange.barrier()
+    exchange.barrier()
+    if rank == 0:
+        print("All matched CSV files have been processed.")
+    for name in sorted(os.listdir(out_dir))[rank::world]:   # the final pass over the files, split over the ranks
+        sort_matched_csv(f"{out_dir}/{name}")
+    exchange.barrier()
+    if rank == 0:
+        print("All matched CSV files have been sorted by date and time.")
     return 0
 
 

@@ -68,7 +68,7 @@ def main():
         c4 = time.perf_counter(); t['gpu_match'] += c4 - c3
         cells = assemble_json_rows(matcher.ckb, hits, dates)
         c5 = time.perf_counter(); t['assemble'] += c5 - c4
-        by, _err = mk._cell_rows(chunk, cells, dates)
+        by, _err, _row = mk._cell_rows(chunk, cells, dates)
         c6 = time.perf_counter(); t['rows'] += c6 - c5
         for ticker, rows in by.items():
             mk._append_rows('yahoo', ticker, rows)

@@ -16,6 +16,7 @@ class OracleMatcher:
         self.ckb = compile_kb(processed)
         self.oracle = orc.Oracle(processed)
         self.pid = {n: i for i, n in enumerate(self.ckb.names)}
+        self.uploads = []        # (documents, arena bytes) of every upload: what this process scanned
 
     def _field(self, s):
         """name -> positions as kw_scan reports them (a name whose regex does not compile keeps its
@@ -48,6 +49,7 @@ class OracleMatcher:
     # the kw_scan-shaped calls of the native ingest path: an arena + offsets "upload", a scan of n documents
     # starting at an offsets slice, the records of the last scan
     def upload(self, arena, off):
+        self.uploads.append(((len(off) - 1) // 2, int(off[-1] - off[0])))
         return arena, off
 
     def scan(self, d_arena, d_off, n_docs, stream=None):

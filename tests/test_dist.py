@@ -98,8 +98,9 @@ def _main_worker(rank, world, port, work, q):
     args = mk._parse(['--info-dir', 'unused', '--articles', os.path.join(work, 'articles.csv'),
                       '--chunksize', str(golden_data.chunksize()), '--gpus', str(world)])
     from tests.oracle_matcher import OracleMatcher
-    rc = mk.run(args, rank, world, None, 'gloo', matcher=OracleMatcher(processed))
-    q.put((rank, rc))
+    m = OracleMatcher(processed)
+    rc = mk.run(args, rank, world, None, 'gloo', matcher=m)
+    q.put((rank, rc, m.uploads))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -121,7 +122,18 @@ def test_gloo_main_sharded_equals_reference_outputs(tmp_path):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res == [(0, 0), (1, 0)]
+    assert [(r, rc) for r, rc, _u in res] == [(0, 0), (1, 0)]
+    # each rank packed and scanned only its own byte-balanced share of every chunk
+    n_rows = len(golden_data.articles_frame())
+    chunk = golden_data.chunksize()
+    ups = [u for _r, _rc, u in res]
+    assert all(len(u) == -(-n_rows // chunk) for u in ups)
+    for c, size in enumerate([min(chunk, n_rows - k) for k in range(0, n_rows, chunk)]):
+        shares = [u[c][0] for u in ups]
+        assert sum(shares) == size, (c, shares)
+        assert all(0 < s < size for s in shares), (c, shares)
+        nbytes = [u[c][1] for u in ups]
+        assert max(nbytes) < 0.75 * sum(nbytes), (c, nbytes)
     out = tmp_path / 'yahoo_ticker_matched_articles'
     want = golden_data.outputs()
     assert sorted(os.listdir(out)) == sorted(want)
