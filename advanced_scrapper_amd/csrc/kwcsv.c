@@ -250,3 +250,85 @@ int64_t kwcsv_records(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_
     starts[rows] = p;
     return rows;
 }
+
+/* one cell of an output row (0, or -1 when out is full) */
+static int put_cell(uint8_t *out, int64_t cap, int64_t *o, const uint8_t *s, int64_t n)
+{
+    /* the csv writer's QUOTE_MINIMAL (pandas to_csv): quoted iff the value holds ',', '"' or '\n' (the
+     * line terminator), quotes doubled; '\r' alone is written as it is */
+    int q = n > 0 && (memchr(s, ',', (size_t)n) || memchr(s, '"', (size_t)n) || memchr(s, '\n', (size_t)n));
+    if (!q) {
+        if (*o + n > cap) return -1;
+        memcpy(out + *o, s, (size_t)n);
+        *o += n;
+        return 0;
+    }
+    if (*o + 2 * n + 2 > cap) return -1;
+    out[(*o)++] = '"';
+    for (int64_t i = 0; i < n; ++i) {
+        if (s[i] == '"') out[(*o)++] = '"';
+        out[(*o)++] = s[i];
+    }
+    out[(*o)++] = '"';
+    return 0;
+}
+
+/*
+ * The output rows of a native chunk as CSV bytes (match_keywords.py:131-146: one row per (article, ticker),
+ * columns time_unix, date_time, text_matches, title_matches, title, url, source, source_url, article_text),
+ * written as the reference's per-row DataFrame.to_csv writes them: the time stamp as a decimal integer, the
+ * JSON cells as given, every other cell from the chunk's tokenized cells (an NA cell = NaN -> empty), each
+ * in QUOTE_MINIMAL form, "\n" line ends.  Rows are emitted in the given order; row r's line is
+ * out[line_off[r], line_off[r + 1]).  cols[6] = the chunk columns of date_time, title, url, source,
+ * source_url, article_text; json3[3r .. 3r+2] = row r's text_matches JSON json[json3[3r], json3[3r+1]) and
+ * title_matches JSON json[json3[3r+1], json3[3r+2]).  flags[r]: bit c (c = 0..7 for output columns 1..8) = that cell is a text
+ * witness (KWCSV_TEXT: no number or bool literal; the JSON cells always are), bit 8 + c = that cell is NA,
+ * bit 16 = a cell holds '\r' (pandas' re-read would split the record there).  Returns 0, -1 when out is too
+ * small, -2 for a NUL character in a cell (the caller's pandas path raises as the reference does).
+ */
+int64_t kwcsv_emit(const uint8_t *cells, const int64_t *coff, const uint8_t *cfl, int32_t ncols, const int32_t *cols,
+                   const int32_t *row_doc, const int64_t *row_stamp, int64_t nrows, const uint8_t *json,
+                   const int64_t *json3, uint8_t *out, int64_t cap, int64_t *line_off, uint32_t *flags)
+{
+    int64_t o = 0;
+    line_off[0] = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+        uint32_t fl = 0;
+        char num[24];
+        int k = 24;
+        int64_t v = row_stamp[r];
+        uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1u : (uint64_t)v;
+        do { num[--k] = (char)('0' + u % 10); u /= 10; } while (u);
+        if (v < 0) num[--k] = '-';
+        if (o + (24 - k) + 1 > cap) return -1;
+        memcpy(out + o, num + k, (size_t)(24 - k));
+        o += 24 - k;
+        for (int c = 0; c < 8; ++c) {
+            out[o++] = ',';
+            const uint8_t *s;
+            int64_t n;
+            int na = 0;
+            if (c == 1 || c == 2) {
+                s = json + json3[3 * r + (c - 1)];
+                n = json3[3 * r + c] - json3[3 * r + (c - 1)];
+            } else {
+                const int32_t col = cols[c == 0 ? 0 : c - 2];
+                const int64_t cell = (int64_t)row_doc[r] * ncols + col;
+                s = cells + coff[cell];
+                n = coff[cell + 1] - coff[cell];
+                na = (cfl[cell] & KWCSV_NA) != 0;
+                if (na) n = 0;
+            }
+            if (n > 0 && memchr(s, 0, (size_t)n)) return -2;
+            if (n > 0 && memchr(s, '\r', (size_t)n)) fl |= 1u << 16;
+            if (na) fl |= 1u << (8 + c);
+            else if (c == 1 || c == 2 || kwcsv_text_witness(s, n)) fl |= 1u << c;
+            if (put_cell(out, cap - 1, &o, s, n)) return -1;
+        }
+        if (o + 1 > cap) return -1;
+        out[o++] = '\n';
+        line_off[r + 1] = o;
+        flags[r] = fl;
+    }
+    return 0;
+}

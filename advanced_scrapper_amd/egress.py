@@ -162,3 +162,157 @@ def _join(cells: Sequence[str]):
 
 
 _FAST_OK = _fast_path_agrees()
+
+
+# --------------------------------------------------------------------- native rows, no final re-read
+_CSV_LIB = None
+
+
+def _csv_lib():
+    global _CSV_LIB
+    if _CSV_LIB is None:
+        import ctypes
+        from .ingest import _lib
+        L = _lib()
+        P, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.kwcsv_emit.restype = i64
+        L.kwcsv_emit.argtypes = [P, P, P, i32, P, P, P, i64, P, P, P, i64, P, P]
+        _CSV_LIB = L
+    return _CSV_LIB
+
+
+_HEADER_COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source',
+                   'source_url', 'article_text')
+PANDAS_BLOCK_ROWS = 65536   # pandas' low_memory reader infers dtypes per block of rows (2^20 // 9 columns -> 2^16)
+_F_WITNESS = 0xFF
+_F_NA_SHIFT = 8
+_F_CR = 1 << 16
+
+
+class RunFiles:
+    """The per-ticker files ONE run creates (none existed when it started), indexed as they are written: each
+    row's time_unix, line length and cell flags (kwcsv_emit).  At the end the reference's re-read + sort +
+    rewrite (match_keywords.py:195-217) is decided from the index: when pandas' re-read provably yields the
+    written values (every non-time column of every 65 536-row block keeps a text witness or is all NaN, no
+    cell holds a lone '\\r'), the sorted file is the written records in ``np.argsort(time_unix,
+    kind='quicksort')`` order -- the records already in that order (ascending, no ties) mean no rewrite at
+    all.  Other files (pre-existing ones, those a row went to by another path) take sort_matched_csv."""
+
+    def __init__(self, out_dir: str):
+        self.out_dir = out_dir
+        self.pre = set(os.listdir(out_dir)) if os.path.isdir(out_dir) else set()
+        self.files = {}          # name -> [stamps list, lengths list, flags list, header bytes]
+        self.other = set()       # names written by another path
+
+    def owned(self, name: str) -> bool:
+        return name not in self.pre and name not in self.other
+
+    def note_other(self, name: str):
+        self.other.add(name)
+        self.files.pop(name, None)
+
+    def add(self, name: str, stamps, lengths, flags, header: bytes):
+        f = self.files.get(name)
+        if f is None:
+            f = self.files[name] = [[], [], [], header]
+        f[0].append(stamps)
+        f[1].append(lengths)
+        f[2].append(flags)
+
+    def finish(self, name: str) -> bool:
+        """Sort one indexed file as the reference's sort_matched_csv does; False = not decidable here."""
+        if not self.owned(name) or name not in self.files:
+            return False
+        st, ln, fl, header = self.files[name]
+        stamps = np.concatenate(st)
+        lens = np.concatenate(ln)
+        flags = np.concatenate(fl)
+        n = len(stamps)
+        if n == 0 or (flags & _F_CR).any():
+            return False
+        for b0 in range(0, n, PANDAS_BLOCK_ROWS):
+            blk = flags[b0:b0 + PANDAS_BLOCK_ROWS]
+            wit = np.bitwise_or.reduce(blk & _F_WITNESS)
+            na_all = np.bitwise_and.reduce(blk >> _F_NA_SHIFT) & 0xFF
+            if (wit | na_all) != 0xFF:
+                return False
+        if n > 1 and not (np.diff(stamps) > 0).all():
+            order = np.argsort(stamps, kind='quicksort')
+            if not (order == np.arange(n)).all():
+                path = os.path.join(self.out_dir, name)
+                with open(path, 'rb') as fh:
+                    data = fh.read()
+                if len(data) != len(header) + int(lens.sum()):
+                    return False
+                ends = len(header) + np.cumsum(lens)
+                starts = ends - lens
+                mv = memoryview(data)
+                body = b''.join([mv[s:e] for s, e in zip(starts[order].tolist(), ends[order].tolist())])
+                with open(path, 'wb') as fh:
+                    fh.write(data[:len(header)])
+                    fh.write(body)
+        return True
+
+
+def render_native(chunk, raw_rows, stamps_by_doc, tickers):
+    """The rows of a native chunk (``raw_rows`` = rows.assemble_json_raw's arrays, document order, KB ticker
+    order) rendered by the C emitter into one buffer, grouped by ticker file: a list of (file name, line
+    bytes, time_unix[], line lengths[], cell flags[]) in KB ticker order, rows in article order within each.
+    ``stamps_by_doc[d]`` = article d's time_unix.  ``None`` when the emitter cannot reproduce the writer (a
+    NUL cell, a platform line end other than "\n"): the caller takes the per-row path."""
+    from .ingest import _p
+    row_doc, row_ti, jbuf, joff = raw_rows
+    n = len(row_doc)
+    if n == 0:
+        return []
+    if not (_FAST_OK and _NL_ONLY):
+        return None
+    order = np.argsort(row_ti, kind='stable')
+    rd = np.ascontiguousarray(row_doc[order], dtype=np.int32)
+    rs = np.ascontiguousarray(stamps_by_doc[rd], dtype=np.int64)
+    j3 = np.empty(3 * n, dtype=np.int64)
+    j3[0::3] = joff[2 * order]
+    j3[1::3] = joff[2 * order + 1]
+    j3[2::3] = joff[2 * order + 2]
+    c = chunk.cells
+    cols = np.asarray([chunk.col[k] for k in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')],
+                      dtype=np.int32)
+    jb = jbuf if len(jbuf) else np.zeros(1, np.uint8)
+    cap = int(2 * (int(c.off[-1]) + len(jbuf)) + 64 * n + 1024)
+    line_off = np.empty(n + 1, dtype=np.int64)
+    flags = np.empty(n, dtype=np.uint32)
+    L = _csv_lib()
+    rc = -1
+    for _ in range(8):
+        out = np.empty(cap, dtype=np.uint8)
+        rc = L.kwcsv_emit(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jb), _p(j3),
+                          _p(out), cap, _p(line_off), _p(flags))
+        if rc != -1:
+            break
+        cap *= 2
+    if rc != 0:
+        return None
+    ti = row_ti[order]
+    cuts = np.flatnonzero(np.r_[True, ti[1:] != ti[:-1], True]).tolist()
+    mv = memoryview(out)
+    return [(f'{tickers[ti[a]]}_match.csv', mv[line_off[a]:line_off[b]], rs[a:b], np.diff(line_off[a:b + 1]),
+             flags[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def header_bytes() -> bytes:
+    return _join(list(_HEADER_COLUMNS)).encode('utf-8')
+
+
+def append_rendered(out_dir: str, rendered, run_files: 'RunFiles' = None):
+    """Append rendered rows (render_native) to their files, the header first in a new file; the run index
+    records the rows of the files this run owns."""
+    header = header_bytes()
+    for name, data, stamps, lens, flags in rendered:
+        path = os.path.join(out_dir, name)
+        new = not os.path.exists(path)
+        with open(path, 'ab') as fh:
+            if new:
+                fh.write(header)
+            fh.write(data)
+        if run_files is not None and run_files.owned(name):
+            run_files.add(name, stamps, lens, flags, header)

@@ -36,7 +36,7 @@ from .ingest import NativeChunk, ShardChunk
 from .dates import parse_date
 from .kb import (ATTRIBUTES, compile_kb, extract_time_periods, is_within_period,  # noqa: F401 (re-export)
                  process_json_data, read_and_process_json_files)
-from .rows import assemble_json_rows
+from .rows import assemble_json_raw, assemble_json_rows
 from .matcher import (GpuMatcher, assemble_ticker_matches, background_sample, field_str, group_hits,  # noqa: F401
                       pack_fields, records_from_tensor)
 
@@ -44,8 +44,16 @@ OUTPUT_COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'ti
                   'source_url', 'article_text')
 
 
+def _output_dir(source_name):
+    return f'{source_name}_ticker_matched_articles'
+
+
 def _output_path(source_name, ticker):
-    return f'{source_name}_ticker_matched_articles/{ticker}_match.csv'
+    return f'{_output_dir(source_name)}/{ticker}_match.csv'
+
+
+# the per-ticker files of the current run() and their rows' index (egress.RunFiles), None outside run()
+_RUN: Optional[egress.RunFiles] = None
 
 
 def _csv_row(matched_names, article):
@@ -72,6 +80,8 @@ def append_to_csv(source_name, ticker, matched_names, article):
 def _append_rows(source_name, ticker, rows):
     """Append row dicts (or value tuples in ``OUTPUT_COLUMNS`` order), one reference append per row."""
     values = (tuple(r[c] for c in OUTPUT_COLUMNS) if isinstance(r, dict) else r for r in rows)
+    if _RUN is not None:
+        _RUN.note_other(f'{ticker}_match.csv')
     egress.append_rows(_output_path(source_name, ticker), OUTPUT_COLUMNS, values)
 
 
@@ -261,8 +271,44 @@ def _hit_rows(chunk, matcher, hits, dates, error):
     return by_ticker, None, None
 
 
+def _native_rows(chunk, matcher, hits, dates, error):
+    """The rows of a native chunk rendered in C (egress.render_native: JSON cells from rows.assemble_json_raw,
+    the other cells straight from the tokenized chunk), up to its first failing article, with that article's
+    exception and row (as :func:`_hit_rows`); ``None`` when only the Python path can answer."""
+    if not isinstance(chunk, NativeChunk) or hits is None:
+        return None
+    raw = assemble_json_raw(matcher.ckb, hits, dates)
+    if raw is None:
+        return None
+    row_doc = raw[0]
+    stamps = np.zeros(max(len(dates), 1), dtype=np.int64)
+    exc, row = None, None
+    for d in np.unique(row_doc).tolist():      # time_unix = int(parse(date_time).timestamp()), :131-132
+        try:
+            stamps[d] = int(dates[d].timestamp())
+        except Exception as e:   # noqa: BLE001 - that article's append raises in the reference
+            exc, row = e, d
+            break
+    if exc is not None:
+        k = int(np.searchsorted(row_doc, row))   # rows are in document order
+        raw = (raw[0][:k], raw[1][:k], raw[2], raw[3][:2 * k + 1])
+    rendered = egress.render_native(chunk, raw, stamps, matcher.ckb.tickers)
+    if rendered is None:
+        return None
+    if exc is None and error is not None:
+        exc, row = error, len(dates)
+    return rendered, exc, row
+
+
 def _write_hits(source_name, chunk, matcher, hits, dates, error):
     """Append the rows of a matched chunk, then raise its first error (see :func:`_hit_rows`)."""
+    nat = _native_rows(chunk, matcher, hits, dates, error)
+    if nat is not None:
+        rendered, exc, _row = nat
+        egress.append_rendered(_output_dir(source_name), rendered, _RUN)
+        if exc is not None:
+            raise exc
+        return
     by_ticker, exc, _row = _hit_rows(chunk, matcher, hits, dates, error)
     for ticker, rows in by_ticker.items():
         _append_rows(source_name, ticker, rows)
@@ -366,13 +412,21 @@ def _write_shard(source_name, chunk: ShardChunk, processed_data, matcher, exchan
         d_arena, d_off = matcher.upload(arena, off[:2 * n_ok + 1])
         matcher.scan(d_arena, d_off, n_ok)
         hits = matcher.fetch()
-    by_ticker, exc, row = _hit_rows(chunk, matcher, hits, dates, error)
+    nat = _native_rows(chunk, matcher, hits, dates, error)
+    if nat is not None:
+        rendered, exc, row = nat
+        by_ticker = None
+    else:
+        by_ticker, exc, row = _hit_rows(chunk, matcher, hits, dates, error)
     never = np.iinfo(np.int64).max
     first = int(exchange.allreduce_min([chunk.lo + row if exc is not None else never])[0])
     for r in range(exchange.world):
         if r == exchange.rank and chunk.lo <= first:
-            for ticker, rows in by_ticker.items():
-                _append_rows(source_name, ticker, rows)
+            if by_ticker is None:
+                egress.append_rendered(_output_dir(source_name), rendered)
+            else:
+                for ticker, rows in by_ticker.items():
+                    _append_rows(source_name, ticker, rows)
         exchange.barrier()
     if first != never:
         if exc is not None and chunk.lo + row == first:
@@ -497,13 +551,13 @@ def main(argv=None):
 
 
 def run(args, rank: int, world: int, device, backend, matcher=None):
-    """The driver loop on one rank: read the chunks, match (sharded over the ranks when world > 1), write on
-    rank 0, then rank 0 sorts every output file (match_keywords.py:226-246)."""
+    """The driver loop on one rank: read the chunks, match (sharded over the ranks when world > 1), write,
+    then sort every output file (match_keywords.py:226-246)."""
+    global _RUN
     processed = read_and_process_json_files(args.info_dir)
     out_dir = f'{args.source}_ticker_matched_articles'
     if rank == 0:
         os.makedirs(out_dir, exist_ok=True)
-    exchange = None
     if world > 1:
         from .dist import Exchange
         exchange = Exchange(rank, world, device, backend)
@@ -513,27 +567,29 @@ def run(args, rank: int, world: int, device, backend, matcher=None):
             return _run_sharded(args, processed, exchange, device, out_dir, matcher)
         finally:
             exchange.close()
+    _RUN = egress.RunFiles(out_dir)
     try:
         # the native tokenizer (ingest.py), chunk by chunk, with pandas' own chunks where it cannot be exact
         for chunk in ingest.read_chunks(args.articles, args.chunksize):
             if isinstance(chunk, NativeChunk):
                 if matcher is None:
                     matcher = get_matcher(processed, device, _native_sample(chunk))
-                matcher = _write_native(args.source, chunk, processed, matcher, exchange)
+                matcher = _write_native(args.source, chunk, processed, matcher)
                 continue
             if matcher is None:
                 matcher = get_matcher(processed, device, [field_str(v) for v in chunk['article_text'].tolist()])
-            if exchange is None:
-                matcher = _write_chunk(args.source, chunk, processed, matcher)
+            matcher = _write_chunk(args.source, chunk, processed, matcher)
+        print("All matched CSV files have been processed.")
+        for name in os.listdir(out_dir):
+            # the files this run created are sorted from their write index (no re-read when already in
+            # time order); the others take the reference's re-read, sort and rewrite
+            if _RUN.finish(name):
+                print(f"Sorted and saved: {out_dir}/{name}")
             else:
-                matcher = _write_chunk_sharded(args.source, chunk, processed, matcher, exchange)
+                sort_matched_csv(f"{out_dir}/{name}")
+        print("All matched CSV files have been sorted by date and time.")
     finally:
-        if exchange is not None:
-            exchange.close()
-    print("All matched CSV files have been processed.")
-    for name in os.listdir(out_dir):
-        sort_matched_csv(f"{out_dir}/{name}")
-    print("All matched CSV files have been sorted by date and time.")
+        _RUN = None
     return 0
 
 

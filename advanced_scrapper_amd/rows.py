@@ -71,12 +71,27 @@ def _ptr(a: np.ndarray):
 
 def assemble_json_rows(ckb: CompiledKB, hits: np.ndarray, dates: Sequence) -> Optional[List[Tuple[int, str, str, str]]]:
     """``[(doc, ticker, text_json, title_json), ...]`` of one chunk, or ``None`` (use the Python path)."""
+    raw = assemble_json_raw(ckb, hits, dates)
+    if raw is None:
+        return None
+    row_doc, row_ti, buf, off = raw
+    n = len(row_doc)
+    text = buf.tobytes().decode('ascii')
+    oo = off.tolist()
+    tickers = ckb.tickers
+    return [(int(row_doc[r]), tickers[row_ti[r]], text[oo[2 * r]:oo[2 * r + 1]], text[oo[2 * r + 1]:oo[2 * r + 2]])
+            for r in range(n)]
+
+
+def assemble_json_raw(ckb: CompiledKB, hits: np.ndarray, dates: Sequence):
+    """The rows of :func:`assemble_json_rows` as arrays: (row_doc int32[n], row_ti int32[n] (KB ticker
+    index), JSON bytes uint8, offsets int64[2n + 1]: row r's text_matches then title_matches), or ``None``."""
     tables = _kb_tables(ckb)
     if tables is None:
         return None
     n_docs = len(dates)
     if len(hits) == 0 or n_docs == 0:
-        return []
+        return (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.uint8), np.zeros(1, np.int64))
     date_us = np.zeros(n_docs, dtype=np.int64)
     date_ok = np.zeros(n_docs, dtype=np.uint8)
     try:
@@ -111,8 +126,4 @@ def assemble_json_rows(ckb: CompiledKB, hits: np.ndarray, dates: Sequence) -> Op
         break
     else:
         raise RuntimeError('kwrows_assemble: output kept overflowing')
-    text = out[:out_off[2 * n]].tobytes().decode('ascii')
-    oo = out_off[:2 * n + 1].tolist()
-    tickers = ckb.tickers
-    return [(int(row_doc[r]), tickers[row_ti[r]], text[oo[2 * r]:oo[2 * r + 1]], text[oo[2 * r + 1]:oo[2 * r + 2]])
-            for r in range(n)]
+    return row_doc[:n], row_ti[:n], out[:out_off[2 * n]], out_off[:2 * n + 1]

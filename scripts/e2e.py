@@ -2,10 +2,10 @@
 
 Generates N synthetic articles (config-2 corpus), writes them as the reference's article CSV, then runs the
 drop-in main loop's phases on chunks of 20 000 rows -- native CSV ingest (libkwcsv), date parse, arena +
-GPU match, JSON cells (libkwrows), row tuples, CSV egress -- and the final sort of every per-ticker file
-(match_keywords.py:243-244, native rewrite with the pandas fallback), and prints one JSON line with seconds
-per phase and the end-to-end articles/s (the reference's CPU path on the same rows is bench.py's
-cpu_baseline).
+GPU match, JSON cells (libkwrows) + rows rendered in C (kwcsv_emit), the per-ticker appends -- and the final
+sort of every per-ticker file (match_keywords.py:243-244: from the run's write index, the re-read path for
+the files it cannot decide), and prints one JSON line with seconds per phase and the end-to-end articles/s
+(the reference's CPU path on the same rows is bench.py's cpu_baseline).
 
     python scripts/e2e.py [--docs 200000] [--chunksize 20000]
 """
@@ -41,9 +41,11 @@ def main():
     synth.to_dataframe(corpus).to_csv(csv_path, index=False)
     os.chdir(work)
     os.makedirs('yahoo_ticker_matched_articles')
-    t = dict(read=0.0, dates=0.0, arena=0.0, gpu_match=0.0, assemble=0.0, rows=0.0, write=0.0, sort=0.0)
+    t = dict(read=0.0, dates=0.0, arena=0.0, gpu_match=0.0, render=0.0, write=0.0, sort=0.0)
     matcher = None
     n_rows = n_native = n_chunks = 0
+    from advanced_scrapper_amd import egress
+    mk._RUN = egress.RunFiles('yahoo_ticker_matched_articles')
     t_all = time.perf_counter()
     c0 = time.perf_counter()
     for chunk in ingest.read_chunks(csv_path, args.chunksize):
@@ -66,24 +68,25 @@ def main():
         matcher.scan(d_arena, d_off, len(dates))
         hits = matcher.fetch()
         c4 = time.perf_counter(); t['gpu_match'] += c4 - c3
-        cells = assemble_json_rows(matcher.ckb, hits, dates)
-        c5 = time.perf_counter(); t['assemble'] += c5 - c4
-        by, _err, _row = mk._cell_rows(chunk, cells, dates)
-        c6 = time.perf_counter(); t['rows'] += c6 - c5
-        for ticker, rows in by.items():
-            mk._append_rows('yahoo', ticker, rows)
-            n_rows += len(rows)
-        c0 = time.perf_counter(); t['write'] += c0 - c6
+        rendered, exc, _row = mk._native_rows(chunk, matcher, hits, dates, error)
+        c5 = time.perf_counter(); t['render'] += c5 - c4
+        egress.append_rendered('yahoo_ticker_matched_articles', rendered, mk._RUN)
+        n_rows += sum(len(r[2]) for r in rendered)
+        c0 = time.perf_counter(); t['write'] += c0 - c5
     c7 = time.perf_counter()
     import contextlib
     import io
+    n_reread = 0
     with contextlib.redirect_stdout(io.StringIO()):
         for name in os.listdir('yahoo_ticker_matched_articles'):
-            mk.sort_matched_csv(f'yahoo_ticker_matched_articles/{name}')
+            if not mk._RUN.finish(name):
+                n_reread += 1
+                mk.sort_matched_csv(f'yahoo_ticker_matched_articles/{name}')
     t['sort'] = time.perf_counter() - c7
+    mk._RUN = None
     total = time.perf_counter() - t_all
     out = {'docs': args.docs, 'chunksize': args.chunksize, 'chunks': n_chunks, 'native_chunks': n_native,
-           'rows': n_rows, 'total_s': round(total, 3), 'articles_per_s': round(args.docs / total, 1),
+           'rows': n_rows, 'files_reread_for_sort': n_reread, 'total_s': round(total, 3), 'articles_per_s': round(args.docs / total, 1),
            'phases_s': {k: round(v, 3) for k, v in t.items()}}
     print(json.dumps(out), flush=True)
     os.chdir(REPO)

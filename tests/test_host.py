@@ -471,3 +471,67 @@ def test_egress_fast_path_probe(monkeypatch, tmp_path):
     monkeypatch.setattr(egress, '_FAST_OK', False)
     egress.append_rows(str(p2), ('c1', 'c2', 'c3'), rows)
     assert p1.read_bytes() == p2.read_bytes()
+
+
+def _run_main(tmp_path, csv_bytes, chunksize, force_reread=False, monkeypatch=None):
+    """match_keywords.run over csv_bytes in a fresh directory (the scan by the oracle stand-in); returns
+    {file: bytes}.  force_reread: every output file takes the reference's re-read + sort."""
+    import time
+    from advanced_scrapper_amd import egress
+    from advanced_scrapper_amd import match_keywords as mk
+    from tests import golden_data
+    from tests.oracle_matcher import OracleMatcher
+    work = tmp_path / ('reread' if force_reread else 'indexed')
+    work.mkdir()
+    (work / 'articles.csv').write_bytes(csv_bytes)
+    monkeypatch.setenv('TZ', 'UTC')
+    time.tzset()
+    monkeypatch.chdir(work)
+    processed = golden_data.kb_processed()
+    monkeypatch.setattr(mk, 'read_and_process_json_files', lambda _d: processed)
+    calls = {'finish': 0}
+    real = egress.RunFiles.finish
+
+    def finish(self, name):
+        if force_reread:
+            return False
+        ok = real(self, name)
+        calls['finish'] += ok
+        return ok
+    monkeypatch.setattr(egress.RunFiles, 'finish', finish)
+    args = mk._parse(['--info-dir', 'unused', '--articles', str(work / 'articles.csv'), '--chunksize', str(chunksize)])
+    assert mk.run(args, 0, 1, None, None, matcher=OracleMatcher(processed)) == 0
+    out = work / 'yahoo_ticker_matched_articles'
+    return {fn: (out / fn).read_bytes() for fn in sorted(os.listdir(out))}, calls['finish']
+
+
+def test_indexed_sort_equals_reread_on_shuffled_rows_with_ties(golden, tmp_path, monkeypatch):
+    """The run index's sort (no re-read) writes the bytes of the reference's re-read + quicksort + rewrite,
+    on rows out of time order with repeated timestamps (the unstable sort's tie order)."""
+    import io
+    import pandas as pd
+    frame = golden.articles_frame()
+    rng = np.random.default_rng(7)
+    frame = frame.iloc[rng.permutation(len(frame))].reset_index(drop=True)
+    frame.loc[frame.index % 5 == 0, 'date_time'] = '2016-03-04 05:06:07'     # ties across many articles
+    data = frame.to_csv(index=False).encode('utf-8')
+    fast, n_fast = _run_main(tmp_path, data, 150, monkeypatch=monkeypatch)
+    slow, _ = _run_main(tmp_path, data, 150, force_reread=True, monkeypatch=monkeypatch)
+    assert n_fast > 0 and sorted(fast) == sorted(slow)
+    for fn in slow:
+        assert fast[fn] == slow[fn], fn
+
+
+def test_indexed_sort_declines_numeric_only_block(golden, tmp_path, monkeypatch):
+    """A pandas read block (shrunk to 4 rows here) whose title cells all look numeric would be re-read as
+    numbers: the index declines and the file takes the re-read path, with the same bytes as a forced re-read."""
+    from advanced_scrapper_amd import egress
+    monkeypatch.setattr(egress, 'PANDAS_BLOCK_ROWS', 4)
+    frame = golden.articles_frame().iloc[500:600].reset_index(drop=True)
+    frame['title'] = [f'{k}.50' if k % 7 else 'Apple Inc. AAPL' for k in range(len(frame))]
+    data = frame.to_csv(index=False).encode('utf-8')
+    fast, _ = _run_main(tmp_path, data, 40, monkeypatch=monkeypatch)
+    slow, _ = _run_main(tmp_path, data, 40, force_reread=True, monkeypatch=monkeypatch)
+    assert sorted(fast) == sorted(slow)
+    for fn in slow:
+        assert fast[fn] == slow[fn], fn
