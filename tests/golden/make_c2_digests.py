@@ -1,4 +1,5 @@
-"""Pin the WHOLE config-2 bench corpus: per-document oracle digests (tests/golden/c2_digests.npz).
+"""Pin the WHOLE config-2 (and config-4) bench corpus: per-document oracle digests (tests/golden/c2_digests.npz,
+tests/golden/c4_digests.npz).
 
 The bench corpus is bench.py's: 1M synthetic ~2 KB articles (csrc/synth.c,
 seed 20250905, documents 0..999 999) against the reference KB
@@ -13,6 +14,8 @@ Runs in the build container on CPU (a spawn pool, ~5 ms of oracle per
 article), never on GPU minutes:
 
     python tests/golden/make_c2_digests.py [--procs 7] [--docs 1000000]
+    python tests/golden/make_c2_digests.py --config 4     # bench.py --workload kb50k's corpus and KB
+                                                          # (~40 ms of oracle per article: ~1.5 h on 7 cores)
 
 Output: c2_digests.npz (digest uint64[n], count uint16[n]) + c2_digests.json
 (seed, n_docs, corpus fingerprint, total digest, total records).
@@ -37,12 +40,20 @@ BLOCK = 2000
 _W = {}
 
 
-def _init():
+def kb_for(config: int):
+    """The bench's KB of a config: 2 = the reference's info/ticker subset, 4 = synth_kb's ~52k names."""
+    if config == 4:
+        from advanced_scrapper_amd.synth_kb import synthetic_kb
+        return synthetic_kb(2300, SEED)
+    from tests import golden_data
+    return golden_data.kb_processed()
+
+
+def _init(config):
     from advanced_scrapper_amd import synth
     from advanced_scrapper_amd.kb import compile_kb
     from oracle import kwmatch_oracle as orc
-    from tests import golden_data
-    processed = golden_data.kb_processed()
+    processed = kb_for(config)
     ckb = compile_kb(processed)
     _W['names'] = synth.injectable_names(ckb)
     _W['pid'] = {n: i for i, n in enumerate(ckb.names)}
@@ -87,14 +98,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--procs', type=int, default=7)
     ap.add_argument('--docs', type=int, default=1_000_000)
-    ap.add_argument('--out', default=os.path.join(HERE, 'c2_digests'))
+    ap.add_argument('--config', type=int, choices=(2, 4), default=2)
+    ap.add_argument('--out', default=None)
     args = ap.parse_args()
+    args.out = args.out or os.path.join(HERE, f'c{args.config}_digests')
     from advanced_scrapper_amd import synth
     from advanced_scrapper_amd.kb import compile_kb
     from tests import corpus_digest as cd
-    from tests import golden_data
     n = args.docs
-    ckb = compile_kb(golden_data.kb_processed())
+    ckb = compile_kb(kb_for(args.config))
     names, kinds = synth.injectable_names(ckb)
     corpus = synth.generate(n, names, kinds, seed=SEED, doc_base=0)
     fp = cd.corpus_fingerprint(corpus)
@@ -105,7 +117,7 @@ def main():
     blocks = [(lo, min(lo + BLOCK, n)) for lo in range(0, n, BLOCK)]
     t0 = time.time()
     ctx = mp.get_context('spawn')
-    with ctx.Pool(args.procs, initializer=_init) as pool:
+    with ctx.Pool(args.procs, initializer=_init, initargs=(args.config,)) as pool:
         for k, (lo, d, c) in enumerate(pool.imap_unordered(_block, blocks)):
             dig[lo:lo + len(d)] = d
             cnt[lo:lo + len(c)] = c
@@ -115,7 +127,8 @@ def main():
     np.savez_compressed(args.out + '.npz', digest=dig, count=cnt.astype(np.uint16))
     meta = {'generator': 'tests/golden/make_c2_digests.py (CPU oracle, oracle/kwmatch_oracle.py)',
             'seed': SEED, 'n_docs': n, 'corpus_bytes': n_bytes, 'corpus_fingerprint': fp,
-            'kb': 'tests/golden/kb_processed.json.gz', 'total_records': int(cnt.sum()),
+            'kb': ('advanced_scrapper_amd/synth_kb.py synthetic_kb(2300, seed)' if args.config == 4
+                   else 'tests/golden/kb_processed.json.gz'), 'config': args.config, 'total_records': int(cnt.sum()),
             'hits_digest': cd.total(dig), 'oracle_seconds': round(time.time() - t0, 1), 'procs': args.procs}
     with open(args.out + '.json', 'w') as fh:
         json.dump(meta, fh, indent=1)
