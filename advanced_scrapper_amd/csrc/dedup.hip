@@ -5,14 +5,11 @@
 //
 //   dd_transform_kernel  find the cut (first "html" after a code point that is
 //                        not '\n'), rewrite the prefix (':80' removed, 'http:'
-//                        -> 'https:'), append ".html", flag 'news/%' / "news/'"
-//                        and hash the normalised URL (two independent 64-bit
-//                        word hashes).  Rows whose only ':' is the scheme's (all
-//                        but a few) are a splice of their input bytes: only the
-//                        splice ("cut" word: prefix end, 's' inserted) is kept
-//                        and every later kernel re-reads the input row through
-//                        norm8(); the rest run the byte-serial rewrite into a
-//                        sparse side arena (dd_slow_kernel).
+//                        -> 'https:'), append ".html", flag 'news/%' / "news/'",
+//                        write the normalised URL into a sparse 8-aligned arena
+//                        and hash it (two independent 64-bit word hashes).
+//                        Rows whose only ':' is the scheme's take a word-wide
+//                        copy; the rest run the byte-serial rewrite.
 //   dd_insert_kernel     open-addressing table of 64-bit slots {tag, row}: the
 //                        first inserter claims a slot by CAS, rows with the same
 //                        tag keep the smallest row by atomicMin (keep='first').
@@ -47,10 +44,6 @@ constexpr uint32_t HTML4 = 0x6C6D7468u;            // "html"
 constexpr uint32_t NEWS4 = 0x7377656Eu;            // "news"
 constexpr uint64_t DOTHTML = 0x6C6D74682Eull;      // ".html"
 constexpr uint8_t CODE_COLLIDE = 4;                // internal: tag shared with a different URL
-constexpr uint32_t CUT_INS = 1u << 30;             // 'http:' -> 'https:' at the scheme (an 's' after byte 4)
-constexpr uint32_t CUT_SLOW = 1u << 31;            // the normalised bytes are in the side arena (Scratch::out)
-constexpr uint32_t CUT_E = CUT_INS - 1;
-constexpr int64_t ROW_MAX = CUT_E - 8;             // longer rows: KW_EUNSUPPORTED (stats: ST_LONG_ROW)
 
 // sparse output arena: row i's normalised URL starts at obase(off[i], i) (8-aligned, room for
 // len + len/5 + 16 bytes: at most one extra 's' per 5 input bytes, ".html", word padding)
@@ -103,11 +96,9 @@ __host__ __device__ __forceinline__ uint64_t fmix(uint64_t h)
 }
 
 struct Scratch {
-    uint8_t *out;            // sparse normalised URLs of the byte-serial rows only (obase)
+    uint8_t *out;            // sparse normalised URLs
     uint64_t *h1, *h2;       // per row
     uint32_t *len3;          // per row: normalised length
-    uint32_t *cut;           // per row: E (normalised prefix bytes) | CUT_INS | CUT_SLOW
-    uint64_t tail;           // ".html" (normalising) or 0 (raw keep-first)
     unsigned long long *table;
     uint64_t mask;
     unsigned long long *cnt;   // [0..4] per code
@@ -248,67 +239,24 @@ __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j
     R.flush(Em);
     Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
     Em.finish();
-    S.cut[i] = CUT_SLOW;
     finish_row(Em.h1, Em.h2, Em.len, Em.bad, i, code, S);
-}
-
-// bytes [y, y + 8) of row i's normalised URL (zeros from len3 on; y < len3).  A spliced row is re-read from
-// the input: [0, E) = the row's bytes with an 's' after byte 4 when CUT_INS, then the tail (".html").
-__device__ __forceinline__ uint64_t norm8(const uint8_t *__restrict__ arena, int64_t b, uint32_t cut, int64_t i,
-                                          int64_t y, uint32_t len3, const Scratch &S)
-{
-    uint64_t w;
-    if (cut & CUT_SLOW) {
-        w = ld64(S.out + obase(b, i), y);
-    } else {
-        const int64_t E = cut & CUT_E;
-        w = 0;
-        if (y < E) {
-            if (!(cut & CUT_INS)) {
-                w = ld64(arena, b + y);
-            } else if (y >= 5) {
-                w = ld64(arena, b + y - 1);
-            } else {
-                const uint64_t h0 = 0x7370747468ull | (ld64(arena, b + 4) << 40);   // "https" + u[4, 7)
-                w = y ? (h0 >> (8 * y)) | (ld64(arena, b + 7) << (64 - 8 * y)) : h0;
-            }
-        }
-        if (E < y + 8) {   // the tail at E
-            if (E >= y) {
-                const int sh = (int)(E - y) * 8;
-                w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (sh < 64 ? S.tail << sh : 0ull);
-            } else {
-                const int64_t d = y - E;
-                w = d < 8 ? S.tail >> (8 * d) : 0ull;
-            }
-        }
-    }
-    const int64_t r = (int64_t)len3 - y;
-    return r >= 8 ? w : (w & ((1ull << (8 * r)) - 1));
 }
 
 // one row: returns -1 when done, or the cut j of a row that needs slow_row
 template <class Src>
 __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int64_t L, int64_t i,
-                                                 uint8_t *__restrict__ code, const Scratch &S)
+                                                 uint8_t *__restrict__ code, const Scratch &S, uint8_t *out)
 {
-    if (L > ROW_MAX) {   // (the cut word holds 30 bits of length)
-        atomicOr(S.nslow + 1, 1ull);
-        code[i] = KW_URL_NO_HTML;
-        S.len3[i] = 0;
-        S.cut[i] = 0;
-        return -1;
-    }
     if (!S.normalize) {
         // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
         uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
         for (int64_t x0 = 0; x0 < L; x0 += 8) {
             uint64_t w = src.ld64(b + x0);
             if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
+            *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
             h2 = mix2(h2, w);
         }
-        S.cut[i] = (uint32_t)L;
         h1 = fmix(h1 ^ (uint64_t)L);
         h2 = fmix(h2 ^ ((uint64_t)L * 0x9E3779B97F4A7C15ull));
         if (S.weak) h1 &= 0xFull;
@@ -390,10 +338,10 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
                     w = DOTHTML >> ((x0 - E) * 8);
                 }
             }
+            *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
             h2 = mix2(h2, w);
         }
-        S.cut[i] = (uint32_t)E | (ins ? CUT_INS : 0u);
     } else {
         return j;   // the byte-serial rewrite runs in dd_slow_kernel, off the divergent path
     }
@@ -431,10 +379,10 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             LdsSrc src{(const uint32_t *)stage, base};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S);
+            if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
         } else {
             GlobalSrc src{arena};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S);
+            if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
         }
         // rows for the byte-serial rewrite -> the slow list (one atomic per wave)
         const uint64_t sm = __ballot(jslow >= 0);
@@ -490,8 +438,7 @@ __global__ __launch_bounds__(BLOCK) void dd_insert_kernel(const uint8_t *__restr
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void dd_decide_kernel(const uint8_t *__restrict__ arena, int64_t n,
-                                                          uint8_t *__restrict__ code, Scratch S,
+__global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__restrict__ code, Scratch S,
                                                           const int64_t *__restrict__ off)
 {
     unsigned long long c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
@@ -511,10 +458,10 @@ __global__ __launch_bounds__(BLOCK) void dd_decide_kernel(const uint8_t *__restr
             if (rep != i) {
                 bool eq = S.len3[rep] == S.len3[i] && S.h2[rep] == S.h2[i];
                 if (eq) {
-                    const uint32_t len = S.len3[i], ci = S.cut[i], cr = S.cut[rep];
-                    const int64_t bi = off[i], br = off[rep];
-                    for (uint32_t y = 0; y < len && eq; y += 8)
-                        eq = norm8(arena, bi, ci, i, y, len, S) == norm8(arena, br, cr, rep, y, len, S);
+                    const uint64_t *a = (const uint64_t *)(S.out + obase(off[i], i));
+                    const uint64_t *r = (const uint64_t *)(S.out + obase(off[rep], rep));
+                    const uint32_t nw = (S.len3[i] + 7) / 8;
+                    for (uint32_t w = 0; w < nw && eq; ++w) eq = a[w] == r[w];
                 }
                 k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
                 code[i] = k;
@@ -639,12 +586,11 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
 
 // dense kept rows: a wave owns kept rows [k0, k0 + 64) whose dense bytes are one contiguous range
 // [D0, D1).  Lane l handles the 8-aligned destination chunks D0 & ~7 + 8 (l + 64 t): a chunk inside
-// one row is one norm8() (one unaligned 8-byte load of the input row, or of the side arena) and one
-// aligned 8-byte store; a chunk with a row boundary (or a range edge) is assembled from the norm8() of
-// each of the (up to 8) rows it covers, whose offsets all lanes fetch with the same shuffles.  The
-// owner row of a byte is the last of the 64 whose dense offset is <= it (binary search over shuffles).
-__global__ __launch_bounds__(BLOCK) void dd_copy_kernel(const uint8_t *__restrict__ arena, int64_t n_kept,
-                                                        const int64_t *__restrict__ kept_off,
+// one row is one unaligned 8-byte load from the sparse arena and one aligned 8-byte store; a chunk
+// with a row boundary (or a range edge) is written byte by byte from up to 8 rows, whose offsets all
+// lanes fetch with the same shuffles.  The owner row of a byte is the last of the 64 whose dense
+// offset is <= it (binary search over shuffles).
+__global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                         const int64_t *__restrict__ kept_row,
                                                         const int64_t *__restrict__ off, Scratch S,
                                                         uint8_t *__restrict__ dst)
@@ -656,13 +602,11 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(const uint8_t *__restric
         const int64_t kk = k0 + lane;
         const int64_t kend = k0 + 64 < n_kept ? k0 + 64 : n_kept;
         const int64_t D1 = kept_off[kend];
-        int64_t d0 = D1, row = 0, b = 0;   // lanes past the end hold the range end
-        uint32_t cut = 0;
+        int64_t d0 = D1, src = 0;   // lanes past the end hold the range end
         if (kk < n_kept) {
-            row = kept_row[kk];
+            const int64_t row = kept_row[kk];
             d0 = kept_off[kk];
-            b = off[row];
-            cut = S.cut[row];
+            src = obase(off[row], row);
         }
         const int64_t D0 = __shfl(d0, 0, 64);
         for (int64_t x0 = (D0 & ~(int64_t)7) + 8 * (int64_t)lane; x0 - 8 * (int64_t)lane < D1; x0 += 64 * 8) {
@@ -675,13 +619,12 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(const uint8_t *__restric
                 const int64_t dc = __shfl(d0, c & 63, 64);
                 if (c < 64 && dc <= xs) o = c;
             }
-            const int64_t od = __shfl(d0, o, 64), ob = __shfl(b, o, 64), orow = __shfl(row, o, 64);
-            const uint32_t oc = (uint32_t)__shfl((int)cut, o, 64);
+            const int64_t od = __shfl(d0, o, 64), os = __shfl(src, o, 64);
             int64_t nd = __shfl(d0, (o + 1) & 63, 64);
             if (o == 63) nd = D1;
             const bool inner = live && xs == x0 && xe == x0 + 8;   // the whole chunk is this group's
             const bool full = inner && x0 + 8 <= nd;
-            if (full) *(uint64_t *)(dst + x0) = norm8(arena, ob, oc, orow, x0 - od, (uint32_t)(nd - od), S);
+            if (full) *(uint64_t *)(dst + x0) = ld64(S.out, os + (x0 - od));
             const bool edge = live && !full;
             if (__ballot(edge)) {
                 uint64_t w = 0;
@@ -689,21 +632,15 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(const uint8_t *__restric
                 for (int r = 0; r < 8; ++r) {
                     const int idx = o + r;
                     // every lane runs every shuffle (a lane that skips one would not serve its value)
-                    const int64_t sd = __shfl(d0, idx & 63, 64), sb = __shfl(b, idx & 63, 64);
-                    const int64_t srow = __shfl(row, idx & 63, 64);
-                    const uint32_t sc = (uint32_t)__shfl((int)cut, idx & 63, 64);
+                    const int64_t sd = __shfl(d0, idx & 63, 64), rs = __shfl(src, idx & 63, 64);
                     const int64_t sn = __shfl(d0, (idx + 1) & 63, 64);
                     const int64_t rd = idx < 64 ? sd : D1, rn = idx + 1 < 64 ? sn : D1;
                     if (edge) {
                         const int64_t y0 = xs > rd ? xs : rd, y1 = xe < rn ? xe : rn;
-                        if (y1 > y0) {
-                            const uint64_t v = norm8(arena, sb, sc, srow, y0 - rd, (uint32_t)(rn - rd), S);
-                            if (inner) {
-                                w |= v << (8 * (y0 - x0));   // (v's bytes past the row's end are zero)
-                            } else {
-                                for (int64_t y = y0; y < y1; ++y)   // a chunk shared with the neighbouring group
-                                    dst[y] = (uint8_t)(v >> (8 * (y - y0)));
-                            }
+                        for (int64_t y = y0; y < y1; ++y) {
+                            const uint32_t c = S.out[rs + (y - rd)];
+                            if (inner) w |= (uint64_t)c << (8 * (y - x0));
+                            else dst[y] = (uint8_t)c;   // a chunk shared with the neighbouring group
                         }
                     }
                 }
@@ -761,30 +698,20 @@ extern "C" int kw_dedup_create(int32_t device, kw_dedup **out)
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // exact keep-first over the rows that share a hash tag with a different URL
-static int resolve_collisions(kw_dedup *h, const uint8_t *d_arena, const int64_t *d_off, int64_t n, uint8_t *d_code,
-                              hipStream_t st)
+static int resolve_collisions(kw_dedup *h, const int64_t *d_off, int64_t n, uint8_t *d_code, hipStream_t st)
 {
     std::vector<uint8_t> code(n);
     DDCHK(h, hipMemcpyAsync(code.data(), d_code, n, hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
     std::unordered_set<std::string> seen;
-    int64_t b = 0;
-    uint32_t len = 0, cut = 0;
+    std::vector<int64_t> offs(2);
+    std::vector<uint32_t> len(1);
     for (int64_t i = 0; i < n; ++i) {
         if (code[i] != CODE_COLLIDE) continue;
-        DDCHK(h, hipMemcpy(&b, d_off + i, 8, hipMemcpyDeviceToHost));
-        DDCHK(h, hipMemcpy(&len, h->S.len3 + i, 4, hipMemcpyDeviceToHost));
-        DDCHK(h, hipMemcpy(&cut, h->S.cut + i, 4, hipMemcpyDeviceToHost));
-        std::string s(len, '\0');
-        if (len && (cut & CUT_SLOW)) {
-            DDCHK(h, hipMemcpy(&s[0], h->S.out + obase(b, i), len, hipMemcpyDeviceToHost));
-        } else if (len) {   // the splice norm8() reads: [0, E) of the row ('s' after byte 4 if CUT_INS), the tail
-            const uint32_t E = cut & CUT_E, ins = (cut & CUT_INS) ? 1u : 0u;
-            std::string u(E - ins, '\0');
-            if (E > ins) DDCHK(h, hipMemcpy(&u[0], d_arena + b, E - ins, hipMemcpyDeviceToHost));
-            if (ins) u.insert(4, 1, 's');
-            s = u + std::string((const char *)&h->S.tail, len - E);
-        }
+        DDCHK(h, hipMemcpy(offs.data(), d_off + i, 8, hipMemcpyDeviceToHost));
+        DDCHK(h, hipMemcpy(len.data(), h->S.len3 + i, 4, hipMemcpyDeviceToHost));
+        std::string s(len[0], '\0');
+        if (len[0]) DDCHK(h, hipMemcpy(&s[0], h->S.out + obase(offs[0], i), len[0], hipMemcpyDeviceToHost));
         const uint8_t k = seen.insert(s).second ? (uint8_t)KW_URL_KEPT : (uint8_t)KW_URL_DUPLICATE;
         DDCHK(h, hipMemcpy(d_code + i, &k, 1, hipMemcpyHostToDevice));
         ++h->counts[k];
@@ -814,7 +741,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     while (tsize < 2 * (uint64_t)n) tsize <<= 1;
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
-    const size_t need = out_bytes + align256(8 * (size_t)n) * 3 + 2 * align256(4 * (size_t)n) + align256(8 * tsize) +
+    const size_t need = out_bytes + align256(8 * (size_t)n) * 3 + align256(4 * (size_t)n) + align256(8 * tsize) +
                         align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
                         2 * align256(8 * ((size_t)n + 1));
     if (need > h->buf_bytes) {
@@ -831,7 +758,6 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.h1 = (uint64_t *)carve(8 * (size_t)n);
     S.h2 = (uint64_t *)carve(8 * (size_t)n);
     S.len3 = (uint32_t *)carve(4 * (size_t)n);
-    S.cut = (uint32_t *)carve(4 * (size_t)n);
     S.table = (unsigned long long *)carve(8 * tsize);
     S.mask = tsize - 1;
     S.cnt = (unsigned long long *)carve(8 * 8);
@@ -839,7 +765,6 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.slow = (uint2 *)carve(8 * (size_t)n);
     S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
-    S.tail = S.normalize ? DOTHTML : 0ull;
     h->tile_cnt = (unsigned long long *)carve(8 * (size_t)ntiles);
     h->tile_bytes = (unsigned long long *)carve(8 * (size_t)ntiles);
     h->totals = (unsigned long long *)carve(16);
@@ -857,18 +782,14 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     hipLaunchKernelGGL(dd_insert_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S);
     DDCHK(h, hipGetLastError());
     DDCHK(h, hipEventRecord(h->ev[2], st));
-    hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, n, d_code, S, d_off);
+    hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, n, d_code, S, d_off);
     DDCHK(h, hipGetLastError());
-    unsigned long long cnt[8];
+    unsigned long long cnt[5];
     DDCHK(h, hipMemcpyAsync(cnt, S.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
-    if (cnt[7]) {
-        h->err = "kw_dedup_run: a row longer than " + std::to_string(ROW_MAX) + " bytes";
-        return KW_EUNSUPPORTED;
-    }
     for (int k = 0; k < 4; ++k) h->counts[k] = (int64_t)cnt[k];
     if (cnt[CODE_COLLIDE]) {
-        int rc = resolve_collisions(h, d_arena, d_off, n, d_code, st);
+        int rc = resolve_collisions(h, d_off, n, d_code, st);
         if (rc) return rc;
     }
     DDCHK(h, hipEventRecord(h->ev[3], st));
@@ -894,7 +815,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->kept_bytes = (uint8_t *)h->d_kept;
     if (h->n_kept > 0) {
         const int cgrid = (int)std::min<int64_t>((h->n_kept + 63) / 64 * 64 / BLOCK + 1, (int64_t)h->cus * 8);
-        hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, d_arena, h->n_kept, (const int64_t *)h->kept_off,
+        hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, h->n_kept, (const int64_t *)h->kept_off,
                            (const int64_t *)h->kept_row, d_off, S, h->kept_bytes);
         DDCHK(h, hipGetLastError());
     }
