@@ -190,9 +190,10 @@ struct QStats {
 };
 
 struct FastBuild {
-    std::vector<uint32_t> mid, p2, l2, t3, b2, edge_pre, edge_suf;
+    std::vector<uint32_t> s1, p2, l2, t3, b2, edge_pre, edge_suf;
     int has_short = 0;
     int has_t3 = 0;
+    uint32_t gate[6] = {0, 0, 0, 0, 0, 0};   // stage-1 pair box (FastTables::gate)
     std::vector<uint64_t> ht_key, as_head, sig, bsig;
     std::vector<uint32_t> ht_begin, ht_cnt, kl, as_len, as_use_begin, as_use_cnt, use_pat, use_info0, use_info1,
         rxk, boff;
@@ -446,27 +447,46 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         }
     }
     if (B.use_pat.size() > IT_USE_MASK) { err = "kw_compile: more than 2^19 anchor uses"; return KW_EUNSUPPORTED; }
-    // ---- LDS filters (stage 1: mid entries + exact pair table; stage 2: l2 / t3 / b2), global hash table
-    B.mid.assign(2 * (size_t)FK_MID_ENTRIES, 0);
+    // ---- LDS filters (stage 1: 4-gram table + exact pair table; stage 2: l2 / t3 / b2), global hash table
+    B.s1.assign(FK_S1_WORDS, 0);
     B.p2.assign(FK_P2_WORDS, 0);
     B.l2.assign(FK_L2_WORDS, 0);
     B.t3.assign(FK_T3_WORDS, 0);
     B.b2.assign(FK_B2_WORDS, 0);
     std::unordered_map<uint64_t, std::vector<uint32_t>> keys;
+    uint32_t s1_ext = 0;                         // 4-grams the fuzzy 3-byte anchors added to the stage-1 table
+    uint32_t box[4] = {255u, 0u, 255u, 0u};      // first byte lo / hi, second byte lo / hi of the boxed anchors
     for (uint32_t a = 0; a < na; ++a) {
         const std::string &st = astr[a];
         const uint8_t *p = (const uint8_t *)st.data();
         if (st.size() >= 4) {
             const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-            // start at an even position E: entry of bytes 1..3, low word; at E + 1: entry of bytes 0..2, high word
-            B.mid[2 * (size_t)fk_mid_entry(k4 >> 8)] |= 1u << fk_fold0(p[0], p[1]);
-            B.mid[2 * (size_t)fk_mid_entry(k4) + 1] |= 1u << fk_fold(p[3]);
+            const uint32_t h1 = fk_s1_hash(k4, k4 >> 8);
+            B.s1[fk_s1_word(h1)] |= 1u << (h1 & 31);
             B.l2[fk_l2_index(k4) >> 5] |= 1u << (fk_l2_index(k4) & 31);
             keys[(4ull << 32) | k4].push_back(a);
         } else if (st.size() >= 2) {
             const uint32_t k2 = (uint32_t)p[0] | ((uint32_t)p[1] << 8);
             B.p2[fk_b2_index(k2) >> 5] |= 1u << (fk_b2_index(k2) & 31);
-            B.has_short = 1;
+            // stage 1: a fuzzy 3-byte anchor (a whole name, found anywhere) as the 256 4-grams that start with
+            // it while their number is small; every other short anchor (the uppercase names' whole 2-3 bytes)
+            // through the pair box
+            bool upper_only = true;
+            for (const auto &u : auses[a]) upper_only = upper_only && (u.i0 & 0xFFu) == FU_UPPER;
+            if (st.size() == 3 && !upper_only && s1_ext < FK_S1_EXT_MAX) {
+                for (uint32_t x = 0; x < 256; ++x) {
+                    const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (x << 24);
+                    const uint32_t h1 = fk_s1_hash(k4, k4 >> 8);
+                    B.s1[fk_s1_word(h1)] |= 1u << (h1 & 31);
+                }
+                s1_ext += 256;
+            } else {
+                box[0] = std::min<uint32_t>(box[0], p[0]);
+                box[1] = std::max<uint32_t>(box[1], p[0]);
+                box[2] = std::min<uint32_t>(box[2], p[1]);
+                box[3] = std::max<uint32_t>(box[3], p[1]);
+                B.has_short = 1;
+            }
             if (st.size() == 3) {
                 const uint32_t k3 = k2 | ((uint32_t)p[2] << 16);
                 B.t3[fk_t3_index(k3) >> 5] |= 1u << (fk_t3_index(k3) & 31);
@@ -479,6 +499,18 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         } else {
             err = "kw_compile: one-byte anchor";
             return KW_EUNSUPPORTED;
+        }
+    }
+    // the box as SWAR range constants per byte: bytes < 0x80 in [lo, hi] by two additions, bytes >= 0x80 all
+    // in (one flag) when the range reaches them
+    if (B.has_short) {
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t lo = box[2 * r], hi = box[2 * r + 1];
+            const uint32_t alo = std::min(lo, 0x80u), ahi = std::min(hi, 0x7Fu);
+            const uint32_t A = alo <= ahi ? 0x80u - alo : 0u, Bc = alo <= ahi ? 0x7Fu - ahi : 0u;
+            B.gate[3 * r] = A * 0x01010101u;
+            B.gate[3 * r + 1] = Bc * 0x01010101u;
+            B.gate[3 * r + 2] = hi >= 0x80u ? 0x80808080u : 0u;
         }
     }
     uint32_t hs = 1024;
@@ -921,7 +953,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            o_rxa = push_array(blob, atoms), o_wb = push_array(blob, wb), o_fc = push_array(blob, f_count_ge),
            o_sk = push_array(blob, sub_key), o_sb = push_array(blob, sub_begin), o_sc = push_array(blob, sub_cnt),
            o_sp = push_array(blob, sub_pat);
-    size_t f_mid = push_array(blob, FB.mid), f_p2 = push_array(blob, FB.p2), f_b2 = push_array(blob, FB.b2), f_l2 = push_array(blob, FB.l2),
+    size_t f_s1 = push_array(blob, FB.s1), f_p2 = push_array(blob, FB.p2), f_b2 = push_array(blob, FB.b2), f_l2 = push_array(blob, FB.l2),
            f_t3 = push_array(blob, FB.t3), f_epre = push_array(blob, FB.edge_pre), f_esuf = push_array(blob, FB.edge_suf), f_htk = push_array(blob, FB.ht_key),
            f_htb = push_array(blob, FB.ht_begin), f_htc = push_array(blob, FB.ht_cnt), f_kl = push_array(blob, FB.kl),
            f_ash = push_array(blob, FB.as_head), f_asl = push_array(blob, FB.as_len),
@@ -981,7 +1013,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     T.empty_pat = empty_pat;
 
     FastTables &F = h->FT;
-    F.mid = (const uint2 *)(B + f_mid);
+    F.s1 = (const uint32_t *)(B + f_s1);
     F.p2 = (const uint32_t *)(B + f_p2);
     F.b2 = (const uint32_t *)(B + f_b2);
     F.l2 = (const uint32_t *)(B + f_l2);
@@ -990,6 +1022,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.edge_suf = (const uint32_t *)(B + f_esuf);
     F.has_t3 = FB.has_t3;
     F.has_short = FB.has_short;
+    for (int r = 0; r < 6; ++r) F.gate[r] = FB.gate[r];
     F.ht_key = (const uint64_t *)(B + f_htk);
     F.ht_begin = (const uint32_t *)(B + f_htb);
     F.ht_cnt = (const uint32_t *)(B + f_htc);

@@ -19,25 +19,22 @@
 // over its field after the decision (rx_positions).
 // Any anchor choice is correct; only the speed depends on the statistics.
 //
-// Filters (all in LDS).  Stage 1 looks at every EVEN byte position E and
-// decides for the two starts E and E+1 at once: one 64-bit "mid" entry chosen
-// by the three bytes E+1..E+3 holds two 32-bit families, bit fold(b[E]) of
-// the low word for an anchor (>= 4 bytes) starting at E and bit fold(b[E+4])
-// of the high word for one starting at E+1 (an anchor's first four bytes set
-// one bit in each family).  Anchors of 2-3 bytes: their first two bytes in an
-// exact 64K-bit pair table, tested for the pairs (E, E+1) and (E+1, E+2).
-// Stage 2, compacted survivors only: an independent hash of the 4-byte key
-// (2^17 bits), of the 3-byte key (2^14 bits) or of the 2-byte key (2^14 bits)
-// must hit before the global anchor hash table is probed.  Field edges: the
-// first / last four bytes of a field are tested against the prefix / suffix
-// keys of the one-deletion variants (2 x 2^15 bits); only flagged fields run
-// the edge check.
+// Filters (all in LDS).  Stage 1 looks at every byte position j: the 4-gram
+// starting there is hashed (two 24-bit products: bytes j..j+2 and j+1..j+3,
+// fk_s1_hash) into a 2^19-bit table of the anchors' first four bytes; anchors
+// of 2-3 bytes: their first two bytes in an exact 64K-bit pair table.  Only the
+// survivors (~1 % of the positions) run stage 2, each in its own lane: an
+// independent hash of the 4-byte key (2^17 bits), of the 3-byte key (2^14 bits)
+// or of the 2-byte key (2^14 bits) must hit before the global anchor hash
+// table is probed.  Field edges: the first / last four bytes of a field are
+// tested against the prefix / suffix keys of the one-deletion variants
+// (2 x 2^15 bits); only flagged fields run the edge check.
 #pragma once
 #include "kwmatch_device.hpp"
 
 namespace kw {
 
-constexpr int FK_MID_ENTRIES = 4096;            // stage 1: 4096 x 64 bits = 32 KB
+constexpr int FK_S1_BITS = 19;                  // stage 1: 2^19 bits = 64 KB
 constexpr int FK_P2_WORDS = 2048;               // stage 1, 2-3 byte anchors: exact pair table, 8 KB
 constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
 constexpr int FK_T3_BITS = 14;                  // stage 2, 3-byte keys: 2 KB
@@ -56,6 +53,10 @@ constexpr uint32_t FK_MUL2 = 0x85EBCA6Bu;
 constexpr uint32_t FK_MUL3 = 0xC2B2AE35u;
 constexpr uint32_t FK_MUL4 = 0x27D4EB2Fu;
 
+constexpr int FK_S1_WORDS = 1 << (FK_S1_BITS - 5);
+constexpr uint32_t FK_S1_M1 = 0xD2511Fu;        // stage-1 hash multipliers (24 bits: v_mul_u32_u24 / v_mad_u32_u24)
+constexpr uint32_t FK_S1_M2 = 0x9E3779u;
+constexpr uint32_t FK_S1_EXT_MAX = 16384;       // stage-1 4-grams of the fuzzy 3-byte anchors (256 each)
 constexpr int FK_L2_WORDS = 1 << (FK_L2_BITS - 5);
 constexpr int FK_T3_WORDS = 1 << (FK_T3_BITS - 5);
 constexpr int FK_B2_WORDS = 1 << (FK_B2_BITS - 5);
@@ -86,14 +87,15 @@ constexpr uint32_t DH_RESOLVE = 1u << 24;       // non-ASCII document left to th
 static_assert(FK_ITEMS0 < 1024 && FK_ITEMS1 < 128, "item counts must fit the document header");
 
 struct FastTables {
-    const uint2 *mid;           // FK_MID_ENTRIES: {start at E: bit fk_fold0, start at E+1: bit fk_fold(b[E+4])}
+    const uint32_t *s1;         // FK_S1_WORDS: the anchors' first four bytes (fk_s1_hash)
     const uint32_t *p2;         // FK_P2_WORDS: first two bytes of the 2-3 byte anchors (exact)
     const uint32_t *l2;         // FK_L2_WORDS
     const uint32_t *t3;         // FK_T3_WORDS
     const uint32_t *b2;         // FK_B2_WORDS
     const uint32_t *edge_pre;   // FK_EDGE_WORDS
     const uint32_t *edge_suf;   // FK_EDGE_WORDS
-    int has_short;              // any 2- or 3-byte anchor
+    int has_short;              // any 2- or 3-byte anchor in the stage-1 pair box
+    uint32_t gate[6];           // the pair box: first byte {A, B, N}, second byte {A, B, N} (fk_in_box)
     int has_t3;                 // any 3-byte anchor
     const uint64_t *ht_key;     // (len << 32) | key bytes; ~0 = empty
     const uint32_t *ht_begin;
@@ -200,19 +202,14 @@ struct FastScratch {
 };
 
 // host + device hashes of the LDS tables
-// stage-1 mid entry of three bytes (low 24 bits of k3): bits 20..31 of the 24-bit product (the high half of a
-// v_mul_hi would hardly depend on the low byte)
-__host__ __device__ __forceinline__ uint32_t fk_mid_entry(uint32_t k3) { return ((k3 & 0xFFFFFFu) * FK_MUL1) >> 20; }
-// a byte folded to 5 bits: b + (b >> 5) keeps upper and lower case apart
-__host__ __device__ __forceinline__ uint32_t fk_fold(uint32_t b) { return (b + (b >> 5)) & 31u; }
-// the start-at-E family's bit: the device adds the byte and the dword shifted right by 8 * jj + 5, whose low
-// five bits also carry the next byte's bits 0..1 (v_add_u32 with a byte select; v_bfe_u32 reads 5 bits)
-__host__ __device__ __forceinline__ uint32_t fk_fold0(uint32_t b0, uint32_t b1)
+// stage 1: the 4-gram b0..b3 at a position as k0 = b0 | b1 << 8 | b2 << 16 and k1 = b1 | b2 << 8 | b3 << 16 (the
+// next position's k0): h = k0 * M1 + k1 * M2 (mod 2^32; on the device one v_mul_u32_u24 per position and one
+// v_mad_u32_u24 whose k1 is the next position's key).  Word h >> 18 of the table, bit h & 31.
+__host__ __device__ __forceinline__ uint32_t fk_s1_hash(uint32_t k0, uint32_t k1)
 {
-    return (b0 + (b0 >> 5) + ((b1 & 3u) << 3)) & 31u;
+    return (k0 & 0xFFFFFFu) * FK_S1_M1 + (k1 & 0xFFFFFFu) * FK_S1_M2;
 }
-// device: the mid entry's LDS byte offset (= 8 * fk_mid_entry)
-__device__ __forceinline__ uint32_t fk_mid_byte(uint32_t k3) { return (__umul24(k3, FK_MUL1) >> 17) & (8u * FK_MID_ENTRIES - 8u); }
+__host__ __device__ __forceinline__ uint32_t fk_s1_word(uint32_t h) { return h >> (32 - FK_S1_BITS + 5); }
 __device__ __forceinline__ uint32_t lds_word_at(const uint32_t *t, uint32_t byte_off)
 {
     return *(const uint32_t *)((const uint8_t *)t + byte_off);

@@ -1,11 +1,11 @@
 // The fast path's byte scan as three kernels (gfx950).  Included after kwmatch_fast_kernel.hpp, whose
 // probe, epilogue and field helpers it reuses.
 //
-//   kw_filter_kernel  one wave per document (grid-stride): the LDS filters over every byte position; the
+//   kw_filter_kernel  a wave per 32-document group (grid-stride): the LDS filters over every byte position; the
 //                     stage-2 survivors ("candidates", 4 bytes: position in the document << 8 | document
 //                     in its group << 3 | key lengths to probe, after a header record per group) go to the
 //                     wave's region in HBM in document and position order, with the document's flags (non-ASCII fields, edge prefilter, field
-//                     too long) in its header.  Few registers, 64 KiB of LDS: two workgroups per CU.
+//                     too long) in its header.  96 KiB of LDS: one 16-wave workgroup per CU.
 //   kw_probe_kernel   one wave per filter region: the region's candidates 64 at a time, whatever document
 //                     they belong to (a document averages ~13 candidates, so per-document batches left most
 //                     lanes idle): anchor hash probe, head compare, then the (candidate, use) pairs spread
@@ -28,10 +28,7 @@
 namespace kw {
 
 #ifndef FS_WAVES_CFG
-#define FS_WAVES_CFG 8
-#endif
-#ifndef FS_AHEAD
-#define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
+#define FS_WAVES_CFG 16
 #endif
 #ifndef FS_MINW
 #define FS_MINW 1
@@ -60,15 +57,15 @@ constexpr int EK_BLOCK = EK_WAVES * WAVE;
 constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range; 5 bits of a candidate)
 
 struct __attribute__((aligned(16))) FilterLds {
-    uint2 mid[FK_MID_ENTRIES];
+    uint32_t s1[FK_S1_WORDS];
     uint32_t p2[FK_P2_WORDS];
     uint32_t l2[FK_L2_WORDS];
     uint32_t t3[FK_T3_WORDS];
     uint32_t b2[FK_B2_WORDS];
-    uint32_t tile[FS_WAVES][4 * WAVE + 4];    // the tile's bytes (+ the word after it) for stage 2's keys
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
-    uint32_t stg[FS_WAVES][WAVE];             // stage-2 starts of one round (lane << 4 | j | flags)
+    uint32_t skey[FS_WAVES][2 * WAVE];        // stage 2: the queue of survivors' 4-byte keys ...
+    uint32_t spos[FS_WAVES][2 * WAVE];        // ... and group-relative positions (a ring of 128)
 };
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
@@ -93,41 +90,85 @@ __device__ __forceinline__ uint32_t fk_b2_mul(uint32_t key)
     return r;
 }
 
-// Stage 1 of one lane's 16 bytes W[0..3] (+ W[4], the next lane's first word): bit j of `hit` = an anchor of
-// >= 4 bytes may start at position j, bit j of `gate` = a 2-3 byte anchor may (its first two bytes are an
-// exact pair).  Only even positions E are looked up; each decides the starts E and E + 1.
-template <bool SHORT>
-__device__ __forceinline__ void fk_stage1(const FilterLds &L, const uint32_t (&W)[5], uint32_t &hit, uint32_t &gate)
+// the four bytes at lane position j (0..15) of W[0..3] (+ W[4], the next lane's first word); j is not a
+// compile-time constant: the words are selected without dynamic register indexing
+__device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], uint32_t j)
 {
-    uint2 mw[8];
-    uint32_t pw[16], pm[16];
+    // bit-select masks (v_bfi_b32): a select chain written with ?: is turned into an indexed array, and the
+    // array of every tile in flight into LDS
+    const uint32_t m1 = 0u - ((j >> 2) & 1u), m2 = 0u - ((j >> 3) & 1u);
+    const uint32_t l01 = (W[0] & ~m1) | (W[1] & m1), l23 = (W[2] & ~m1) | (W[3] & m1);
+    const uint32_t h01 = (W[1] & ~m1) | (W[2] & m1), h23 = (W[3] & ~m1) | (W[4] & m1);
+    const uint32_t lo = (l01 & ~m2) | (l23 & m2), hi = (h01 & ~m2) | (h23 & m2);
+    return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
+}
+
+// Stage-1 masks use the transposed bit order of a lane's 16 positions: position j = 4 q + r (q = its word, r =
+// its byte) is bit q + 8 r, the order in which the pair box's per-byte flags of the four words combine with
+// one shift each.
+__device__ __forceinline__ constexpr uint32_t fk_tbit(int j) { return (uint32_t)((j >> 2) + 8 * (j & 3)); }
+__device__ __forceinline__ uint32_t fk_tpos(uint32_t b) { return ((b & 7u) << 2) + (b >> 3); }
+// position order of a transposed mask: the bytes' nibbles packed (row r = byte, column q), then a 4 x 4 bit
+// transpose by two delta swaps
+__device__ __forceinline__ uint32_t fk_untranspose(uint32_t t)
+{
+    uint32_t x = (t & 0xFu) | ((t >> 4) & 0xF0u) | ((t >> 8) & 0xF00u) | ((t >> 12) & 0xF000u);
+    uint32_t d = (x ^ (x >> 3)) & 0x0A0Au;
+    x ^= d ^ (d << 3);
+    d = (x ^ (x >> 6)) & 0x00CCu;
+    x ^= d ^ (d << 6);
+    return x;
+}
+__device__ __forceinline__ uint32_t fk_transpose16(uint32_t v)
+{
+    uint32_t t = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int j = 2 * e, q = j >> 2, jj = j & 3;
-        const uint32_t km = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj + 1);   // bytes j+1 .. j+4
-        mw[e] = *(const uint2 *)((const uint8_t *)L.mid + fk_mid_byte(km));
-        if (SHORT) {
-            const uint32_t k0 = jj ? (W[q] >> 16) : W[q];                           // bytes j, j+1
-            pm[2 * e] = fk_b2_mul(k0);
-            pm[2 * e + 1] = fk_b2_mul(km);
-            pw[2 * e] = lds_word_at(L.p2, (pm[2 * e] >> 3) & (4u * FK_P2_WORDS - 4u));
-            pw[2 * e + 1] = lds_word_at(L.p2, (pm[2 * e + 1] >> 3) & (4u * FK_P2_WORDS - 4u));
+    for (int j = 0; j < 16; ++j) t |= ((v >> j) & 1u) << fk_tbit(j);
+    return t;
+}
+
+// the pair box's byte flags of a word: bit 7 of byte i set iff byte i is in the box's range {A, B, N}
+__device__ __forceinline__ uint32_t fk_in_box(uint32_t x, uint32_t A, uint32_t B, uint32_t N)
+{
+    const uint32_t t = x & 0x7F7F7F7Fu;
+    return (((t + A) & ~(t + B) & ~x) | (x & N)) & 0x80808080u;
+}
+
+// Stage 1 of one lane's 16 bytes W[0..3] (+ W[4]): `hit` = positions where an anchor of >= 4 bytes may start
+// (its first four bytes' bit in the 4-gram table; also the fuzzy 3-byte anchors' 4-grams), `gate` = positions
+// whose first two bytes lie in the pair box of the other 2-3 byte anchors (SWAR, no lookup); transposed bit
+// order (fk_tbit).  The 4-gram hash of position j reuses position j + 1's key (fk_s1_hash): one
+// v_mul_u32_u24 and one v_mad_u32_u24 per position.
+template <bool SHORT>
+__device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds &L, const uint32_t (&W)[5],
+                                          uint32_t &hit, uint32_t &gate)
+{
+    uint32_t k[17];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) k[j] = (j & 3) ? __builtin_amdgcn_alignbyte(W[(j >> 2) + 1], W[j >> 2], j & 3) : W[j >> 2];
+    k[16] = W[4];
+    uint32_t hh[16], sw[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        hh[j] = __umul24(k[j], FK_S1_M1) + __umul24(k[j + 1], FK_S1_M2);
+        sw[j] = lds_word_at(L.s1, (hh[j] >> 16) & (4u * FK_S1_WORDS - 4u));
+    }
+    uint32_t g = 0;
+    if (SHORT) {
+        uint32_t f0[4], f1[5];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f0[q] = fk_in_box(W[q], FT.gate[0], FT.gate[1], FT.gate[2]);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) f1[q] = fk_in_box(W[q], FT.gate[3], FT.gate[4], FT.gate[5]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pr = f0[q] & __builtin_amdgcn_alignbyte(f1[q + 1], f1[q], 1);   // byte i: b[i], b[i+1]
+            g |= pr >> (7 - q);
         }
     }
-    uint32_t h = 0, g = 0;
+    uint32_t h = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int j = 2 * e, q = j >> 2, jj = j & 3;
-        const uint32_t km = __builtin_amdgcn_alignbyte(W[q + 1], W[q], jj + 1);
-        const uint32_t o0 = __builtin_amdgcn_ubfe(W[q], 8 * jj, 8) + (W[q] >> (8 * jj + 5));   // fk_fold0
-        const uint32_t o1 = (km >> 24) + (km >> 29);                                           // fk_fold(b[j+4])
-        h |= __builtin_amdgcn_ubfe(mw[e].x, o0, 1) << j;
-        h |= __builtin_amdgcn_ubfe(mw[e].y, o1, 1) << (j + 1);
-        if (SHORT) {
-            g |= __builtin_amdgcn_ubfe(pw[2 * e], pm[2 * e], 1) << j;
-            g |= __builtin_amdgcn_ubfe(pw[2 * e + 1], pm[2 * e + 1], 1) << (j + 1);
-        }
-    }
+    for (int j = 0; j < 16; ++j) h |= __builtin_amdgcn_ubfe(sw[j], hh[j], 1) << fk_tbit(j);
     hit = h;
     gate = g;
 }
@@ -147,11 +188,10 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const int lane = lane_id();
     const uint32_t *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
-    uint32_t *stg = L.stg[wib];
-    uint32_t *tbuf = L.tile[wib];
+    uint32_t *skey = L.skey[wib], *spos = L.spos[wib];
     uint32_t *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
-    const bool has_t3 = FT.has_t3 != 0;
+    const uint32_t t3on = FT.has_t3 ? 1u : 0u;
     const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
     for (int64_t g = wave; g < n_groups; g += n_waves) {
         const int64_t d0 = g * FG_DOCS;
@@ -169,8 +209,9 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         if (lane < nd) dtitle[lane] = (uint32_t)(o1 - gb);
         wave_sync();
         int64_t blk = gb & ~(int64_t)15;
-        uint32_t kdoc = 0;   // document of the current tile's first byte (candidate emission)
+        uint32_t kdoc = 0;   // document of the current stage-2 round's first survivor (candidate emission)
         bool ghdr = true;    // the group's header record is not written yet
+        uint32_t qh = 0, qn = 0;   // the survivor queue's head and length (wave-uniform)
         // Three tiles in flight per wave, each in its own registers (the loop is unrolled by three, so no
         // register copy waits for a load).  Loads are unconditional: an address past the group's last
         // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
@@ -180,6 +221,49 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const int64_t a = tb + 16 * (int64_t)lane, e = tb + 1024;
             v = *(const uint4 *)(arena + (a < glast ? a : glast));
             w = *(const uint32_t *)(arena + (e < glast ? e : glast));
+        };
+        // Stage 2, one round: the queue's first n (<= 64) survivors, lane = survivor, in position order; the
+        // three second filters (every key length's: a superset of what the stage-1 family asked for, the short
+        // keys behind the exact pair table); the final survivors ("candidates") ranked by ballot and written
+        // with their document
+        auto round = [&](uint32_t n) {
+            wave_sync();
+            const bool act = (uint32_t)lane < n;
+            const uint32_t slot = (qh + (uint32_t)lane) & (2u * WAVE - 1u);
+            const uint32_t key = skey[slot], r = spos[slot];
+            wave_sync();
+            qh = (qh + n) & (2u * WAVE - 1u);
+            qn -= n;
+            const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
+            const uint32_t pr = (uint32_t)lds_bit(L.p2, fk_b2_index(key));
+            const uint32_t b3 = pr & t3on & (uint32_t)lds_bit(t3, fk_t3_index(key));
+            const uint32_t bb = pr & (uint32_t)lds_bit(b2, fk_b2h_index(key));
+            const uint32_t fl = b4 | (b3 << 1) | (bb << 2);
+            {
+                const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);   // the round's first position
+                while (dstart[kdoc + 1] <= r0) ++kdoc;
+            }
+            bool keep = act && fl != 0u;
+            uint32_t k = kdoc, pd = 0;
+            if (keep) {
+                while (dstart[k + 1] <= r) ++k;
+                pd = r - dstart[k];
+                keep = pd < (1u << 24);   // (a longer document has a field over 8 MiB: the generic kernel's)
+            }
+            const uint64_t pm = __ballot(keep);
+            if (pm) {
+                // the group's header record precedes its first candidate (fl = 0: the group index)
+                if (ghdr) {
+                    if (lane == 0 && ccur < ccap) cand[ccur] = (uint32_t)g << 3;
+                    ++ccur;
+                    ghdr = false;
+                }
+                const uint32_t kk = ccur + mbcnt(pm);
+                if (keep && kk < ccap) cand[kk] = (pd << 8) | (k << 3) | fl;
+            }
+            const uint32_t np = (uint32_t)__popcll(pm);
+            ccur += np;
+            ncand2 += (lane == 0) ? np : 0u;
         };
         auto tile = [&](const uint4 &v, uint32_t w4, int64_t tb) {
             const int64_t lp = tb + 16 * (int64_t)lane;
@@ -196,7 +280,8 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const int jlo = rlo <= 0 ? 0 : (rlo >= 16 ? 16 : rlo);                // capped at 2^31 bytes
             const int jhi = rhi <= 0 ? 0 : (rhi >= 16 ? 16 : rhi);
             const uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
-            const uint32_t rel = (uint32_t)(lp - gb);   // group-relative byte of this lane's position 0
+            const uint32_t rel = (uint32_t)(lp - gb);   // group-relative byte of this lane's position 0 (wraps
+                                                        // below the group start: only valid positions are used)
             if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
                 uint32_t hb = 0;
 #pragma unroll
@@ -217,74 +302,34 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 }
             }
             uint32_t hit, gate;
-            fk_stage1<SHORT>(L, W, hit, gate);
-            hit &= valid;
-            gate &= valid;
-            ncand += (uint32_t)__popc(hit);
-            // stage 2 over the wave: the tile's stage-1 starts compacted into 64-entry rounds (lane = start;
-            // usually one round), their keys read back from the tile staged in LDS, the stage-2 lookups,
-            // then the survivors ("candidates") ranked by ballot and written with their document
-            const uint32_t sm = hit | gate;
+            fk_stage1<SHORT>(FT, L, W, hit, gate);
+            const uint32_t tvalid = valid == 0xFFFFu ? 0x0F0F0F0Fu : fk_transpose16(valid);
+            const uint32_t sm = (hit | gate) & tvalid;
+            ncand += (uint32_t)__popc(sm);
+            // the tile's survivors join the wave's queue in position order (each written by the lane that owns
+            // it: its 4-byte key and group-relative position); stage 2 runs on full rounds of 64
             int ts;
             const int sx = wave_excl_scan_dpp(__popc(sm), &ts);
             if (ts == 0) return;
-            *(uint4 *)(tbuf + 4 * lane) = v;
-            if (lane == WAVE - 1) tbuf[4 * WAVE] = w4;
-            {
-                const int64_t r0 = tb - gb;
-                const uint32_t rt = r0 > 0 ? (uint32_t)r0 : 0u;
-                while (dstart[kdoc + 1] <= rt) ++kdoc;
-            }
-            const uint32_t rtile = (uint32_t)(tb - gb);   // group-relative byte of lane 0's position 0 (wraps
-                                                          // below the group start: only valid positions are read)
-            for (int c0 = 0; c0 < ts; c0 += WAVE) {
+            const uint32_t smp = fk_untranspose(sm);   // position order: the candidates' order
+            for (int c0 = 0; c0 < ts;) {
+                const int take = min((int)(2u * WAVE - qn), ts - c0);
                 {
-                    uint32_t hm = sm;
                     int rk = sx;
-                    while (hm) {
-                        const int j = __ffs(hm) - 1;
-                        hm &= hm - 1;
-                        if (rk >= c0 + WAVE) break;
-                        if (rk >= c0)
-                            stg[rk - c0] = ((uint32_t)lane << 4) | (uint32_t)j | (((hit >> j) & 1u) << 10) |
-                                           (((gate >> j) & 1u) << 11);
+                    for (uint32_t hm = smp; hm; hm &= hm - 1u) {
+                        if (rk >= c0 + take) break;
+                        if (rk >= c0) {
+                            const uint32_t j = (uint32_t)(__ffs(hm) - 1);
+                            const uint32_t slot = (qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u);
+                            skey[slot] = fk_key_at(W, j);
+                            spos[slot] = rel + j;
+                        }
                         ++rk;
                     }
                 }
-                wave_sync();
-                const bool act = c0 + lane < ts;
-                const uint32_t e = act ? stg[lane] : 0u;
-                const uint32_t ob = e & 1023u;   // byte of the start in the staged tile
-                const uint32_t key = __builtin_amdgcn_alignbyte(tbuf[(ob >> 2) + 1], tbuf[ob >> 2], ob & 3u);
-                wave_sync();
-                const bool h1 = (e >> 10) & 1u, g1 = (e >> 11) & 1u;
-                const uint32_t b4 = (h1 && lds_bit(l2, fk_l2_index(key))) ? 1u : 0u;
-                const uint32_t b3 = (g1 && has_t3 && lds_bit(t3, fk_t3_index(key))) ? 2u : 0u;
-                const uint32_t bb = (g1 && lds_bit(b2, fk_b2h_index(key))) ? 4u : 0u;
-                const uint32_t fl = b4 | b3 | bb;
-                const bool pass = act && fl != 0u;
-                uint32_t k = kdoc, pd = 0;
-                bool keep = pass;
-                if (pass) {
-                    const uint32_t r = rtile + ob;
-                    while (dstart[k + 1] <= r) ++k;
-                    pd = r - dstart[k];
-                    keep = pd < (1u << 24);   // (a longer document has a field over 8 MiB: the generic kernel's)
-                }
-                const uint64_t pm = __ballot(keep);
-                if (pm) {
-                    // the group's header record precedes its first candidate (fl = 0: the group index)
-                    if (ghdr) {
-                        if (lane == 0 && ccur < ccap) cand[ccur] = (uint32_t)g << 3;
-                        ++ccur;
-                        ghdr = false;
-                    }
-                    const uint32_t kk = ccur + mbcnt(pm);
-                    if (keep && kk < ccap) cand[kk] = (pd << 8) | (k << 3) | fl;
-                }
-                const uint32_t np = (uint32_t)__popcll(pm);
-                ccur += np;
-                ncand2 += (lane == 0) ? np : 0u;
+                qn += (uint32_t)take;
+                c0 += take;
+                while (qn >= (uint32_t)WAVE) round(WAVE);
             }
         };
         uint4 v0, v1, v2;
@@ -306,6 +351,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             load(v2, w2, blk + 3072);
             blk += 1024;
         }
+        while (qn) round(qn < (uint32_t)WAVE ? qn : (uint32_t)WAVE);   // the group's last survivors
     }
 }
 
@@ -315,9 +361,9 @@ __global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables
 {
     __shared__ FilterLds L;
     {
-        const uint4 *src = (const uint4 *)FT.mid;
-        uint4 *dst = (uint4 *)L.mid;
-        for (int i = threadIdx.x; i < FK_MID_ENTRIES / 2; i += FS_BLOCK) dst[i] = src[i];
+        const uint4 *src = (const uint4 *)FT.s1;
+        uint4 *dst = (uint4 *)L.s1;
+        for (int i = threadIdx.x; i < FK_S1_WORDS / 4; i += FS_BLOCK) dst[i] = src[i];
     }
     for (int i = threadIdx.x; i < FK_P2_WORDS; i += FS_BLOCK) L.p2[i] = FT.p2[i];
     for (int i = threadIdx.x; i < FK_L2_WORDS; i += FS_BLOCK) L.l2[i] = FT.l2[i];
