@@ -132,3 +132,51 @@ def test_c4_gpu_vs_live_oracle(c4, c4_gpu):
     for d in bad[:3]:
         print(d, got[d], want_t[d], want_i[d])
     assert not bad, f"config-4 GPU results differ from the oracle on docs {bad[:20]}"
+
+
+@pytest.mark.gpu
+def test_c4_whole_corpus_vs_oracle_digests():
+    """EVERY document of bench.py --workload kb50k's 1M-article corpus (config 4: the ~52k-name synthetic KB):
+    the GPU's per-document record digest equals the CPU oracle's (tests/golden/c4_digests.npz, made in the
+    build container by tests/golden/make_c2_digests.py --config 4), and so do the record count and the
+    bench line's hits_digest."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    import bench
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher, background_sample, records_from_tensor
+    from advanced_scrapper_amd.synth_kb import synthetic_kb
+    from tests import corpus_digest as cd
+    meta = json.load(open(os.path.join(HERE, 'c4_digests.json')))
+    z = np.load(os.path.join(HERE, 'c4_digests.npz'))
+    n, seed = meta['n_docs'], meta['seed']
+    processed = synthetic_kb(2300, seed)
+    ckb = compile_kb(processed)
+    names, kinds = synth.injectable_names(ckb)
+    corpus = synth.generate(n, names, kinds, seed=seed, doc_base=0)
+    assert cd.corpus_fingerprint(corpus) == meta['corpus_fingerprint'], 'the generator no longer makes the pinned corpus'
+    bg = synth.generate(2000, names, kinds, seed=seed + 7777, doc_base=0)
+    m = GpuMatcher(ckb, 0, background_sample(bg.texts() + bg.titles()))
+    d_arena, d_off = m.upload(corpus.arena, corpus.off)
+    m.scan(d_arena, d_off, n)
+    hits = m.hits_device().clone()
+    rec = records_from_tensor(hits)
+    dig, cnt = cd.per_doc(rec, n)
+    bad = np.flatnonzero((dig != z['digest']) | (cnt != z['count'].astype(np.int64)))
+    if len(bad):
+        from advanced_scrapper_amd.matcher import group_hits
+        g = group_hits(rec[np.isin(rec['doc'], bad[:3].astype(np.uint32))])
+        want = oracle_pool.field_results(processed, [s for d in bad[:3].tolist()
+                                                     for s in (corpus.text(d), corpus.title(d))], 3)
+        for k, d in enumerate(bad[:3].tolist()):
+            for f in (0, 1):
+                got = {ckb.names[p]: v for p, v in g.get(d, {}).get(f, {}).items()}
+                w = want[2 * k + f]
+                print('doc', d, 'field', f, {x: (got.get(x), w.get(x)) for x in set(got) | set(w) if got.get(x) != w.get(x)})
+    assert not len(bad), f'{len(bad)} of {n} documents differ from the oracle; first: {bad[:20].tolist()}'
+    assert int(cnt.sum()) == meta['total_records']
+    assert cd.total(dig) == meta['hits_digest'] == bench.hits_digest(hits)
+    m.close()
