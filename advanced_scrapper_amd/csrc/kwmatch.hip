@@ -792,6 +792,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     std::vector<uint32_t> pat_tcps;
     std::vector<uint8_t> pat_tbytes;
     int tx_unsafe_short = 0, tx_unsafe_edge = 0;
+    std::vector<uint32_t> txu_pat;   // the PI_TXUNSAFE names (the epilogue's short-field test)
     {
         std::map<uint32_t, uint64_t> freq;
         for (int i = f_first; i < n_pat; ++i)
@@ -832,6 +833,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
             if (unmapped || (nonascii && quantified)) {
                 pat_info[i] |= PI_TXUNSAFE;
                 tx_unsafe_short = 1;
+                txu_pat.push_back((uint32_t)i);
                 const uint32_t m = (uint32_t)cps[i].size();
                 if (m >= EDGE_MIN_M && m <= EDGE_MAX_M) tx_unsafe_edge = 1;
             }
@@ -969,7 +971,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
            f_ht4 = push_array(blob, FB.ht4), f_arec = push_array(blob, FB.arec), f_urec = push_array(blob, FB.urec),
            f_urec2 = push_array(blob, FB.urec2), f_tcps = push_array(blob, pat_tcps), f_txk = push_array(blob, tx_key),
            f_txv = push_array(blob, tx_val), f_txi = push_array(blob, tx_inv), f_tb = push_array(blob, pat_tbytes),
-           f_uw = push_array(blob, FB.use_wild), f_prxl = push_array(blob, FB.rxl);
+           f_uw = push_array(blob, FB.use_wild), f_prxl = push_array(blob, FB.rxl), f_txu = push_array(blob, txu_pat);
 
     HIPCHK(h, hipSetDevice(device));
     HIPCHK(h, hipMalloc(&h->d_tables, blob.size()));
@@ -1074,6 +1076,8 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     F.tx_val = (const uint32_t *)(B + f_txv);
     F.tx_inv = (const uint32_t *)(B + f_txi);
     F.tx_unsafe_short = tx_unsafe_short;
+    F.txu_pat = (const uint32_t *)(B + f_txu);
+    F.n_txu = (uint32_t)txu_pat.size();
     F.use_wild = (const uint64_t *)(B + f_uw);
     F.pat_rxl = (const uint32_t *)(B + f_prxl);
     F.tx_unsafe_edge = tx_unsafe_edge;

@@ -151,6 +151,8 @@ struct FastTables {
     const uint32_t *tx_val;
     const uint32_t *tx_inv;     // [128] marker - 0x80 -> code point (~0 for 0x80: no name holds it)
     int tx_unsafe_short;        // a name the view cannot decide (PI_TXUNSAFE) may decide a short field
+    const uint32_t *txu_pat;    // those names (n_txu)
+    uint32_t n_txu;
     int tx_unsafe_edge;         // ... or an edge window
     const uint64_t *use_wild;   // per use: wildcard positions of an RXM program string
     const uint32_t *pat_rxl;    // per pattern: its RXM program length (0: no RXM use; positions by the rx tasks)

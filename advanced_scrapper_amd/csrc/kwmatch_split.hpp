@@ -902,6 +902,56 @@ __device__ __forceinline__ uint64_t it_with_pos(uint64_t it, uint32_t pos)
     return (it & ~((uint64_t)IT_POS_MASK << IT_POS_SHIFT)) | ((uint64_t)pos << IT_POS_SHIFT);
 }
 
+// Whether a name the transcoded view cannot decide (PI_TXUNSAFE) and at least as long as a short field of n
+// code points (tf: its transcoded bytes) passes the short kernel's signature test for it (popcount(field
+// signature & ~name signature) <= (2n - 1) / 20: a name's signature has the bits of its code points and of
+// their transcoded bytes, so a code point the two share never counts); only then may the field decide such a
+// name, which the resolve kernel must do.  Whole wave.
+__device__ __forceinline__ bool fk_txu_short(const FastTables &FT, const uint8_t *tf, uint32_t n)
+{
+    const int lane = lane_id();
+    if (n == 0 || n > (uint32_t)MAXM) return false;
+    if (FT.n_txu > 8u * WAVE) return true;
+    uint64_t fsig = (uint32_t)lane < n ? 1ull << (tf[lane] & 63u) : 0ull;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) fsig |= __shfl_xor(fsig, d, WAVE);
+    const uint32_t allow = (2 * n - 1) / 20;
+    bool c = false;
+    for (uint32_t i = (uint32_t)lane; i < FT.n_txu; i += WAVE) {
+        const uint32_t p = FT.txu_pat[i];
+        c |= pi_m(FT.pat_info[p]) >= n && (uint32_t)__popcll(fsig & ~FT.pat_sig[p]) <= allow;
+    }
+    return __ballot(c) != 0;
+}
+
+// Whether a name the transcoded view cannot decide, of EDGE_MIN_M..EDGE_MAX_M code points, may have a one-deletion
+// edge window in a field of n code points (tf: its transcoded bytes): the window (its first or last m - 1 code
+// points) holds only code points of the name, so its signature has no bit the name's lacks.  Whole wave.
+__device__ __forceinline__ bool fk_txu_edge(const FastTables &FT, const uint8_t *tf, uint32_t n)
+{
+    const int lane = lane_id();
+    if (n + 1 < EDGE_MIN_M) return false;
+    if (FT.n_txu > 8u * WAVE) return true;
+    const uint32_t w = n < EDGE_MAX_M ? n : EDGE_MAX_M;   // (a window has at most EDGE_MAX_M - 1 code points)
+    uint64_t bp = (uint32_t)lane < w ? 1ull << (tf[lane] & 63u) : 0ull;
+    uint64_t bs = (uint32_t)lane < w ? 1ull << (tf[n - 1 - lane] & 63u) : 0ull;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) {   // inclusive prefix OR: lane k - 1 = the first / last k code points
+        const uint64_t up = __shfl_up(bp, d, WAVE), us = __shfl_up(bs, d, WAVE);
+        if (lane >= d) { bp |= up; bs |= us; }
+    }
+    bool c = false;
+    for (uint32_t k = EDGE_MIN_M - 1; k < EDGE_MAX_M && k <= n; ++k) {
+        const uint64_t sp = __shfl(bp, (int)k - 1, WAVE), ss = __shfl(bs, (int)k - 1, WAVE);
+        for (uint32_t i = (uint32_t)lane; i < FT.n_txu; i += WAVE) {
+            const uint32_t p = FT.txu_pat[i];
+            const uint64_t sg = FT.pat_sig[p];
+            c |= pi_m(FT.pat_info[p]) == k + 1 && ((sp & ~sg) == 0ull || (ss & ~sg) == 0ull);
+        }
+    }
+    return __ballot(c) != 0;
+}
+
 // Finish a transcoded document (V = its vrec) in the epilogue.  D0: the document in the arena, flags: its
 // dflags | edge flags (of the arena bytes).  Returns false, before anything is emitted, when the resolve
 // kernel must take it; otherwise *done = the epilogue's result (false: the generic kernel).
@@ -911,13 +961,16 @@ __device__ bool epi_tx_doc(const FastTables &FT, const FastScratch &S, const Dev
 {
     const int lane = lane_id();
     if (V.y == TX_NONE || (flags & DH_DEFER) || n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1) return false;
-    if (FT.tx_unsafe_edge && (((flags & DH_NA0) && (flags & DH_EDGE0)) || ((flags & DH_NA1) && (flags & DH_EDGE1))))
-        return false;
     const uint32_t c0 = V.z, c1 = V.w;
-    // a short non-ASCII field meets every name at least as long: one the view cannot decide may be among them
-    if (FT.tx_unsafe_short && (((flags & DH_NA0) && c0 <= (uint32_t)MAXM) || ((flags & DH_NA1) && c1 <= (uint32_t)MAXM)))
-        return false;
     const int64_t tb = (int64_t)(((uint64_t)(V.y & 0x7FFFFFFFu) << 32) | V.x);
+    // an edge-flagged non-ASCII field: a one-deletion edge window of a name the view cannot decide may be there
+    if (FT.tx_unsafe_edge && (((flags & DH_NA0) && (flags & DH_EDGE0) && fk_txu_edge(FT, S.tarena + tb, c0)) ||
+                              ((flags & DH_NA1) && (flags & DH_EDGE1) && fk_txu_edge(FT, S.tarena + tb + c0, c1))))
+        return false;
+    // a short non-ASCII field meets every name at least as long: one the view cannot decide may be among them
+    if (FT.tx_unsafe_short && (((flags & DH_NA0) && fk_txu_short(FT, S.tarena + tb, c0)) ||
+                               ((flags & DH_NA1) && fk_txu_short(FT, S.tarena + tb + c0, c1))))
+        return false;
     const uint64_t nb = tx_bytes(D0.t1 - D0.t0, D0.t2 - D0.t1);
     const uint16_t *ch0 = (const uint16_t *)(S.tarena + tb + nb);
     const uint16_t *ch1 = ch0 + ((flags & DH_NA0) ? tx_nchunks(D0.t0, D0.t1) : 0u);
