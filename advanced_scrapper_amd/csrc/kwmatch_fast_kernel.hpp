@@ -2129,10 +2129,13 @@ __global__ __launch_bounds__(RK_BLOCK, RK_OCC) void kw_resolve_kernel(FastTables
     FK_T0(tall0);
 
     const int64_t n_list = (int64_t)min(*S.res_cnt, S.defer_cap);
-    for (int64_t c0 = wave * WAVE; c0 < n_list; c0 += n_waves * WAVE) {
+    // chunks of up to 64 documents per wave, fewer when the list is short (each wave finishes its chunk's
+    // documents one after another: a short list spread over every wave)
+    const int64_t ch = max((int64_t)1, min((int64_t)WAVE, (n_list + n_waves - 1) / n_waves));
+    for (int64_t c0 = wave * ch; c0 < n_list; c0 += n_waves * ch) {
         // lane = document: this kernel owns the documents the epilogue left to it (res_list, DH_RESOLVE: a
         // non-ASCII field its transcoded view cannot take); it runs beside the task kernels, after the epilogue
-        const int64_t dl = c0 + lane < n_list ? (int64_t)S.res_list[c0 + lane] : n_docs;
+        const int64_t dl = (lane < ch && c0 + lane < n_list) ? (int64_t)S.res_list[c0 + lane] : n_docs;
         uint2 hl = make_uint2(0u, 0u);
         bool dfr = false, dfr_items = false;
         {

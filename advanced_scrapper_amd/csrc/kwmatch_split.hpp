@@ -955,12 +955,14 @@ __device__ __forceinline__ bool fk_txu_edge(const FastTables &FT, const uint8_t 
 // Finish a transcoded document (V = its vrec) in the epilogue.  D0: the document in the arena, flags: its
 // dflags | edge flags (of the arena bytes).  Returns false, before anything is emitted, when the resolve
 // kernel must take it; otherwise *done = the epilogue's result (false: the generic kernel).
+// CAP0 / CAP1: the item buffers' sizes (one wave's, or a big document's: the workgroup's LDS).
+template <uint32_t CAP0 = FK_ITEMS0, uint32_t CAP1 = FK_ITEMS1>
 __device__ bool epi_tx_doc(const FastTables &FT, const FastScratch &S, const DevScratch &GS, const FastDoc &D0, uint4 V,
                            uint32_t ibeg, uint32_t n0, uint32_t n1, uint32_t flags, uint64_t *items, int64_t wave,
                            OutCtx &O, TaskCounts &TC, bool *done)
 {
     const int lane = lane_id();
-    if (V.y == TX_NONE || (flags & DH_DEFER) || n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1) return false;
+    if (V.y == TX_NONE || (flags & DH_DEFER) || n0 > CAP0 || n1 > CAP1) return false;
     const uint32_t c0 = V.z, c1 = V.w;
     const int64_t tb = (int64_t)(((uint64_t)(V.y & 0x7FFFFFFFu) << 32) | V.x);
     // an edge-flagged non-ASCII field: a one-deletion edge window of a name the view cannot decide may be there
@@ -983,7 +985,7 @@ __device__ bool epi_tx_doc(const FastTables &FT, const FastScratch &S, const Dev
         unsafe |= (FT.pat_info[it_pat(it)] & PI_TXUNSAFE) != 0;
         if (flags & (t ? DH_NA0 : DH_NA1))
             it = it_with_pos(it, tx_pos(D0.arena, t ? D0.t0 : D0.t1, t ? ch0 : ch1, it_pos(it)));
-        items[t ? i : FK_ITEMS0 + (i - n0)] = it;
+        items[t ? i : CAP0 + (i - n0)] = it;
     }
     if (__ballot(unsafe)) return false;
     wave_sync();
@@ -995,15 +997,20 @@ __device__ bool epi_tx_doc(const FastTables &FT, const FastScratch &S, const Dev
     D.doc = D0.doc;
     D.l1 = (int32_t)c0;
     D.l2 = (int32_t)(c0 + c1);
-    *done = fk_scan_epilogue(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
+    *done = fk_scan_epilogue<CAP0>(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
     return true;
 }
 
-// ---------------------------------------------------------------- big all-ASCII documents
-// An all-ASCII document with more items than one epilogue wave's LDS holds (FK_ITEMS0 / FK_ITEMS1; a
-// 50k-name KB has pieces that many names share), up to FK_BIG0 / FK_BIG1: finished by the same epilogue
-// after the workgroup's loop, by its wave 0 with the whole workgroup's LDS (items), in wave 0's hit and
-// task regions.  Returns 1 if the document went to the generic kernel (a name with > 64 items).
+constexpr uint32_t EK_TXBIG = 0x80000000u;   // blk_docs entry: a transcoded big document (epi_big_doc)
+
+// ---------------------------------------------------------------- big documents
+// A document with more items than one epilogue wave's LDS holds (FK_ITEMS0 / FK_ITEMS1; a 50k-name KB has
+// pieces that many names share), up to FK_BIG0 / FK_BIG1: finished by the same epilogue after the
+// workgroup's loop, by its wave 0 with the whole workgroup's LDS (items), in wave 0's hit and task regions.
+// An entry with EK_TXBIG is a document with a non-ASCII field: finished on its transcoded view (epi_tx_doc's
+// tests and item positions), else left to the resolve kernel.  Returns bit 0: the document went to the
+// generic kernel (a name with > 64 items), bit 1: finished on its transcoded view, bit 2: left to the
+// resolve kernel, bit 3: a deferral of the transcoded view's.
 #ifndef EK_BIG_NOINLINE   // 1: epi_big_doc as a called function (a call frame; 0: inlined into the epilogue)
 #define EK_BIG_NOINLINE 0
 #endif
@@ -1014,10 +1021,12 @@ __device__ __forceinline__
 #endif
 uint32_t epi_big_doc(const FastTables &FT, const FastScratch &S, const DevScratch &GS,
                                                           const uint8_t *__restrict__ arena, const int64_t *__restrict__ off,
-                                                          uint32_t d, uint64_t *items, int64_t wave, OutCtx &O,
+                                                          uint32_t e, uint64_t *items, int64_t wave, OutCtx &O,
                                                           TaskCounts &TC)
 {
     const int lane = lane_id();
+    const bool tx = (e & EK_TXBIG) != 0;
+    const uint32_t d = e & ~EK_TXBIG;
     const int64_t ov = lane < 3 ? off[2 * (int64_t)d + lane] : 0;
     const uint2 hv = lane == 3 ? S.hdr[d] : (lane == 4 ? S.ncnt[d] : (lane == 5 ? make_uint2(0u, S.dflags[d]) :
                                                                     make_uint2(0u, 0u)));
@@ -1030,13 +1039,57 @@ uint32_t epi_big_doc(const FastTables &FT, const FastScratch &S, const DevScratc
     D.l1 = (int32_t)(D.t1 - D.t0);
     D.l2 = (int32_t)(D.t2 - D.t0);
     const uint32_t ibeg = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 3);
-    uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5) & ~DH_DEFER;
+    const uint32_t dfl = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 5);
+    uint32_t flags = dfl & ~DH_DEFER;
     const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)hv.x, 4);
     const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)hv.y, 4);
     flags |= fk_edge_flags(FT, D);
     const uint64_t *src = S.items + ibeg;
-    for (uint32_t k = (uint32_t)lane; k < n0; k += WAVE) items[k] = src[k];
-    for (uint32_t k = (uint32_t)lane; k < n1; k += WAVE) items[FK_BIG0 + k] = src[n0 + k];
+    bool view = true;
+    if (tx) {
+        // the transcoded view: epi_tx_doc's tests, item positions as code points, the document's bytes
+        const uint4 V = S.vrec[d];
+        const uint32_t c0 = V.z, c1 = V.w;
+        const int64_t tb = (int64_t)(((uint64_t)(V.y & 0x7FFFFFFFu) << 32) | V.x);
+        view = V.y != TX_NONE && !(dfl & DH_DEFER) &&
+               !(FT.tx_unsafe_edge && (((flags & DH_NA0) && (flags & DH_EDGE0) && fk_txu_edge(FT, S.tarena + tb, c0)) ||
+                                       ((flags & DH_NA1) && (flags & DH_EDGE1) && fk_txu_edge(FT, S.tarena + tb + c0, c1)))) &&
+               !(FT.tx_unsafe_short && (((flags & DH_NA0) && fk_txu_short(FT, S.tarena + tb, c0)) ||
+                                        ((flags & DH_NA1) && fk_txu_short(FT, S.tarena + tb + c0, c1))));
+        if (view) {
+            const uint64_t nb = tx_bytes(D.t1 - D.t0, D.t2 - D.t1);
+            const uint16_t *ch0 = (const uint16_t *)(S.tarena + tb + nb);
+            const uint16_t *ch1 = ch0 + ((flags & DH_NA0) ? tx_nchunks(D.t0, D.t1) : 0u);
+            bool unsafe = false;
+            for (uint32_t i = (uint32_t)lane; i < n0 + n1; i += WAVE) {
+                uint64_t it = src[i];
+                const bool t = i < n0;
+                unsafe |= (FT.pat_info[it_pat(it)] & PI_TXUNSAFE) != 0;
+                if (flags & (t ? DH_NA0 : DH_NA1))
+                    it = it_with_pos(it, tx_pos(arena, t ? D.t0 : D.t1, t ? ch0 : ch1, it_pos(it)));
+                items[t ? i : FK_BIG0 + (i - n0)] = it;
+            }
+            view = __ballot(unsafe) == 0ull;
+            D.arena = S.tarena;
+            D.t0 = tb;
+            D.t1 = D.t0 + c0;
+            D.t2 = D.t1 + c1;
+            D.l1 = (int32_t)c0;
+            D.l2 = (int32_t)(c0 + c1);
+        }
+        if (!view) {
+            if (lane == 0) {
+                S.dflags[d] = dfl | DH_RESOLVE;
+                const uint32_t i = atomicAdd(S.res_cnt, 1u);
+                if (i < S.defer_cap) S.res_list[i] = d;
+            }
+            wave_sync();
+            return 4u;
+        }
+    } else {
+        for (uint32_t k = (uint32_t)lane; k < n0; k += WAVE) items[k] = src[k];
+        for (uint32_t k = (uint32_t)lane; k < n1; k += WAVE) items[FK_BIG0 + k] = src[n0 + k];
+    }
     wave_sync();
     const bool done = fk_scan_epilogue<FK_BIG0>(FT, S, GS, D, items, n0, n1, flags, wave, O, TC);
     uint2 h;
@@ -1047,17 +1100,18 @@ uint32_t epi_big_doc(const FastTables &FT, const FastScratch &S, const DevScratc
             const uint32_t j = atomicAdd(S.defer_cnt, 1u);
             if (j < S.defer_cap) S.defer_list[j] = d;
             else atomicOr(&S.status[0], ST_ITEM_OVERFLOW);
-            atomicAdd(&S.stats[5], 1ull);
+            if (!tx) atomicAdd(&S.stats[5], 1ull);
             atomicAdd(&S.stats[13], 1ull);
         }
     } else {
         // (the header's counts saturate: informational only past the resolve kernel)
-        h.y = min(n0, 1023u) | (min(n1, 127u) << DH_N1_SHIFT) | flags;
-        if (lane == 0) S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
+        h.y = min(n0, 1023u) | (min(n1, 127u) << DH_N1_SHIFT) | (flags & ~DH_DEFER) | (tx ? DH_TX : 0u);
+        if (lane == 0 && !tx)
+            S.vrec[d] = make_uint4((uint32_t)D.t0, (uint32_t)((uint64_t)D.t0 >> 32), (uint32_t)(D.t1 - D.t0), (uint32_t)(D.t2 - D.t1));
     }
     if (lane == 0) S.hdr[d] = h;
     wave_sync();
-    return done ? 0u : 1u;
+    return (done ? 0u : 1u) | (tx ? 2u : 0u) | ((tx && !done) ? 8u : 0u);
 }
 
 // the epilogue's per-document loads: lanes 0..2 the offsets, lane 3 the header, lane 4 the item counts,
@@ -1254,7 +1308,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
     __syncthreads();
     const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
     if (wib == 0 && nb) {
-        for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC);
+        for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC) & 1u;
         if (lane == 0) atomicAdd(&S.stats[16], (unsigned long long)nb);
     }
     if (lane == 0) {
@@ -1533,6 +1587,18 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
             const uint32_t dflags = (uint32_t)__builtin_amdgcn_readlane((int)flags, l);
             if (dfl & (DH_NA0 | DH_NA1)) {
                 bool done = false;
+                if (FK_TX && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1) && n0 <= (uint32_t)FK_BIG0 &&
+                    n1 <= (uint32_t)FK_BIG1 && !(dflags & DH_DEFER)) {
+                    // more items than a wave holds: the workgroup's big documents, on its LDS after the loop
+                    uint32_t bi = 0;
+                    if (lane == 0) bi = atomicAdd(&blk_n, 1u);
+                    bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
+                    if (bi < (uint32_t)EK_BIGQ) {
+                        if (lane == 0) blk_docs[bi] = (uint32_t)dd | EK_TXBIG;
+                        wave_sync();
+                        continue;
+                    }
+                }
                 if (FK_TX && epi_tx_doc(FT, S, GS, D, S.vrec[dd], ibeg, n0, n1, dflags, items, wave, O, TC, &done)) {
                     ++ntx;
                     uint2 h;
@@ -1612,7 +1678,13 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
     __syncthreads();
     const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
     if (wib == 0 && nb) {
-        for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC);
+        for (uint32_t i = 0; i < nb; ++i) {
+            const uint32_t r = epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC);
+            ndefer += r & 1u;
+            ndef_items += (r >> 3) & 1u;
+            ntx += (r >> 1) & 1u;
+            nres += (r >> 2) & 1u;
+        }
         if (lane == 0) atomicAdd(&S.stats[16], (unsigned long long)nb);
     }
     if (lane == 0) {
