@@ -33,6 +33,9 @@ namespace kw {
 #ifndef FS_MINW
 #define FS_MINW 1
 #endif
+#ifndef FS_AHEAD
+#define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
+#endif
 constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
 constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
@@ -64,8 +67,7 @@ struct __attribute__((aligned(16))) FilterLds {
     uint32_t b2[FK_B2_WORDS];
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
-    uint32_t skey[FS_WAVES][2 * WAVE];        // stage 2: the queue of survivors' 4-byte keys ...
-    uint32_t spos[FS_WAVES][2 * WAVE];        // ... and group-relative positions (a ring of 128)
+    uint32_t spos[FS_WAVES][2 * WAVE];        // stage 2: the queue of survivors' group-relative positions (a ring)
 };
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
@@ -88,19 +90,6 @@ __device__ __forceinline__ uint32_t fk_b2_mul(uint32_t key)
     uint32_t r;
     asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(40503u), "v"(key));
     return r;
-}
-
-// the four bytes at lane position j (0..15) of W[0..3] (+ W[4], the next lane's first word); j is not a
-// compile-time constant: the words are selected without dynamic register indexing
-__device__ __forceinline__ uint32_t fk_key_at(const uint32_t (&W)[5], uint32_t j)
-{
-    // bit-select masks (v_bfi_b32): a select chain written with ?: is turned into an indexed array, and the
-    // array of every tile in flight into LDS
-    const uint32_t m1 = 0u - ((j >> 2) & 1u), m2 = 0u - ((j >> 3) & 1u);
-    const uint32_t l01 = (W[0] & ~m1) | (W[1] & m1), l23 = (W[2] & ~m1) | (W[3] & m1);
-    const uint32_t h01 = (W[1] & ~m1) | (W[2] & m1), h23 = (W[3] & ~m1) | (W[4] & m1);
-    const uint32_t lo = (l01 & ~m2) | (l23 & m2), hi = (h01 & ~m2) | (h23 & m2);
-    return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
 }
 
 // Stage-1 masks use the transposed bit order of a lane's 16 positions: position j = 4 q + r (q = its word, r =
@@ -188,7 +177,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const int lane = lane_id();
     const uint32_t *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
-    uint32_t *skey = L.skey[wib], *spos = L.spos[wib];
+    uint32_t *spos = L.spos[wib];
     uint32_t *cand = S.cand + (size_t)wave * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const uint32_t t3on = FT.has_t3 ? 1u : 0u;
@@ -212,7 +201,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         uint32_t kdoc = 0;   // document of the current stage-2 round's first survivor (candidate emission)
         bool ghdr = true;    // the group's header record is not written yet
         uint32_t qh = 0, qn = 0;   // the survivor queue's head and length (wave-uniform)
-        // Three tiles in flight per wave, each in its own registers (the loop is unrolled by three, so no
+        // FS_AHEAD tiles in flight per wave, each in its own registers (the loop is unrolled by FS_AHEAD, so no
         // register copy waits for a load).  Loads are unconditional: an address past the group's last
         // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
         // comes with the word after it (lane 63's fifth word).
@@ -230,8 +219,10 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             wave_sync();
             const bool act = (uint32_t)lane < n;
             const uint32_t slot = (qh + (uint32_t)lane) & (2u * WAVE - 1u);
-            const uint32_t key = skey[slot], r = spos[slot];
+            const uint32_t r = spos[slot];
             wave_sync();
+            // the 4-byte key at the position (the group's bytes were just streamed: a cache hit)
+            const uint32_t key = act ? ld_u32_unaligned(arena, gb + (int64_t)r) : 0u;
             qh = (qh + n) & (2u * WAVE - 1u);
             qn -= n;
             const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
@@ -307,7 +298,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const uint32_t sm = (hit | gate) & tvalid;
             ncand += (uint32_t)__popc(sm);
             // the tile's survivors join the wave's queue in position order (each written by the lane that owns
-            // it: its 4-byte key and group-relative position); stage 2 runs on full rounds of 64
+            // it: its group-relative position); stage 2 runs on full rounds of 64
             int ts;
             const int sx = wave_excl_scan_dpp(__popc(sm), &ts);
             if (ts == 0) return;
@@ -318,12 +309,8 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                     int rk = sx;
                     for (uint32_t hm = smp; hm; hm &= hm - 1u) {
                         if (rk >= c0 + take) break;
-                        if (rk >= c0) {
-                            const uint32_t j = (uint32_t)(__ffs(hm) - 1);
-                            const uint32_t slot = (qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u);
-                            skey[slot] = fk_key_at(W, j);
-                            spos[slot] = rel + j;
-                        }
+                        if (rk >= c0)
+                            spos[(qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u)] = rel + (uint32_t)(__ffs(hm) - 1);
                         ++rk;
                     }
                 }
@@ -332,24 +319,18 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 while (qn >= (uint32_t)WAVE) round(WAVE);
             }
         };
-        uint4 v0, v1, v2;
-        uint32_t w0, w1, w2;
-        load(v0, w0, blk);
-        load(v1, w1, blk + 1024);
-        load(v2, w2, blk + 2048);
-        for (;;) {
-            if (blk >= ge) break;
-            tile(v0, w0, blk);
-            load(v0, w0, blk + 3072);
-            blk += 1024;
-            if (blk >= ge) break;
-            tile(v1, w1, blk);
-            load(v1, w1, blk + 3072);
-            blk += 1024;
-            if (blk >= ge) break;
-            tile(v2, w2, blk);
-            load(v2, w2, blk + 3072);
-            blk += 1024;
+        uint4 v[FS_AHEAD];
+        uint32_t w[FS_AHEAD];
+#pragma unroll
+        for (int k = 0; k < FS_AHEAD; ++k) load(v[k], w[k], blk + 1024 * k);
+        for (bool more = true; more;) {
+#pragma unroll
+            for (int k = 0; k < FS_AHEAD; ++k) {   // (unrolled: each tile in flight keeps its own registers)
+                if (blk >= ge) { more = false; break; }
+                tile(v[k], w[k], blk);
+                load(v[k], w[k], blk + 1024 * FS_AHEAD);
+                blk += 1024;
+            }
         }
         while (qn) round(qn < (uint32_t)WAVE ? qn : (uint32_t)WAVE);   // the group's last survivors
     }
