@@ -18,6 +18,7 @@
  * kwcsv_utf8_ok validity of UTF-8 cells (pandas raises UnicodeDecodeError on the others)
  */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define KWCSV_QUOTED 1u   /* the cell was quoted */
@@ -286,49 +287,104 @@ static int put_cell(uint8_t *out, int64_t cap, int64_t *o, const uint8_t *s, int
  * bit 16 = a cell holds '\r' (pandas' re-read would split the record there).  Returns 0, -1 when out is too
  * small, -2 for a NUL character in a cell (the caller's pandas path raises as the reference does).
  */
+/* one chunk cell of an output row into out (NA: empty); *fl gets its bits for output column c; 0, -1 when out
+ * is full, -2 for a NUL character */
+static int emit_chunk_cell(const uint8_t *cells, const int64_t *coff, const uint8_t *cfl, int64_t cell, int c,
+                           uint8_t *out, int64_t cap, int64_t *o, uint32_t *fl)
+{
+    const uint8_t *s = cells + coff[cell];
+    int64_t n = coff[cell + 1] - coff[cell];
+    const int na = (cfl[cell] & KWCSV_NA) != 0;
+    if (na) n = 0;
+    if (n > 0 && memchr(s, 0, (size_t)n)) return -2;
+    if (n > 0 && memchr(s, '\r', (size_t)n)) *fl |= 1u << 16;
+    if (na) *fl |= 1u << (8 + c);
+    else if (kwcsv_text_witness(s, n)) *fl |= 1u << c;
+    return put_cell(out, cap, o, s, n) ? -1 : 0;
+}
+
 int64_t kwcsv_emit(const uint8_t *cells, const int64_t *coff, const uint8_t *cfl, int32_t ncols, const int32_t *cols,
                    const int32_t *row_doc, const int64_t *row_stamp, int64_t nrows, const uint8_t *json,
                    const int64_t *json3, uint8_t *out, int64_t cap, int64_t *line_off, uint32_t *flags)
 {
+    /* An article's chunk cells are the same in every row it has (one per matched ticker): each article's
+     * date_time cell and its title .. article_text cells are rendered (QUOTE_MINIMAL, flags) once, at the
+     * end of out, and copied into its rows. */
+    int32_t dmax = -1;
+    for (int64_t r = 0; r < nrows; ++r) if (row_doc[r] > dmax) dmax = row_doc[r];
+    int64_t *part = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(dmax + 1));   /* A start, B start, B end */
+    uint32_t *dfl = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(dmax + 1));
+    if (!part || !dfl) { free(part); free(dfl); return -3; }
+    for (int32_t d = 0; d <= dmax; ++d) part[3 * d] = -1;
+    int64_t hi = cap;   /* the rendered articles grow down from the end of out */
+    int64_t rc = 0;
+    for (int64_t r = 0; r < nrows && rc == 0; ++r) {
+        const int32_t d = row_doc[r];
+        if (part[3 * d] >= 0) continue;
+        /* render into a scratch position after the rows' room: measure first by rendering at the low end
+         * of the free space [hi - need, hi) is unknown, so render at a fixed probe offset below hi */
+        const int64_t base = (int64_t)d * ncols;
+        int64_t need = 16;
+        for (int c = 0; c < 6; ++c) {
+            const int64_t cell = base + cols[c];
+            need += 2 * (coff[cell + 1] - coff[cell]) + 3;
+        }
+        if (hi - need < 0) { rc = -1; break; }
+        int64_t o = hi - need;
+        const int64_t a0 = o;
+        uint32_t fl = 0;
+        int e = emit_chunk_cell(cells, coff, cfl, base + cols[0], 0, out, cap, &o, &fl);
+        const int64_t b0 = o;
+        for (int c = 3; c < 8 && e == 0; ++c) {
+            if (c > 3) out[o++] = ',';
+            e = emit_chunk_cell(cells, coff, cfl, base + cols[c - 2], c, out, cap, &o, &fl);
+        }
+        if (e) { rc = e; break; }
+        /* move the rendering to the top of the free space */
+        const int64_t len = o - a0;
+        memmove(out + hi - len, out + a0, (size_t)len);
+        part[3 * d] = hi - len;
+        part[3 * d + 1] = hi - len + (b0 - a0);
+        part[3 * d + 2] = hi;
+        dfl[d] = fl;
+        hi -= len;
+    }
     int64_t o = 0;
     line_off[0] = 0;
-    for (int64_t r = 0; r < nrows; ++r) {
-        uint32_t fl = 0;
+    for (int64_t r = 0; r < nrows && rc == 0; ++r) {
+        const int32_t d = row_doc[r];
+        uint32_t fl = dfl[d] | 6u;   /* the JSON cells are text witnesses */
         char num[24];
         int k = 24;
         int64_t v = row_stamp[r];
         uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1u : (uint64_t)v;
         do { num[--k] = (char)('0' + u % 10); u /= 10; } while (u);
         if (v < 0) num[--k] = '-';
-        if (o + (24 - k) + 1 > cap) return -1;
+        const int64_t la = part[3 * d + 1] - part[3 * d], lb = part[3 * d + 2] - part[3 * d + 1];
+        if (o + (24 - k) + la + lb + 8 > hi) { rc = -1; break; }
         memcpy(out + o, num + k, (size_t)(24 - k));
         o += 24 - k;
-        for (int c = 0; c < 8; ++c) {
-            out[o++] = ',';
-            const uint8_t *s;
-            int64_t n;
-            int na = 0;
-            if (c == 1 || c == 2) {
-                s = json + json3[3 * r + (c - 1)];
-                n = json3[3 * r + c] - json3[3 * r + (c - 1)];
-            } else {
-                const int32_t col = cols[c == 0 ? 0 : c - 2];
-                const int64_t cell = (int64_t)row_doc[r] * ncols + col;
-                s = cells + coff[cell];
-                n = coff[cell + 1] - coff[cell];
-                na = (cfl[cell] & KWCSV_NA) != 0;
-                if (na) n = 0;
-            }
-            if (n > 0 && memchr(s, 0, (size_t)n)) return -2;
+        out[o++] = ',';
+        memcpy(out + o, out + part[3 * d], (size_t)la);
+        o += la;
+        for (int c = 1; c < 3; ++c) {
+            const uint8_t *s = json + json3[3 * r + (c - 1)];
+            const int64_t n = json3[3 * r + c] - json3[3 * r + (c - 1)];
+            if (n > 0 && memchr(s, 0, (size_t)n)) { rc = -2; break; }
             if (n > 0 && memchr(s, '\r', (size_t)n)) fl |= 1u << 16;
-            if (na) fl |= 1u << (8 + c);
-            else if (c == 1 || c == 2 || kwcsv_text_witness(s, n)) fl |= 1u << c;
-            if (put_cell(out, cap - 1, &o, s, n)) return -1;
+            out[o++] = ',';
+            if (put_cell(out, hi - 1, &o, s, n)) { rc = -1; break; }
         }
-        if (o + 1 > cap) return -1;
+        if (rc) break;
+        if (o + lb + 2 > hi) { rc = -1; break; }
+        out[o++] = ',';
+        memcpy(out + o, out + part[3 * d + 1], (size_t)lb);
+        o += lb;
         out[o++] = '\n';
         line_off[r + 1] = o;
         flags[r] = fl;
     }
-    return 0;
+    free(part);
+    free(dfl);
+    return rc;
 }

@@ -254,6 +254,17 @@ class RunFiles:
         return True
 
 
+_EMIT_BUF = [np.zeros(0, dtype=np.uint8)]
+
+
+def _emit_buffer(cap: int) -> np.ndarray:
+    """The emitter's output buffer, kept across chunks (a fresh 100+ MB buffer per chunk costs its page faults):
+    render_native's views are valid until its next call, and every caller writes them out before that."""
+    if len(_EMIT_BUF[0]) < cap:
+        _EMIT_BUF[0] = np.empty(cap + cap // 4, dtype=np.uint8)
+    return _EMIT_BUF[0]
+
+
 def render_native(chunk, raw_rows, stamps_by_doc, tickers):
     """The rows of a native chunk (``raw_rows`` = rows.assemble_json_raw's arrays, document order, KB ticker
     order) rendered by the C emitter into one buffer, grouped by ticker file: a list of (file name, line
@@ -278,13 +289,19 @@ def render_native(chunk, raw_rows, stamps_by_doc, tickers):
     cols = np.asarray([chunk.col[k] for k in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')],
                       dtype=np.int32)
     jb = jbuf if len(jbuf) else np.zeros(1, np.uint8)
-    cap = int(2 * (int(c.off[-1]) + len(jbuf)) + 64 * n + 1024)
+    # room: every row's cells (quoted: at most doubled) + the articles' cells rendered once (kwcsv_emit)
+    cell_len = np.zeros(len(c.off) // c.ncols + 1, dtype=np.int64)
+    nd = (len(c.off) - 1) // c.ncols
+    for k in cols.tolist():
+        idx = np.arange(nd, dtype=np.int64) * c.ncols + k
+        cell_len[:nd] += c.off[idx + 1] - c.off[idx]
+    cap = int(2 * (int(cell_len[rd].sum()) + len(jbuf) + int(cell_len.sum())) + 64 * n + 1024)
     line_off = np.empty(n + 1, dtype=np.int64)
     flags = np.empty(n, dtype=np.uint32)
     L = _csv_lib()
     rc = -1
     for _ in range(8):
-        out = np.empty(cap, dtype=np.uint8)
+        out = _emit_buffer(cap)
         rc = L.kwcsv_emit(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jb), _p(j3),
                           _p(out), cap, _p(line_off), _p(flags))
         if rc != -1:
