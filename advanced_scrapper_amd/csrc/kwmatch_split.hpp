@@ -506,9 +506,11 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
                 b1 = b2; e1 = e2;
                 b2 = e2 = 0;
             }
+            // a lane that took its last anchor records is done (no extra round of the wave for it)
+            if (more && tcur >= tend && b1 >= e1 && b2 >= e2) more = false;
             // stage B: (candidate, use) pairs over the lanes
             int total;
-            const int ex = wave_excl_scan((int)(uc + uc1), &total);
+            const int ex = wave_excl_scan_dpp((int)(uc + uc1), &total);
             for (int g0 = 0; g0 < total; g0 += WAVE) {
                 const int g = g0 + lane;
                 bool pass = false;
@@ -588,7 +590,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
         const uint32_t nmine = scnt[lane];
         const bool ovf = pn > (uint32_t)PK_POOL;   // the pool dropped items: the batch's documents defer
         int itotal;
-        const int iex = wave_excl_scan((int)nmine, &itotal);
+        const int iex = wave_excl_scan_dpp((int)nmine, &itotal);
         const uint64_t withm = __ballot(nmine > 0);
         if (withm) {
             const uint64_t below = (1ull << lane) - 1;
@@ -740,11 +742,13 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
         lead &= valid;
         high &= valid;
         int total;
-        const int ex = wave_excl_scan(__popc(lead), &total);
+        const int ex = wave_excl_scan_dpp(__popc(lead), &total);
         if (chunk && lp < fe) chunk[(lp - base) >> 4] = (uint16_t)(count + (uint32_t)ex);
-        // the block's output, staged: lanes without a multi-byte character copy their bytes
+        // the block's output, staged at the output's alignment (stg byte (g0 & 15) + k = output byte g0 + k):
+        // lanes without a multi-byte character copy their bytes
         wave_sync();
-        uint32_t k = (uint32_t)ex;
+        const uint32_t g0 = o0 + count, g1 = g0 + (uint32_t)total, sh = g0 & 15u;
+        uint32_t k = (uint32_t)ex + sh;
         if (high == 0) {
 #pragma unroll
             for (int j = 0; j < 16; ++j)
@@ -770,23 +774,17 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
             }
         }
         wave_sync();
-        // out[count, count + total): 16-byte stores for the aligned body, byte stores at the two ends
-        const uint32_t g0 = o0 + count, g1 = g0 + (uint32_t)total;
+        // out[g0, g1): 16-byte stores of aligned staged chunks (ds_read_b128) for the body, byte stores at the
+        // two ends
+        const uint32_t gb = g0 & ~15u;
         const uint32_t a0 = (g0 + 15u) & ~15u, a1 = g1 & ~15u;
         if (a0 < a1) {
-            if ((uint32_t)lane < a0 - g0) out[g0 + lane] = stg[lane];
-            if ((uint32_t)lane < g1 - a1) out[a1 + lane] = stg[a1 - g0 + lane];
-            for (uint32_t q = a0 + 16u * (uint32_t)lane; q < a1; q += 16u * WAVE) {
-                const uint32_t so = q - g0;
-                uint32_t w[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    w[i] = (uint32_t)stg[so + 4 * i] | ((uint32_t)stg[so + 4 * i + 1] << 8) |
-                           ((uint32_t)stg[so + 4 * i + 2] << 16) | ((uint32_t)stg[so + 4 * i + 3] << 24);
-                *(uint4 *)(out + q) = make_uint4(w[0], w[1], w[2], w[3]);
-            }
+            if ((uint32_t)lane < a0 - g0) out[g0 + lane] = stg[g0 - gb + lane];
+            if ((uint32_t)lane < g1 - a1) out[a1 + lane] = stg[a1 - gb + lane];
+            for (uint32_t q = a0 + 16u * (uint32_t)lane; q < a1; q += 16u * WAVE)
+                *(uint4 *)(out + q) = *(const uint4 *)(stg + (q - gb));
         } else {
-            for (uint32_t q = g0 + (uint32_t)lane; q < g1; q += WAVE) out[q] = stg[q - g0];
+            for (uint32_t q = g0 + (uint32_t)lane; q < g1; q += WAVE) out[q] = stg[q - gb];
         }
         count += (uint32_t)total;
     }
@@ -799,7 +797,7 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
 __global__ __launch_bounds__(TX_BLOCK, TX_MINW) void kw_tx_kernel(FastTables FT, const uint8_t *__restrict__ arena,
                                                          const int64_t *__restrict__ off, int64_t n_docs, FastScratch S)
 {
-    __shared__ uint32_t stg_all[TX_WAVES * (1040 / 4)];
+    __shared__ __attribute__((aligned(16))) uint32_t stg_all[TX_WAVES * (1040 / 4)];   // (16-byte chunks: ds_read_b128)
     __shared__ uint32_t txk[256], txv[256];
     for (int i = threadIdx.x; i < 256; i += TX_BLOCK) {
         txk[i] = FT.tx_key[i];
@@ -1381,7 +1379,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         const uint32_t sz = s_flat ? (sf ? s_n1 : s_n0) : 0u;
         const uint32_t st = s_beg + (sf ? s_n0 : 0u);
         int stot;
-        const uint32_t soff = (uint32_t)wave_excl_scan((int)sz, &stot);
+        const uint32_t soff = (uint32_t)wave_excl_scan_dpp((int)sz, &stot);
         const uint32_t s_l0 = (uint32_t)__shfl((int)(uint32_t)l0, sd, WAVE), s_l1 = (uint32_t)__shfl((int)(uint32_t)l1, sd, WAVE);
         const uint32_t s_len = sf ? s_l1 : s_l0;   // the segment's field bytes (= code points: ASCII)
         // ---- batches of whole segments, <= 64 items each
