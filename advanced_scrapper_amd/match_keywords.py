@@ -464,9 +464,13 @@ def _sort_native(file_path) -> bool:
     n, nc = cells.nrows, cells.ncols
     ti = names.index('time_unix')
     fl = cells.flags.reshape(n, nc)
-    for c in range(nc):
-        if c != ti and n and not ((fl[:, c] & TEXT).any() or (fl[:, c] & NA).all()):
-            return False
+    # pandas' low-memory reader infers each column's type per block of rows: every block must keep every
+    # non-time column text (a witness) or all-NA, or a numeric-looking block would be re-rendered by pandas
+    for b0 in range(0, n, egress.PANDAS_BLOCK_ROWS):
+        blk = fl[b0:b0 + egress.PANDAS_BLOCK_ROWS]
+        for c in range(nc):
+            if c != ti and not ((blk[:, c] & TEXT).any() or (blk[:, c] & NA).all()):
+                return False
     raw = [bytes(cells._mv[cells.off[r * nc + ti]:cells.off[r * nc + ti + 1]]) for r in range(n)]
     if n and (fl[:, ti] & (NA | TEXT)).any():
         return False

@@ -535,3 +535,26 @@ def test_indexed_sort_declines_numeric_only_block(golden, tmp_path, monkeypatch)
     assert sorted(fast) == sorted(slow)
     for fn in slow:
         assert fast[fn] == slow[fn], fn
+
+
+def test_native_sort_defers_numeric_looking_block(tmp_path):
+    """pandas' low-memory reader infers types per 65 536-row block: a block whose title cells all look
+    numeric ('007') would come back re-rendered ('7'), so the native sort must hand such a file to the
+    pandas path, while the same rows with one text title per block stay native."""
+    from advanced_scrapper_amd import egress
+    from advanced_scrapper_amd import match_keywords as mk
+    n = egress.PANDAS_BLOCK_ROWS + 10
+    head = 'time_unix,date_time,text_matches,title_matches,title,url,source,source_url,article_text\n'
+
+    def write(path, titles):
+        with open(path, 'w') as fh:
+            fh.write(head)
+            for i, t in enumerate(titles):
+                fh.write(f'{n - i},d{i},"{{}}","{{}}",{t},u{i},s,su,text {i}\n')
+
+    bad = tmp_path / 'bad.csv'
+    write(bad, ['007'] * egress.PANDAS_BLOCK_ROWS + ['abc'] * 10)
+    assert mk._sort_native(str(bad)) is False
+    good = tmp_path / 'good.csv'
+    write(good, ['abc'] + ['007'] * (egress.PANDAS_BLOCK_ROWS - 1) + ['abc'] + ['007'] * 9)
+    assert mk._sort_native(str(good)) is True
