@@ -104,7 +104,9 @@ struct Scratch {
     unsigned long long *cnt;   // [0..4] per code
     int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
     int normalize;           // KW_DEDUP_NORMALIZE: apply :63-76; else keep-first over the raw strings
-    uint2 *slow;             // rows (index, cut) for the byte-serial rewrite
+    uint2 *slow;             // rows (index, cut) for the byte-serial rewrite: slow_cap per transform wave
+    uint32_t *wslow;         // per transform wave: its slow rows (no shared counter: one address for every
+    uint32_t slow_cap;       //   wave's atomic serialised the transform)
     unsigned long long *nslow;
 };
 
@@ -363,6 +365,8 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
     const int64_t n_groups = (n + 63) / 64;
     const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + wib;
     const int64_t n_waves = (int64_t)gridDim.x * (BLOCK / 64);
+    uint32_t ns = 0;   // this wave's rows for the byte-serial rewrite (wave-uniform)
+    uint2 *wsl = S.slow + (size_t)wave * S.slow_cap;
     for (int64_t g = wave; g < n_groups; g += n_waves) {
         const int64_t i0 = g * 64, i1 = i0 + 64 < n ? i0 + 64 : n;
         const int64_t A0 = off[i0], A1 = off[i1];
@@ -384,28 +388,29 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
             GlobalSrc src{arena};
             if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
         }
-        // rows for the byte-serial rewrite -> the slow list (one atomic per wave)
+        // rows for the byte-serial rewrite -> the wave's slow list
         const uint64_t sm = __ballot(jslow >= 0);
         if (sm) {
-            unsigned long long at = 0;
-            if (lane == 0) at = atomicAdd(S.nslow, (unsigned long long)__popcll(sm));
-            at = __shfl(at, 0, 64);
             if (jslow >= 0) {
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                S.slow[at + r] = make_uint2((uint32_t)i, (uint32_t)jslow);
+                wsl[ns + r] = make_uint2((uint32_t)i, (uint32_t)jslow);
             }
+            ns += (uint32_t)__popcll(sm);
         }
     }
+    if (lane == 0) S.wslow[wave] = ns;
 }
 
 __global__ __launch_bounds__(BLOCK) void dd_slow_kernel(const uint8_t *__restrict__ arena,
                                                         const int64_t *__restrict__ off, uint8_t *__restrict__ code,
                                                         Scratch S)
 {
-    const unsigned long long ns = *S.nslow;
-    for (unsigned long long k = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x; k < ns;
-         k += (unsigned long long)gridDim.x * BLOCK) {
-        const uint2 e = S.slow[k];
+    // wave w takes transform wave w's list (the same grid)
+    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const uint32_t ns = S.wslow[wave];
+    const uint2 *wsl = S.slow + (size_t)wave * S.slow_cap;
+    for (uint32_t k = threadIdx.x & 63u; k < ns; k += 64u) {
+        const uint2 e = wsl[k];
         slow_row(arena, off[e.x], (int64_t)e.y, (int64_t)e.x, code, S);
     }
 }
@@ -740,8 +745,13 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     uint64_t tsize = 1024;
     while (tsize < 2 * (uint64_t)n) tsize <<= 1;
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    // the transform's grid: its waves' slow lists are sized from the groups of 64 rows each wave takes
+    const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 8);
+    const int64_t n_tw = (int64_t)tgrid * (BLOCK / 64);
+    h->S.slow_cap = (uint32_t)(((n + 63) / 64 + n_tw - 1) / n_tw * 64);
     const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
-    const size_t need = out_bytes + align256(8 * (size_t)n) * 3 + align256(4 * (size_t)n) + align256(8 * tsize) +
+    const size_t need = out_bytes + align256(8 * (size_t)n) * 2 + align256(8 * (size_t)n_tw * h->S.slow_cap) +
+                        align256(4 * (size_t)n_tw) + align256(4 * (size_t)n) + align256(8 * tsize) +
                         align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
                         2 * align256(8 * ((size_t)n + 1));
     if (need > h->buf_bytes) {
@@ -762,7 +772,8 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.mask = tsize - 1;
     S.cnt = (unsigned long long *)carve(8 * 8);
     S.nslow = S.cnt + 6;
-    S.slow = (uint2 *)carve(8 * (size_t)n);
+    S.slow = (uint2 *)carve(8 * ((size_t)n_tw * S.slow_cap));
+    S.wslow = (uint32_t *)carve(4 * (size_t)n_tw);
     S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
     h->tile_cnt = (unsigned long long *)carve(8 * (size_t)ntiles);
@@ -774,9 +785,8 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
     const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
     DDCHK(h, hipEventRecord(h->ev[0], st));
-    const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 8);
     hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
-    hipLaunchKernelGGL(dd_slow_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
+    hipLaunchKernelGGL(dd_slow_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
     DDCHK(h, hipGetLastError());
     DDCHK(h, hipEventRecord(h->ev[1], st));
     hipLaunchKernelGGL(dd_insert_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S);
