@@ -527,33 +527,56 @@ __global__ __launch_bounds__(BLOCK) void dd_count_kernel(const uint8_t *__restri
     if (threadIdx.x == 0) { tile_cnt[blockIdx.x] = ta; tile_bytes[blockIdx.x] = tb; }
 }
 
+// exclusive scan of the per-tile (count, bytes) pairs in one 1024-thread block: each thread sums a contiguous
+// segment (loads unrolled by 8, in flight together), the 1024 segment sums are scanned by wave shuffles and
+// LDS (16 wave totals), then each thread rewrites its segment
 __global__ __launch_bounds__(1024) void dd_scan_tiles_kernel(unsigned long long *__restrict__ tile_cnt,
                                                              unsigned long long *__restrict__ tile_bytes, int64_t nt,
                                                              unsigned long long *__restrict__ totals)
 {
-    __shared__ unsigned long long pc[1024], pb[1024];
-    const int t = threadIdx.x;
+    __shared__ unsigned long long wc[16], wb[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t per = (nt + 1023) / 1024;
+    const int64_t k0 = t * per, k1 = (t + 1) * per < nt ? (t + 1) * per : nt;
     unsigned long long sc = 0, sb = 0;
-    for (int64_t k = t * per; k < (t + 1) * per && k < nt; ++k) { sc += tile_cnt[k]; sb += tile_bytes[k]; }
-    pc[t] = sc;
-    pb[t] = sb;
-    __syncthreads();
-    if (t == 0) {
-        unsigned long long ac = 0, ab = 0;
-        for (int k = 0; k < 1024; ++k) {
-            const unsigned long long vc = pc[k], vb = pb[k];
-            pc[k] = ac;
-            pb[k] = ab;
-            ac += vc;
-            ab += vb;
-        }
-        totals[0] = ac;
-        totals[1] = ab;
+    int64_t k = k0;
+    for (; k + 8 <= k1; k += 8) {
+        unsigned long long c[8], b[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { c[i] = tile_cnt[k + i]; b[i] = tile_bytes[k + i]; }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { sc += c[i]; sb += b[i]; }
     }
+    for (; k < k1; ++k) { sc += tile_cnt[k]; sb += tile_bytes[k]; }
+    // inclusive scan of (sc, sb) over the wave, then over the 16 waves
+    unsigned long long xc = sc, xb = sb;
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long yc = __shfl_up(xc, d, 64), yb = __shfl_up(xb, d, 64);
+        if (lane >= d) { xc += yc; xb += yb; }
+    }
+    if (lane == 63) { wc[wv] = xc; wb[wv] = xb; }
     __syncthreads();
-    unsigned long long ac = pc[t], ab = pb[t];
-    for (int64_t k = t * per; k < (t + 1) * per && k < nt; ++k) {
+    unsigned long long pc = 0, pb = 0, tc = 0, tb = 0;
+    for (int w = 0; w < 16; ++w) {
+        if (w < wv) { pc += wc[w]; pb += wb[w]; }
+        tc += wc[w];
+        tb += wb[w];
+    }
+    if (t == 0) { totals[0] = tc; totals[1] = tb; }
+    unsigned long long ac = pc + xc - sc, ab = pb + xb - sb;   // exclusive prefix of this thread's segment
+    for (k = k0; k + 8 <= k1; k += 8) {
+        unsigned long long c[8], b[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { c[i] = tile_cnt[k + i]; b[i] = tile_bytes[k + i]; }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            tile_cnt[k + i] = ac;
+            tile_bytes[k + i] = ab;
+            ac += c[i];
+            ab += b[i];
+        }
+    }
+    for (; k < k1; ++k) {
         const unsigned long long vc = tile_cnt[k], vb = tile_bytes[k];
         tile_cnt[k] = ac;
         tile_bytes[k] = ab;
