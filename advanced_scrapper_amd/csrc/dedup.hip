@@ -612,21 +612,19 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
     }
 }
 
-// dense kept rows: a wave owns kept rows [k0, k0 + 64) whose dense bytes are one contiguous range
+// (groups whose dense range exceeds a wave's LDS stage) dense kept rows: a wave owns kept rows [k0, k0 + 64) whose dense bytes are one contiguous range
 // [D0, D1).  Lane l handles the 8-aligned destination chunks D0 & ~7 + 8 (l + 64 t): a chunk inside
 // one row is one unaligned 8-byte load from the sparse arena and one aligned 8-byte store; a chunk
 // with a row boundary (or a range edge) is written byte by byte from up to 8 rows, whose offsets all
 // lanes fetch with the same shuffles.  The owner row of a byte is the last of the 64 whose dense
 // offset is <= it (binary search over shuffles).
-__global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
-                                                        const int64_t *__restrict__ kept_row,
-                                                        const int64_t *__restrict__ off, Scratch S,
-                                                        uint8_t *__restrict__ dst)
+__device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_kept, const int64_t *__restrict__ kept_off,
+                                                         const int64_t *__restrict__ kept_row,
+                                                         const int64_t *__restrict__ off, const Scratch &S,
+                                                         uint8_t *__restrict__ dst)
 {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
-    const int64_t n_waves = ((int64_t)gridDim.x * BLOCK) >> 6;
-    for (int64_t k0 = wave * 64; k0 < n_kept; k0 += n_waves * 64) {
+    {
         const int64_t kk = k0 + lane;
         const int64_t kend = k0 + 64 < n_kept ? k0 + 64 : n_kept;
         const int64_t D1 = kept_off[kend];
@@ -674,6 +672,77 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
                 }
                 if (edge && inner) *(uint64_t *)(dst + x0) = w;   // assembled from several rows: one full store
             }
+        }
+    }
+}
+
+
+// dense kept rows: a wave owns kept rows [k0, k0 + 64) whose dense bytes are one contiguous range [D0, D1).
+// The range is staged in the wave's LDS (zeroed, then every lane ORs its row's dwords in at the row's dense
+// offset: the partial dwords two rows share merge by ds_or_b32) and written out with aligned 16-byte stores,
+// the two partial 16-byte chunks it may share with the neighbouring groups byte by byte.  A group whose range
+// exceeds the stage takes copy_group_shfl.
+constexpr int CP_STAGE = 8192;   // bytes of LDS per wave
+__global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
+                                                        const int64_t *__restrict__ kept_row,
+                                                        const int64_t *__restrict__ off, Scratch S,
+                                                        uint8_t *__restrict__ dst)
+{
+    __shared__ uint4 stage_all[(BLOCK / 64) * (CP_STAGE / 16)];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    uint4 *st16 = stage_all + wib * (CP_STAGE / 16);
+    uint32_t *st32 = (uint32_t *)st16;
+    const uint8_t *st8 = (const uint8_t *)st16;
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    for (int64_t k0 = wave * 64; k0 < n_kept; k0 += n_waves * 64) {
+        const int64_t kk = k0 + lane;
+        const int64_t kend = k0 + 64 < n_kept ? k0 + 64 : n_kept;
+        const int64_t D0 = kept_off[k0], D1 = kept_off[kend];
+        const int64_t A = D0 & ~(int64_t)15;
+        if (D1 - A > CP_STAGE) {   // (wave-uniform)
+            copy_group_shfl(k0, n_kept, kept_off, kept_row, off, S, dst);
+            continue;
+        }
+        int64_t d0 = 0, len = 0, src = 0;
+        if (kk < n_kept) {
+            const int64_t row = kept_row[kk];
+            d0 = kept_off[kk];
+            len = kept_off[kk + 1] - d0;
+            src = obase(off[row], row);
+        }
+        const int nz = (int)((D1 - A + 15) >> 4);
+        __builtin_amdgcn_wave_barrier();
+        for (int c = lane; c < nz; c += 64) st16[c] = make_uint4(0u, 0u, 0u, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (len > 0) {
+            // the row's bytes are zero past its end within its last 8-byte word of the sparse arena
+            const int64_t o = d0 - A;
+            const uint32_t sh = (uint32_t)(o & 3) * 8u;
+            uint32_t *dw = st32 + (o >> 2);
+            const uint32_t *sw = (const uint32_t *)(S.out + src);
+            const int nw = (int)((len + 3) >> 2);
+            for (int i = 0; i < nw; ++i) {
+                const uint32_t v = sw[i];
+                atomicOr(&dw[i], v << sh);
+                // (the spill holds only the row's own bytes, all inside [A, D1): zero spills are not written)
+                if (sh && (v >> (32u - sh))) atomicOr(&dw[i + 1], v >> (32u - sh));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t a0 = (D0 + 15) & ~(int64_t)15, a1 = D1 & ~(int64_t)15;
+        if (a0 >= a1) {
+            for (int64_t x = D0 + lane; x < D1; x += 64) dst[x] = st8[x - A];
+        } else {
+            if (D0 + lane < a0) dst[D0 + lane] = st8[D0 + lane - A];
+            if (a1 + lane < D1) dst[a1 + lane] = st8[a1 + lane - A];
+            for (int64_t q = a0 + 16 * (int64_t)lane; q < a1; q += 16 * 64)
+                *(uint4 *)(dst + q) = st16[(q - A) >> 4];
         }
     }
 }
