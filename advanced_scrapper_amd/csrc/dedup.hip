@@ -269,7 +269,7 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
         return -1;
     }
     // ---- pass 1: the cut j, the first extra ':' and the first 'news/%' | "news/'" end
-    int64_t j = -1, ec = INT64_MAX, kf = INT64_MAX;
+    int64_t j = -1, ec = INT64_MAX, ec2 = INT64_MAX, kf = INT64_MAX;   // ec / ec2: first two extra ':' 
     bool scheme_http = false;
     for (int64_t t = 0; t < L && j < 0; t += 4) {
         const uint32_t x = src.ld32(b + t);
@@ -285,7 +285,8 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
             const bool p80 = q + 3 <= L && (src.ld32(b + q) & 0xFFFFFFu) == 0x30383Au;
             if (!p80 && q == 4 && src.ld32(b) == 0x70747468u) { scheme_http = true; continue; }
             if (!p80 && q == 5 && src.ld32(b) == 0x70747468u && (src.ld32(b + 4) & 0xFFFFu) == 0x3A73u) continue;
-            if (q < ec) ec = q;
+            if (q < ec) { ec2 = ec; ec = q; }
+            else if (q < ec2) ec2 = q;
         }
         while (nm) {
             const int64_t q = t + (__builtin_ctz(nm) >> 3);
@@ -319,27 +320,67 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
     uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
     int64_t len3;
     bool bad;
-    if (ec >= j) {
-        // ---- fast path: no ':80' and no 'http:' in the prefix except the scheme's
+    const bool gap = ec < j;
+    if (!gap || (ec2 >= j && ec > 5 && ec + 3 <= j && (src.ld32(b + ec) & 0xFFFFFFu) == 0x30383Au)) {
+        // ---- fast path: the prefix u[0, j) minus at most one ':80' after the scheme (a splice with one gap at
+        // G; with no other extra ':' left neither a new ':80' nor a new 'http:' can form), 'http:' -> 'https:'
+        // at the scheme, ".html" at E.  Every lane runs the same word loop; only the filter window across the
+        // gap is extra work for the gap rows
         const int ins = (scheme_http && j > 4) ? 1 : 0;
-        const int64_t E = j + ins;
+        const int64_t G = gap ? ec + ins : INT64_MAX / 2, E = j + ins - (gap ? 3 : 0);
         len3 = E + 5;
-        bad = kf < j;
-        for (int64_t x0 = 0; x0 < len3; x0 += 8) {
-            uint64_t w = 0;
-            if (x0 < E) {
-                if (!ins) w = src.ld64(b + x0);
-                else if (x0 == 0) w = 0x7370747468ull | (src.ld64(b + 4) << 40);   // "https" + u[4..7)
-                else w = src.ld64(b + x0 - 1);
+        auto body = [&](int64_t x) -> uint64_t {   // bytes [x, x + 8) of the normalised prefix, x < E, x % 8 == 0
+            uint64_t w = (ins && x == 0) ? 0x7370747468ull | (src.ld64(b + 4) << 40)   // "https" + u[4..7)
+                                         : src.ld64(b + x - ins + (x >= G ? 3 : 0));
+            if (x < G && G < x + 8) {
+                const int k = (int)(G - x) * 8;
+                w = (w & ((1ull << k) - 1)) | (src.ld64(b + G - ins + 3) << k);
             }
-            if (E < x0 + 8) {   // splice ".html" at E, zeros after it
-                if (E >= x0) {
-                    const int sh = (int)(E - x0) * 8;
+            return w;
+        };
+        auto splice = [&](uint64_t w, int64_t x) -> uint64_t {   // ".html" at E, zeros after it
+            if (E < x + 8) {
+                if (E >= x) {
+                    const int sh = (int)(E - x) * 8;
                     w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
                 } else {
-                    w = DOTHTML >> ((x0 - E) * 8);
+                    const int64_t d = x - E;
+                    w = d < 8 ? DOTHTML >> (8 * d) : 0ull;
                 }
             }
+            return w;
+        };
+        bool jn = false;
+        if (gap) {
+            // 'news/%' | "news/'" across the gap: windows starting at G - 5 .. G - 1 (G >= 6)
+            auto seg1 = [&](int64_t x) -> uint64_t {   // bytes [x, x + 8) of u[0, ec) after the 's' insertion
+                if (!ins) return src.ld64(b + x);
+                if (x >= 5) return src.ld64(b + x - 1);
+                const uint64_t h0 = 0x7370747468ull | (src.ld64(b + 4) << 40);
+                return x ? (h0 >> (8 * x)) | (src.ld64(b + 7) << (64 - 8 * x)) : h0;
+            };
+            auto nword = [&](int64_t x) -> uint64_t {
+                uint64_t w = 0;
+                if (x < E) {
+                    if (x + 8 <= G) w = seg1(x);
+                    else if (x >= G) w = src.ld64(b + x - ins + 3);
+                    else {
+                        const int k = (int)(G - x) * 8;
+                        w = (seg1(x) & ((1ull << k) - 1)) | (src.ld64(b + G - ins + 3) << k);
+                    }
+                }
+                return splice(w, x);
+            };
+            const uint64_t lo = nword(G - 5), hi = nword(G + 3);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint64_t win = ((lo >> (8 * k)) | (k ? hi << (64 - 8 * k) : 0ull)) & 0xFFFFFFFFFFFFull;
+                jn |= win == 0x252F7377656Eull || win == 0x272F7377656Eull;
+            }
+        }
+        bad = kf < j || jn;
+        for (int64_t x0 = 0; x0 < len3; x0 += 8) {
+            const uint64_t w = splice(x0 < E ? body(x0) : 0ull, x0);
             *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
             h2 = mix2(h2, w);
