@@ -107,7 +107,6 @@ struct Scratch {
     uint2 *slow;             // rows (index, cut) for the byte-serial rewrite: slow_cap per transform wave
     uint32_t *wslow;         // per transform wave: its slow rows (no shared counter: one address for every
     uint32_t slow_cap;       //   wave's atomic serialised the transform)
-    unsigned long long *nslow;
 };
 
 // byte-serial writer of the normalised URL: 8-byte words to the sparse arena + hashes + filter window
@@ -456,6 +455,25 @@ __global__ __launch_bounds__(BLOCK) void dd_slow_kernel(const uint8_t *__restric
     }
 }
 
+// the normalised bytes of rows a and b (same length len) in the sparse arena are equal: 8 word pairs in flight
+// per round (a loop that tests each word before loading the next waits one memory round trip per word)
+__device__ __forceinline__ bool same_url(const Scratch &S, const int64_t *__restrict__ off, int64_t a, int64_t b,
+                                         uint32_t len)
+{
+    const int64_t oa = off[a], ob = off[b];
+    const uint64_t *x = (const uint64_t *)(S.out + obase(oa, a));
+    const uint64_t *y = (const uint64_t *)(S.out + obase(ob, b));
+    const uint32_t nw = (len + 7) / 8;
+    for (uint32_t w = 0; w < nw; w += 8) {
+        uint64_t d = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (w + q < nw) d |= x[w + q] ^ y[w + q];
+        if (d) return false;
+    }
+    return true;
+}
+
 __device__ __forceinline__ uint64_t slot_key(uint64_t h1, int64_t row)
 {
     const uint32_t tag = (uint32_t)(h1 >> 32) | 1u;   // never 0 (0 = empty slot)
@@ -502,13 +520,8 @@ __global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__
             }
             const int64_t rep = (int64_t)(uint32_t)cur;
             if (rep != i) {
-                bool eq = S.len3[rep] == S.len3[i] && S.h2[rep] == S.h2[i];
-                if (eq) {
-                    const uint64_t *a = (const uint64_t *)(S.out + obase(off[i], i));
-                    const uint64_t *r = (const uint64_t *)(S.out + obase(off[rep], rep));
-                    const uint32_t nw = (S.len3[i] + 7) / 8;
-                    for (uint32_t w = 0; w < nw && eq; ++w) eq = a[w] == r[w];
-                }
+                const uint32_t len = S.len3[i];
+                const bool eq = S.len3[rep] == len && S.h2[rep] == S.h2[i] && same_url(S, off, i, rep, len);
                 k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
                 code[i] = k;
             }
@@ -524,6 +537,18 @@ __global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__
         unsigned long long v = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : c4;
         for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
         if ((threadIdx.x & 63) == 0 && v) atomicAdd(&S.cnt[q], v);
+    }
+}
+
+// the CODE_COLLIDE rows (rare: a 32-bit tag shared by two URLs in one probe run), listed for the host's exact pass
+__global__ __launch_bounds__(BLOCK) void dd_collect_kernel(const uint8_t *__restrict__ code, int64_t n,
+                                                           unsigned long long *__restrict__ count,
+                                                           uint32_t *__restrict__ list, uint32_t cap)
+{
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        if (code[i] != CODE_COLLIDE) continue;
+        const unsigned long long p = atomicAdd(count, 1ull);
+        if (p < cap) list[p] = (uint32_t)i;
     }
 }
 
@@ -804,6 +829,7 @@ struct kw_dedup {
     uint8_t *kept_bytes = nullptr;
     size_t kept_bytes_cap = 0;
     void *d_kept = nullptr;
+    void *d_collide = nullptr;   // count + list of the CODE_COLLIDE rows
     int64_t n = 0, n_kept = 0, n_kept_bytes = 0;
     int64_t counts[4] = {0, 0, 0, 0};
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -835,17 +861,36 @@ extern "C" int kw_dedup_create(int32_t device, kw_dedup **out)
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// exact keep-first over the rows that share a hash tag with a different URL
+// exact keep-first over the rows that share a hash tag with a different URL (in row order)
 static int resolve_collisions(kw_dedup *h, const int64_t *d_off, int64_t n, uint8_t *d_code, hipStream_t st)
 {
-    std::vector<uint8_t> code(n);
-    DDCHK(h, hipMemcpyAsync(code.data(), d_code, n, hipMemcpyDeviceToHost, st));
+    constexpr uint32_t CAP = 1u << 16;
+    std::vector<int64_t> rows;
+    if (!h->d_collide) DDCHK(h, hipMalloc(&h->d_collide, 8 + 4 * (size_t)CAP));
+    unsigned long long *d_cnt = (unsigned long long *)h->d_collide;
+    DDCHK(h, hipMemsetAsync(d_cnt, 0, 8, st));
+    const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
+    hipLaunchKernelGGL(dd_collect_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, d_cnt,
+                       (uint32_t *)(d_cnt + 1), CAP);
+    DDCHK(h, hipGetLastError());
+    unsigned long long m = 0;
+    DDCHK(h, hipMemcpyAsync(&m, d_cnt, 8, hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
+    if (m <= CAP) {
+        std::vector<uint32_t> l(m);
+        if (m) DDCHK(h, hipMemcpy(l.data(), d_cnt + 1, 4 * m, hipMemcpyDeviceToHost));
+        rows.assign(l.begin(), l.end());
+        std::sort(rows.begin(), rows.end());
+    } else {
+        std::vector<uint8_t> code(n);
+        DDCHK(h, hipMemcpy(code.data(), d_code, n, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n; ++i)
+            if (code[i] == CODE_COLLIDE) rows.push_back(i);
+    }
     std::unordered_set<std::string> seen;
     std::vector<int64_t> offs(2);
     std::vector<uint32_t> len(1);
-    for (int64_t i = 0; i < n; ++i) {
-        if (code[i] != CODE_COLLIDE) continue;
+    for (const int64_t i : rows) {
         DDCHK(h, hipMemcpy(offs.data(), d_off + i, 8, hipMemcpyDeviceToHost));
         DDCHK(h, hipMemcpy(len.data(), h->S.len3 + i, 4, hipMemcpyDeviceToHost));
         std::string s(len[0], '\0');
@@ -904,7 +949,6 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.table = (unsigned long long *)carve(8 * tsize);
     S.mask = tsize - 1;
     S.cnt = (unsigned long long *)carve(8 * 8);
-    S.nslow = S.cnt + 6;
     S.slow = (uint2 *)carve(8 * ((size_t)n_tw * S.slow_cap));
     S.wslow = (uint32_t *)carve(4 * (size_t)n_tw);
     S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
@@ -914,9 +958,9 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->totals = (unsigned long long *)carve(16);
     h->kept_off = (int64_t *)carve(8 * ((size_t)n + 1));
     h->kept_row = (int64_t *)carve(8 * ((size_t)n + 1));
-    DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
     DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
     const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
+    DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
     DDCHK(h, hipEventRecord(h->ev[0], st));
     hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
     hipLaunchKernelGGL(dd_slow_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
@@ -1018,6 +1062,7 @@ extern "C" int kw_dedup_destroy(kw_dedup *h)
     (void)hipSetDevice(h->device);
     if (h->d_buf) (void)hipFree(h->d_buf);
     if (h->d_kept) (void)hipFree(h->d_kept);
+    if (h->d_collide) (void)hipFree(h->d_collide);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     delete h;
