@@ -7,17 +7,17 @@
 //                        not '\n'), rewrite the prefix (':80' removed, 'http:'
 //                        -> 'https:'), append ".html", flag 'news/%' / "news/'",
 //                        write the normalised URL into a sparse 8-aligned arena
-//                        and hash it (two independent 64-bit word hashes).
-//                        Rows whose only ':' is the scheme's take a word-wide
-//                        copy; the rest run the byte-serial rewrite.
+//                        and hash it (one 64-bit word hash: tag and slot).
+//                        Rows whose only extra ':' is at most one ':80' take a
+//                        word-wide copy; the rest run the byte-serial rewrite.
 //   dd_insert_kernel     open-addressing table of 64-bit slots {tag, row}: the
 //                        first inserter claims a slot by CAS, rows with the same
 //                        tag keep the smallest row by atomicMin (keep='first').
 //   dd_decide_kernel     each row finds its slot; rep == row -> kept, else the
 //                        row is a duplicate iff its normalised bytes equal the
-//                        rep's (length, second hash, then every word).  Rows
-//                        that share a tag with a different URL (a 64-bit hash
-//                        collision) are resolved exactly on the host.
+//                        rep's (length, then every word).  Rows that share a
+//                        32-bit tag with a different URL are resolved exactly
+//                        on the host.
 //   dd_count / dd_scan / dd_place / dd_copy
 //                        dense offsets, source rows and bytes of the kept rows.
 //
@@ -70,21 +70,16 @@ __device__ __forceinline__ uint64_t ld64(const uint8_t *__restrict__ a, int64_t 
     return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, s) << 32);
 }
 
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t v)   // high bit set in (at least) every zero byte
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t v, uint32_t pat)   // 0x80 in exactly the bytes equal to pat's
 {
-    return (v - 0x01010101u) & ~v & 0x80808080u;
+    const uint32_t d = v ^ pat;
+    return ~(((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
 }
 
 __host__ __device__ __forceinline__ uint64_t mix1(uint64_t h, uint64_t w)
 {
     h = (h ^ w) * 0x9E3779B97F4A7C15ull;
     return h ^ (h >> 32);
-}
-__host__ __device__ __forceinline__ uint64_t mix2(uint64_t h, uint64_t w)
-{
-    h = (h ^ w) * 0xC2B2AE3D27D4EB4Full;
-    h ^= h >> 29;
-    return h * 0x165667B19E3779F9ull;
 }
 __host__ __device__ __forceinline__ uint64_t fmix(uint64_t h)
 {
@@ -97,7 +92,7 @@ __host__ __device__ __forceinline__ uint64_t fmix(uint64_t h)
 
 struct Scratch {
     uint8_t *out;            // sparse normalised URLs
-    uint64_t *h1, *h2;       // per row
+    uint64_t *h1;            // per row: the normalised URL's 64-bit hash (tag + slot; equality is decided on bytes)
     uint32_t *len3;          // per row: normalised length
     unsigned long long *table;
     uint64_t mask;
@@ -111,7 +106,7 @@ struct Scratch {
 
 // byte-serial writer of the normalised URL: 8-byte words to the sparse arena + hashes + filter window
 struct Emit {
-    uint64_t w, win, h1, h2;
+    uint64_t w, win, h1;
     int64_t pos, len;
     int nb;
     bool bad;
@@ -128,7 +123,6 @@ struct Emit {
         if (nb == 8) {
             *(uint64_t *)(out + pos) = w;
             h1 = mix1(h1, w);
-            h2 = mix2(h2, w);
             pos += 8;
             w = 0;
             nb = 0;
@@ -139,7 +133,6 @@ struct Emit {
         if (nb) {
             *(uint64_t *)(out + pos) = w;
             h1 = mix1(h1, w);
-            h2 = mix2(h2, w);
         }
     }
 };
@@ -211,14 +204,12 @@ struct LdsSrc {
 };
 
 // finish a row: hashes, length, code
-__device__ __forceinline__ void finish_row(uint64_t h1, uint64_t h2, int64_t len3, bool bad, int64_t i,
+__device__ __forceinline__ void finish_row(uint64_t h1, int64_t len3, bool bad, int64_t i,
                                            uint8_t *__restrict__ code, const Scratch &S)
 {
     h1 = fmix(h1 ^ (uint64_t)len3);
-    h2 = fmix(h2 ^ ((uint64_t)len3 * 0x9E3779B97F4A7C15ull));
     if (S.weak) h1 &= 0xFull;
     S.h1[i] = h1;
-    S.h2[i] = h2;
     S.len3[i] = (uint32_t)len3;
     code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
 }
@@ -228,7 +219,7 @@ __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j
                          uint8_t *__restrict__ code, const Scratch &S)
 {
     Emit Em;
-    Em.w = 0; Em.win = 0; Em.h1 = 0x243F6A8885A308D3ull; Em.h2 = 0x13198A2E03707344ull;
+    Em.w = 0; Em.win = 0; Em.h1 = 0x243F6A8885A308D3ull;
     Em.pos = 0; Em.len = 0; Em.nb = 0; Em.bad = false; Em.out = S.out + obase(b, i);
     Rewrite R;
     R.P = 0; R.np = 0; R.Q = 0; R.nq = 0;
@@ -240,7 +231,7 @@ __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j
     R.flush(Em);
     Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
     Em.finish();
-    finish_row(Em.h1, Em.h2, Em.len, Em.bad, i, code, S);
+    finish_row(Em.h1, Em.len, Em.bad, i, code, S);
 }
 
 // one row: returns -1 when done, or the cut j of a row that needs slow_row
@@ -250,73 +241,78 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
 {
     if (!S.normalize) {
         // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
-        uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
+        uint64_t h1 = 0x243F6A8885A308D3ull;
         for (int64_t x0 = 0; x0 < L; x0 += 8) {
             uint64_t w = src.ld64(b + x0);
             if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
             *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
-            h2 = mix2(h2, w);
         }
         h1 = fmix(h1 ^ (uint64_t)L);
-        h2 = fmix(h2 ^ ((uint64_t)L * 0x9E3779B97F4A7C15ull));
         if (S.weak) h1 &= 0xFull;
         S.h1[i] = h1;
-        S.h2[i] = h2;
         S.len3[i] = (uint32_t)L;
         code[i] = KW_URL_KEPT;
         return -1;
     }
-    // ---- pass 1: the cut j, the first extra ':' and the first 'news/%' | "news/'" end
-    int64_t j = -1, ec = INT64_MAX, ec2 = INT64_MAX, kf = INT64_MAX;   // ec / ec2: first two extra ':' 
+    // ---- pass 1: the cut j, the first two extra ':' and the first 'news/%' | "news/'" end, one 4-byte word a
+    // step with per-byte masks and no per-event loops (every event kind happens in some lane of nearly every
+    // step, so per-event loops ran in nearly every step); only the rare '%' / "'" bytes take a loop
+    int64_t j = -1, ec = INT64_MAX, ec2 = INT64_MAX, kf = INT64_MAX;   // ec / ec2: first two extra ':'
     bool scheme_http = false;
-    for (int64_t t = 0; t < L && j < 0; t += 4) {
-        const uint32_t x = src.ld32(b + t);
-        uint32_t hm = zero_bytes(x ^ 0x68686868u);   // 'h'
-        uint32_t cm = zero_bytes(x ^ 0x3A3A3A3Au);   // ':'
-        uint32_t nm = zero_bytes(x ^ 0x6E6E6E6Eu);   // 'n'
-        while (cm) {
-            const int64_t q = t + (__builtin_ctz(cm) >> 3);
-            cm &= cm - 1;
-            if (q >= L) break;
-            if (((src.ld32(b + q) ^ 0x3Au) & 0xFFu) != 0) continue;   // false positive of zero_bytes
-            // the scheme's colon ("http:" / "https:"), unless it starts a ':80'
-            const bool p80 = q + 3 <= L && (src.ld32(b + q) & 0xFFFFFFu) == 0x30383Au;
-            if (!p80 && q == 4 && src.ld32(b) == 0x70747468u) { scheme_http = true; continue; }
-            if (!p80 && q == 5 && src.ld32(b) == 0x70747468u && (src.ld32(b + 4) & 0xFFFFu) == 0x3A73u) continue;
-            if (q < ec) { ec2 = ec; ec = q; }
-            else if (q < ec2) ec2 = q;
+    uint32_t excl = 0;   // the scheme's ':' (q == 4 of "http:", q == 5 of "https:", neither starting ':80')
+    if (L >= 5 && src.ld32(b) == 0x70747468u) {
+        const uint32_t w4 = src.ld32(b + 4);
+        if ((w4 & 0xFFu) == 0x3Au && !(L >= 7 && (w4 & 0xFFFFFFu) == 0x30383Au)) { scheme_http = true; excl = 0x80u; }
+        if (L >= 6 && (w4 & 0xFFFFu) == 0x3A73u && !(L >= 8 && (w4 >> 8) == 0x30383Au)) excl = 0x8000u;
+    }
+    uint32_t x = src.ld32(b), xp = 0;
+    for (int64_t t = 0; t < L; t += 4) {
+        const uint32_t y = src.ld32(b + t + 4);
+        const int64_t r = L - t;
+        const uint32_t in = r >= 4 ? 0x80808080u : 0x80808080u & ((1u << (8 * r)) - 1u);   // positions < L
+        // extra colons: the first two positions (all new positions lie past the recorded ones)
+        uint32_t cm = eq_bytes(x, 0x3A3A3A3Au) & in;
+        if (t == 4) cm &= ~excl;
+        const uint32_t cm1 = cm & (cm - 1u);
+        const int64_t c0 = cm ? t + (__builtin_ctz(cm) >> 3) : INT64_MAX;
+        const int64_t c1 = cm1 ? t + (__builtin_ctz(cm1) >> 3) : INT64_MAX;
+        ec2 = ec == INT64_MAX ? c1 : (ec2 == INT64_MAX ? c0 : ec2);
+        ec = ec == INT64_MAX ? c0 : ec;
+        // 'news/%' | "news/'": from the (rare) '%' / "'" byte p back to its "news/" (kf = p = q + 5)
+        uint32_t pm = (eq_bytes(x, 0x25252525u) | eq_bytes(x, 0x27272727u)) & in;
+        while (pm) {
+            const int64_t p = t + (__builtin_ctz(pm) >> 3);
+            pm &= pm - 1u;
+            if (p >= 5 && p < kf && src.ld32(b + p - 5) == NEWS4 && (src.ld32(b + p - 1) & 0xFFu) == 0x2Fu) kf = p;
         }
-        while (nm) {
-            const int64_t q = t + (__builtin_ctz(nm) >> 3);
-            nm &= nm - 1;
-            if (q + 6 > L || q + 5 >= kf) continue;
-            if (src.ld32(b + q) != NEWS4) continue;
-            const uint32_t y = src.ld32(b + q + 4);
-            if ((y & 0xFF) == '/' && (((y >> 8) & 0xFF) == '%' || ((y >> 8) & 0xFF) == '\'')) kf = q + 5;
-        }
-        while (hm) {
+        // "html" at q with q >= 1, q + 4 <= L and no '\n' before it
+        uint32_t hm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hm |= __builtin_amdgcn_alignbyte(y, x, k) == HTML4 ? 0x80u << (8 * k) : 0u;
+        const int64_t r3 = r - 3;
+        hm &= r3 >= 4 ? 0x80808080u : (r3 <= 0 ? 0u : 0x80808080u & ((1u << (8 * r3)) - 1u));
+        hm &= ~eq_bytes(__builtin_amdgcn_alignbyte(x, xp, 3), 0x0A0A0A0Au);
+        if (t == 0) hm &= ~0x80u;
+        if (hm) {
             const int64_t q = t + (__builtin_ctz(hm) >> 3);
-            hm &= hm - 1;
-            if (q < 1 || q + 4 > L) continue;
-            if (src.ld32(b + q) != HTML4) continue;
-            const uint32_t pv = src.ld32(b + q - 1) & 0xFFu;
-            if (pv == '\n') continue;
             // the code point before "html" starts at its lead byte
             int64_t s = q - 1;
-            if (pv >= 0x80) {
+            if ((src.ld32(b + s) & 0xFFu) >= 0x80u) {
                 while (s > 0 && (src.ld32(b + s) & 0xC0u) == 0x80u && q - s < 4) --s;
             }
             j = s;
             break;
         }
+        xp = x;
+        x = y;
     }
     if (j < 0) {
         code[i] = KW_URL_NO_HTML;
         S.len3[i] = 0;
         return -1;
     }
-    uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;
+    uint64_t h1 = 0x243F6A8885A308D3ull;
     int64_t len3;
     bool bad;
     const bool gap = ec < j;
@@ -382,12 +378,11 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
             const uint64_t w = splice(x0 < E ? body(x0) : 0ull, x0);
             *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
-            h2 = mix2(h2, w);
         }
     } else {
         return j;   // the byte-serial rewrite runs in dd_slow_kernel, off the divergent path
     }
-    finish_row(h1, h2, len3, bad, i, code, S);
+    finish_row(h1, len3, bad, i, code, S);
     return -1;
 }
 
@@ -521,7 +516,7 @@ __global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__
             const int64_t rep = (int64_t)(uint32_t)cur;
             if (rep != i) {
                 const uint32_t len = S.len3[i];
-                const bool eq = S.len3[rep] == len && S.h2[rep] == S.h2[i] && same_url(S, off, i, rep, len);
+                const bool eq = S.len3[rep] == len && same_url(S, off, i, rep, len);
                 k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
                 code[i] = k;
             }
@@ -785,17 +780,32 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (len > 0) {
-            // the row's bytes are zero past its end within its last 8-byte word of the sparse arena
+            // the row's bytes are zero past its end within its last 8-byte word of the sparse arena (8-aligned):
+            // 16 source dwords per round from 8 loads in flight, each destination dword the shifted pair of
+            // source dwords; the first and last destination dwords may hold a neighbour's bytes (ds_or), the
+            // rest are this row's alone (plain stores into the zeroed stage)
             const int64_t o = d0 - A;
             const uint32_t sh = (uint32_t)(o & 3) * 8u;
             uint32_t *dw = st32 + (o >> 2);
-            const uint32_t *sw = (const uint32_t *)(S.out + src);
-            const int nw = (int)((len + 3) >> 2);
-            for (int i = 0; i < nw; ++i) {
-                const uint32_t v = sw[i];
-                atomicOr(&dw[i], v << sh);
-                // (the spill holds only the row's own bytes, all inside [A, D1): zero spills are not written)
-                if (sh && (v >> (32u - sh))) atomicOr(&dw[i + 1], v >> (32u - sh));
+            const uint2 *sw = (const uint2 *)(S.out + src);
+            const int nw8 = (int)((len + 7) >> 3);
+            const int K = (int)(((o & 3) + len + 3) >> 2);
+            uint32_t prev = 0;
+            for (int k0 = 0; k0 < K; k0 += 16) {
+                uint2 v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = (k0 >> 1) + q < nw8 ? sw[(k0 >> 1) + q] : make_uint2(0u, 0u);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t cur = (j & 1) ? v[j >> 1].y : v[j >> 1].x;
+                    const uint32_t out = sh ? (cur << sh) | (prev >> (32u - sh)) : cur;
+                    prev = cur;
+                    const int k = k0 + j;
+                    if (k < K) {
+                        if (k == 0 || k == K - 1) atomicOr(&dw[k], out);
+                        else dw[k] = out;
+                    }
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -928,7 +938,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     const int64_t n_tw = (int64_t)tgrid * (BLOCK / 64);
     h->S.slow_cap = (uint32_t)(((n + 63) / 64 + n_tw - 1) / n_tw * 64);
     const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
-    const size_t need = out_bytes + align256(8 * (size_t)n) * 2 + align256(8 * (size_t)n_tw * h->S.slow_cap) +
+    const size_t need = out_bytes + align256(8 * (size_t)n) + align256(8 * (size_t)n_tw * h->S.slow_cap) +
                         align256(4 * (size_t)n_tw) + align256(4 * (size_t)n) + align256(8 * tsize) +
                         align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
                         2 * align256(8 * ((size_t)n + 1));
@@ -944,7 +954,6 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     Scratch &S = h->S;
     S.out = carve(out_bytes);
     S.h1 = (uint64_t *)carve(8 * (size_t)n);
-    S.h2 = (uint64_t *)carve(8 * (size_t)n);
     S.len3 = (uint32_t *)carve(4 * (size_t)n);
     S.table = (unsigned long long *)carve(8 * tsize);
     S.mask = tsize - 1;
