@@ -274,13 +274,15 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
         // extra colons: the first two positions (all new positions lie past the recorded ones)
         uint32_t cm = eq_bytes(x, 0x3A3A3A3Au) & in;
         if (t == 4) cm &= ~excl;
-        const uint32_t cm1 = cm & (cm - 1u);
-        const int64_t c0 = cm ? t + (__builtin_ctz(cm) >> 3) : INT64_MAX;
-        const int64_t c1 = cm1 ? t + (__builtin_ctz(cm1) >> 3) : INT64_MAX;
-        ec2 = ec == INT64_MAX ? c1 : (ec2 == INT64_MAX ? c0 : ec2);
-        ec = ec == INT64_MAX ? c0 : ec;
+        if (cm) {   // rare once the scheme's ':' is masked out
+            const uint32_t cm1 = cm & (cm - 1u);
+            const int64_t c0 = t + (__builtin_ctz(cm) >> 3);
+            const int64_t c1 = cm1 ? t + (__builtin_ctz(cm1) >> 3) : INT64_MAX;
+            ec2 = ec == INT64_MAX ? c1 : (ec2 == INT64_MAX ? c0 : ec2);
+            ec = ec == INT64_MAX ? c0 : ec;
+        }
         // 'news/%' | "news/'": from the (rare) '%' / "'" byte p back to its "news/" (kf = p = q + 5)
-        uint32_t pm = (eq_bytes(x, 0x25252525u) | eq_bytes(x, 0x27272727u)) & in;
+        uint32_t pm = eq_bytes(x | 0x02020202u, 0x27272727u) & in;   // '%' (0x25) and "'" (0x27) differ in bit 1 only
         while (pm) {
             const int64_t p = t + (__builtin_ctz(pm) >> 3);
             pm &= pm - 1u;
@@ -290,10 +292,12 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
         uint32_t hm = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) hm |= __builtin_amdgcn_alignbyte(y, x, k) == HTML4 ? 0x80u << (8 * k) : 0u;
-        const int64_t r3 = r - 3;
-        hm &= r3 >= 4 ? 0x80808080u : (r3 <= 0 ? 0u : 0x80808080u & ((1u << (8 * r3)) - 1u));
-        hm &= ~eq_bytes(__builtin_amdgcn_alignbyte(x, xp, 3), 0x0A0A0A0Au);
-        if (t == 0) hm &= ~0x80u;
+        if (hm) {   // (once a row, at its end) validate: q + 4 <= L, q >= 1, no '\n' before q
+            const int64_t r3 = r - 3;
+            hm &= r3 >= 4 ? 0x80808080u : (r3 <= 0 ? 0u : 0x80808080u & ((1u << (8 * r3)) - 1u));
+            hm &= ~eq_bytes(__builtin_amdgcn_alignbyte(x, xp, 3), 0x0A0A0A0Au);
+            if (t == 0) hm &= ~0x80u;
+        }
         if (hm) {
             const int64_t q = t + (__builtin_ctz(hm) >> 3);
             // the code point before "html" starts at its lead byte
