@@ -148,6 +148,20 @@ class Exchange:
         td.all_reduce(t, op=td.ReduceOp.MIN)
         return t.cpu().numpy()
 
+    def exchange_objects(self, send: list) -> list:
+        """``send[r]`` (a picklable object) goes to rank r; returns what every rank sent to this one, in rank
+        order (one gather per destination rank; host-side bookkeeping, e.g. the output files' write index)."""
+        if self.world == 1:
+            return [send[0]]
+        import torch.distributed as td
+        recv = None
+        for dst in range(self.world):
+            lst = [None] * self.world if dst == self.rank else None
+            td.gather_object(send[dst], lst, dst=dst)
+            if dst == self.rank:
+                recv = lst
+        return recv
+
     def barrier(self):
         if self.world > 1:
             import torch.distributed as td

@@ -196,12 +196,16 @@ class RunFiles:
     written values (every non-time column of every 65 536-row block keeps a text witness or is all NaN, no
     cell holds a lone '\\r'), the sorted file is the written records in ``np.argsort(time_unix,
     kind='quicksort')`` order -- the records already in that order (ascending, no ties) mean no rewrite at
-    all.  Other files (pre-existing ones, those a row went to by another path) take sort_matched_csv."""
+    all.  Other files (pre-existing ones, those a row went to by another path) take sort_matched_csv.
+
+    Under ``--gpus N`` every rank appends its share of each chunk in rank order: each append is keyed
+    ``(chunk's first row, rank)``, the ranks' indexes of a file meet at the rank that sorts it
+    (:meth:`export` / :meth:`absorb`), and the key order is the file's row order."""
 
     def __init__(self, out_dir: str):
         self.out_dir = out_dir
         self.pre = set(os.listdir(out_dir)) if os.path.isdir(out_dir) else set()
-        self.files = {}          # name -> [stamps list, lengths list, flags list, header bytes]
+        self.files = {}          # name -> [[(key, stamps, lengths, flags), ...], header bytes]
         self.other = set()       # names written by another path
 
     def owned(self, name: str) -> bool:
@@ -211,22 +215,37 @@ class RunFiles:
         self.other.add(name)
         self.files.pop(name, None)
 
-    def add(self, name: str, stamps, lengths, flags, header: bytes):
+    def add(self, name: str, stamps, lengths, flags, header: bytes, key=(0, 0)):
         f = self.files.get(name)
         if f is None:
-            f = self.files[name] = [[], [], [], header]
-        f[0].append(stamps)
-        f[1].append(lengths)
-        f[2].append(flags)
+            f = self.files[name] = [[], header]
+        f[0].append((key, stamps, lengths, flags))
+
+    def export(self, names) -> dict:
+        """The index entries of ``names`` (those this run indexed), to be absorbed by another rank."""
+        return {n: self.files[n] for n in names if n in self.files}
+
+    def absorb(self, exported: dict, other=()):
+        """Merge another rank's exported entries (and the names it wrote by another path)."""
+        for n in other:
+            self.note_other(n)
+        for n, (entries, header) in exported.items():
+            if n in self.other:
+                continue
+            f = self.files.get(n)
+            if f is None:
+                f = self.files[n] = [[], header]
+            f[0].extend(entries)
 
     def finish(self, name: str) -> bool:
         """Sort one indexed file as the reference's sort_matched_csv does; False = not decidable here."""
         if not self.owned(name) or name not in self.files:
             return False
-        st, ln, fl, header = self.files[name]
-        stamps = np.concatenate(st)
-        lens = np.concatenate(ln)
-        flags = np.concatenate(fl)
+        entries, header = self.files[name]
+        entries = sorted(entries, key=lambda e: e[0])     # stable: one process's appends keep their order
+        stamps = np.concatenate([e[1] for e in entries])
+        lens = np.concatenate([e[2] for e in entries])
+        flags = np.concatenate([e[3] for e in entries])
         n = len(stamps)
         if n == 0 or (flags & _F_CR).any():
             return False
@@ -236,14 +255,14 @@ class RunFiles:
             na_all = np.bitwise_and.reduce(blk >> _F_NA_SHIFT) & 0xFF
             if (wit | na_all) != 0xFF:
                 return False
+        path = os.path.join(self.out_dir, name)
+        if os.path.getsize(path) != len(header) + int(lens.sum()):
+            return False                                  # the index does not describe the file
         if n > 1 and not (np.diff(stamps) > 0).all():
             order = np.argsort(stamps, kind='quicksort')
             if not (order == np.arange(n)).all():
-                path = os.path.join(self.out_dir, name)
                 with open(path, 'rb') as fh:
                     data = fh.read()
-                if len(data) != len(header) + int(lens.sum()):
-                    return False
                 ends = len(header) + np.cumsum(lens)
                 starts = ends - lens
                 mv = memoryview(data)
@@ -320,9 +339,9 @@ def header_bytes() -> bytes:
     return _join(list(_HEADER_COLUMNS)).encode('utf-8')
 
 
-def append_rendered(out_dir: str, rendered, run_files: 'RunFiles' = None):
+def append_rendered(out_dir: str, rendered, run_files: 'RunFiles' = None, key=(0, 0)):
     """Append rendered rows (render_native) to their files, the header first in a new file; the run index
-    records the rows of the files this run owns."""
+    records the rows of the files this run owns (under ``key``, see RunFiles)."""
     header = header_bytes()
     for name, data, stamps, lens, flags in rendered:
         path = os.path.join(out_dir, name)
@@ -332,4 +351,4 @@ def append_rendered(out_dir: str, rendered, run_files: 'RunFiles' = None):
                 fh.write(header)
             fh.write(data)
         if run_files is not None and run_files.owned(name):
-            run_files.add(name, stamps, lens, flags, header)
+            run_files.add(name, stamps, lens, flags, header, key)

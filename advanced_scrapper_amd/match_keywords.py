@@ -300,18 +300,23 @@ def _native_rows(chunk, matcher, hits, dates, error):
     return rendered, exc, row
 
 
-def _write_hits(source_name, chunk, matcher, hits, dates, error):
-    """Append the rows of a matched chunk, then raise its first error (see :func:`_hit_rows`)."""
+def _append_hits(source_name, chunk, matcher, hits, dates, error):
+    """Append the rows of a matched chunk up to its first failing article; returns that article's exception
+    and row (``None, None`` if none fails, see :func:`_hit_rows`)."""
     nat = _native_rows(chunk, matcher, hits, dates, error)
     if nat is not None:
-        rendered, exc, _row = nat
+        rendered, exc, row = nat
         egress.append_rendered(_output_dir(source_name), rendered, _RUN)
-        if exc is not None:
-            raise exc
-        return
-    by_ticker, exc, _row = _hit_rows(chunk, matcher, hits, dates, error)
+        return exc, row
+    by_ticker, exc, row = _hit_rows(chunk, matcher, hits, dates, error)
     for ticker, rows in by_ticker.items():
         _append_rows(source_name, ticker, rows)
+    return exc, row
+
+
+def _write_hits(source_name, chunk, matcher, hits, dates, error):
+    """Append the rows of a matched chunk, then raise its first error (see :func:`_hit_rows`)."""
+    exc, _row = _append_hits(source_name, chunk, matcher, hits, dates, error)
     if exc is not None:
         raise exc
 
@@ -339,7 +344,9 @@ def _write_chunk_sharded(source_name, chunk, processed_data, matcher, exchange):
     """``process_chunk`` over ``exchange.world`` GPUs (the reference's Pool over sub-chunks,
     match_keywords.py:231-238): every rank matches its byte-balanced row range of the chunk, the hit
     records move to rank 0 (RCCL), and rank 0 -- the single writer -- appends the rows in article order.
-    Every rank raises the chunk's first error after rank 0 has written the rows before it."""
+    Rank 0's first failing row (a date, assembly or output-cell error) reaches every rank by a MIN
+    all-reduce before anyone raises, so all ranks leave the chunk together: rank 0 raises the reference's
+    exception, the others the same date error (every rank parsed the dates) or :class:`ShardError`."""
     if len(chunk) == 0:
         return matcher
     texts, titles, dates, error = _prepare(chunk)
@@ -348,11 +355,21 @@ def _write_chunk_sharded(source_name, chunk, processed_data, matcher, exchange):
     lo, hi = shard_rows(texts, titles, n_ok, exchange.rank, exchange.world)
     local = matcher.match_device(texts[lo:hi], titles[lo:hi])
     allh = exchange.gather(local, lo)
+    never = np.iinfo(np.int64).max
+    exc, row = None, None
     if exchange.rank == 0:
         hits = records_from_tensor(allh) if n_ok else None
-        _write_hits(source_name, chunk, matcher, hits, dates, error)
-    elif error is not None:
-        raise error
+        try:
+            exc, row = _append_hits(source_name, chunk, matcher, hits, dates, error)
+        except Exception as e:   # noqa: BLE001 - an unexpected writer error still releases the other ranks
+            exc, row = e, -1
+    first = int(exchange.allreduce_min([row if exc is not None else never])[0])
+    if first != never:
+        if exc is not None:
+            raise exc
+        if error is not None and first == n_ok:
+            raise error
+        raise ShardError(f'process_chunk stopped at row {first} of a chunk (on rank 0)')
     return matcher
 
 
@@ -419,15 +436,26 @@ def _write_shard(source_name, chunk: ShardChunk, processed_data, matcher, exchan
     else:
         by_ticker, exc, row = _hit_rows(chunk, matcher, hits, dates, error)
     never = np.iinfo(np.int64).max
-    first = int(exchange.allreduce_min([chunk.lo + row if exc is not None else never])[0])
-    for r in range(exchange.world):
-        if r == exchange.rank and chunk.lo <= first:
+    # one MIN all-reduce: the chunk's first failing row, each rank's first row, and which ranks have rows
+    # to append (0 = rows); a rank whose share starts after the failing row writes nothing
+    w = exchange.world
+    v = np.full(1 + 2 * w, never, dtype=np.int64)
+    v[0] = chunk.lo + row if exc is not None else never
+    v[1 + exchange.rank] = chunk.lo
+    v[1 + w:] = 1
+    v[1 + w + exchange.rank] = 0 if (rendered if by_ticker is None else by_ticker) else 1
+    agreed = exchange.allreduce_min(v)
+    first = int(agreed[0])
+    writers = [r for r in range(w) if agreed[1 + w + r] == 0 and agreed[1 + r] <= first]
+    for k, r in enumerate(writers):          # rank order = article order; a barrier only between writers
+        if r == exchange.rank:
             if by_ticker is None:
-                egress.append_rendered(_output_dir(source_name), rendered)
+                egress.append_rendered(_output_dir(source_name), rendered, _RUN, (chunk.chunk_index0, r))
             else:
                 for ticker, rows in by_ticker.items():
                     _append_rows(source_name, ticker, rows)
-        exchange.barrier()
+        if k + 1 < len(writers):
+            exchange.barrier()
     if first != never:
         if exc is not None and chunk.lo + row == first:
             raise exc
@@ -601,24 +629,40 @@ def _run_sharded(args, processed, exchange, device, out_dir, matcher=None):
     """``--gpus N``: every rank reads its byte-balanced share of each chunk (ingest.read_chunks_sharded),
     matches and writes it (rank order per chunk); then the ranks sort disjoint sets of the output files.
     A chunk pandas must parse (the native tokenizer cannot prove its dtypes) is parsed whole by every rank,
-    matched in shares and written by rank 0."""
+    matched in shares and written by rank 0.  Every rank indexes the rows it appends (egress.RunFiles, keyed
+    by chunk and rank); each file's index meets at the rank that sorts it, so the files this run created are
+    sorted from the index, without the reference's re-read (match_keywords.py:243-244)."""
+    global _RUN
     rank, world = exchange.rank, exchange.world
-    for chunk in ingest.read_chunks_sharded(args.articles, args.chunksize, rank, world, exchange.allreduce_min):
-        if isinstance(chunk, ShardChunk):
+    _RUN = egress.RunFiles(out_dir)          # every rank lists the directory before any rank writes
+    try:
+        for chunk in ingest.read_chunks_sharded(args.articles, args.chunksize, rank, world, exchange.allreduce_min):
+            if isinstance(chunk, ShardChunk):
+                if matcher is None:
+                    matcher = get_matcher(processed, device, _native_sample(chunk))
+                matcher = _write_shard(args.source, chunk, processed, matcher, exchange)
+                continue
             if matcher is None:
-                matcher = get_matcher(processed, device, _native_sample(chunk))
-            matcher = _write_shard(args.source, chunk, processed, matcher, exchange)
-            continue
-        if matcher is None:
-            matcher = get_matcher(processed, device, [field_str(v) for v in chunk['article_text'].tolist()])
-        matcher = _write_chunk_sharded(args.source, chunk, processed, matcher, exchange)
+                matcher = get_matcher(processed, device, [field_str(v) for v in chunk['article_text'].tolist()])
+            matcher = _write_chunk_sharded(args.source, chunk, processed, matcher, exchange)
         exchange.barrier()
-    exchange.barrier()
-    if rank == 0:
-        print("All matched CSV files have been processed.")
-    for name in sorted(os.listdir(out_dir))[rank::world]:   # the final pass over the files, split over the ranks
-        sort_matched_csv(f"{out_dir}/{name}")
-    exchange.barrier()
+        if rank == 0:
+            print("All matched CSV files have been processed.")
+        names = sorted(os.listdir(out_dir))
+        mine = names[rank::world]             # the final pass over the files, split over the ranks
+        parts = exchange.exchange_objects([(_RUN.export(names[r::world]), sorted(_RUN.other))
+                                           for r in range(world)])
+        for src, (exported, other) in enumerate(parts):
+            if src != rank:
+                _RUN.absorb(exported, other)
+        for name in mine:
+            if _RUN.finish(name):
+                print(f"Sorted and saved: {out_dir}/{name}")
+            else:
+                sort_matched_csv(f"{out_dir}/{name}")
+        exchange.barrier()
+    finally:
+        _RUN = None
     if rank == 0:
         print("All matched CSV files have been sorted by date and time.")
     return 0

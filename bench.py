@@ -2,8 +2,11 @@
 
 One step = one kw_scan pass (scan + resolve + result compaction) over the
 rank's whole shard of synthetic articles, already resident in HBM, followed
-by the all-gather of the per-rank hit counts (N > 1).  Weak scaling: every
-rank owns ``--docs-per-gpu`` documents (default 1M = config 2).
+by the exchange of the per-rank hits (N > 1).  Workloads (BASELINE.json):
+N = 1 scans config 2's 1M documents; N > 1 scans config 3's 10M documents
+(documents 0..9 999 999 of the seeded generator) as N contiguous shards of
+10M / N (strong scaling).  ``--total-docs T`` fixes another total,
+``--docs-per-gpu D`` gives every rank D documents (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -37,7 +40,11 @@ def _parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--docs-per-gpu', type=int, default=1_000_000)
+    ap.add_argument('--docs-per-gpu', type=int, default=None,
+                    help='documents per rank (weak scaling); default: the --total-docs split over the ranks')
+    ap.add_argument('--total-docs', type=int, default=None,
+                    help='documents of the whole job, split in contiguous shards (default: 1M = config 2 at N = 1, '
+                         '10M = config 3 at N > 1)')
     ap.add_argument('--seed', type=int, default=20250905)
     ap.add_argument('--cpu-sample', type=int, default=10000,
                     help='docs of the same corpus timed on the CPU port of the reference loop (0 = skip)')
@@ -82,6 +89,47 @@ def _launch_ranks(args) -> int:
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
            '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd)
+
+
+CONFIG2_DOCS = 1_000_000
+CONFIG3_DOCS = 10_000_000
+
+
+def shard_plan(args, rank: int, world: int):
+    """(first document, documents of this rank, documents of the job, scaling) of the bench's workload."""
+    if args.docs_per_gpu is not None:
+        n = args.docs_per_gpu
+        return rank * n, n, n * world, 'weak'
+    total = args.total_docs if args.total_docs is not None else (CONFIG2_DOCS if world == 1 else CONFIG3_DOCS)
+    per = -(-total // world)
+    lo = min(rank * per, total)
+    return lo, min(per, total - lo), total, 'strong'
+
+
+def workload_label(total_docs: int, world: int) -> str:
+    if total_docs == CONFIG3_DOCS:
+        return 'config 3'
+    if total_docs == CONFIG2_DOCS and world == 1:
+        return 'config 2'
+    return f'{total_docs} documents'
+
+
+def load_kb(kb_dir: str):
+    """The reference KB (info/ticker, 216 tickers after its filter) through the product's own loader: the KB
+    JSON files (tests/golden/kb_bundle.json.gz, written by make_golden.py from the reference's info/ticker)
+    are materialised in kb_dir and read by kb.read_and_process_json_files in the reference's listdir order."""
+    import gzip
+    import io
+    from contextlib import redirect_stdout
+    from advanced_scrapper_amd.kb import read_and_process_json_files
+    b = json.loads(gzip.decompress(open(os.path.join(REPO, 'tests', 'golden', 'kb_bundle.json.gz'), 'rb').read()))
+    os.makedirs(kb_dir, exist_ok=True)
+    for fn, text in b['files'].items():
+        with open(os.path.join(kb_dir, fn), 'wb') as fh:
+            fh.write(text.encode('utf-8'))
+    order = list(b['listdir'])
+    with redirect_stdout(io.StringIO()):          # the reference prints every ticker and the whole dict
+        return read_and_process_json_files(kb_dir, _listdir=lambda _d: order)
 
 
 def hits_digest(hits) -> str:
@@ -129,21 +177,23 @@ def main():
     from advanced_scrapper_amd import _native, dist, synth
     from advanced_scrapper_amd.kb import compile_kb
     from advanced_scrapper_amd.matcher import GpuMatcher, background_sample
-    from tests import golden_data
 
     rank, world, local = dist.init('nccl')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
+    t_kb = time.perf_counter()
     if args.workload == 'kb50k':                     # config 4: synthetic Wikidata-style KB, ~52k names
         from advanced_scrapper_amd.synth_kb import synthetic_kb
         processed = synthetic_kb(2300, args.seed)
     else:
-        processed = golden_data.kb_processed()      # info/ticker KB (S&P500 subset), 216 tickers
+        import tempfile
+        with tempfile.TemporaryDirectory() as tmp:  # info/ticker KB (S&P500 subset), 216 tickers
+            processed = load_kb(os.path.join(tmp, 'ticker'))
     ckb = compile_kb(processed)
+    t_kb = time.perf_counter() - t_kb
     names, kinds = synth.injectable_names(ckb)
-    n_local = args.docs_per_gpu
-    doc_base = rank * n_local
+    doc_base, n_local, total_docs, scaling = shard_plan(args, rank, world)
     t_gen = time.perf_counter()
     corpus = synth.generate(n_local, names, kinds, seed=args.seed, doc_base=doc_base)
     t_gen = time.perf_counter() - t_gen
@@ -269,11 +319,12 @@ def main():
         metric = 'article GB/s keyword-matched (~50k-pattern synthetic KB, config 4); % of HBM peak'
         data = 'synthetic (seeded generators: csrc/synth.c articles, synth_kb.py KB)'
     else:
-        cfg = 'config 2' if world == 1 else 'config 3'
+        cfg = workload_label(total_docs, world)
         workload = (f'{cfg}: S&P500 KB (216 tickers, 2462 active names) vs synthetic ~2 KB articles, '
-                    f'{n_local} docs per GPU')
+                    f'{total_docs} docs in {world} contiguous shard(s), {n_local} on rank 0')
         metric = METRIC
-        data = 'synthetic (seeded generator, csrc/synth.c; KB = reference info/ticker via tests/golden)'
+        data = ('synthetic (seeded generator, csrc/synth.c, documents 0..total_docs-1; KB = the reference\'s '
+                'info/ticker JSON files read by the product\'s read_and_process_json_files)')
     exch = {'root': 'RCCL send/recv of every hit record to rank 0',
             'all': 'RCCL all-gather of every hit record', 'none': 'RCCL all-gather of counts'}[args.hits]
     out = {
@@ -285,13 +336,13 @@ def main():
         'warmup': args.warmup,
         'ms_per_step': round(ms_per_step, 4),
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': scaling,
         'vs_baseline': None,
         'dtype': 'u8',
         'data': data,
         'config': {
             'workload': workload,
-            'docs_per_gpu': n_local, 'total_docs': n_local * world, 'bytes_per_gpu': local_bytes,
+            'docs_per_gpu': n_local, 'total_docs': total_docs, 'bytes_per_gpu': local_bytes,
             'total_bytes': int(total_bytes), 'hits_total': int(sum(counts)) if counts else None,
             'hits_digest': digest,
             'parallelism': (f'dp{world} (contiguous document shards; per step: {exch}, overlapped with the '
@@ -311,7 +362,7 @@ def main():
         'cpu_baseline': cpu,
         'scan_stats': st,
         'library': _native.lib_identity(),
-        'host': {'generate_s': round(t_gen, 2), 'h2d_s': round(t_up, 3),
+        'host': {'kb_load_compile_s': round(t_kb, 3), 'generate_s': round(t_gen, 2), 'h2d_s': round(t_up, 3),
                  'h2d_GBps_pcie_inclusive': round(local_bytes / t_up / 1e9, 2) if t_up > 0 else None,
                  **host_cpus()},
     }

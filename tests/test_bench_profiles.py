@@ -14,3 +14,22 @@ def test_traffic_lookup_refuses_other_workloads():
     assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=10_000, seed=20250905) is None
     assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=1) is None
     assert bench.pmc_traffic('none', 'kw_filter_kernel') is None
+
+
+def test_shard_plan_config3_and_labels():
+    import argparse
+    a = argparse.Namespace(docs_per_gpu=None, total_docs=None)
+    assert bench.shard_plan(a, 0, 1) == (0, 1_000_000, 1_000_000, 'strong')
+    plans = [bench.shard_plan(a, r, 8) for r in range(8)]
+    assert [p[0] for p in plans] == [r * 1_250_000 for r in range(8)]
+    assert sum(p[1] for p in plans) == 10_000_000 and {p[2] for p in plans} == {10_000_000}
+    plans = [bench.shard_plan(a, r, 3) for r in range(3)]     # ragged: the last shard takes the remainder
+    assert sum(p[1] for p in plans) == 10_000_000 and plans[2][0] + plans[2][1] == 10_000_000
+    assert bench.workload_label(10_000_000, 8) == 'config 3' and bench.workload_label(10_000_000, 1) == 'config 3'
+    assert bench.workload_label(1_000_000, 1) == 'config 2' and bench.workload_label(8_000_000, 8) != 'config 3'
+    w = argparse.Namespace(docs_per_gpu=1000, total_docs=None)
+    assert bench.shard_plan(w, 3, 4) == (3000, 1000, 4000, 'weak')
+
+
+def test_bench_kb_is_the_products_loader_on_the_reference_files(tmp_path, golden):
+    assert bench.load_kb(str(tmp_path / 'ticker')) == golden.kb_processed()

@@ -99,8 +99,11 @@ def _main_worker(rank, world, port, work, q):
                       '--chunksize', str(golden_data.chunksize()), '--gpus', str(world)])
     from tests.oracle_matcher import OracleMatcher
     m = OracleMatcher(processed)
+    rereads = []
+    real_sort = mk.sort_matched_csv
+    mk.sort_matched_csv = lambda path: (rereads.append(path), real_sort(path))
     rc = mk.run(args, rank, world, None, 'gloo', matcher=m)
-    q.put((rank, rc, m.uploads))
+    q.put((rank, rc, (m.uploads, rereads)))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -123,10 +126,12 @@ def test_gloo_main_sharded_equals_reference_outputs(tmp_path):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert [(r, rc) for r, rc, _u in res] == [(0, 0), (1, 0)]
+    # every output file was sorted from the ranks' merged write index (egress.RunFiles), none re-read
+    assert [u[1] for _r, _rc, u in res] == [[], []]
     # each rank packed and scanned only its own byte-balanced share of every chunk
     n_rows = len(golden_data.articles_frame())
     chunk = golden_data.chunksize()
-    ups = [u for _r, _rc, u in res]
+    ups = [u[0] for _r, _rc, u in res]
     assert all(len(u) == -(-n_rows // chunk) for u in ups)
     for c, size in enumerate([min(chunk, n_rows - k) for k in range(0, n_rows, chunk)]):
         shares = [u[c][0] for u in ups]
@@ -275,3 +280,62 @@ def test_exchange_plan_rejects_bad_arguments():
     for args in ((0, 0, -1, [1]), (2, 2, -1, [1, 1]), (2, 0, 2, [1, 1]), (2, 0, -1, [1, -1])):
         with pytest.raises(_native.KwError):
             _native.exchange_plan(*args)
+
+
+def _error_worker(rank, world, port, work, case, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TZ='UTC')
+    import io
+    import time
+    import pandas as pd
+    time.tzset()
+    from advanced_scrapper_amd import dist
+    from advanced_scrapper_amd import match_keywords as mk
+    from tests import golden_data
+    from tests.oracle_matcher import OracleMatcher
+    dist.init('gloo')
+    os.chdir(work)
+    g = golden_data.error_cases()
+    c = g['cases'][case]
+    processed = golden_data.processed_from(g['kb_processed'])
+    os.makedirs('yahoo_ticker_matched_articles', exist_ok=True)
+    ex = dist.Exchange(rank, world, None, 'gloo')
+    m = OracleMatcher(processed)
+    raised = None
+    try:
+        for chunk in pd.read_csv(io.StringIO(c['articles_csv']), chunksize=g['chunksize']):
+            mk._write_chunk_sharded('yahoo', chunk, processed, m, ex)
+            ex.barrier()
+    except Exception as exc:   # noqa: BLE001
+        raised = type(exc).__name__
+    q.put((rank, raised))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_pandas_chunk_errors_release_every_rank(tmp_path):
+    """A pandas-path chunk (parsed whole by every rank, written by rank 0) whose rows raise -- an in-period
+    invalid-regex name (re.error at :178), a bad date (:152), integer dates (:131) -- ends on EVERY rank
+    (no rank left waiting in a collective): rank 0 raises the reference's exception after writing exactly
+    the reference's partial files, the other rank raises the same date error or ShardError."""
+    from tests import golden_data
+    g = golden_data.error_cases()
+    for case in ('invalid_regex', 'bad_date', 'int_dates'):
+        c = g['cases'][case]
+        work = tmp_path / case
+        work.mkdir()
+        ctx = mp.get_context('spawn')
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_error_worker, args=(r, 2, port, str(work), case, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = dict(q.get(timeout=300) for _ in range(2))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert res[0] == c['exception'], (case, res)
+        assert res[1] in (c['exception'], 'ShardError'), (case, res)
+        out = work / 'yahoo_ticker_matched_articles'
+        got = {fn: (out / fn).read_text(encoding='utf-8') for fn in os.listdir(out)}
+        assert got == c['files'], case
