@@ -86,7 +86,7 @@ def build_kwcsv(force: bool = False) -> str:
     out = os.path.join(LIB, 'libkwcsv.so')
     src = os.path.join(CSRC, 'kwcsv.c')
     if force or _stale(out, [src]):
-        _run(['gcc', '-O2', '-fPIC', '-shared', '-Wall', '-o', out, src])
+        _run(['gcc', '-O2', '-fopenmp', '-fPIC', '-shared', '-Wall', '-o', out, src])
     return out
 
 

@@ -16,10 +16,16 @@
  * kwcsv_pack    the text / title cells of parsed records -> the matcher's byte arena (NaN -> "nan",
  *               match_keywords.py:150-151) and its 2n+1 offsets
  * kwcsv_utf8_ok validity of UTF-8 cells (pandas raises UnicodeDecodeError on the others)
+ *
+ * The *_mt entry points split a chunk's records over host threads (OpenMP; the reference spreads its
+ * per-article work over mp.cpu_count() processes, match_keywords.py:231-236): kwcsv_parse_mt tokenizes row
+ * ranges in parallel and compacts them into kwcsv_parse's exact layout, kwcsv_utf8_ok_mt checks several
+ * columns at once, kwcsv_pack_mt packs the arena, kwcsv_dates parses the dataset's date layout.
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <omp.h>
 
 #define KWCSV_QUOTED 1u   /* the cell was quoted */
 #define KWCSV_NA 2u       /* the cell is one of the NA strings: NaN */
@@ -76,12 +82,12 @@ static int kwcsv_text_witness(const uint8_t *s, int64_t n)
  * field count differs from ncols.  rspan (optional, 2 per record) gets each record's byte span without
  * its terminator.
  */
-int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_rows, int32_t ncols,
-                    const uint8_t *na, const int32_t *na_off, int32_t n_na, uint8_t *out, int64_t cap,
-                    int64_t *coff, uint8_t *cfl, int64_t *pos_out, int64_t *rspan)
+/* kwcsv_parse without writing coff[0] (the threaded form's ranges share that slot with the previous range) */
+static int64_t parse_body(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_rows, int32_t ncols,
+                          const uint8_t *na, const int32_t *na_off, int32_t n_na, uint8_t *out, int64_t cap,
+                          int64_t *coff, uint8_t *cfl, int64_t *pos_out, int64_t *rspan)
 {
     int64_t p = pos, o = 0, rows = 0;
-    coff[0] = 0;
     while (rows < max_rows) {
         /* blank lines -- empty or blanks only -- are skipped, as pandas' skip_blank_lines does */
         for (;;) {
@@ -146,6 +152,46 @@ int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_ro
     return rows;
 }
 
+/* one cell is valid UTF-8 (strict: no overlongs, surrogates or code points above U+10FFFF); ASCII runs are
+ * skipped eight bytes at a time */
+static int utf8_cell_ok(const uint8_t *s, int64_t n)
+{
+    int64_t i = 0;
+    while (i < n) {
+        while (i + 8 <= n) {
+            uint64_t w;
+            memcpy(&w, s + i, 8);
+            if (w & 0x8080808080808080ull) break;
+            i += 8;
+        }
+        if (i >= n) break;
+        const uint8_t b = s[i];
+        int64_t k;
+        uint32_t cp;
+        if (b < 0x80) { ++i; continue; }
+        if (b >= 0xC2 && b <= 0xDF) { k = 1; cp = b & 0x1F; }
+        else if (b >= 0xE0 && b <= 0xEF) { k = 2; cp = b & 0x0F; }
+        else if (b >= 0xF0 && b <= 0xF4) { k = 3; cp = b & 0x07; }
+        else return 0;
+        for (int64_t j = 1; j <= k; ++j) {
+            if (i + j >= n || (s[i + j] & 0xC0) != 0x80) return 0;
+            cp = (cp << 6) | (s[i + j] & 0x3F);
+        }
+        if ((k == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (k == 3 && (cp < 0x10000 || cp > 0x10FFFF)))
+            return 0;
+        i += k + 1;
+    }
+    return 1;
+}
+
+int64_t kwcsv_parse(const uint8_t *buf, int64_t len, int64_t pos, int64_t max_rows, int32_t ncols,
+                    const uint8_t *na, const int32_t *na_off, int32_t n_na, uint8_t *out, int64_t cap,
+                    int64_t *coff, uint8_t *cfl, int64_t *pos_out, int64_t *rspan)
+{
+    coff[0] = 0;
+    return parse_body(buf, len, pos, max_rows, ncols, na, na_off, n_na, out, cap, coff, cfl, pos_out, rspan);
+}
+
 /* Every cell of column `col` of rows [0, nrows) is valid UTF-8 (or NA).  Returns 1 / 0. */
 int32_t kwcsv_utf8_ok(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, int64_t nrows, int32_t ncols,
                       int32_t col)
@@ -153,27 +199,79 @@ int32_t kwcsv_utf8_ok(const uint8_t *out, const int64_t *coff, const uint8_t *cf
     for (int64_t r = 0; r < nrows; ++r) {
         const int64_t c = r * ncols + col;
         if (cfl[c] & KWCSV_NA) continue;
-        const uint8_t *s = out + coff[c];
-        const int64_t n = coff[c + 1] - coff[c];
-        for (int64_t i = 0; i < n;) {
-            const uint8_t b = s[i];
-            int64_t k;
-            uint32_t cp;
-            if (b < 0x80) { ++i; continue; }
-            if (b >= 0xC2 && b <= 0xDF) { k = 1; cp = b & 0x1F; }
-            else if (b >= 0xE0 && b <= 0xEF) { k = 2; cp = b & 0x0F; }
-            else if (b >= 0xF0 && b <= 0xF4) { k = 3; cp = b & 0x07; }
-            else return 0;
-            for (int64_t j = 1; j <= k; ++j) {
-                if (i + j >= n || (s[i + j] & 0xC0) != 0x80) return 0;
-                cp = (cp << 6) | (s[i + j] & 0x3F);
-            }
-            if ((k == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (k == 3 && (cp < 0x10000 || cp > 0x10FFFF)))
-                return 0;
-            i += k + 1;
-        }
+        if (!utf8_cell_ok(out + coff[c], coff[c + 1] - coff[c])) return 0;
     }
     return 1;
+}
+
+/* kwcsv_utf8_ok of ncheck columns at once over nthreads threads: ok[k] = 1 / 0 for column cols[k]. */
+void kwcsv_utf8_ok_mt(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, int64_t nrows, int32_t ncols,
+                      const int32_t *cols, int32_t ncheck, int32_t *ok, int32_t nthreads)
+{
+    for (int32_t k = 0; k < ncheck; ++k) ok[k] = 1;
+    const int64_t nt = nthreads > 1 ? nthreads : 1;
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t a = nrows * t / nt, b = nrows * (t + 1) / nt;
+        for (int32_t k = 0; k < ncheck; ++k) {
+            int good = 1;
+            for (int64_t r = a; r < b && good; ++r) {
+                const int64_t c = r * ncols + cols[k];
+                if (!(cfl[c] & KWCSV_NA) && !utf8_cell_ok(out + coff[c], coff[c + 1] - coff[c])) good = 0;
+            }
+            if (!good) {
+                #pragma omp atomic write
+                ok[k] = 0;
+            }
+        }
+    }
+}
+
+/*
+ * kwcsv_parse of exactly `rows` records whose starts kwcsv_records found (starts[0..rows]), over nthreads
+ * threads: each tokenizes a contiguous row range into out at its records' own byte offset (a record's cells
+ * never take more than its bytes), then the ranges are moved down, in order, so out / coff / cfl are exactly
+ * kwcsv_parse's.  out needs starts[rows] - starts[0] + 16 bytes.  Returns rows, or kwcsv_parse's negative
+ * code of the first failing range.
+ */
+int64_t kwcsv_parse_mt(const uint8_t *buf, int64_t len, const int64_t *starts, int64_t rows, int32_t ncols,
+                       const uint8_t *na, const int32_t *na_off, int32_t n_na, uint8_t *out, int64_t *coff,
+                       uint8_t *cfl, int32_t nthreads)
+{
+    int64_t nt = nthreads > 1 ? nthreads : 1;
+    if (nt > rows / 64 + 1) nt = rows / 64 + 1;
+    int64_t *used = (int64_t *)calloc((size_t)nt, sizeof(int64_t));
+    int64_t *rc = (int64_t *)calloc((size_t)nt, sizeof(int64_t));
+    if (!used || !rc) { free(used); free(rc); return -4; }
+    coff[0] = 0;
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
+        if (b <= a) continue;
+        const int64_t base = starts[a] - starts[0];
+        int64_t pos_out = 0;
+        /* offsets relative to the range's own start; coff[a * ncols] is range t - 1's last end */
+        const int64_t got = parse_body(buf, len, starts[a], b - a, ncols, na, na_off, n_na, out + base,
+                                       starts[b] - starts[a] + 16, coff + a * ncols, cfl + a * ncols, &pos_out,
+                                       NULL);
+        rc[t] = got == b - a ? 0 : (got < 0 ? got : -2);
+        used[t] = got == b - a ? coff[b * ncols] : 0;
+    }
+    /* the ranges are separate: move each down to the end of the previous one, in order (dest <= source) */
+    int64_t dest = 0, err = 0;
+    for (int64_t t = 0; t < nt && !err; ++t) {
+        const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
+        if (rc[t]) { err = rc[t]; break; }
+        if (b <= a) continue;
+        const int64_t base = starts[a] - starts[0];
+        if (dest != base) memmove(out + dest, out + base, (size_t)used[t]);
+        const int64_t shift = dest;
+        for (int64_t j = a * ncols + 1; j <= b * ncols; ++j) coff[j] += shift;
+        dest += used[t];
+    }
+    free(used);
+    free(rc);
+    return err ? err : rows;
 }
 
 /*
@@ -199,6 +297,78 @@ int64_t kwcsv_pack(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, 
         }
     }
     return a;
+}
+
+/* kwcsv_pack over nthreads threads (row lengths, one prefix sum, parallel copies): the same arena / offsets. */
+int64_t kwcsv_pack_mt(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, int64_t nrows, int32_t ncols,
+                      int32_t ct, int32_t ci, uint8_t *arena, int64_t cap, int64_t *off, int32_t nthreads)
+{
+    const int64_t nt = nthreads > 1 ? nthreads : 1;
+    off[0] = 0;
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t r = 0; r < nrows; ++r)
+        for (int k = 0; k < 2; ++k) {
+            const int64_t c = r * ncols + (k ? ci : ct);
+            off[2 * r + k + 1] = (cfl[c] & KWCSV_NA) ? 3 : coff[c + 1] - coff[c];
+        }
+    for (int64_t i = 1; i <= 2 * nrows; ++i) off[i] += off[i - 1];
+    if (off[2 * nrows] > cap) return -1;
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t r = 0; r < nrows; ++r)
+        for (int k = 0; k < 2; ++k) {
+            const int64_t c = r * ncols + (k ? ci : ct);
+            if (cfl[c] & KWCSV_NA) memcpy(arena + off[2 * r + k], "nan", 3);
+            else memcpy(arena + off[2 * r + k], out + coff[c], (size_t)(coff[c + 1] - coff[c]));
+        }
+    return off[2 * nrows];
+}
+
+static int64_t days_from_civil(int64_t y, int64_t m, int64_t d)
+{
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+
+/*
+ * The article dates of column `col` (match_keywords.py:152: dateutil.parse(str(v)) if notna(v) else None),
+ * for the cells whose answer needs no dateutil: kind[r] = 2 for an NA cell (None); kind[r] = 1 for a cell of
+ * exactly the dataset's layout 'YYYY-MM-DD HH:MM:SS' ('T' or ' ' between date and time, ASCII digits)
+ * forming a valid date and time with year >= 1000, which dateutil parses to the naive datetime of those
+ * fields -- us[r] = its epoch microseconds, naive read as UTC (kb.epoch_us); kind[r] = 0 otherwise (the
+ * caller runs dates.parse_date, i.e. dateutil, on that cell).  The same rule as dates.parse_date's fast path.
+ */
+void kwcsv_dates(const uint8_t *out, const int64_t *coff, const uint8_t *cfl, int64_t nrows, int32_t ncols,
+                 int32_t col, int64_t *us, uint8_t *kind, int32_t nthreads)
+{
+    static const int dim[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    const int64_t nt = nthreads > 1 ? nthreads : 1;
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t r = 0; r < nrows; ++r) {
+        const int64_t c = r * ncols + col;
+        us[r] = 0;
+        if (cfl[c] & KWCSV_NA) { kind[r] = 2; continue; }
+        kind[r] = 0;
+        const uint8_t *s = out + coff[c];
+        if (coff[c + 1] - coff[c] != 19) continue;
+        static const int8_t digit_at[19] = {1, 1, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1};
+        int ok = s[4] == '-' && s[7] == '-' && (s[10] == ' ' || s[10] == 'T') && s[13] == ':' && s[16] == ':';
+        for (int i = 0; i < 19 && ok; ++i)
+            if (digit_at[i] && (s[i] < '0' || s[i] > '9')) ok = 0;
+        if (!ok) continue;
+#define D2(i) ((int64_t)(s[i] - '0') * 10 + (s[(i) + 1] - '0'))
+        const int64_t y = D2(0) * 100 + D2(2), mo = D2(5), d = D2(8), hh = D2(11), mi = D2(14), ss = D2(17);
+#undef D2
+        if (y < 1000 || mo < 1 || mo > 12 || hh >= 24 || mi >= 60 || ss >= 60) continue;
+        const int leap = (y % 4 == 0) && (y % 100 != 0 || y % 400 == 0);
+        const int64_t md = (mo == 2 && leap) ? 29 : dim[mo - 1];
+        if (d < 1 || d > md) continue;
+        us[r] = ((days_from_civil(y, mo, d) * 86400) + hh * 3600 + mi * 60 + ss) * 1000000;
+        kind[r] = 1;
+    }
 }
 
 /*

@@ -14,7 +14,7 @@ dateutil's by construction.
 from __future__ import annotations
 
 import re
-from datetime import datetime
+from datetime import datetime, timedelta
 
 from dateutil import parser as _dparser
 
@@ -32,3 +32,66 @@ def parse_date(s: str) -> datetime:
             if 1 <= d <= dim:
                 return datetime(y, mo, d, hh, mi, ss)
     return _dparser.parse(s)
+
+
+_EPOCH_NAIVE = datetime(1970, 1, 1)
+
+
+class Dates:
+    """The parsed article dates of a native chunk's rows (ingest.NativeChunk.dates): a sequence of naive
+    ``datetime`` / ``None`` / dateutil results like the list ``[parse_date(str(v)) if notna(v) else None]``,
+    held as arrays for the rows of the dataset's layout (kind 1: epoch µs, naive read as UTC; kind 2: None)
+    and as objects for the others (kind 0: ``slow[row]``, dateutil's result).  ``epoch_us_arrays`` and
+    ``utc_stamps`` give the write path integer forms without building a ``datetime`` per row."""
+
+    __slots__ = ('us', 'kind', 'slow')
+
+    def __init__(self, us, kind, slow):
+        self.us, self.kind, self.slow = us, kind, slow
+
+    def __len__(self):
+        return len(self.kind)
+
+    def __getitem__(self, i):
+        k = self.kind[i]
+        if k == 1:
+            return _EPOCH_NAIVE + timedelta(microseconds=int(self.us[i]))
+        if k == 2:
+            return None
+        return self.slow[int(i)]
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    def epoch_us_arrays(self):
+        """(epoch µs int64[n], has-date uint8[n]) as kb.epoch_us gives them (naive = UTC); raises TypeError
+        for a date whose tzinfo has no UTC offset, as epoch_us does."""
+        from .kb import epoch_us
+        import numpy as np
+        us = np.array(self.us, dtype=np.int64, copy=True)
+        ok = (self.kind != 2).astype(np.uint8)
+        for r, d in self.slow.items():
+            us[r] = epoch_us(d)
+        return us, ok
+
+    def utc_stamps(self, rows):
+        """``int(d.timestamp())`` of the given rows' dates when the process's local time zone is UTC (a naive
+        datetime's timestamp() reads it in local time, match_keywords.py:131-132), else ``None``.  Rows of
+        the dataset's layout take their epoch seconds; the others call timestamp()."""
+        import numpy as np
+        if not local_zone_is_utc():
+            return None
+        rows = np.asarray(rows, dtype=np.int64)
+        out = self.us[rows] // 1000000
+        for j in np.flatnonzero(self.kind[rows] != 1).tolist():
+            out[j] = int(self[int(rows[j])].timestamp())
+        return out
+
+
+def local_zone_is_utc() -> bool:
+    """The process's local time zone is UTC without transitions (``time.timezone == time.altzone == 0``, no
+    DST, zone name UTC/UCT/GMT): then a naive datetime's ``timestamp()`` equals its epoch seconds read as UTC.
+    Checked on every call (TZ may change with ``time.tzset``)."""
+    import time
+    return (time.timezone == 0 and time.altzone == 0 and not time.daylight and
+            time.tzname[0] in ('UTC', 'UCT', 'GMT', 'Etc/UTC', 'Universal', 'Zulu'))

@@ -44,8 +44,26 @@ def _lib():
         L.kwcsv_utf8_ok.argtypes = [P, P, P, i64, i32, i32]
         L.kwcsv_records.restype = i64
         L.kwcsv_records.argtypes = [P, i64, i64, i64, i32, P]
+        L.kwcsv_parse_mt.restype = i64
+        L.kwcsv_parse_mt.argtypes = [P, i64, P, i64, i32, P, P, i32, P, P, P, i32]
+        L.kwcsv_utf8_ok_mt.restype = None
+        L.kwcsv_utf8_ok_mt.argtypes = [P, P, P, i64, i32, P, i32, P, i32]
+        L.kwcsv_pack_mt.restype = i64
+        L.kwcsv_pack_mt.argtypes = [P, P, P, i64, i32, i32, i32, P, i64, P, i32]
+        L.kwcsv_dates.restype = None
+        L.kwcsv_dates.argtypes = [P, P, P, i64, i32, i32, P, P, i32]
         _LIB = L
     return _LIB
+
+
+def host_threads() -> int:
+    """Host threads of the native ingest / egress: the CPUs this process may use (affinity), at most 16, or
+    ``KW_HOST_THREADS``."""
+    env = os.environ.get('KW_HOST_THREADS')
+    if env:
+        return max(1, int(env))
+    n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    return max(1, min(16, n))
 
 
 def _na_table():
@@ -114,13 +132,34 @@ class NativeChunk:
         c = self.cells
         n = c.nrows
         cap = int(c.off[-1]) + 3 * 2 * n + pad
-        arena = np.zeros(cap, dtype=np.uint8)
+        arena = np.empty(cap, dtype=np.uint8)
         off = np.zeros(2 * n + 1, dtype=np.int64)
-        got = _lib().kwcsv_pack(_p(c.buf), _p(c.off), _p(c.flags), n, c.ncols, self.col['article_text'],
-                                self.col['title'], _p(arena), cap - pad, _p(off))
+        got = _lib().kwcsv_pack_mt(_p(c.buf), _p(c.off), _p(c.flags), n, c.ncols, self.col['article_text'],
+                                   self.col['title'], _p(arena), cap - pad, _p(off), host_threads())
         if got < 0:
             raise RuntimeError('kwcsv_pack: arena too small')
+        arena[got:got + pad] = 0
         return arena[:got + pad], off
+
+    def dates(self):
+        """The reference's per-row ``dateutil.parse(str(v)) if notna(v) else None`` (match_keywords.py:152) of
+        the ``date_time`` column up to the first row that raises: (:class:`dates.Dates`, that exception or
+        ``None``).  Cells of the dataset's layout are parsed in C (kwcsv_dates), the others by
+        dates.parse_date (dateutil)."""
+        from .dates import Dates, parse_date
+        c = self.cells
+        n = c.nrows
+        us = np.empty(max(n, 1), dtype=np.int64)
+        kind = np.empty(max(n, 1), dtype=np.uint8)
+        _lib().kwcsv_dates(_p(c.buf), _p(c.off), _p(c.flags), n, c.ncols, self.col['date_time'], _p(us), _p(kind),
+                           host_threads())
+        slow = {}
+        for r in np.flatnonzero(kind[:n] == 0).tolist():
+            try:
+                slow[r] = parse_date(str(self.value(r, 'date_time')))
+            except Exception as exc:   # noqa: BLE001 - match_keywords.py:152 raises here for this row
+                return Dates(us[:r], kind[:r], {k: v for k, v in slow.items() if k < r}), exc
+        return Dates(us[:n], kind[:n], slow), None
 
     def frame(self) -> pd.DataFrame:
         """The chunk as pandas would give it (object columns; for the drop-in process_chunk API)."""
@@ -130,7 +169,9 @@ class NativeChunk:
 
 def _split_header(buf: bytes):
     """Header fields and the byte position after the header record (simple unquoted or quoted names)."""
-    ends = [k for k in (buf.find(b'\n'), buf.find(b'\r')) if k >= 0]
+    nl = buf.find(b'\n')
+    cr = buf.find(b'\r', 0, nl if nl >= 0 else len(buf))    # only within the first line (not the whole file)
+    ends = [k for k in (nl, cr) if k >= 0]
     end = min(ends) if ends else len(buf)
     head = bytes(buf[:end]).decode('utf-8')
     pos = end
@@ -158,16 +199,16 @@ def read_chunks(path: str, chunksize: int) -> Iterator[Union[NativeChunk, pd.Dat
     yield from read_chunks_bytes(_map(path), chunksize, path)
 
 
-def _pandas_rows(data, pos: int, end: int, index0: int) -> pd.DataFrame:
+def _pandas_rows(data, pos: int, end: int, index0: int, head_end: int) -> pd.DataFrame:
     """pandas on exactly the records in data[pos:end) (dtype inference is per chunk): the header + these bytes."""
-    frame = pd.read_csv(io.BytesIO(bytes(data[:_header_end(data)]) + bytes(data[pos:end])))
+    frame = pd.read_csv(io.BytesIO(bytes(data[:head_end]) + bytes(data[pos:end])))
     frame.index = pd.RangeIndex(index0, index0 + len(frame))
     return frame
 
 
-def _pandas_rest(data, pos: int, chunksize: int, index0: int):
+def _pandas_rest(data, pos: int, chunksize: int, index0: int, head_end: int):
     """A record the tokenizer does not reproduce: pandas takes the rest of the file, chunk by chunk."""
-    tail = bytes(data[:_header_end(data)]) + bytes(data[pos:])
+    tail = bytes(data[:head_end]) + bytes(data[pos:])
     for frame in pd.read_csv(io.BytesIO(tail), chunksize=chunksize):
         frame.index = pd.RangeIndex(index0, index0 + len(frame))
         index0 += len(frame)
@@ -178,29 +219,40 @@ def _header_ok(names) -> bool:
     return len(names) > 0 and len(set(names)) == len(names) and all(n in names for n in NEEDED)
 
 
-def _tokenize(data, buf: np.ndarray, pos: int, end: int, rows: int, ncols: int):
-    """kwcsv_parse of exactly `rows` records in buf[pos:end) -> (Cells, position after them) or None."""
-    na_buf, na_off, n_na = _na_table()
-    out = np.empty(end - pos + 16, dtype=np.uint8)     # a record's cells take at most its bytes
+_NA = None
+
+
+def _tokenize(buf: np.ndarray, starts: np.ndarray, ncols: int):
+    """kwcsv_parse_mt of the records whose starts kwcsv_records found (``starts`` = rows + 1 entries, the last
+    = the position after the last record) -> Cells, or None when a record is not reproduced exactly."""
+    global _NA
+    if _NA is None:
+        _NA = _na_table()
+    na_buf, na_off, n_na = _NA
+    rows = len(starts) - 1
+    starts = np.ascontiguousarray(starts, dtype=np.int64)
+    out = np.empty(int(starts[-1] - starts[0]) + 16, dtype=np.uint8)     # a record's cells take at most its bytes
     coff = np.empty(rows * ncols + 1, dtype=np.int64)
     cfl = np.empty(max(rows * ncols, 1), dtype=np.uint8)
-    newpos = ctypes.c_int64(pos)
-    got = _lib().kwcsv_parse(_p(buf), len(buf), pos, rows, ncols, _p(na_buf), _p(na_off), n_na, _p(out),
-                             len(out), _p(coff), _p(cfl), ctypes.byref(newpos), None)
+    got = _lib().kwcsv_parse_mt(_p(buf), len(buf), _p(starts), rows, ncols, _p(na_buf), _p(na_off), n_na, _p(out),
+                                _p(coff), _p(cfl), host_threads())
     if got != rows:
         return None
-    return Cells(out, coff[:rows * ncols + 1], cfl[:rows * ncols], int(rows), ncols), newpos.value
+    return Cells(out, coff[:rows * ncols + 1], cfl[:rows * ncols], int(rows), ncols)
 
 
 def _native_flags(cells: Cells, need_idx) -> np.ndarray:
     """Per needed column: [no text witness among these rows, invalid UTF-8 among them] (0 / 1)."""
-    L = _lib()
     n, nc = cells.nrows, cells.ncols
     fl = cells.flags.reshape(n, nc) if n else np.zeros((0, nc), np.uint8)
+    cols = np.asarray(need_idx, dtype=np.int32)
+    ok = np.zeros(len(cols), dtype=np.int32)
+    _lib().kwcsv_utf8_ok_mt(_p(cells.buf), _p(cells.off), _p(cells.flags), n, nc, _p(cols), len(cols), _p(ok),
+                            host_threads())
     out = np.zeros(2 * len(need_idx), dtype=np.int64)
     for k, c in enumerate(need_idx):
         out[2 * k] = 0 if (n and (fl[:, c] & TEXT).any()) else 1
-        out[2 * k + 1] = 0 if L.kwcsv_utf8_ok(_p(cells.buf), _p(cells.off), _p(cells.flags), n, nc, c) else 1
+        out[2 * k + 1] = 0 if ok[k] else 1
     return out
 
 
@@ -212,6 +264,7 @@ def read_chunks_bytes(data, chunksize: int, path: Optional[str] = None) -> Itera
         return
     need_idx = [names.index(n) for n in NEEDED]
     buf = np.frombuffer(data, dtype=np.uint8)
+    head_end = pos
     L = _lib()
     index0 = 0
     starts = np.empty(chunksize + 1, dtype=np.int64)
@@ -220,20 +273,19 @@ def read_chunks_bytes(data, chunksize: int, path: Optional[str] = None) -> Itera
         if rows == 0:
             break
         if rows < 0:
-            yield from _pandas_rest(data, pos, chunksize, index0)
+            yield from _pandas_rest(data, pos, chunksize, index0, head_end)
             return
         end = int(starts[rows])
-        tok = _tokenize(data, buf, pos, end, int(rows), ncols)
-        if tok is None:
-            yield from _pandas_rest(data, pos, chunksize, index0)
+        cells = _tokenize(buf, starts[:rows + 1], ncols)
+        if cells is None:
+            yield from _pandas_rest(data, pos, chunksize, index0, head_end)
             return
-        cells, newpos = tok
         if not _native_flags(cells, need_idx).any():
             yield NativeChunk(cells, names, index0)
         else:
-            yield _pandas_rows(data, pos, newpos, index0)
+            yield _pandas_rows(data, pos, end, index0, head_end)
         index0 += int(rows)
-        pos = newpos
+        pos = end
 
 
 class ShardChunk(NativeChunk):
@@ -275,6 +327,7 @@ def read_chunks_sharded(path: str, chunksize: int, rank: int, world: int, allred
         return
     need_idx = [names.index(n) for n in NEEDED]
     buf = np.frombuffer(data, dtype=np.uint8)
+    head_end = pos
     L = _lib()
     index0 = 0
     starts = np.empty(chunksize + 1, dtype=np.int64)
@@ -283,36 +336,32 @@ def read_chunks_sharded(path: str, chunksize: int, rank: int, world: int, allred
         if rows == 0:
             break
         if rows < 0:
-            yield from _pandas_rest(data, pos, chunksize, index0)
+            yield from _pandas_rest(data, pos, chunksize, index0, head_end)
             return
         rows = int(rows)
         end = int(starts[rows])
         lo, hi = balanced_cuts(starts[:rows + 1], world)[rank]
         if hi > lo:
-            tok = _tokenize(data, buf, int(starts[lo]), int(starts[hi]), hi - lo, ncols)
+            # the share's last record ends where the next share's first begins (blank lines are skipped)
+            tok = _tokenize(buf, starts[lo:hi + 1], ncols)
         else:   # no rows on this rank: nothing to witness, nothing invalid
-            tok = (Cells(np.zeros(16, np.uint8), np.zeros(1, np.int64), np.zeros(1, np.uint8), 0, ncols), end)
+            tok = Cells(np.zeros(16, np.uint8), np.zeros(1, np.int64), np.zeros(1, np.uint8), 0, ncols)
         local = np.zeros(2 * len(need_idx) + 1, dtype=np.int64)
         if tok is None:
             local[-1] = 1
         else:
-            local[:-1] = _native_flags(tok[0], need_idx)
+            local[:-1] = _native_flags(tok, need_idx)
         # witness: some rank has one (MIN of "no witness" = 0); UTF-8 and tokenizing: every rank is fine
         # (MIN of the negated flags, i.e. MAX of the failures, through -x)
         red = allreduce_min(np.concatenate([local[0:-1:2], -local[1:-1:2], -local[-1:]]))
         k = len(need_idx)
         native = not red[:k].any() and not (red[k:] < 0).any()
         if native:
-            yield ShardChunk(tok[0], names, index0, lo, hi, rows)
+            yield ShardChunk(tok, names, index0, lo, hi, rows)
         else:
-            yield _pandas_rows(data, pos, end, index0)
+            yield _pandas_rows(data, pos, end, index0, head_end)
         index0 += rows
         pos = end
-
-
-def _header_end(data: bytes) -> int:
-    _names, _head, pos = _split_header(data)
-    return pos
 
 
 def parse_all(data: bytes):

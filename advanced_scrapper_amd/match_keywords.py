@@ -283,12 +283,17 @@ def _native_rows(chunk, matcher, hits, dates, error):
     row_doc = raw[0]
     stamps = np.zeros(max(len(dates), 1), dtype=np.int64)
     exc, row = None, None
-    for d in np.unique(row_doc).tolist():      # time_unix = int(parse(date_time).timestamp()), :131-132
-        try:
-            stamps[d] = int(dates[d].timestamp())
-        except Exception as e:   # noqa: BLE001 - that article's append raises in the reference
-            exc, row = e, d
-            break
+    docs = np.unique(row_doc)
+    fast = dates.utc_stamps(docs) if hasattr(dates, 'utc_stamps') else None
+    if fast is not None:                       # a UTC process: naive dates' timestamp() = their epoch seconds
+        stamps[docs] = fast
+    else:
+        for d in docs.tolist():                # time_unix = int(parse(date_time).timestamp()), :131-132
+            try:
+                stamps[d] = int(dates[d].timestamp())
+            except Exception as e:   # noqa: BLE001 - that article's append raises in the reference
+                exc, row = e, d
+                break
     if exc is not None:
         k = int(np.searchsorted(row_doc, row))   # rows are in document order
         raw = (raw[0][:k], raw[1][:k], raw[2], raw[3][:2 * k + 1])
@@ -383,7 +388,7 @@ def _native_match(chunk: NativeChunk, processed_data, matcher, exchange=None):
     """Hits of a natively read chunk: the arena is packed in C from the tokenized cells (no per-row
     ``str``); with an exchange, this rank matches its byte-balanced row range and rank 0 gets all."""
     from .dist import byte_balanced_ranges
-    dates, error = _dates(chunk.column_list('date_time'))
+    dates, error = chunk.dates()
     n_ok = len(dates)
     matcher = matcher or get_matcher(processed_data, sample_texts=_native_sample(chunk))
     if n_ok == 0:
@@ -421,7 +426,7 @@ def _write_shard(source_name, chunk: ShardChunk, processed_data, matcher, exchan
     (ingest.read_chunks_sharded).  The chunk's first failing row is agreed on by a MIN all-reduce, and the
     ranks append their rows in rank order (= article order: shares are contiguous) up to it, one rank at a
     time, so every per-ticker file receives the rows in the order the reference's loop appends them."""
-    dates, error = _dates(chunk.column_list('date_time'))
+    dates, error = chunk.dates()
     n_ok = len(dates)
     hits = None
     if n_ok:

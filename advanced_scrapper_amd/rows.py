@@ -92,13 +92,16 @@ def assemble_json_raw(ckb: CompiledKB, hits: np.ndarray, dates: Sequence):
     n_docs = len(dates)
     if len(hits) == 0 or n_docs == 0:
         return (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.uint8), np.zeros(1, np.int64))
-    date_us = np.zeros(n_docs, dtype=np.int64)
-    date_ok = np.zeros(n_docs, dtype=np.uint8)
     try:
-        for i, d in enumerate(dates):
-            if d is not None:
-                date_us[i] = epoch_us(d)
-                date_ok[i] = 1
+        if hasattr(dates, 'epoch_us_arrays'):            # dates.Dates: integer forms without datetimes
+            date_us, date_ok = dates.epoch_us_arrays()
+        else:
+            date_us = np.zeros(n_docs, dtype=np.int64)
+            date_ok = np.zeros(n_docs, dtype=np.uint8)
+            for i, d in enumerate(dates):
+                if d is not None:
+                    date_us[i] = epoch_us(d)
+                    date_ok[i] = 1
     except TypeError:
         return None
     h = np.ascontiguousarray(hits[np.lexsort((hits['pos'], hits['pattern'], hits['field'], hits['doc']))])

@@ -118,3 +118,77 @@ def test_sort_native_equals_pandas(tmp_path, seed0):
             mk.sort_matched_csv(str(p1))
         assert p1.read_bytes() == p2.read_bytes(), (seed, native)
     assert taken > 25
+
+
+@pytest.mark.parametrize('threads', ['1', '3', '7'])
+def test_threaded_tokenizer_equals_pandas(monkeypatch, threads):
+    """kwcsv_parse_mt over several threads (row ranges tokenized apart, then compacted) gives pandas' cells,
+    the single-thread arena and the same chunk decisions, on chunks large enough to split."""
+    from advanced_scrapper_amd import ingest
+    from advanced_scrapper_amd.matcher import field_str, pack_fields
+    monkeypatch.setenv('KW_HOST_THREADS', threads)
+    atoms = [a for a in ATOMS if '\r' not in a]   # (an unquoted lone CR ends a record: pandas' own chunks)
+    for seed in (3, 4):
+        rng = np.random.default_rng(seed)
+        rows = [{c: ''.join(atoms[rng.integers(len(atoms))] for _ in range(int(rng.integers(1, 4)))) for c in COLS}
+                for _ in range(700)]
+        buf = io.StringIO()
+        pd.DataFrame(rows).to_csv(buf, index=False, lineterminator='\r\n' if seed % 2 else '\n')
+        data = buf.getvalue().encode('utf-8').replace(b'\n', b'\n\n  \n', 5)
+        want = list(pd.read_csv(io.BytesIO(data), chunksize=500))
+        got = list(ingest.read_chunks_bytes(data, 500))
+        assert len(want) == len(got)
+        assert all(isinstance(g, ingest.NativeChunk) for g in got)
+        for w, g in zip(want, got):
+            f = g.frame()
+            for c in COLS:
+                assert _same(w[c].tolist(), f[c].tolist()), (seed, c)
+            ar, off = g.arena()
+            ar2, off2 = pack_fields([field_str(v) for v in w['article_text'].tolist()],
+                                    [field_str(v) for v in w['title'].tolist()])
+            assert np.array_equal(off, off2) and bytes(ar[:off[-1]]) == bytes(ar2[:off2[-1]]), seed
+
+
+def test_native_dates_equal_parse_date(monkeypatch):
+    """NativeChunk.dates (kwcsv_dates + dateutil for the other layouts) == [parse_date(str(v)) if notna(v) else
+    None] row by row, stopping at the same row with the same exception; epoch_us_arrays == kb.epoch_us."""
+    import time
+    from advanced_scrapper_amd import ingest
+    from advanced_scrapper_amd.dates import parse_date
+    from advanced_scrapper_amd.kb import epoch_us
+    monkeypatch.setenv('TZ', 'UTC')
+    time.tzset()
+    cells = ['2020-02-29 12:34:56', '2021-02-29 12:34:56', '1999-12-31T23:59:59', '0999-01-01 00:00:00',
+             '1000-01-01 00:00:00', '9999-12-31 23:59:59', '2020-13-01 00:00:00', '2020-01-01 24:00:00',
+             '2020-01-01 00:00', '2020-01-01 00:00:00.5', '２０２０-01-01 00:00:00', 'June 5 2020 10:00',
+             '2020-06-05 10:00:00+02:00', '', 'NA', '1900-02-29 00:00:00', '2000-02-29 00:00:00', '2024-06-01 00:60:00']
+    rows = [{'article_text': 'a', 'title': 't', 'date_time': d, 'url': 'u', 'source': 's', 'source_url': 'x'}
+            for d in cells]
+    buf = io.StringIO()
+    pd.DataFrame(rows).to_csv(buf, index=False)
+    data = buf.getvalue().encode('utf-8')
+    (chunk,) = list(ingest.read_chunks_bytes(data, 100))
+    assert isinstance(chunk, ingest.NativeChunk)
+    vals = pd.read_csv(io.BytesIO(data))['date_time'].tolist()
+    want, want_exc = [], None
+    for v in vals:
+        try:
+            want.append(parse_date(str(v)) if pd.notna(v) else None)
+        except Exception as exc:   # noqa: BLE001
+            want_exc = exc
+            break
+    got, exc = chunk.dates()
+    assert type(exc) is type(want_exc) and str(exc) == str(want_exc)
+    assert list(got) == want and len(got) == len(want)
+    us, ok = got.epoch_us_arrays()
+    assert ok.tolist() == [d is not None for d in want]
+    assert [int(u) for u, d in zip(us, want) if d is not None] == [epoch_us(d) for d in want if d is not None]
+    rows_ = [i for i, d in enumerate(want) if d is not None]
+    assert got.utc_stamps(rows_).tolist() == [int(want[i].timestamp()) for i in rows_]
+    monkeypatch.setenv('TZ', 'America/New_York')
+    time.tzset()
+    try:
+        assert got.utc_stamps(rows_) is None        # a zone with transitions: the caller calls timestamp()
+    finally:
+        monkeypatch.setenv('TZ', 'UTC')
+        time.tzset()
