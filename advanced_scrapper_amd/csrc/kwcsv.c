@@ -558,3 +558,158 @@ int64_t kwcsv_emit(const uint8_t *cells, const int64_t *coff, const uint8_t *cfl
     free(dfl);
     return rc;
 }
+
+/* QUOTE_MINIMAL length of one cell (put_cell's output length) */
+static int64_t cell_len_q(const uint8_t *s, int64_t n)
+{
+    if (n <= 0) return 0;
+    if (!memchr(s, ',', (size_t)n) && !memchr(s, '"', (size_t)n) && !memchr(s, '\n', (size_t)n)) return n;
+    int64_t q = 0;
+    for (const uint8_t *p = s; (p = (const uint8_t *)memchr(p, '"', (size_t)(s + n - p))) != NULL; ++p) ++q;
+    return n + q + 2;
+}
+
+/*
+ * kwcsv_emit over nthreads threads, the same bytes, line_off and flags: (1) each article that has rows renders
+ * its date_time cell and its title .. article_text cells once, in parallel, into `art` (at a bound computed
+ * from its cell lengths); (2) every row's line length (its time stamp digits, the article's two parts, its
+ * quoted JSON cells) and a prefix sum give each row its offset; (3) the rows are written in parallel.
+ * art needs kwcsv_emit_art_bytes() bytes.  Returns 0, -1 when out is too small (line_off[nrows] then holds
+ * the bytes needed), -2 for a NUL character in a cell, -3 on an allocation failure.
+ */
+int64_t kwcsv_emit_art_bytes(const int64_t *coff, int32_t ncols, const int32_t *cols, const int32_t *row_doc,
+                             int64_t nrows)
+{
+    int32_t dmax = -1;
+    for (int64_t r = 0; r < nrows; ++r) if (row_doc[r] > dmax) dmax = row_doc[r];
+    int64_t total = 0;
+    for (int32_t d = 0; d <= dmax; ++d) {
+        const int64_t base = (int64_t)d * ncols;
+        total += 16;
+        for (int c = 0; c < 6; ++c) total += 2 * (coff[base + cols[c] + 1] - coff[base + cols[c]]) + 3;
+    }
+    return total + 64;
+}
+
+/* put_cell without a capacity check: the caller sized the line with cell_len_q */
+static void put_cell_sized(uint8_t *out, int64_t *o, const uint8_t *s, int64_t n)
+{
+    if (cell_len_q(s, n) == n) {
+        memcpy(out + *o, s, (size_t)n);
+        *o += n;
+        return;
+    }
+    out[(*o)++] = '"';
+    for (int64_t i = 0; i < n; ++i) {
+        if (s[i] == '"') out[(*o)++] = '"';
+        out[(*o)++] = s[i];
+    }
+    out[(*o)++] = '"';
+}
+
+static int stamp_digits(int64_t v, char *num)   /* decimal text of v at the end of num[24]; returns the start */
+{
+    int k = 24;
+    uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1u : (uint64_t)v;
+    do { num[--k] = (char)('0' + u % 10); u /= 10; } while (u);
+    if (v < 0) num[--k] = '-';
+    return k;
+}
+
+int64_t kwcsv_emit_mt(const uint8_t *cells, const int64_t *coff, const uint8_t *cfl, int32_t ncols,
+                      const int32_t *cols, const int32_t *row_doc, const int64_t *row_stamp, int64_t nrows,
+                      const uint8_t *json, const int64_t *json3, uint8_t *out, int64_t cap, int64_t *line_off,
+                      uint32_t *flags, uint8_t *art, int32_t nthreads)
+{
+    const int64_t nt = nthreads > 1 ? nthreads : 1;
+    int32_t dmax = -1;
+    for (int64_t r = 0; r < nrows; ++r) if (row_doc[r] > dmax) dmax = row_doc[r];
+    const int64_t nd = (int64_t)dmax + 1;
+    int64_t *part = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(nd > 0 ? nd : 1));   /* A start, B start, B end */
+    int64_t *abase = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nd + 1));
+    uint32_t *dfl = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(nd > 0 ? nd : 1));
+    uint8_t *used = (uint8_t *)calloc((size_t)(nd > 0 ? nd : 1), 1);
+    if (!part || !abase || !dfl || !used) { free(part); free(abase); free(dfl); free(used); return -3; }
+    for (int64_t r = 0; r < nrows; ++r) used[row_doc[r]] = 1;
+    abase[0] = 0;
+    for (int64_t d = 0; d < nd; ++d) {
+        const int64_t base = d * ncols;
+        int64_t need = 16;
+        for (int c = 0; c < 6; ++c) need += 2 * (coff[base + cols[c] + 1] - coff[base + cols[c]]) + 3;
+        abase[d + 1] = abase[d] + (used[d] ? need : 0);
+    }
+    int64_t err = 0;
+    /* (1) the articles' shared cells */
+    #pragma omp parallel for num_threads(nt) schedule(dynamic, 64) reduction(min : err)
+    for (int64_t d = 0; d < nd; ++d) {
+        if (!used[d]) continue;
+        const int64_t base = d * ncols;
+        const int64_t lim = abase[d + 1];
+        int64_t o = abase[d];
+        uint32_t fl = 0;
+        int e = emit_chunk_cell(cells, coff, cfl, base + cols[0], 0, art, lim, &o, &fl);
+        const int64_t b0 = o;
+        for (int c = 3; c < 8 && e == 0; ++c) {
+            if (c > 3) art[o++] = ',';
+            e = emit_chunk_cell(cells, coff, cfl, base + cols[c - 2], c, art, lim, &o, &fl);
+        }
+        if (e) { err = e < err ? e : err; continue; }
+        part[3 * d] = abase[d];
+        part[3 * d + 1] = b0;
+        part[3 * d + 2] = o;
+        dfl[d] = fl;
+    }
+    if (err) { free(part); free(abase); free(dfl); free(used); return err; }
+    /* (2) line lengths -> offsets */
+    #pragma omp parallel for num_threads(nt) schedule(static) reduction(min : err)
+    for (int64_t r = 0; r < nrows; ++r) {
+        const int32_t d = row_doc[r];
+        char num[24];
+        int64_t n = 24 - stamp_digits(row_stamp[r], num);
+        n += 1 + (part[3 * d + 1] - part[3 * d]);
+        uint32_t fl = dfl[d] | 6u;   /* the JSON cells are text witnesses */
+        for (int c = 1; c < 3; ++c) {
+            const uint8_t *s = json + json3[3 * r + (c - 1)];
+            const int64_t m = json3[3 * r + c] - json3[3 * r + (c - 1)];
+            if (m > 0 && memchr(s, 0, (size_t)m)) err = -2;
+            if (m > 0 && memchr(s, '\r', (size_t)m)) fl |= 1u << 16;
+            n += 1 + cell_len_q(s, m);
+        }
+        n += 1 + (part[3 * d + 2] - part[3 * d + 1]) + 1;
+        line_off[r + 1] = n;
+        flags[r] = fl;
+    }
+    if (err) { free(part); free(abase); free(dfl); free(used); return err; }
+    line_off[0] = 0;
+    for (int64_t r = 0; r < nrows; ++r) line_off[r + 1] += line_off[r];
+    if (line_off[nrows] > cap) { free(part); free(abase); free(dfl); free(used); return -1; }
+    /* (3) the rows */
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t r = 0; r < nrows; ++r) {
+        const int32_t d = row_doc[r];
+        char num[24];
+        const int k = stamp_digits(row_stamp[r], num);
+        int64_t o = line_off[r];
+        memcpy(out + o, num + k, (size_t)(24 - k));
+        o += 24 - k;
+        out[o++] = ',';
+        const int64_t la = part[3 * d + 1] - part[3 * d], lb = part[3 * d + 2] - part[3 * d + 1];
+        memcpy(out + o, art + part[3 * d], (size_t)la);
+        o += la;
+        for (int c = 1; c < 3; ++c) {
+            const uint8_t *s = json + json3[3 * r + (c - 1)];
+            const int64_t m = json3[3 * r + c] - json3[3 * r + (c - 1)];
+            out[o++] = ',';
+            put_cell_sized(out, &o, s, m);
+        }
+        out[o++] = ',';
+        memcpy(out + o, art + part[3 * d + 1], (size_t)lb);
+        o += lb;
+        out[o++] = '\n';
+    }
+    free(part);
+    free(abase);
+    free(dfl);
+    free(used);
+    return 0;
+}

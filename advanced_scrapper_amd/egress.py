@@ -177,6 +177,10 @@ def _csv_lib():
         P, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
         L.kwcsv_emit.restype = i64
         L.kwcsv_emit.argtypes = [P, P, P, i32, P, P, P, i64, P, P, P, i64, P, P]
+        L.kwcsv_emit_mt.restype = i64
+        L.kwcsv_emit_mt.argtypes = [P, P, P, i32, P, P, P, i64, P, P, P, i64, P, P, P, i32]
+        L.kwcsv_emit_art_bytes.restype = i64
+        L.kwcsv_emit_art_bytes.argtypes = [P, i32, P, P, i64]
         _CSV_LIB = L
     return _CSV_LIB
 
@@ -273,7 +277,14 @@ class RunFiles:
         return True
 
 
-_EMIT_BUF = [np.zeros(0, dtype=np.uint8)]
+_EMIT_BUF = [np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=np.uint8)]
+
+
+def _scratch(k: int, cap: int) -> np.ndarray:
+    """Scratch buffer k of the emitter, kept across chunks (k = 1: the articles' rendered cells)."""
+    if len(_EMIT_BUF[k]) < cap:
+        _EMIT_BUF[k] = np.empty(cap + cap // 4, dtype=np.uint8)
+    return _EMIT_BUF[k]
 
 
 def _emit_buffer(cap: int) -> np.ndarray:
@@ -308,24 +319,20 @@ def render_native(chunk, raw_rows, stamps_by_doc, tickers):
     cols = np.asarray([chunk.col[k] for k in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')],
                       dtype=np.int32)
     jb = jbuf if len(jbuf) else np.zeros(1, np.uint8)
-    # room: every row's cells (quoted: at most doubled) + the articles' cells rendered once (kwcsv_emit)
-    cell_len = np.zeros(len(c.off) // c.ncols + 1, dtype=np.int64)
-    nd = (len(c.off) - 1) // c.ncols
-    for k in cols.tolist():
-        idx = np.arange(nd, dtype=np.int64) * c.ncols + k
-        cell_len[:nd] += c.off[idx + 1] - c.off[idx]
-    cap = int(2 * (int(cell_len[rd].sum()) + len(jbuf) + int(cell_len.sum())) + 64 * n + 1024)
     line_off = np.empty(n + 1, dtype=np.int64)
     flags = np.empty(n, dtype=np.uint32)
     L = _csv_lib()
+    art = _scratch(1, int(L.kwcsv_emit_art_bytes(_p(c.off), c.ncols, _p(cols), _p(rd), n)))
+    from .ingest import host_threads
+    cap = len(_EMIT_BUF[0])
     rc = -1
-    for _ in range(8):
+    for _ in range(2):      # -1: out too small, line_off[n] = the bytes the rows need
         out = _emit_buffer(cap)
-        rc = L.kwcsv_emit(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jb), _p(j3),
-                          _p(out), cap, _p(line_off), _p(flags))
+        rc = L.kwcsv_emit_mt(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jb), _p(j3),
+                             _p(out), len(out), _p(line_off), _p(flags), _p(art), host_threads())
         if rc != -1:
             break
-        cap *= 2
+        cap = int(line_off[n])
     if rc != 0:
         return None
     ti = row_ti[order]
@@ -339,16 +346,40 @@ def header_bytes() -> bytes:
     return _join(list(_HEADER_COLUMNS)).encode('utf-8')
 
 
+_POOL = None
+
+
+def _write_pool():
+    """Host threads for the per-ticker appends (file writes release the GIL)."""
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        from .ingest import host_threads
+        _POOL = ThreadPoolExecutor(max_workers=min(8, host_threads()), thread_name_prefix='kw-egress')
+    return _POOL
+
+
+def _append_file(path: str, header: bytes, data) -> None:
+    new = not os.path.exists(path)
+    with open(path, 'ab') as fh:
+        if new:
+            fh.write(header)
+        fh.write(data)
+
+
 def append_rendered(out_dir: str, rendered, run_files: 'RunFiles' = None, key=(0, 0)):
     """Append rendered rows (render_native) to their files, the header first in a new file; the run index
-    records the rows of the files this run owns (under ``key``, see RunFiles)."""
+    records the rows of the files this run owns (under ``key``, see RunFiles).  Each file is written by one
+    thread (the files of a chunk are distinct), so every file receives its rows in order."""
     header = header_bytes()
-    for name, data, stamps, lens, flags in rendered:
-        path = os.path.join(out_dir, name)
-        new = not os.path.exists(path)
-        with open(path, 'ab') as fh:
-            if new:
-                fh.write(header)
-            fh.write(data)
-        if run_files is not None and run_files.owned(name):
-            run_files.add(name, stamps, lens, flags, header, key)
+    if len(rendered) > 4:
+        jobs = [_write_pool().submit(_append_file, os.path.join(out_dir, r[0]), header, r[1]) for r in rendered]
+        for j in jobs:
+            j.result()
+    else:
+        for r in rendered:
+            _append_file(os.path.join(out_dir, r[0]), header, r[1])
+    if run_files is not None:
+        for name, data, stamps, lens, flags in rendered:
+            if run_files.owned(name):
+                run_files.add(name, stamps, lens, flags, header, key)

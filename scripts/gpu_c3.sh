@@ -7,3 +7,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_c3.py -x -v -s --timeout 50
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-sample 0 > gpurun_out/bench_c2.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-sample 0 --total-docs 10000000 > gpurun_out/bench_c3n1.log 2>&1 || exit $?
 timeout -k 10 120 python scripts/dump_hits.py > gpurun_out/dump_hits.log 2>&1 || exit $?
+timeout -k 10 300 python scripts/e2e.py > gpurun_out/e2e.log 2>&1 || exit $?

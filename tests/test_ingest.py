@@ -192,3 +192,46 @@ def test_native_dates_equal_parse_date(monkeypatch):
     finally:
         monkeypatch.setenv('TZ', 'UTC')
         time.tzset()
+
+
+@pytest.mark.parametrize('threads', [1, 5])
+def test_threaded_emitter_equals_serial(threads):
+    """kwcsv_emit_mt (articles rendered in parallel, row offsets by prefix sum, rows in parallel) writes the
+    serial kwcsv_emit's bytes, line offsets and cell flags (NA cells, quoting, '\\r', negative stamps)."""
+    from advanced_scrapper_amd import egress, ingest
+    from advanced_scrapper_amd.ingest import _p
+    L = egress._csv_lib()
+    rng = np.random.default_rng(11)
+    rows = [{c: _cell(rng) for c in COLS} for _ in range(900)]
+    buf = io.StringIO()
+    pd.DataFrame(rows).to_csv(buf, index=False, lineterminator='\r\n')
+    (chunk,) = [g for g in ingest.read_chunks_bytes(buf.getvalue().encode('utf-8'), 1000)]
+    assert isinstance(chunk, ingest.NativeChunk)
+    c = chunk.cells
+    cols = np.asarray([chunk.col[k] for k in ('date_time', 'title', 'url', 'source', 'source_url', 'article_text')],
+                      dtype=np.int32)
+    n = 2500
+    rd = np.sort(rng.integers(0, len(chunk), n)).astype(np.int32)
+    rd = rd[np.argsort(rng.integers(0, 40, n), kind='stable')]          # ticker-grouped order
+    rs = rng.integers(-2**40, 2**40, n).astype(np.int64)
+    js = [('{"A": [%d]}' % k if k % 3 else '{}') + ('"\r' if k % 17 == 0 else '') + ('"x", ' * (k % 50))
+          for k in range(2 * n)]                                        # long quoted cells too
+    jbuf = np.frombuffer(''.join(js).encode(), dtype=np.uint8).copy()
+    joff = np.zeros(2 * n + 1, dtype=np.int64)
+    joff[1:] = np.cumsum([len(j) for j in js])
+    j3 = np.empty(3 * n, dtype=np.int64)
+    j3[0::3], j3[1::3], j3[2::3] = joff[0:-1:2], joff[1::2], joff[2::2]
+    cap = 64 << 20
+    o1, l1, f1 = np.empty(cap, np.uint8), np.empty(n + 1, np.int64), np.empty(n, np.uint32)
+    assert L.kwcsv_emit(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jbuf), _p(j3),
+                        _p(o1), cap, _p(l1), _p(f1)) == 0
+    art = np.empty(int(L.kwcsv_emit_art_bytes(_p(c.off), c.ncols, _p(cols), _p(rd), n)), np.uint8)
+    o2, l2, f2 = np.empty(cap, np.uint8), np.empty(n + 1, np.int64), np.empty(n, np.uint32)
+    assert L.kwcsv_emit_mt(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jbuf),
+                           _p(j3), _p(o2), cap, _p(l2), _p(f2), _p(art), threads) == 0
+    assert np.array_equal(l1, l2) and np.array_equal(f1, f2)
+    assert bytes(o1[:l1[-1]]) == bytes(o2[:l2[-1]])
+    small = np.empty(16, np.uint8)           # too small: -1 and the bytes needed
+    assert L.kwcsv_emit_mt(_p(c.buf), _p(c.off), _p(c.flags), c.ncols, _p(cols), _p(rd), _p(rs), n, _p(jbuf),
+                           _p(j3), _p(small), 16, _p(l2), _p(f2), _p(art), threads) == -1
+    assert l2[-1] == l1[-1]
