@@ -587,10 +587,70 @@ def main(argv=None):
     return run(args, 0, 1, args.device, None)
 
 
+def _prefetch(chunks, depth: int = 1):
+    """Yield the items of ``chunks`` while a background thread already produces the next ``depth`` of them
+    (the next chunk's tokenizing overlaps this chunk's matching and writing: the native ingest runs in C
+    with the GIL released).  Order and exceptions are the producer's."""
+    import queue
+    import threading
+    q: queue.Queue = queue.Queue(maxsize=depth)
+    stop = threading.Event()
+    done = object()
+
+    def produce():
+        try:
+            for item in chunks:
+                while not stop.is_set():
+                    try:
+                        q.put((item, None), timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+                if stop.is_set():
+                    return
+            q.put((done, None))
+        except BaseException as exc:   # noqa: BLE001 - re-raised in the consumer, in order
+            q.put((done, exc))
+
+    th = threading.Thread(target=produce, name='kw-ingest', daemon=True)
+    th.start()
+    try:
+        while True:
+            item, exc = q.get()
+            if item is done:
+                if exc is not None:
+                    raise exc
+                return
+            yield item
+    finally:
+        stop.set()
+        th.join(timeout=5)
+
+
+def _warm_device(device):
+    """Initialise the HIP runtime and the device context in a background thread (the first CUDA call costs a
+    fixed ~second) while the KB loads and the first chunk is tokenized."""
+    import threading
+
+    def warm():
+        try:
+            import torch
+            if torch.cuda.is_available():
+                dev = torch.cuda.current_device() if device is None else int(device)
+                torch.empty(1, device=torch.device('cuda', dev))
+        except Exception:   # noqa: BLE001 - the matcher's own initialisation reports any error
+            pass
+
+    th = threading.Thread(target=warm, name='kw-device-init', daemon=True)
+    th.start()
+    return th
+
+
 def run(args, rank: int, world: int, device, backend, matcher=None):
     """The driver loop on one rank: read the chunks, match (sharded over the ranks when world > 1), write,
     then sort every output file (match_keywords.py:226-246)."""
     global _RUN
+    warm = _warm_device(device) if (world == 1 and matcher is None) else None
     processed = read_and_process_json_files(args.info_dir)
     out_dir = f'{args.source}_ticker_matched_articles'
     if rank == 0:
@@ -606,8 +666,12 @@ def run(args, rank: int, world: int, device, backend, matcher=None):
             exchange.close()
     _RUN = egress.RunFiles(out_dir)
     try:
-        # the native tokenizer (ingest.py), chunk by chunk, with pandas' own chunks where it cannot be exact
-        for chunk in ingest.read_chunks(args.articles, args.chunksize):
+        # the native tokenizer (ingest.py), chunk by chunk, with pandas' own chunks where it cannot be exact;
+        # the next chunk is read while this one is matched and written
+        for chunk in _prefetch(ingest.read_chunks(args.articles, args.chunksize)):
+            if warm is not None:
+                warm.join()
+                warm = None
             if isinstance(chunk, NativeChunk):
                 if matcher is None:
                     matcher = get_matcher(processed, device, _native_sample(chunk))
