@@ -76,7 +76,7 @@ def build_kwrows(force: bool = False) -> str:
     out = os.path.join(LIB, 'libkwrows.so')
     src = os.path.join(CSRC, 'kwrows.c')
     if force or _stale(out, [src]):
-        _run(['gcc', '-O2', '-fPIC', '-shared', '-Wall', '-o', out, src])
+        _run(['gcc', '-O2', '-fopenmp', '-fPIC', '-shared', '-Wall', '-o', out, src])
     return out
 
 

@@ -67,6 +67,7 @@ struct kw_handle {
     size_t scratch_bytes = 0;
     void *d_small = nullptr;       // status, stats, out_cnt, offsets
     unsigned long long *d_offs = nullptr;
+    unsigned long long *d_total = nullptr;   // in d_small: the scan's record count
     kw_hit *d_hits = nullptr;
     size_t hits_cap = 0;
     // last scan
@@ -1205,6 +1206,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.stats = (unsigned long long *)(q + 128);      // 32 x u64 (fast path; 21.. developer counters)
     h->FS.tx_used = (unsigned long long *)(q + 384);    // transcoded-view bytes handed out
     h->FS.res_cnt = (uint32_t *)(q + 392);              // documents left to the resolve kernel
+    h->d_total = (unsigned long long *)(q + 400);       // hit records of the scan (kw_offsets_kernel)
     uint32_t *cnts = (uint32_t *)(q + 1024);
     h->out_cnt_all = cnts;
     h->FS.kout_cnt = cnts;
@@ -1300,7 +1302,7 @@ static int launch_scan(kw_handle *h)
     int rc = ensure_scratch(h, w);
     if (rc) return rc;
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
-    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 400, st));   // status .. stats, tx_used, res_cnt
+    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 408, st));   // status .. stats, tx_used, res_cnt, total
     HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
@@ -1387,7 +1389,8 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipEventRecord(h->evg, st));
     const int nw = 2 * nk + h->nr + h->ng;
     if (n_docs > 0) {
-        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->out_cnt_all, nw, h->out_cap, h->d_offs);
+        hipLaunchKernelGGL(kw_offsets_kernel, dim3(1), dim3(1024), 0, st, h->out_cnt_all, nw, h->out_cap, h->d_offs,
+                           h->d_total);
         hipLaunchKernelGGL(kw_gather_kernel, dim3(nw), dim3(256), 0, st, h->out_all, h->out_cap, h->out_cnt_all,
                            h->d_offs, h->d_hits);
         HIPCHK(h, hipGetLastError());
@@ -1419,8 +1422,12 @@ static int finish(kw_handle *h)
     if (h->fetched) return KW_OK;
     for (int attempt = 0; attempt < 6; ++attempt) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        // the scan's small results in one copy: status (0), generic stats (64), fast-path stats (128),
+        // transcoded-view bytes (384), record count (400)
+        unsigned long long small[51];
+        HIPCHK(h, hipMemcpy(small, h->S.status, sizeof(small), hipMemcpyDeviceToHost));
         uint32_t status[4];
-        HIPCHK(h, hipMemcpy(status, h->S.status, sizeof(status), hipMemcpyDeviceToHost));
+        memcpy(status, small, sizeof(status));
         if (h->n_docs == 0) { h->n_hits = 0; h->fetched = true; return KW_OK; }
         if (status[0] & ST_FIELD_TOO_LONG) {
             char buf[256];
@@ -1486,11 +1493,8 @@ static int finish(kw_handle *h)
             if (rc) return rc;
             continue;
         }
-        unsigned long long tot = 0;
-        HIPCHK(h, hipMemcpy(&tot, h->d_offs + h->launched_waves, sizeof(tot), hipMemcpyDeviceToHost));
-        unsigned long long gst[3], fst[32];
-        HIPCHK(h, hipMemcpy(gst, h->S.stats, sizeof(gst), hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy(fst, h->FS.stats, sizeof(fst), hipMemcpyDeviceToHost));
+        const unsigned long long tot = small[50];
+        const unsigned long long *gst = small + 8, *fst = small + 16;
         h->stats[0] = fst[0] + gst[0];
         h->stats[1] = fst[1] + gst[1];
         h->stats[2] = fst[2] + gst[2];
@@ -1498,8 +1502,7 @@ static int finish(kw_handle *h)
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
         h->stats[17] = (unsigned long long)h->rescans;
         {   // the transcoded view: documents it took / left to the resolve kernel; the next scan's capacity
-            unsigned long long used = 0;
-            HIPCHK(h, hipMemcpy(&used, h->FS.tx_used, sizeof(used), hipMemcpyDeviceToHost));
+            const unsigned long long used = small[48];
             if (used > h->caps.tx_cap && !getenv("KW_TEST_TX_CAP")) h->tx_need = used + used / 8;
         }
         if (getenv("KW_DUMP_TIMING")) {   // FK_TIMING builds: resolve-kernel cycles summed over waves

@@ -968,22 +968,28 @@ constexpr size_t kScanLds = (size_t)FILT_WORDS * 4 + (size_t)WAVES_PER_BLOCK * (
 
 // exclusive scan of the per-wave record counts (one block)
 __global__ void kw_offsets_kernel(const uint32_t *__restrict__ cnt, int n_waves, uint32_t cap,
-                                  unsigned long long *__restrict__ offs)
+                                  unsigned long long *__restrict__ offs, unsigned long long *__restrict__ total)
 {
-    __shared__ unsigned long long part[1024];
+    __shared__ unsigned long long part[2][1024];
     const int t = threadIdx.x;
     const int per = (n_waves + 1023) / 1024;
     unsigned long long s = 0;
     for (int i = t * per; i < (t + 1) * per && i < n_waves; ++i) s += (cnt[i] < cap ? cnt[i] : cap);
-    part[t] = s;
+    // inclusive block scan (Hillis-Steele over the 1024 partial sums, double-buffered)
+    int b = 0;
+    part[0][t] = s;
     __syncthreads();
-    if (t == 0) {
-        unsigned long long acc = 0;
-        for (int i = 0; i < 1024; ++i) { unsigned long long v = part[i]; part[i] = acc; acc += v; }
-        offs[n_waves] = acc;
+    for (int d = 1; d < 1024; d <<= 1) {
+        const unsigned long long v = part[b][t] + (t >= d ? part[b][t - d] : 0ull);
+        b ^= 1;
+        part[b][t] = v;
+        __syncthreads();
     }
-    __syncthreads();
-    unsigned long long acc = part[t];
+    unsigned long long acc = part[b][t] - s;      // exclusive
+    if (t == 1023) {
+        offs[n_waves] = part[b][t];
+        *total = part[b][t];
+    }
     for (int i = t * per; i < (t + 1) * per && i < n_waves; ++i) {
         offs[i] = acc;
         acc += (cnt[i] < cap ? cnt[i] : cap);

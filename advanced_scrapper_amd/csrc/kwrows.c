@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <omp.h>
 
 typedef struct { uint32_t doc, pattern, pos, field; } kw_hit_rec;
 typedef struct { int32_t ti, field, rank, pat; int64_t hs, he; } entry_t;
@@ -66,6 +67,8 @@ static void put_dict(sink_t *s, const entry_t *e0, const entry_t *e1, const kw_h
     }
     put(s, "}", 1);
 }
+
+static int64_t max_rows_guess(int64_t n_hits) { return n_hits + 1024; }
 
 int64_t kwrows_assemble(const kw_hit_rec *h, int64_t n_hits, const int64_t *date_us, const uint8_t *date_ok,
                         int64_t n_docs, const int64_t *occ_off, const int32_t *occ_ti, const int32_t *occ_rank,
@@ -131,4 +134,95 @@ int64_t kwrows_assemble(const kw_hit_rec *h, int64_t n_hits, const int64_t *date
     free(seen);
     free(ent);
     return rc ? rc : rows;
+}
+
+/*
+ * kwrows_assemble over nthreads threads: the sorted hit records are cut at document boundaries into one slice
+ * per thread, each slice is assembled into the thread's own buffers (kwrows_assemble on the slice), and the
+ * slices are concatenated in document order -- the same rows, JSON text and offsets as one kwrows_assemble
+ * call.  need[0..1] gets the rows and JSON bytes of the whole result; returns the rows, -1 when row_cap or
+ * out_cap is smaller than need (nothing written; call again with need), -2 / -3 as kwrows_assemble (the
+ * first slice's error in document order).
+ */
+int64_t kwrows_assemble_mt(const kw_hit_rec *h, int64_t n_hits, const int64_t *date_us, const uint8_t *date_ok,
+                           int64_t n_docs, const int64_t *occ_off, const int32_t *occ_ti, const int32_t *occ_rank,
+                           const int64_t *occ_lo, const int64_t *occ_hi, const uint8_t *invalid_rx,
+                           const char *keys, const int64_t *key_off, int32_t n_tickers, int32_t *row_doc,
+                           int32_t *row_ti, int64_t row_cap, char *out, int64_t *out_off, int64_t out_cap,
+                           int64_t *need, int32_t nthreads)
+{
+    int64_t nt = nthreads > 1 ? nthreads : 1;
+    if (nt > n_hits / 4096 + 1) nt = n_hits / 4096 + 1;
+    int64_t *cut = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nt + 1));
+    int64_t *rows = (int64_t *)calloc((size_t)nt, sizeof(int64_t));
+    int32_t **rd = (int32_t **)calloc((size_t)nt, sizeof(int32_t *));
+    int32_t **rt = (int32_t **)calloc((size_t)nt, sizeof(int32_t *));
+    char **ob = (char **)calloc((size_t)nt, sizeof(char *));
+    int64_t **oo = (int64_t **)calloc((size_t)nt, sizeof(int64_t *));
+    if (!cut || !rows || !rd || !rt || !ob || !oo) { free(cut); free(rows); free(rd); free(rt); free(ob); free(oo); return -3; }
+    cut[0] = 0;
+    for (int64_t t = 1; t < nt; ++t) {   /* slice starts at document boundaries */
+        int64_t c = n_hits * t / nt;
+        if (c < cut[t - 1]) c = cut[t - 1];
+        while (c > cut[t - 1] && c < n_hits && h[c].doc == h[c - 1].doc) ++c;
+        cut[t] = c;
+    }
+    cut[nt] = n_hits;
+    #pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t a = cut[t], b = cut[t + 1];
+        if (b <= a) { rows[t] = 0; continue; }
+        int64_t rc_ = max_rows_guess(b - a), oc = 64 * (b - a) + 4096;
+        for (;;) {
+            rd[t] = (int32_t *)realloc(rd[t], sizeof(int32_t) * (size_t)rc_);
+            rt[t] = (int32_t *)realloc(rt[t], sizeof(int32_t) * (size_t)rc_);
+            ob[t] = (char *)realloc(ob[t], (size_t)oc);
+            oo[t] = (int64_t *)realloc(oo[t], sizeof(int64_t) * (size_t)(2 * rc_ + 1));
+            if (!rd[t] || !rt[t] || !ob[t] || !oo[t]) { rows[t] = -3; break; }
+            const int64_t r = kwrows_assemble(h + a, b - a, date_us, date_ok, n_docs, occ_off, occ_ti, occ_rank, occ_lo,
+                                              occ_hi, invalid_rx, keys, key_off, n_tickers, rd[t], rt[t], rc_, ob[t],
+                                              oo[t], oc);
+            if (r == -1) { rc_ *= 2; oc *= 2; continue; }
+            rows[t] = r;
+            break;
+        }
+    }
+    int64_t rc = 0, nr = 0, nb = 0;
+    for (int64_t t = 0; t < nt && rc == 0; ++t) {
+        if (rows[t] < 0) rc = rows[t];
+        else { nr += rows[t]; nb += rows[t] ? oo[t][2 * rows[t]] : 0; }
+    }
+    if (rc == 0) {
+        need[0] = nr;
+        need[1] = nb;
+        if (nr > row_cap || nb > out_cap) rc = -1;
+    }
+    if (rc == 0) {
+        int64_t *r0 = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nt + 1));
+        int64_t *b0 = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nt + 1));
+        if (!r0 || !b0) rc = -3;
+        else {
+            r0[0] = b0[0] = 0;
+            for (int64_t t = 0; t < nt; ++t) {
+                r0[t + 1] = r0[t] + rows[t];
+                b0[t + 1] = b0[t] + (rows[t] ? oo[t][2 * rows[t]] : 0);
+            }
+            out_off[0] = 0;
+            #pragma omp parallel for num_threads(nt) schedule(static)
+            for (int64_t t = 0; t < nt; ++t) {
+                const int64_t k = rows[t];
+                if (!k) continue;
+                memcpy(row_doc + r0[t], rd[t], sizeof(int32_t) * (size_t)k);
+                memcpy(row_ti + r0[t], rt[t], sizeof(int32_t) * (size_t)k);
+                memcpy(out + b0[t], ob[t], (size_t)oo[t][2 * k]);
+                for (int64_t j = 1; j <= 2 * k; ++j) out_off[2 * r0[t] + j] = oo[t][j] + b0[t];
+            }
+            rc = nr;
+        }
+        free(r0);
+        free(b0);
+    }
+    for (int64_t t = 0; t < nt; ++t) { free(rd[t]); free(rt[t]); free(ob[t]); free(oo[t]); }
+    free(cut); free(rows); free(rd); free(rt); free(ob); free(oo);
+    return rc;
 }

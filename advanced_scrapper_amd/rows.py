@@ -35,6 +35,9 @@ def _lib():
         lib.kwrows_assemble.restype = ctypes.c_int64
         lib.kwrows_assemble.argtypes = [P, ctypes.c_int64, P, P, ctypes.c_int64, P, P, P, P, P, P, P, P,
                                         ctypes.c_int32, P, P, ctypes.c_int64, P, P, ctypes.c_int64]
+        lib.kwrows_assemble_mt.restype = ctypes.c_int64
+        lib.kwrows_assemble_mt.argtypes = [P, ctypes.c_int64, P, P, ctypes.c_int64, P, P, P, P, P, P, P, P,
+                                           ctypes.c_int32, P, P, ctypes.c_int64, P, P, ctypes.c_int64, P, ctypes.c_int32]
         _LIB = lib
     return _LIB
 
@@ -107,24 +110,25 @@ def assemble_json_raw(ckb: CompiledKB, hits: np.ndarray, dates: Sequence):
     h = np.ascontiguousarray(hits[np.lexsort((hits['pos'], hits['pattern'], hits['field'], hits['doc']))])
     assert h.dtype == _native.HIT_DTYPE
     off, ti, rank, lo, hi, invalid, key_buf, key_off = tables
-    row_cap = max(1024, len(h))
-    out_cap = max(1 << 16, 64 * len(h))
-    for _attempt in range(24):
+    from .ingest import host_threads
+    row_cap = max(1024, len(h) + len(h) // 2)
+    out_cap = max(1 << 16, 48 * len(h))
+    need = np.zeros(2, dtype=np.int64)
+    for _attempt in range(2):      # -1: the rows / text need more room than guessed (need = the exact sizes)
         row_doc = np.empty(row_cap, dtype=np.int32)
         row_ti = np.empty(row_cap, dtype=np.int32)
         out = np.empty(out_cap, dtype=np.uint8)
         out_off = np.empty(2 * row_cap + 1, dtype=np.int64)
-        n = _lib().kwrows_assemble(_ptr(h), len(h), _ptr(date_us), _ptr(date_ok), n_docs, _ptr(off), _ptr(ti),
-                                   _ptr(rank), _ptr(lo), _ptr(hi), _ptr(invalid), _ptr(key_buf), _ptr(key_off),
-                                   len(ckb.tickers), _ptr(row_doc), _ptr(row_ti), row_cap, _ptr(out),
-                                   _ptr(out_off), out_cap)
+        n = _lib().kwrows_assemble_mt(_ptr(h), len(h), _ptr(date_us), _ptr(date_ok), n_docs, _ptr(off), _ptr(ti),
+                                      _ptr(rank), _ptr(lo), _ptr(hi), _ptr(invalid), _ptr(key_buf), _ptr(key_off),
+                                      len(ckb.tickers), _ptr(row_doc), _ptr(row_ti), row_cap, _ptr(out),
+                                      _ptr(out_off), out_cap, _ptr(need), host_threads())
         if n == -2:
             return None
         if n == -3:
             raise MemoryError('kwrows_assemble: allocation failed')
-        if n == -1:                      # row or text capacity too small: grow and redo
-            row_cap *= 2
-            out_cap *= 2
+        if n == -1:
+            row_cap, out_cap = int(need[0]) + 1, int(need[1]) + 1
             continue
         break
     else:

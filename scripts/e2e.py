@@ -79,6 +79,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--docs', type=int, default=200000)
     ap.add_argument('--chunksize', type=int, default=20000)
+    ap.add_argument('--profile', action='store_true', help='cProfile main() (top functions by cumulative time)')
     args = ap.parse_args()
     os.environ.setdefault('TZ', 'UTC')
     time.tzset()
@@ -96,11 +97,20 @@ def main():
     os.chdir(work)
     # 1) the product's driver, end to end
     sink = io.StringIO()
+    prof = None
+    if args.profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     with contextlib.redirect_stdout(sink):
         rc = mk.main(['--info-dir', os.path.join(work, 'ticker'), '--articles', csv_path,
                       '--chunksize', str(args.chunksize), '--device', '0'])
     total = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats('cumtime').print_stats(40)
     assert rc == 0
     d_main = _digest('yahoo_ticker_matched_articles')
     n_files = len(os.listdir('yahoo_ticker_matched_articles'))

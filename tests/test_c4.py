@@ -180,3 +180,63 @@ def test_c4_whole_corpus_vs_oracle_digests():
     assert int(cnt.sum()) == meta['total_records']
     assert cd.total(dig) == meta['hits_digest'] == bench.hits_digest(hits)
     m.close()
+
+
+@pytest.mark.gpu
+def test_c4_ten_million_vs_oracle():
+    """Config 4 at its stated size: the ~52k-name KB against 10M articles in ONE kw_scan (~22.9 GB resident).
+    Documents 0..999 999 per document against tests/golden/c4_digests.npz, and the strided 1000-document
+    blocks beyond 1M that tests/golden/c4_blocks.npz pins (make_c2_digests.py --config 4 --strided 10
+    --lo 1000000 --docs 10000000 --blocks c4_blocks, CPU oracle in the build container)."""
+    import time
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from advanced_scrapper_amd.matcher import GpuMatcher, background_sample, records_from_tensor
+    from advanced_scrapper_amd.synth_kb import synthetic_kb
+    from tests import corpus_digest as cd
+    meta = json.load(open(os.path.join(HERE, 'c4_blocks.json')))
+    z = np.load(os.path.join(HERE, 'c4_blocks.npz'))
+    z1 = np.load(os.path.join(HERE, 'c4_digests.npz'))
+    n, seed, blk = meta['n_docs'], meta['seed'], meta['docs_per_block']
+    assert n == 10_000_000 and meta['config'] == 4
+    processed = synthetic_kb(2300, seed)
+    ckb = compile_kb(processed)
+    names, kinds = synth.injectable_names(ckb)
+    t0 = time.time()
+    corpus = synth.generate(n, names, kinds, seed=seed, doc_base=0)
+    bg = synth.generate(2000, names, kinds, seed=seed + 7777, doc_base=0)
+    m = GpuMatcher(ckb, 0, background_sample(bg.texts() + bg.titles()))
+    d_arena, d_off = m.upload(corpus.arena, corpus.off)
+    m.scan(d_arena, d_off, n)
+    hits = m.hits_device()
+    print(f'c4 10M: {hits.shape[0]} records, {time.time() - t0:.1f} s, stats {m.stats()}', flush=True)
+    dig, cnt = cd.per_doc(records_from_tensor(hits), n)
+    del hits
+    bad = np.flatnonzero((dig[:1_000_000] != z1['digest']) | (cnt[:1_000_000] != z1['count'].astype(np.int64)))
+    assert not len(bad), f'{len(bad)} of the first 1M documents differ from the oracle; first: {bad[:20].tolist()}'
+    with np.errstate(over='ignore'):
+        bdig = dig.reshape(-1, blk).sum(axis=1, dtype=np.uint64)
+    bcnt = cnt.reshape(-1, blk).sum(axis=1)
+    sel = z['block'].astype(np.int64)
+    beyond = sel[sel >= 1_000_000 // blk]
+    assert len(beyond) >= 10
+    badb = np.flatnonzero((bdig[sel] != z['digest']) | (bcnt[sel] != z['count'].astype(np.int64)))
+    if len(badb):
+        lo = int(sel[badb[0]]) * blk
+        want = oracle_pool.field_results(processed, [s for d in range(lo, lo + blk)
+                                                     for s in (corpus.text(d), corpus.title(d))])
+        pid = {x: i for i, x in enumerate(ckb.names)}
+        rows = []
+        for i in range(blk):
+            rows += cd.oracle_records(lo + i, [want[2 * i], want[2 * i + 1]], pid)
+        a = np.asarray(rows, dtype=np.uint32).reshape(-1, 4).view(
+            np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('field', '<u4')])).reshape(-1)
+        wd, wc = cd.per_doc(a, blk, lo)
+        print('block', lo // blk, 'differing documents',
+              (lo + np.flatnonzero((wd != dig[lo:lo + blk]) | (wc != cnt[lo:lo + blk]))).tolist()[:20])
+    assert not len(badb), f'{len(badb)} of {len(sel)} pinned blocks differ; first: {sel[badb[:10]].tolist()}'
+    m.close()

@@ -558,3 +558,32 @@ def test_native_sort_defers_numeric_looking_block(tmp_path):
     good = tmp_path / 'good.csv'
     write(good, ['abc'] + ['007'] * (egress.PANDAS_BLOCK_ROWS - 1) + ['abc'] + ['007'] * 9)
     assert mk._sort_native(str(good)) is True
+
+
+def test_threaded_json_rows_equal_serial(golden, monkeypatch):
+    """kwrows_assemble_mt (hit records cut at document boundaries, slices assembled apart, concatenated) gives
+    the serial kwrows_assemble's rows, tickers and JSON text on a large synthetic hit set."""
+    from datetime import datetime, timedelta
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd import rows as R
+    from advanced_scrapper_amd.kb import compile_kb
+    ckb = compile_kb(golden.kb_processed())
+    rng = np.random.default_rng(5)
+    n_docs, n = 3000, 40000
+    doc = np.sort(rng.integers(0, n_docs, n)).astype(np.uint32)
+    pat = rng.integers(0, ckb.n_patterns, n).astype(np.uint32)
+    pos = np.where(rng.random(n) < 0.2, 0xFFFFFFFF, rng.integers(0, 5000, n)).astype(np.uint32)
+    fld = rng.integers(0, 2, n).astype(np.uint32)
+    hits = np.zeros(n, dtype=_native.HIT_DTYPE)
+    hits['doc'], hits['pattern'], hits['pos'], hits['field'] = doc, pat, pos, fld
+    valid = np.array([not x for x in ckb.invalid_regex])
+    hits = hits[valid[hits['pattern']]]
+    base = datetime(1980, 1, 1)
+    dates = [None if d % 97 == 0 else base + timedelta(seconds=int(d) * 470000) for d in range(n_docs)]
+    monkeypatch.setenv('KW_HOST_THREADS', '1')
+    one = R.assemble_json_raw(ckb, hits, dates)
+    monkeypatch.setenv('KW_HOST_THREADS', '6')
+    six = R.assemble_json_raw(ckb, hits, dates)
+    assert one is not None and len(one[0]) > 10000
+    for a, b in zip(one, six):
+        assert np.array_equal(a, b)
