@@ -353,7 +353,9 @@ def main():
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
             'traffic': (pmc_traffic(args.traffic_json or TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=n_local, seed=args.seed)
-                        if args.workload == 'match' else None),
+                        if args.workload == 'match' else
+                        pmc_traffic(args.traffic_json or TRAFFIC_C4, 'kw_filter_kernel', docs_per_gpu=n_local,
+                                    seed=args.seed, workload='kb50k')),
             'algorithmic_bytes_per_launch': local_bytes,
             'kernel': 'kw::kw_filter_kernel', 'kernel_ms_avg': round(scan_avg, 4),
             'kernels_ms_avg': {k: round(v, 4) for k, v in kavg.items()},
@@ -466,6 +468,7 @@ def cpu_baseline_dedup(rows, n_sample: int):
 
 TRAFFIC_KW = os.path.join(REPO, 'profiles', 'traffic_r03.json')
 TRAFFIC_DEDUP = os.path.join(REPO, 'profiles', 'traffic_dedup_r03.json')
+TRAFFIC_C4 = os.path.join(REPO, 'profiles', 'traffic_c4_r04.json')
 
 
 def pmc_traffic(path: str, kernel: str, **workload):
