@@ -587,3 +587,11 @@ def test_threaded_json_rows_equal_serial(golden, monkeypatch):
     assert one is not None and len(one[0]) > 10000
     for a, b in zip(one, six):
         assert np.array_equal(a, b)
+
+
+def test_word_bitmap_is_cpython_word_class():
+    """kb.word_bitmap (re's \\w over every code point) == chr(c).isalnum() or c == '_' for all of 0..0x10FFFF."""
+    from advanced_scrapper_amd import kb
+    flags = np.fromiter((chr(c).isalnum() for c in range(0x110000)), dtype=bool, count=0x110000)
+    flags[0x5F] = True
+    assert np.array_equal(kb.word_bitmap(), np.packbits(flags, bitorder='little').view(np.uint32))
