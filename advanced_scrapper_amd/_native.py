@@ -40,6 +40,7 @@ HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('fiel
 # every symbol include/kwmatch.h and include/kwdedup.h declare
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
            'kw_last_kernel_times', 'kw_doc_routes', 'kw_last_error', 'kw_destroy',
+           'kw_scan_host', 'kw_hits_host', 'kw_device_count', 'kw_device_init',
            'kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_exchange_plan',
            'kw_comm_last_error', 'kw_comm_destroy',
            'kw_dedup_create', 'kw_dedup_run', 'kw_dedup_counts', 'kw_dedup_kept_size', 'kw_dedup_kept_copy',
@@ -103,6 +104,14 @@ def lib() -> ctypes.CDLL:
     L.kw_last_kernel_times.restype = ctypes.c_int
     L.kw_doc_routes.argtypes = [vp, vp, i64]
     L.kw_doc_routes.restype = ctypes.c_int
+    L.kw_scan_host.argtypes = [vp, vp, i64, vp, i64]
+    L.kw_scan_host.restype = ctypes.c_int
+    L.kw_hits_host.argtypes = [vp, vp, i64, ctypes.POINTER(i64)]
+    L.kw_hits_host.restype = ctypes.c_int
+    L.kw_device_count.argtypes = [ctypes.POINTER(i32)]
+    L.kw_device_count.restype = ctypes.c_int
+    L.kw_device_init.argtypes = [i32]
+    L.kw_device_init.restype = ctypes.c_int
     L.kw_comm_unique_id.argtypes = [vp]
     L.kw_comm_init.argtypes = [i32, i32, vp, i32, ctypes.POINTER(vp)]
     L.kw_allgather_counts.argtypes = [vp, i64, vp, vp]
@@ -131,6 +140,13 @@ def lib_identity() -> dict:
     return {'path': os.path.relpath(LIB_PATH, os.path.dirname(LIB_DIR)), 'sha256': digest,
             'default': LIB_PATH == DEFAULT_LIB,
             'env': {k: v for k, v in sorted(os.environ.items()) if k.startswith('KW_')}}
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (libkwmatch's hipGetDeviceCount; no torch)."""
+    n = ctypes.c_int32()
+    lib().kw_device_count(ctypes.byref(n))
+    return int(n.value)
 
 
 def exchange_plan(nranks: int, rank: int, root: int, counts):

@@ -68,6 +68,11 @@ struct kw_handle {
     void *d_small = nullptr;       // status, stats, out_cnt, offsets
     unsigned long long *d_offs = nullptr;
     unsigned long long *d_total = nullptr;   // in d_small: the scan's record count
+    // kw_scan_host: library-owned device copies of a host arena / offsets, and the stream they use
+    uint8_t *h_arena = nullptr;
+    int64_t *h_off = nullptr;
+    size_t h_arena_cap = 0, h_off_cap = 0;
+    hipStream_t own = nullptr;
     kw_hit *d_hits = nullptr;
     size_t hits_cap = 0;
     // last scan
@@ -1416,6 +1421,61 @@ extern "C" int kw_scan(kw_handle *h, const uint8_t *d_arena, const int64_t *d_do
     return launch_scan(h);
 }
 
+extern "C" int kw_scan_host(kw_handle *h, const uint8_t *arena, int64_t arena_bytes, const int64_t *doc_off,
+                            int64_t n_docs)
+{
+    if (!h) return KW_EINVAL;
+    if (n_docs < 0 || arena_bytes < 0 || (n_docs > 0 && (!arena || !doc_off))) {
+        h->err = "kw_scan_host: bad arguments";
+        return KW_EINVAL;
+    }
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!h->own) HIPCHK(h, hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking));
+    const size_t ab = (size_t)arena_bytes + 64, ob = (size_t)(2 * n_docs + 1) * sizeof(int64_t);
+    if (ab > h->h_arena_cap) {
+        if (h->h_arena) HIPCHK(h, hipFree(h->h_arena));
+        h->h_arena = nullptr;
+        h->h_arena_cap = ab + ab / 4;
+        HIPCHK(h, hipMalloc((void **)&h->h_arena, h->h_arena_cap));
+    }
+    if (ob > h->h_off_cap) {
+        if (h->h_off) HIPCHK(h, hipFree(h->h_off));
+        h->h_off = nullptr;
+        h->h_off_cap = ob + ob / 4;
+        HIPCHK(h, hipMalloc((void **)&h->h_off, h->h_off_cap));
+    }
+    if (arena_bytes > 0) HIPCHK(h, hipMemcpyAsync(h->h_arena, arena, (size_t)arena_bytes, hipMemcpyHostToDevice, h->own));
+    HIPCHK(h, hipMemsetAsync(h->h_arena + arena_bytes, 0, 64, h->own));   // the tiles' read-past pad
+    if (n_docs > 0) HIPCHK(h, hipMemcpyAsync(h->h_off, doc_off, ob, hipMemcpyHostToDevice, h->own));
+    return kw_scan(h, h->h_arena, h->h_off, n_docs, h->own);
+}
+
+extern "C" int kw_hits_host(kw_handle *h, kw_hit *dst, int64_t cap, int64_t *n_hits)
+{
+    if (!h || !n_hits) return KW_EINVAL;
+    const kw_hit *d = nullptr;
+    int rc = kw_hits(h, n_hits, &d);
+    if (rc) return rc;
+    if (*n_hits > cap) { h->err = "kw_hits_host: destination too small"; return KW_EINVAL; }
+    if (*n_hits > 0) HIPCHK(h, hipMemcpy(dst, d, (size_t)*n_hits * sizeof(kw_hit), hipMemcpyDeviceToHost));
+    return KW_OK;
+}
+
+extern "C" int kw_device_count(int32_t *n)
+{
+    if (!n) return KW_EINVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return KW_OK;
+}
+
+extern "C" int kw_device_init(int32_t device)
+{
+    if (hipSetDevice(device) != hipSuccess) return KW_EHIP;
+    return hipFree(nullptr) == hipSuccess ? KW_OK : KW_EHIP;   // creates the device context
+}
+
 static int finish(kw_handle *h)
 {
     if (!h->scanned) { h->err = "kw_hits: no scan"; return KW_ESTATE; }
@@ -1623,6 +1683,9 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->evt) (void)hipEventDestroy(h->evt);
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
+    if (h->own) (void)hipStreamDestroy(h->own);
+    if (h->h_arena) (void)hipFree(h->h_arena);
+    if (h->h_off) (void)hipFree(h->h_off);
     if (h->eve) (void)hipEventDestroy(h->eve);
     if (h->evq) (void)hipEventDestroy(h->evq);
     if (h->evx) (void)hipEventDestroy(h->evx);

@@ -396,9 +396,8 @@ def _native_match(chunk: NativeChunk, processed_data, matcher, exchange=None):
     arena, off = chunk.arena()
     off = off[:2 * n_ok + 1]
     if exchange is None:
-        d_arena, d_off = matcher.upload(arena, off)
-        matcher.scan(d_arena, d_off, n_ok)
-        return matcher.fetch(), dates, error, matcher
+        matcher.scan_host(arena, off, n_ok)          # libkwmatch's own device buffers: no torch in this path
+        return matcher.fetch_host(), dates, error, matcher
     lo, hi = byte_balanced_ranges(off, exchange.world)[exchange.rank]
     d_arena, d_off = matcher.upload(arena, off)
     matcher.scan(d_arena, d_off[2 * lo:], hi - lo)
@@ -628,16 +627,15 @@ def _prefetch(chunks, depth: int = 1):
 
 
 def _warm_device(device):
-    """Initialise the HIP runtime and the device context in a background thread (the first CUDA call costs a
-    fixed ~second) while the KB loads and the first chunk is tokenized."""
+    """Start the HIP runtime and create the device context on a background thread (libkwmatch's
+    kw_device_init, in C with the GIL released: the runtime's start-up costs a fixed fraction of a second)
+    while the KB loads and the first chunk is tokenized."""
     import threading
 
     def warm():
         try:
-            import torch
-            if torch.cuda.is_available():
-                dev = torch.cuda.current_device() if device is None else int(device)
-                torch.empty(1, device=torch.device('cuda', dev))
+            from . import _native
+            _native.lib().kw_device_init(0 if device is None else int(device))
         except Exception:   # noqa: BLE001 - the matcher's own initialisation reports any error
             pass
 

@@ -66,13 +66,18 @@ class GpuMatcher:
 
     def __init__(self, ckb: CompiledKB, device: Optional[int] = None, background: Optional[bytes] = None):
         """``background``: a sample of the article text whose 4-byte statistics
-        price the anchor choice (speed only; results never depend on it)."""
-        import torch
-        if not torch.cuda.is_available():
-            raise RuntimeError("GpuMatcher needs a ROCm GPU (torch.cuda.is_available() is False)")
-        self.torch = torch
+        price the anchor choice (speed only; results never depend on it).
+
+        No torch is needed for the host-buffer methods (:meth:`scan_host`, :meth:`fetch_host`,
+        :meth:`match_strings`); the device-tensor methods import it on first use."""
+        import sys
+        if _native.device_count() == 0:
+            raise RuntimeError("GpuMatcher needs a ROCm GPU (no HIP device visible)")
         self.ckb = ckb
-        self.device = torch.cuda.current_device() if device is None else int(device)
+        if device is None:
+            torch = sys.modules.get('torch')
+            device = torch.cuda.current_device() if torch is not None and torch.cuda.is_initialized() else 0
+        self.device = int(device)
         L = _native.lib()
         h = ctypes.c_void_p()
         rx = np.ascontiguousarray(ckb.rx_atoms, dtype=np.int32)
@@ -89,6 +94,11 @@ class GpuMatcher:
             raise _native.KwError(rc, msg.decode() if msg else '')
         self.h = h
         self._keep = None
+
+    @property
+    def torch(self):
+        import torch
+        return torch
 
     @classmethod
     def from_processed_data(cls, processed_data, device=None, background=None) -> "GpuMatcher":
@@ -181,8 +191,28 @@ class GpuMatcher:
         return float(a.value), float(b.value), float(c.value)
 
     def match_strings(self, texts: Sequence[str], titles: Sequence[str]) -> np.ndarray:
-        """Convenience: pack, upload, scan and fetch."""
-        return records_from_tensor(self.match_device(texts, titles))
+        """Convenience: pack, scan through the host-buffer entry points, fetch (no torch)."""
+        arena, off = pack_fields(texts, titles)
+        self.scan_host(arena, off, len(texts))
+        return self.fetch_host()
+
+    # -- host buffers (kw_scan_host / kw_hits_host): the drop-in driver's single-GPU path, no torch
+    def scan_host(self, arena: np.ndarray, off: np.ndarray, n_docs: int) -> None:
+        """Copy a host arena (its padding included) and its 2n+1 offsets to library-owned device buffers and
+        scan them (asynchronous until :meth:`fetch_host`)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        off = np.ascontiguousarray(off[:2 * int(n_docs) + 1], dtype=np.int64)
+        self._keep = (arena, off)
+        _native.check(_native.lib().kw_scan_host(self.h, _native.ptr(arena), int(arena.size), _native.ptr(off),
+                                                 int(n_docs)), self.h)
+
+    def fetch_host(self) -> np.ndarray:
+        """Records of the last scan on the host (structured HIT_DTYPE array)."""
+        n = self.n_hits()
+        out = np.empty(max(n, 1), dtype=_native.HIT_DTYPE)
+        cnt = ctypes.c_int64()
+        _native.check(_native.lib().kw_hits_host(self.h, _native.ptr(out), n, ctypes.byref(cnt)), self.h)
+        return out[:cnt.value]
 
     def match_device(self, texts: Sequence[str], titles: Sequence[str]):
         """Pack, upload and scan; the records as a device tensor [n, 4] (int32 view of kw_hit)."""

@@ -150,6 +150,22 @@ int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 #define KW_ROUTE_TRANSCODE 3
 int kw_doc_routes(kw_handle *h, uint8_t *routes, int64_t n);
 
+/* Host-buffer forms of kw_scan / kw_hits_copy for callers with no device allocator of their own (the
+ * drop-in driver's single-GPU path runs without torch).  kw_scan_host copies the host arena
+ * (arena_bytes bytes) and the 2*n_docs+1 offsets into library-owned device buffers (grown on demand, kept
+ * across calls) on a stream of the handle, then scans them (asynchronous; the host buffers may be reused
+ * once kw_hits_host returns).  kw_hits_host waits for the scan and copies its records into dst (host, cap
+ * records); *n_hits receives the count. */
+int kw_scan_host(kw_handle *h, const uint8_t *arena, int64_t arena_bytes, const int64_t *doc_off, int64_t n_docs);
+int kw_hits_host(kw_handle *h, kw_hit *dst, int64_t cap, int64_t *n_hits);
+
+/* HIP devices visible to this process (0 when the runtime finds none). */
+int kw_device_count(int32_t *n);
+
+/* Select `device` and create its context, so a caller can start the HIP runtime early (e.g. on a
+ * thread, while it reads its inputs); every other entry point does this on first use anyway. */
+int kw_device_init(int32_t device);
+
 const char *kw_last_error(kw_handle *h);
 int kw_destroy(kw_handle *h);
 

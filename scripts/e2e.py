@@ -57,9 +57,8 @@ def phases(args, csv_path, processed):
         arena, off = chunk.arena()
         off = off[:2 * len(dates) + 1]
         c3 = time.perf_counter(); t['arena'] += c3 - c2
-        d_arena, d_off = matcher.upload(arena, off)
-        matcher.scan(d_arena, d_off, len(dates))
-        hits = matcher.fetch()
+        matcher.scan_host(arena, off, len(dates))
+        hits = matcher.fetch_host()
         c4 = time.perf_counter(); t['gpu_match'] += c4 - c3
         rendered, exc, _row = mk._native_rows(chunk, matcher, hits, dates, error)
         c5 = time.perf_counter(); t['render'] += c5 - c4

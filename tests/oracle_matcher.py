@@ -58,6 +58,13 @@ class OracleMatcher:
         titles = [b[d_off[2 * i + 1]:d_off[2 * i + 2]].decode('utf-8', 'surrogatepass') for i in range(n_docs)]
         self._last = self.match_device(texts, titles)
 
+    def scan_host(self, arena, off, n_docs):
+        self.upload(arena, off[:2 * n_docs + 1])
+        self.scan(arena, off, n_docs)
+
+    def fetch_host(self):
+        return self.fetch()
+
     def hits_device(self):
         return self._last
 
