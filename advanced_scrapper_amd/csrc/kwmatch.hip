@@ -519,8 +519,11 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
             B.gate[3 * r + 2] = hi >= 0x80u ? 0x80808080u : 0u;
         }
     }
-    uint32_t hs = 1024;
-    while (hs < 2 * keys.size()) hs <<= 1;
+    // open addressing with linear probing: a candidate whose key is absent (most stage-2 survivors of the
+    // shorter key lengths) walks to an empty slot, one dependent load per slot; KW_HT_SCALE = slots per key
+    uint32_t hs = 1024, hscale = 2;
+    if (const char *e = getenv("KW_HT_SCALE")) hscale = (uint32_t)std::max(1, atoi(e));
+    while (hs < (size_t)hscale * keys.size()) hs <<= 1;
     B.ht_mask = hs - 1;
     B.ht_key.assign(hs, ~0ull);
     B.ht_begin.assign(hs, 0);
