@@ -1215,6 +1215,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.tx_used = (unsigned long long *)(q + 384);    // transcoded-view bytes handed out
     h->FS.res_cnt = (uint32_t *)(q + 392);              // documents left to the resolve kernel
     h->d_total = (unsigned long long *)(q + 400);       // hit records of the scan (kw_offsets_kernel)
+    h->FS.gnext = (uint32_t *)(q + 408);                // 2 x u32: the filter's / epilogue's next group
     uint32_t *cnts = (uint32_t *)(q + 1024);
     h->out_cnt_all = cnts;
     h->FS.kout_cnt = cnts;
@@ -1259,7 +1260,14 @@ static int launch_scan(kw_handle *h)
     if (nsb < 1) nsb = 1;
     int neb = (int)std::min<int64_t>((n_docs + EK_WAVES - 1) / EK_WAVES, (int64_t)h->cus * h->epi_blocks_per_cu);
     if (neb < 1) neb = 1;
-    const int n_regions = nsb * FS_WAVES;
+    // candidate regions: the filter's work units of K consecutive 32-document groups, about four per filter wave
+    // (claimed dynamically by the filter waves; one probe wave each)
+    const int64_t n_groups_all = (n_docs + FG_DOCS - 1) / FG_DOCS;
+    int64_t kchunk = std::max<int64_t>(1, n_groups_all / ((int64_t)nsb * FS_WAVES * 4));
+    if (const char *e = getenv("KW_CHUNK_GROUPS")) kchunk = std::max(1, atoi(e));
+    const bool dyn_groups = getenv("KW_STATIC_GROUPS") == nullptr;   // (A/B: grid-stride, one chunk per wave)
+    if (!dyn_groups && !getenv("KW_CHUNK_GROUPS")) kchunk = (n_groups_all + (int64_t)nsb * FS_WAVES - 1) / ((int64_t)nsb * FS_WAVES);
+    const int n_regions = (int)std::max<int64_t>(1, (n_groups_all + kchunk - 1) / kchunk);
     const int n_epi = neb * EK_WAVES;
     int rmul = 2;   // resolve blocks per resident slot: later blocks balance the uneven documents (measured: 2-3 % faster than 1)
     if (const char *e = getenv("KW_RESOLVE_MUL")) rmul = std::max(1, atoi(e));
@@ -1285,8 +1293,9 @@ static int launch_scan(kw_handle *h)
     w.ng = ngb * WAVES_PER_BLOCK;
     const int64_t docs_per_k = (n_docs + w.nk - 1) / w.nk;
     const int64_t docs_per_s = (n_docs + w.ns - 1) / w.ns;
-    w.item_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_s * 32), (int64_t)1 << 26);
-    w.cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, docs_per_s * 40), (int64_t)1 << 26);
+    // (regions of a few groups: a 1024 floor; a region that needs more grows every region and rescans)
+    w.item_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1024, docs_per_s * 32), (int64_t)1 << 26);
+    w.cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1024, docs_per_s * 40), (int64_t)1 << 26);
     if (const char *e = getenv("KW_TEST_CAND_CAP")) w.cand_cap = w.item_cap = (uint32_t)std::max(1, atoi(e));
     const int64_t docs_per_r = (n_docs + w.nr - 1) / w.nr;
     w.out_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, std::max(docs_per_r, docs_per_k) * 48),
@@ -1309,8 +1318,10 @@ static int launch_scan(kw_handle *h)
     if (const char *e = getenv("KW_TEST_TX_CAP")) w.tx_cap = (uint64_t)std::max<long long>(16, atoll(e));
     int rc = ensure_scratch(h, w);
     if (rc) return rc;
+    h->FS.dyn = dyn_groups ? 1 : 0;
+    h->FS.chunk_groups = kchunk;
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
-    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 408, st));   // status .. stats, tx_used, res_cnt, total
+    HIPCHK(h, hipMemsetAsync(h->S.status, 0, 416, st));   // status .. stats, tx_used, res_cnt, total, gnext
     HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
     HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
@@ -1332,7 +1343,9 @@ static int launch_scan(kw_handle *h)
                            dim3(TX_BLOCK), 0, side, h->FT, h->arena, h->doc_off, n_docs, h->FS);
     HIPCHK(h, hipEventRecord(h->evx, side));
     if (n_docs > 0)
-        hipLaunchKernelGGL(kw_probe_kernel, dim3((n_regions + PK_WAVES - 1) / PK_WAVES), dim3(PK_BLOCK), 0, st, h->FT,
+        // probe waves: at most the filter's wave count (each claims regions until none are left)
+        hipLaunchKernelGGL(kw_probe_kernel, dim3((std::min(n_regions, nsb * FS_WAVES) + PK_WAVES - 1) / PK_WAVES),
+                           dim3(PK_BLOCK), 0, st, h->FT,
                            h->T, h->arena, h->doc_off, n_regions, h->FS);
     HIPCHK(h, hipEventRecord(h->evp, st));
     HIPCHK(h, hipStreamWaitEvent(st, h->evx, 0));

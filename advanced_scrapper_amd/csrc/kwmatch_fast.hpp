@@ -201,7 +201,22 @@ struct FastScratch {
     uint4 *vrec;                // per document: {text start lo, hi | transcoded << 31, text / title code points}
     uint32_t *res_list;         // documents the epilogue left to the resolve kernel (DH_RESOLVE; defer_cap)
     uint32_t *res_cnt;
+    // dynamic work distribution: [0] the filter's next 32-document group, [1] the epilogue's (zeroed per scan);
+    // dyn = 0: grid-stride groups (KW_STATIC_GROUPS=1)
+    uint32_t *gnext;
+    int dyn;
+    int64_t chunk_groups;       // groups per filter work unit = candidate region (kwmatch_split.hpp)
 };
+
+// the next group a wave takes: grid-stride (g += n_waves) or, with S.dyn, the next one of a per-kernel counter
+// (groups of uneven cost then end together; a wave's groups still ascend)
+__device__ __forceinline__ int64_t fk_next_group(uint32_t *ctr, bool dyn, int64_t g, int64_t n_waves)
+{
+    if (!dyn) return g + n_waves;
+    uint32_t v = 0;
+    if (lane_id() == 0) v = atomicAdd(ctr, 1u);
+    return (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
 
 // host + device hashes of the LDS tables
 // stage 1: the 4-gram b0..b3 at a position as k0 = b0 | b1 << 8 | b2 << 16 and k1 = b1 | b2 << 8 | b3 << 16 (the

@@ -171,18 +171,17 @@ __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds 
 template <bool SHORT>
 __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds &L, const uint8_t *__restrict__ arena,
                                                  const int64_t *__restrict__ off, int64_t n_docs, const FastScratch &S,
-                                                 int64_t wave, int64_t n_waves, int wib, uint32_t &ncand, uint32_t &ncand2,
-                                                 uint32_t &ccur)
+                                                 int64_t region, int64_t g_lo, int64_t g_hi, int wib, uint32_t &ncand,
+                                                 uint32_t &ncand2, uint32_t &ccur)
 {
     const int lane = lane_id();
     const uint32_t *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
     uint32_t *spos = L.spos[wib];
-    uint32_t *cand = S.cand + (size_t)wave * S.cand_cap;
+    uint32_t *cand = S.cand + (size_t)region * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const uint32_t t3on = FT.has_t3 ? 1u : 0u;
-    const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
-    for (int64_t g = wave; g < n_groups; g += n_waves) {
+    for (int64_t g = g_lo; g < g_hi; ++g) {
         const int64_t d0 = g * FG_DOCS;
         const int nd = (int)(n_docs - d0 < FG_DOCS ? n_docs - d0 : FG_DOCS);
         const int64_t o0 = lane <= nd ? off[2 * (d0 + lane)] : 0;
@@ -355,16 +354,27 @@ __global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables
     const int wib = threadIdx.x / WAVE;
     const int64_t wave = (int64_t)blockIdx.x * FS_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * FS_WAVES;
-    uint32_t ncand = 0, ncand2 = 0, ccur = 0;
-    if (FT.has_short)
-        fk_filter_groups<true>(FT, L, arena, off, n_docs, S, wave, n_waves, wib, ncand, ncand2, ccur);
-    else
-        fk_filter_groups<false>(FT, L, arena, off, n_docs, S, wave, n_waves, wib, ncand, ncand2, ccur);
-    if (lane == 0) {
-        S.ccnt[wave] = ccur;
-        if (ccur > S.cand_cap) {
-            atomicOr(&S.status[0], ST_CAND_OVERFLOW);
-            atomicMax(&S.cmax[0], ccur);
+    uint32_t ncand = 0, ncand2 = 0;
+    // work units ("chunks", one candidate region each): S.chunk_groups consecutive 32-document groups; a wave
+    // claims the next chunk from a counter when it finishes one (S.dyn; else grid-stride), so the waves end
+    // together, and the probe's regions stay small and even
+    const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
+    const int64_t K = S.chunk_groups;
+    const int64_t n_chunks = (n_groups + K - 1) / K;
+    for (int64_t c = S.dyn ? fk_next_group(S.gnext, true, 0, 0) : wave; c < n_chunks;
+         c = fk_next_group(S.gnext, S.dyn, c, n_waves)) {
+        uint32_t ccur = 0;
+        const int64_t g_lo = c * K, g_hi = g_lo + K < n_groups ? g_lo + K : n_groups;
+        if (FT.has_short)
+            fk_filter_groups<true>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
+        else
+            fk_filter_groups<false>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
+        if (lane == 0) {
+            S.ccnt[c] = ccur;
+            if (ccur > S.cand_cap) {
+                atomicOr(&S.status[0], ST_CAND_OVERFLOW);
+                atomicMax(&S.cmax[0], ccur);
+            }
         }
     }
     unsigned long long c1 = ncand;
@@ -404,11 +414,14 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     __shared__ uint32_t scnt_all[PK_WAVES * WAVE];
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
-    const int64_t region = (int64_t)blockIdx.x * PK_WAVES + wib;
-    if (region >= n_regions) return;
     uint64_t *pool = pool_all + wib * PK_POOL;
     uint8_t *pown = pown_all + wib * PK_POOL;
     uint32_t *scnt = scnt_all + wib * WAVE;
+    uint32_t nanchor = 0;
+    // regions (the filter's work units, a few groups each) claimed from a counter: the waves end together
+    const int64_t n_waves = (int64_t)gridDim.x * PK_WAVES;
+    for (int64_t region = S.dyn ? fk_next_group(S.gnext + 1, true, 0, 0) : (int64_t)blockIdx.x * PK_WAVES + wib;
+         region < n_regions; region = fk_next_group(S.gnext + 1, S.dyn, region, n_waves)) {
     const uint32_t *cand = S.cand + (size_t)region * S.cand_cap;
     int32_t cur_group = -1;                 // group of the region's last header record so far (wave-uniform)
     const uint32_t nc = min(S.ccnt[region], S.cand_cap);
@@ -417,7 +430,6 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     const uint32_t ibase = (uint32_t)((size_t)region * S.item_cap);
     uint32_t icur = 0;                      // items of this region (wave-uniform)
     uint32_t last_doc = 0xFFFFFFFFu;        // document of the region's last item so far
-    uint32_t nanchor = 0;
     scnt[lane] = 0;
     for (uint32_t c0 = 0; c0 < nc; c0 += WAVE) {
         const bool inb = c0 + (uint32_t)lane < nc;
@@ -588,9 +600,11 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
         // the batch's items grouped by candidate (candidate order; any order within a candidate, the
         // epilogue sorts): lane L's items start at icur + (items of lanes < L)
         const uint32_t nmine = scnt[lane];
-        const bool ovf = pn > (uint32_t)PK_POOL;   // the pool dropped items: the batch's documents defer
         int itotal;
         const int iex = wave_excl_scan_dpp((int)nmine, &itotal);
+        // the pool dropped items, or the batch's items do not fit the region (the scan is redone with larger
+        // regions, ST_CAND_OVERFLOW): the batch's documents defer, so nothing reads items that were not written
+        const bool ovf = pn > (uint32_t)PK_POOL || icur + (uint32_t)itotal > icap;
         const uint64_t withm = __ballot(nmine > 0);
         if (withm) {
             const uint64_t below = (1ull << lane) - 1;
@@ -620,6 +634,8 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
     if (lane == 0 && icur > icap) {
         atomicOr(&S.status[0], ST_CAND_OVERFLOW);
         atomicMax(&S.cmax[1], icur);
+    }
+    wave_sync();
     }
     unsigned long long a = nanchor;
 #pragma unroll
