@@ -764,30 +764,24 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
         // lanes without a multi-byte character copy their bytes
         wave_sync();
         const uint32_t g0 = o0 + count, g1 = g0 + (uint32_t)total, sh = g0 & 15u;
-        uint32_t k = (uint32_t)ex + sh;
-        if (high == 0) {
+        const uint32_t k = (uint32_t)ex + sh;
+        // every lead byte's output at its rank among the lane's lead bytes: the ASCII ones unrolled (one
+        // predicated store each), then a loop over the lane's few multi-byte characters only (decode, marker)
+        const uint32_t hl = lead & high;
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if ((lead >> j) & 1u) stg[k++] = (uint8_t)(W[j >> 2] >> (8 * (j & 3)));
-        } else {
-            uint32_t lm = lead;
-            while (lm) {
-                const int j = __ffs(lm) - 1;
-                lm &= lm - 1;
-                const uint32_t b0 = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                uint32_t c = b0;
-                if (b0 >= 0x80u) {
-                    const uint32_t n = (b0 >= 0xF0u) ? 4u : (b0 >= 0xE0u) ? 3u : 2u;
-                    c = b0 & (0x7Fu >> n);
-                    for (uint32_t q = 1; q < n; ++q) {
-                        const int jj = j + (int)q;
-                        const uint32_t bk = (lp + jj < fe) ? ((W[jj >> 2] >> (8 * (jj & 3))) & 0xFFu) : 0x80u;
-                        c = (c << 6) | (bk & 0x3Fu);
-                    }
-                    c = tx_marker(txk, txv, c);
-                }
-                stg[k++] = (uint8_t)c;
+        for (int j = 0; j < 16; ++j)
+            if (((lead & ~hl) >> j) & 1u) stg[k + (uint32_t)__popc(lead & ((1u << j) - 1u))] = (uint8_t)(W[j >> 2] >> (8 * (j & 3)));
+        for (uint32_t lm = hl; lm; lm &= lm - 1) {
+            const int j = __ffs(lm) - 1;
+            const uint32_t b0 = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t n = (b0 >= 0xF0u) ? 4u : (b0 >= 0xE0u) ? 3u : 2u;
+            uint32_t c = b0 & (0x7Fu >> n);
+            for (uint32_t q = 1; q < n; ++q) {
+                const int jj = j + (int)q;
+                const uint32_t bk = (lp + jj < fe) ? ((W[jj >> 2] >> (8 * (jj & 3))) & 0xFFu) : 0x80u;
+                c = (c << 6) | (bk & 0x3Fu);
             }
+            stg[k + (uint32_t)__popc(lead & ((1u << j) - 1u))] = (uint8_t)tx_marker(txk, txv, c);
         }
         wave_sync();
         // out[g0, g1): 16-byte stores of aligned staged chunks (ds_read_b128) for the body, byte stores at the
