@@ -10,14 +10,19 @@
 //                        and hash it (one 64-bit word hash: tag and slot).
 //                        Rows whose only extra ':' is at most one ':80' take a
 //                        word-wide copy; the rest run the byte-serial rewrite.
-//   dd_insert_kernel     open-addressing table of 64-bit slots {tag, row}: the
-//                        first inserter claims a slot by CAS, rows with the same
-//                        tag keep the smallest row by atomicMin (keep='first').
-//   dd_decide_kernel     each row finds its slot; rep == row -> kept, else the
-//                        row is a duplicate iff its normalised bytes equal the
-//                        rep's (length, then every word).  Rows that share a
-//                        32-bit tag with a different URL are resolved exactly
-//                        on the host.
+//                        Waves claim groups of 64 rows in row order.  Each
+//                        kept row is inserted at once (table_insert):
+//                        open-addressing slots {tag, position}, the first
+//                        inserter claims a slot by CAS, an earlier row
+//                        displaces the holder by atomicMin (keep='first'); a
+//                        row that finds an earlier holder keeps its position
+//                        as its hint, a displaced holder gets a `moved` bit.
+//   dd_decide_kernel     a row with a hint is a duplicate iff its normalised
+//                        bytes equal the hinted row's (length, then every
+//                        word); a moved row or a differing one is compared
+//                        with its tag's first row from the table.  Rows that
+//                        share a tag with a different URL are resolved
+//                        exactly on the host.
 //   dd_count / dd_scan / dd_place / dd_copy
 //                        dense offsets, source rows and bytes of the kept rows.
 //
@@ -46,11 +51,15 @@ constexpr uint64_t DOTHTML = 0x6C6D74682Eull;      // ".html"
 constexpr uint8_t CODE_COLLIDE = 4;                // internal: tag shared with a different URL
 
 // sparse output arena: row i's normalised URL starts at obase(off[i], i) (8-aligned, room for
-// len + len/5 + 16 bytes: at most one extra 's' per 5 input bytes, ".html", word padding)
+// len + len/5 + 16 bytes: at most one extra 's' per 5 input bytes, ".html", word padding), after an 8-byte
+// header word holding its length (a duplicate's compare reads the rep's length with its first bytes)
 __host__ __device__ __forceinline__ int64_t obase(int64_t off_i, int64_t i)
 {
-    return (off_i + off_i / 5 + 24 * i + 7) & ~(int64_t)7;
+    return ((off_i + off_i / 5 + 32 * i + 7) & ~(int64_t)7) + 8;
 }
+constexpr uint64_t NO_HINT = ~0ull;
+constexpr int POS_BITS = 35;                        // a table slot: hash tag (29 bits) | sparse position / 8
+constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1;
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *__restrict__ a, int64_t p)
 {
@@ -92,12 +101,15 @@ __host__ __device__ __forceinline__ uint64_t fmix(uint64_t h)
 
 struct Scratch {
     uint8_t *out;            // sparse normalised URLs
-    uint64_t *h1;            // per row: the normalised URL's 64-bit hash (tag + slot; equality is decided on bytes)
     uint32_t *len3;          // per row: normalised length
     unsigned long long *table;
+    uint64_t *hint;          // per kept row: the sparse position of an earlier row with its tag, or NO_HINT
+    uint32_t *moved;         // bit per sparse 8-byte word: the row starting there lost its slot to an earlier row
     uint64_t mask;
     unsigned long long *cnt;   // [0..4] per code
+    unsigned long long *gnext;   // the transform's next group of 64 rows
     int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
+    int stats;               // KW_DEDUP_STATS: count the rows decide looks up in the table (cnt[5] moved, [6] other)
     int normalize;           // KW_DEDUP_NORMALIZE: apply :63-76; else keep-first over the raw strings
     uint2 *slow;             // rows (index, cut) for the byte-serial rewrite: slow_cap per transform wave
     uint32_t *wslow;         // per transform wave: its slow rows (no shared counter: one address for every
@@ -203,15 +215,54 @@ struct LdsSrc {
     }
 };
 
-// finish a row: hashes, length, code
+// Open-addressing table of 64-bit slots {tag, position}: the first inserter of a tag claims a slot by CAS, an
+// earlier row (smaller position: obase grows with the row) displaces the holder by atomicMin, so the slot ends
+// with the tag's first row (keep='first').  Every kept row writes its own hint: the position of the earlier
+// holder it found, or NO_HINT when it took the slot; a row that displaces the holder sets the holder's bit in
+// `moved` (each row leaves its slot at most once).  The plain load is only a hint of the slot (a slot's tag
+// never changes once claimed; its position only decreases).  Nothing another row wrote in this kernel is read
+// (no cross-XCD visibility is assumed): decide reads the hints, bits and bytes after the kernel boundary.
+__device__ __forceinline__ void table_insert(const Scratch &S, uint64_t h, int64_t i, int64_t pos)
+{
+    const unsigned long long key = ((h >> POS_BITS) << POS_BITS) | ((uint64_t)pos >> 3);
+    uint64_t slot = (h ^ (h >> 29)) & S.mask;
+    unsigned long long cur = S.table[slot];
+    uint64_t hint = NO_HINT;
+    for (;;) {
+        if (cur == 0ull) {
+            cur = atomicCAS(&S.table[slot], 0ull, key);
+            if (cur == 0ull) break;
+            continue;   // claimed meanwhile: look at the claimer
+        }
+        if ((cur >> POS_BITS) == (key >> POS_BITS)) {
+            if (cur > key) {
+                cur = atomicMin(&S.table[slot], key);
+                if (cur > key) {   // displaced the holder
+                    const uint64_t q = cur & POS_MASK;
+                    atomicOr(&S.moved[q >> 5], 1u << (uint32_t)(q & 31));
+                    break;
+                }
+            }
+            hint = (cur & POS_MASK) << 3;
+            break;
+        }
+        slot = (slot + 1) & S.mask;
+        cur = S.table[slot];
+    }
+    S.hint[i] = hint;
+}
+
+// finish a row: hashes, length (also in the header word before its bytes at out), code; a kept row goes into
+// the table
 __device__ __forceinline__ void finish_row(uint64_t h1, int64_t len3, bool bad, int64_t i,
-                                           uint8_t *__restrict__ code, const Scratch &S)
+                                           uint8_t *__restrict__ code, const Scratch &S, uint8_t *out)
 {
     h1 = fmix(h1 ^ (uint64_t)len3);
     if (S.weak) h1 &= 0xFull;
-    S.h1[i] = h1;
     S.len3[i] = (uint32_t)len3;
+    *(uint64_t *)(out - 8) = (uint64_t)len3;
     code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
+    if (!bad) table_insert(S, h1, i, out - S.out);
 }
 
 // the general rewrite of the cut prefix u[0, j), byte by byte (rows with ':80' or a second 'http:')
@@ -231,7 +282,7 @@ __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j
     R.flush(Em);
     Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
     Em.finish();
-    finish_row(Em.h1, Em.len, Em.bad, i, code, S);
+    finish_row(Em.h1, Em.len, Em.bad, i, code, S, Em.out);
 }
 
 // one row: returns -1 when done, or the cut j of a row that needs slow_row
@@ -248,11 +299,7 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
             *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
         }
-        h1 = fmix(h1 ^ (uint64_t)L);
-        if (S.weak) h1 &= 0xFull;
-        S.h1[i] = h1;
-        S.len3[i] = (uint32_t)L;
-        code[i] = KW_URL_KEPT;
+        finish_row(h1, L, false, i, code, S, out);
         return -1;
     }
     // ---- pass 1: the cut j, the first two extra ':' and the first 'news/%' | "news/'" end, one 4-byte word a
@@ -386,11 +433,12 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
     } else {
         return j;   // the byte-serial rewrite runs in dd_slow_kernel, off the divergent path
     }
-    finish_row(h1, len3, bad, i, code, S);
+    finish_row(h1, len3, bad, i, code, S, out);
     return -1;
 }
 
 constexpr int STAGE_BYTES = 8192;   // per-wave LDS copy of the wave's 64 rows
+constexpr int TCLAIM = 8;           // groups of 64 rows a transform wave claims at once
 
 // lane = row; the wave's 64 rows are staged into LDS with coalesced 16-byte loads when they fit
 __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__restrict__ arena,
@@ -403,10 +451,20 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
     uint4 *stage = stage_all + wib * (STAGE_BYTES / 16);
     const int64_t n_groups = (n + 63) / 64;
     const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + wib;
-    const int64_t n_waves = (int64_t)gridDim.x * (BLOCK / 64);
     uint32_t ns = 0;   // this wave's rows for the byte-serial rewrite (wave-uniform)
     uint2 *wsl = S.slow + (size_t)wave * S.slow_cap;
-    for (int64_t g = wave; g < n_groups; g += n_waves) {
+    // groups of 64 rows claimed from a counter in row order: rows enter the table in about row order, so few
+    // earlier duplicates displace a later row already there (grid-stride let waves drift apart: 16-26 % of the
+    // duplicates were displaced rows, which decide looks up in the table again)
+    // (TCLAIM groups per claim: one counter address for every group serialised the transform, 98 vs 68 ms)
+    auto claim = [&]() -> int64_t {
+        uint64_t g = 0;
+        if (lane == 0) g = atomicAdd(S.gnext, (unsigned long long)TCLAIM);
+        return (int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g) |
+               ((int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32);
+    };
+    int64_t g = claim(), gend = g + TCLAIM;
+    for (; g < n_groups; g = (g + 1 < gend) ? g + 1 : (gend = claim() + TCLAIM) - TCLAIM) {
         const int64_t i0 = g * 64, i1 = i0 + 64 < n ? i0 + 64 : n;
         const int64_t A0 = off[i0], A1 = off[i1];
         const int64_t base = A0 & ~(int64_t)15;
@@ -429,7 +487,9 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
         }
         // rows for the byte-serial rewrite -> the wave's slow list
         const uint64_t sm = __ballot(jslow >= 0);
-        if (sm) {
+        if (sm && ns + (uint32_t)__popcll(sm) > S.slow_cap) {   // (a wave that claimed more than its share)
+            if (jslow >= 0) slow_row(arena, b, jslow, i, code, S);
+        } else if (sm) {
             if (jslow >= 0) {
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
                 wsl[ns + r] = make_uint2((uint32_t)i, (uint32_t)jslow);
@@ -454,53 +514,47 @@ __global__ __launch_bounds__(BLOCK) void dd_slow_kernel(const uint8_t *__restric
     }
 }
 
-// the normalised bytes of rows a and b (same length len) in the sparse arena are equal: 8 word pairs in flight
-// per round (a loop that tests each word before loading the next waits one memory round trip per word)
-__device__ __forceinline__ bool same_url(const Scratch &S, const int64_t *__restrict__ off, int64_t a, int64_t b,
-                                         uint32_t len)
+// the normalised bytes of rows a and b are equal (their header words, i.e. lengths, first): 16 word pairs in
+// flight per round, so a URL of up to 120 bytes takes one memory round trip (8 per round: 33.2 ms decide)
+constexpr int SAME_U = 16;
+__device__ __forceinline__ bool same_url(const Scratch &S, int64_t oa, int64_t ob, uint32_t len)
 {
-    const int64_t oa = off[a], ob = off[b];
-    const uint64_t *x = (const uint64_t *)(S.out + obase(oa, a));
-    const uint64_t *y = (const uint64_t *)(S.out + obase(ob, b));
-    const uint32_t nw = (len + 7) / 8;
-    for (uint32_t w = 0; w < nw; w += 8) {
+    const uint64_t *x = (const uint64_t *)(S.out + oa) - 1;
+    const uint64_t *y = (const uint64_t *)(S.out + ob) - 1;
+    const uint32_t nw = (len + 7) / 8 + 1;
+    for (uint32_t w = 0; w < nw; w += SAME_U) {
         uint64_t d = 0;
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < SAME_U; ++q)
             if (w + q < nw) d |= x[w + q] ^ y[w + q];
         if (d) return false;
     }
     return true;
 }
 
-__device__ __forceinline__ uint64_t slot_key(uint64_t h1, int64_t row)
+// a row's hash again from its normalised words (as the transform made it), 8 loads in flight per round
+__device__ __forceinline__ uint64_t row_hash(const Scratch &S, int64_t o, uint32_t len)
 {
-    const uint32_t tag = (uint32_t)(h1 >> 32) | 1u;   // never 0 (0 = empty slot)
-    return ((uint64_t)tag << 32) | (uint64_t)(uint32_t)row;
-}
-
-__global__ __launch_bounds__(BLOCK) void dd_insert_kernel(const uint8_t *__restrict__ code, int64_t n, Scratch S)
-{
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
-        if (code[i] != KW_URL_KEPT) continue;
-        const uint64_t h = S.h1[i];
-        const unsigned long long key = slot_key(h, i);
-        uint64_t slot = (h ^ (h >> 29)) & S.mask;
-        for (;;) {
-            unsigned long long cur = S.table[slot];
-            if (cur == 0ull) {
-                cur = atomicCAS(&S.table[slot], 0ull, key);
-                if (cur == 0ull) break;
-            }
-            if ((cur >> 32) == (key >> 32)) {
-                if ((uint32_t)cur > (uint32_t)key) atomicMin(&S.table[slot], key);
-                break;
-            }
-            slot = (slot + 1) & S.mask;
-        }
+    const uint64_t *x = (const uint64_t *)(S.out + o);
+    uint64_t h = 0x243F6A8885A308D3ull;
+    const uint32_t nw = (len + 7) / 8;
+    for (uint32_t w = 0; w < nw; w += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = w + q < nw ? x[w + q] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (w + q < nw) h = mix1(h, v[q]);
     }
+    h = fmix(h ^ (uint64_t)len);
+    return S.weak ? h & 0xFull : h;
 }
 
+// A kept row with a hint is a duplicate iff its bytes equal the hinted (earlier) row's; a row without one is
+// kept unless it lost its slot (its `moved` bit).  A hinted row that differs, or a moved row, is compared with
+// its tag's first row from the table (a tag shared by different URLs: rare): equal -> duplicate, else
+// CODE_COLLIDE, which the host resolves exactly among those rows (every row of a URL other than the first
+// row's gets it, so their keep-first is complete)
 __global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__restrict__ code, Scratch S,
                                                           const int64_t *__restrict__ off)
 {
@@ -508,19 +562,24 @@ __global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
         uint8_t k = code[i];
         if (k == KW_URL_KEPT) {
-            const uint64_t h = S.h1[i];
-            const uint32_t tag = (uint32_t)(h >> 32) | 1u;
-            uint64_t slot = (h ^ (h >> 29)) & S.mask;
-            unsigned long long cur;
-            for (;;) {
-                cur = S.table[slot];
-                if ((uint32_t)(cur >> 32) == tag) break;
-                slot = (slot + 1) & S.mask;
-            }
-            const int64_t rep = (int64_t)(uint32_t)cur;
-            if (rep != i) {
+            const uint64_t hp = S.hint[i];
+            const int64_t oi = obase(off[i], i);
+            const uint64_t q = (uint64_t)oi >> 3;
+            if (hp != NO_HINT || ((S.moved[q >> 5] >> (uint32_t)(q & 31)) & 1u)) {
                 const uint32_t len = S.len3[i];
-                const bool eq = S.len3[rep] == len && same_url(S, off, i, rep, len);
+                bool eq = hp != NO_HINT && same_url(S, oi, (int64_t)hp, len);
+                if (!eq) {
+                    if (S.stats) atomicAdd(&S.cnt[hp == NO_HINT ? 5 : 6], 1ull);
+                    const uint64_t h = row_hash(S, oi, len);
+                    uint64_t slot = (h ^ (h >> 29)) & S.mask;
+                    unsigned long long cur;
+                    for (;;) {
+                        cur = S.table[slot];
+                        if ((cur >> POS_BITS) == (h >> POS_BITS)) break;
+                        slot = (slot + 1) & S.mask;
+                    }
+                    eq = same_url(S, oi, (int64_t)((cur & POS_MASK) << 3), len);
+                }
                 k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
                 code[i] = k;
             }
@@ -942,8 +1001,10 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     const int64_t n_tw = (int64_t)tgrid * (BLOCK / 64);
     h->S.slow_cap = (uint32_t)(((n + 63) / 64 + n_tw - 1) / n_tw * 64);
     const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
+    if (out_bytes >> (POS_BITS + 3)) { h->err = "kw_dedup_run: URL bytes beyond the table's 35-bit positions"; return KW_EUNSUPPORTED; }
     const size_t need = out_bytes + align256(8 * (size_t)n) + align256(8 * (size_t)n_tw * h->S.slow_cap) +
                         align256(4 * (size_t)n_tw) + align256(4 * (size_t)n) + align256(8 * tsize) +
+                        align256(out_bytes / 64 + 4) +
                         align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
                         2 * align256(8 * ((size_t)n + 1));
     if (need > h->buf_bytes) {
@@ -957,14 +1018,17 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     auto carve = [&](size_t bytes) { uint8_t *r = p; p += align256(bytes); return r; };
     Scratch &S = h->S;
     S.out = carve(out_bytes);
-    S.h1 = (uint64_t *)carve(8 * (size_t)n);
     S.len3 = (uint32_t *)carve(4 * (size_t)n);
     S.table = (unsigned long long *)carve(8 * tsize);
+    S.hint = (uint64_t *)carve(8 * (size_t)n);
+    S.moved = (uint32_t *)carve(out_bytes / 64 + 4);
     S.mask = tsize - 1;
     S.cnt = (unsigned long long *)carve(8 * 8);
+    S.gnext = S.cnt + 7;
     S.slow = (uint2 *)carve(8 * ((size_t)n_tw * S.slow_cap));
     S.wslow = (uint32_t *)carve(4 * (size_t)n_tw);
     S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
+    S.stats = getenv("KW_DEDUP_STATS") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
     h->tile_cnt = (unsigned long long *)carve(8 * (size_t)ntiles);
     h->tile_bytes = (unsigned long long *)carve(8 * (size_t)ntiles);
@@ -974,19 +1038,19 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
     const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
     DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
+    DDCHK(h, hipMemsetAsync(S.moved, 0, out_bytes / 64 + 4, st));
     DDCHK(h, hipEventRecord(h->ev[0], st));
     hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
-    hipLaunchKernelGGL(dd_slow_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
-    DDCHK(h, hipGetLastError());
     DDCHK(h, hipEventRecord(h->ev[1], st));
-    hipLaunchKernelGGL(dd_insert_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, S);
+    hipLaunchKernelGGL(dd_slow_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
     DDCHK(h, hipGetLastError());
     DDCHK(h, hipEventRecord(h->ev[2], st));
     hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, n, d_code, S, d_off);
     DDCHK(h, hipGetLastError());
-    unsigned long long cnt[5];
+    unsigned long long cnt[7];
     DDCHK(h, hipMemcpyAsync(cnt, S.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
+    if (S.stats) fprintf(stderr, "kw_dedup: table lookups in decide: %llu moved, %llu hint mismatches\n", cnt[5], cnt[6]);
     for (int k = 0; k < 4; ++k) h->counts[k] = (int64_t)cnt[k];
     if (cnt[CODE_COLLIDE]) {
         int rc = resolve_collisions(h, d_off, n, d_code, st);

@@ -59,8 +59,8 @@ int kw_dedup_kept_size(kw_dedup *h, int64_t *n_kept, int64_t *n_bytes);
  * d_bytes (n_bytes), d_off (n_kept + 1 offsets into d_bytes), d_rows (n_kept source row indices). */
 int kw_dedup_kept_copy(kw_dedup *h, uint8_t *d_bytes, int64_t *d_off, int64_t *d_rows, void *stream);
 
-/* Device times (ms) of the last run: [0] transform + hash, [1] table insert,
- * [2] decide (rep compare), [3] kept compaction, [4] total; k <= 5 values. */
+/* Device times (ms) of the last run: [0] transform + hash + table insert, [1] the byte-serial rows
+ * (rewrite + insert), [2] decide (rep compare), [3] kept compaction, [4] total; k <= 5 values. */
 int kw_dedup_last_ms(kw_dedup *h, float *ms, int32_t k);
 
 const char *kw_dedup_last_error(kw_dedup *h);

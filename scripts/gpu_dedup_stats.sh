@@ -1,0 +1,7 @@
+#!/bin/bash
+# config 5 with KW_DEDUP_STATS (decide's table lookups), then the bench line, then tests
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+KW_DEDUP_STATS=1 timeout -k 10 400 python bench.py --workload dedup --steps 2 --warmup 0 --cpu-sample 0 > gpurun_out/dedup_stats.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py --workload dedup --steps 5 --warmup 1 --cpu-sample 0 > gpurun_out/dedup_a.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dedup.py -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_dedup_tests.log 2>&1
