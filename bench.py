@@ -467,7 +467,7 @@ def cpu_baseline_dedup(rows, n_sample: int):
 
 
 TRAFFIC_KW = os.path.join(REPO, 'profiles', 'traffic_r04.json')
-TRAFFIC_DEDUP = os.path.join(REPO, 'profiles', 'traffic_dedup_r03.json')
+TRAFFIC_DEDUP = os.path.join(REPO, 'profiles', 'traffic_dedup_r04.json')
 TRAFFIC_C4 = os.path.join(REPO, 'profiles', 'traffic_c4_r04.json')
 
 
