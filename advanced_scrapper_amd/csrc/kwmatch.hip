@@ -1378,7 +1378,7 @@ static int launch_scan(kw_handle *h)
     if (n_docs > 0) {
         // flat resolve tasks: verify -> short -> regex (regex decisions of the first two queue up);
         // G[k] waves share each epilogue wave's task region
-        int G[4] = {1, 4, 2, 4};   // measured on MI355X (config 2, 4 runs each): 5.88 vs 5.92 ms for {2, 4, 2, 4}, 5.97 for {4, 4, 8, 4}
+        int G[4] = {1, 4, 4, 4};   // measured on MI355X (config 2, 2 runs each): 4.98 vs 5.00-5.01 ms for {1, 4, 2, 4} and {1, 4, 8, 4}, 5.00 {2, 4, 4, 4}, 5.17 {1, 4, 6, 6}, 5.34 {1, 4, 4, 8}
         if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
         auto task = [&](auto kern, int g, hipStream_t s) {
             g = std::max(1, std::min(g, 16));

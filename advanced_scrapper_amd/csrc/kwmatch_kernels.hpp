@@ -973,8 +973,16 @@ __global__ void kw_offsets_kernel(const uint32_t *__restrict__ cnt, int n_waves,
     __shared__ unsigned long long part[2][1024];
     const int t = threadIdx.x;
     const int per = (n_waves + 1023) / 1024;
+    const int i0 = t * per, i1 = min((t + 1) * per, n_waves);
     unsigned long long s = 0;
-    for (int i = t * per; i < (t + 1) * per && i < n_waves; ++i) s += (cnt[i] < cap ? cnt[i] : cap);
+    // a thread's segment 8 loads at a time, in flight together (one load per iteration waited a round trip each)
+    for (int i = i0; i < i1; i += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = i + k < i1 ? cnt[i + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[k] < cap ? v[k] : cap;
+    }
     // inclusive block scan (Hillis-Steele over the 1024 partial sums, double-buffered)
     int b = 0;
     part[0][t] = s;
@@ -990,9 +998,16 @@ __global__ void kw_offsets_kernel(const uint32_t *__restrict__ cnt, int n_waves,
         offs[n_waves] = part[b][t];
         *total = part[b][t];
     }
-    for (int i = t * per; i < (t + 1) * per && i < n_waves; ++i) {
-        offs[i] = acc;
-        acc += (cnt[i] < cap ? cnt[i] : cap);
+    for (int i = i0; i < i1; i += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = i + k < i1 ? cnt[i + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i + k < i1) {
+                offs[i + k] = acc;
+                acc += v[k] < cap ? v[k] : cap;
+            }
     }
 }
 
