@@ -997,7 +997,9 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     while (tsize < 2 * (uint64_t)n) tsize <<= 1;
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     // the transform's grid: its waves' slow lists are sized from the groups of 64 rows each wave takes
-    const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 8);
+    int tbpc = 8;   // transform blocks per CU (KW_DEDUP_TBLOCKS_PER_CU; 4, 5, 8, 16: 130.7-130.8 ms alike)
+    if (const char *e = getenv("KW_DEDUP_TBLOCKS_PER_CU")) tbpc = std::max(1, atoi(e));
+    const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * tbpc);
     const int64_t n_tw = (int64_t)tgrid * (BLOCK / 64);
     h->S.slow_cap = (uint32_t)(((n + 63) / 64 + n_tw - 1) / n_tw * 64);
     const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
