@@ -1502,6 +1502,17 @@ static int finish(kw_handle *h)
         // transcoded-view bytes (384), record count (400)
         unsigned long long small[51];
         HIPCHK(h, hipMemcpy(small, h->S.status, sizeof(small), hipMemcpyDeviceToHost));
+        if (getenv("KW_DEBUG_TASKS") && h->nk > 0) {   // (developer aid) the task regions' queue lengths
+            std::vector<uint32_t> tc((size_t)4 * h->nk);
+            HIPCHK(h, hipMemcpy(tc.data(), h->FS.vcnt, tc.size() * 4, hipMemcpyDeviceToHost));
+            for (int q = 0; q < 4; ++q) {
+                uint64_t sum = 0;
+                uint32_t mx = 0;
+                for (int t = 0; t < h->nk; ++t) { sum += tc[(size_t)q * h->nk + t]; mx = std::max(mx, tc[(size_t)q * h->nk + t]); }
+                fprintf(stderr, "kw tasks %c: %d regions, total %llu, mean %.1f, max %u\n", "vesx"[q], h->nk,
+                        (unsigned long long)sum, (double)sum / h->nk, mx);
+            }
+        }
         uint32_t status[4];
         memcpy(status, small, sizeof(status));
         if (h->n_docs == 0) { h->n_hits = 0; h->fetched = true; return KW_OK; }

@@ -33,7 +33,7 @@
 #define SK_MINW 1
 #endif
 #ifndef RX_MINW
-#define RX_MINW 1
+#define RX_MINW 4   // <= 128 VGPRs (the prefetched task records stay in LDS)
 #endif
 #ifndef SHORT_COUNT
 #define SHORT_COUNT 0
@@ -473,20 +473,39 @@ uint32_t fk_edge_items(const FastTables &FT, const FieldCtx &F, uint64_t *items,
 // number of positions emitted.
 constexpr int RX_TXT = 2048 + 64 + 16 + 16;   // 2048 starts + L - 1 <= 63 tail bytes + alignment slack
 
+// TAB256 (tab holds 256 entries): a transcoded field's marker bytes get their masks in tab[128, 256) first, so
+// its bytes take the unrolled loop like an ASCII field's (one LDS lookup per byte, no per-byte branch)
+template <bool TAB256 = false>
 __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O,
                                           uint32_t P, uint32_t r, uint64_t *tab, uint8_t *txt)
 {
     const int lane = lane_id();
     const uint32_t L = FT.rxf_len[r];
     const uint64_t anym = FT.rxf_any[r];
+    const uint32_t eb = FT.rxf_ext_off[r], ee = FT.rxf_ext_off[r + 1];
     wave_sync();
     tab[lane] = FT.rxf_pm[(size_t)r * 128 + lane];
     tab[lane + 64] = FT.rxf_pm[(size_t)r * 128 + 64 + lane];
+    const bool fast_tx = TAB256 && F.ascii && F.tx;
+    if (fast_tx) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t b = 128u + (uint32_t)lane + 64u * (uint32_t)h;
+            const uint32_t c = FT.tx_inv[b & 0x7Fu];
+            uint64_t B = anym;
+            for (uint32_t e = eb; e < ee; ++e)
+                if (FT.rxf_ext_cp[e] == c) B |= FT.rxf_ext_mask[e];
+            tab[b] = B;
+        }
+    }
+    wave_sync();
     const int64_t n = F.n;
     if (n < (int64_t)L) return 0;
+#if defined(RX_TIMING_SKIP) && RX_TIMING_SKIP == 4
+    return 0;
+#endif
     const int64_t nstarts = n - L + 1;
     const uint64_t fin = 1ull << (L - 1);
-    const uint32_t eb = FT.rxf_ext_off[r], ee = FT.rxf_ext_off[r + 1];
     uint32_t last_end = 0, emitted = 0;
     for (int64_t r0 = 0; r0 < nstarts; r0 += 64 * 32) {
         int64_t tb = 0;   // txt[k] = field byte tb + k
@@ -524,7 +543,11 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
         }
         const int64_t s_lo = r0 + (int64_t)lane * 32;
         uint32_t mask = 0;
+#if defined(RX_TIMING_SKIP) && RX_TIMING_SKIP == 3
+        if (false) {
+#else
         if (s_lo < nstarts) {
+#endif
             const int64_t s_hi = s_lo + 32 < nstarts ? s_lo + 32 : nstarts;
             const int c_cnt = (int)(s_hi + L - 1 - s_lo);
             uint64_t D = 0;
@@ -533,6 +556,12 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
 #pragma unroll 8
                 for (int k = 0; k < c_cnt; ++k) {
                     D = ((D << 1) | 1ull) & tab[t[k] & 0x7Fu];
+                    if (D & fin) mask |= 1u << (uint32_t)(k - (int)(L - 1));
+                }
+            } else if (fast_tx) {
+#pragma unroll 8
+                for (int k = 0; k < c_cnt; ++k) {
+                    D = ((D << 1) | 1ull) & tab[t[k]];
                     if (D & fin) mask |= 1u << (uint32_t)(k - (int)(L - 1));
                 }
             } else {
@@ -1271,7 +1300,7 @@ __device__ __forceinline__ void fk_field_ctx(FieldCtx &F, const uint8_t *arena, 
     F.field = field;
 }
 
-// a decided regex-class name: re.finditer over the field, or `name: []`
+// a decided regex-class name: re.finditer over the field, or `name: []` (rxtab: 256 entries)
 __device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTables &T, const DevScratch &GS,
                                              const FieldCtx &F, OutCtx &O, uint32_t P, uint64_t *rxtab, uint8_t *txt,
                                              unsigned long long &nrx, unsigned long long &nrx_bt,
@@ -1281,7 +1310,7 @@ __device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTabl
     ++nrx;
     nrx_bt += r < 0;
     nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, txt)
+    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, rxtab, txt)
                                 : rx_positions(T, GS, F, O, P);
     if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
 }
@@ -1873,12 +1902,11 @@ __global__ __launch_bounds__(RK_BLOCK, SK_MINW) void kw_short_kernel(FastTables 
 // re.finditer positions of a decided regex name P with an RXM use (program length L) in an ASCII field: the
 // leftmost non-overlapping of the field's RXM items of P (the probe's exact matches of the program).  Returns
 // false, having emitted nothing, when P has more than 64 of them (the field search takes it).
+// (b, n: the field's items in S.items)
 __device__ bool fk_rx_items(const FastScratch &S, const DevScratch &GS, const FieldCtx &F, OutCtx &O, uint32_t P,
-                            uint32_t L)
+                            uint32_t L, uint32_t b, uint32_t n)
 {
     const int lane = lane_id();
-    const uint2 h = S.hdr[F.doc], nc = S.ncnt[F.doc];
-    const uint32_t b = h.x + (F.field ? nc.x : 0u), n = F.field ? nc.y : nc.x;
     uint64_t key = ~0ull;   // (position, lane slot) of this lane's match
     uint32_t k = 0;
     for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
@@ -1918,28 +1946,72 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
                                                               const int64_t *__restrict__ off, int n_regions, int G,
                                                               FastScratch S, DevScratch GS)
 {
-    __shared__ uint64_t rxtab_all[RK_WAVES * 128];
+    __shared__ uint64_t rxtab_all[RK_WAVES * 256];
     __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
+    __shared__ uint4 rxpre_all[RK_WAVES * WAVE * 3];   // per wave: the next 64 tasks' records, fetched lane-parallel
+    const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
     const int64_t t = gw / G;
     const uint32_t sub = (uint32_t)(gw % G);
     if (t >= n_regions) return;
-    uint64_t *rxtab = rxtab_all + wib * 128;
+    uint64_t *rxtab = rxtab_all + wib * 256;
     uint8_t *txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
+    uint4 *pre = rxpre_all + wib * WAVE * 3;
     OutCtx O = tout_region(S, t);
     unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
     FieldCtx F;
     const uint32_t nx = min(S.xcnt[t], S.xcap);
     const uint4 *xq = S.xq + (size_t)t * S.xcap;
-    for (uint32_t k = sub; k < nx; k += (uint32_t)G) {
-        const uint4 tk = xq[k];
-        const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.y);
-        fk_field_ctx(F, arena, S, (uint32_t)__builtin_amdgcn_readfirstlane((int)tk.x), y & 1u);
-        const uint32_t P = y >> 1, L = FT.pat_rxl[P];
-        // a name with an RXM use in an ASCII field: the probe's RXM items are its matches, no search
-        if (L && !(S.dflags[F.doc] & (F.field ? DH_NA1 : DH_NA0)) && fk_rx_items(S, GS, F, O, P, L)) continue;
-        fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+    for (uint32_t k0 = sub; k0 < nx; k0 += (uint32_t)G * WAVE) {
+        // lane j fetches task k0 + j G and its document's view record, flags and item range (one dependent
+        // round for all 64 instead of two per task)
+        {
+            const uint32_t k = k0 + (uint32_t)lane * (uint32_t)G;
+            const bool has = k < nx;
+            const uint4 tk = has ? xq[k] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t doc = tk.x, P = tk.y >> 1, f = tk.y & 1u;
+            const uint4 v = has ? S.vrec[doc] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t L = has ? FT.pat_rxl[P] : 0u;
+            const uint32_t na = has ? (S.dflags[doc] & (f ? DH_NA1 : DH_NA0)) : 0u;
+            const uint2 h = has ? S.hdr[doc] : make_uint2(0u, 0u), nc = has ? S.ncnt[doc] : make_uint2(0u, 0u);
+            wave_sync();
+            pre[3 * lane] = v;
+            pre[3 * lane + 1] = make_uint4(doc, tk.y, na ? 0u : L, h.x + (f ? nc.x : 0u));
+            pre[3 * lane + 2] = make_uint4(f ? nc.y : nc.x, 0u, 0u, 0u);
+            wave_sync();
+        }
+        const uint32_t nj = min((uint32_t)WAVE, (nx - k0 + (uint32_t)G - 1) / (uint32_t)G);
+        for (uint32_t j = 0; j < nj; ++j) {
+            const uint4 vv = pre[3 * j], q = pre[3 * j + 1];
+            const uint4 v = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)vv.x),
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)vv.y),
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)vv.z),
+                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)vv.w));
+            const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.y);
+            const uint32_t f = y & 1u, P = y >> 1;
+            const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.z);
+            F.tx = (v.y >> 31) != 0;
+            F.arena = F.tx ? S.tarena : arena;
+            F.fb = (int64_t)(((uint64_t)(v.y & 0x7FFFFFFFu) << 32) | v.x) + (f ? (int64_t)v.z : 0);
+            F.n = f ? v.w : v.z;
+            F.fe = F.fb + F.n;
+            F.ascii = true;
+            F.cps = nullptr;
+            F.blkcnt = nullptr;
+            F.doc = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.x);
+            F.field = f;
+            // a name with an RXM use in an ASCII field: the probe's RXM items are its matches, no search
+            if (L && fk_rx_items(S, GS, F, O, P, L, (uint32_t)__builtin_amdgcn_readfirstlane((int)q.w),
+                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)pre[3 * j + 2].x)))
+                continue;
+#if defined(RX_TIMING_SKIP) && RX_TIMING_SKIP <= 2   // (timing variants only: 1 skips the backtracking
+                                                      // searches, 2 every search, 3 the shift-and loops, 4 all
+                                                      // but the mask table load)
+            if (RX_TIMING_SKIP == 2 || FT.rxf_idx[P] < 0) continue;
+#endif
+            fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+        }
     }
     task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
 }
