@@ -504,6 +504,25 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
 #if defined(RX_TIMING_SKIP) && RX_TIMING_SKIP == 4
     return 0;
 #endif
+    // the program's literal head: each of its first min(4, L) positions whose matching bytes are exactly one
+    // ASCII byte c (hv byte i = c, hm byte i = 0xFF).  With two or more such bytes a lane tests its 32 starts'
+    // 4-byte windows against the head (SWAR, no per-byte lookup chain) and confirms only the candidates
+    // position by position against the masks
+    uint32_t hv = 0, hm = 0;
+    if (F.ascii && (!F.tx || fast_tx)) {
+        const uint64_t m0 = tab[lane], m1 = tab[lane + 64];
+        const uint64_t mx = fast_tx ? (tab[128 + lane] | tab[192 + lane]) : 0ull;
+        for (uint32_t i = 0; i < 4u && i < L; ++i) {
+            const uint64_t b0 = __ballot((m0 >> i) & 1ull), b1 = __ballot((m1 >> i) & 1ull);
+            const uint64_t bx = __ballot((mx >> i) & 1ull);
+            if (!bx && __popcll(b0) + __popcll(b1) == 1) {
+                const uint32_t c = b0 ? (uint32_t)__builtin_ctzll(b0) : 64u + (uint32_t)__builtin_ctzll(b1);
+                hv |= c << (8 * i);
+                hm |= 0xFFu << (8 * i);
+            }
+        }
+    }
+    const bool use_head = __popc(hm) >= 16;
     const int64_t nstarts = n - L + 1;
     const uint64_t fin = 1ull << (L - 1);
     uint32_t last_end = 0, emitted = 0;
@@ -552,7 +571,33 @@ __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch
             const int c_cnt = (int)(s_hi + L - 1 - s_lo);
             uint64_t D = 0;
             const uint8_t *t = txt + (s_lo - tb);
-            if (F.ascii && !F.tx) {
+            if (use_head) {
+                const uint32_t o = (uint32_t)(s_lo - tb), sh = o & 3u;
+                const uint32_t *tw = (const uint32_t *)txt + (o >> 2);
+                uint32_t wd[10];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) wd[q] = tw[q];
+                // windows at every byte b < 36 of the lane's dwords (constant shifts), then the lane's starts
+                uint64_t cmb = 0;
+#pragma unroll
+                for (int q = 0; q < 9; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t win = r ? __builtin_amdgcn_alignbyte(wd[q + 1], wd[q], r) : wd[q];
+                        cmb |= (uint64_t)(((win ^ hv) & hm) == 0u ? 1u : 0u) << (4 * q + r);
+                    }
+                uint32_t cm = (uint32_t)(cmb >> sh);
+                const int ns = (int)(s_hi - s_lo);
+                if (ns < 32) cm &= (1u << ns) - 1u;
+                const uint32_t bm = fast_tx ? 0xFFu : 0x7Fu;
+                while (cm) {
+                    const int j = __builtin_ctz(cm);
+                    cm &= cm - 1u;
+                    bool ok = true;
+                    for (uint32_t i = 0; i < L && ok; ++i) ok = ((tab[t[j + (int)i] & bm] >> i) & 1ull) != 0;
+                    if (ok) mask |= 1u << j;
+                }
+            } else if (F.ascii && !F.tx) {
 #pragma unroll 8
                 for (int k = 0; k < c_cnt; ++k) {
                     D = ((D << 1) | 1ull) & tab[t[k] & 0x7Fu];
