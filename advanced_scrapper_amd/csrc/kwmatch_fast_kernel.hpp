@@ -475,14 +475,28 @@ constexpr int RX_TXT = 2048 + 64 + 16 + 16;   // 2048 starts + L - 1 <= 63 tail 
 
 // TAB256 (tab holds 256 entries): a transcoded field's marker bytes get their masks in tab[128, 256) first, so
 // its bytes take the unrolled loop like an ASCII field's (one LDS lookup per byte, no per-byte branch)
+struct RxfParams {   // a fixed program's length, any-code-point mask and extended code point range
+    uint32_t L, eb, ee;
+    uint64_t anym;
+};
+__device__ __forceinline__ RxfParams rxf_params(const FastTables &FT, uint32_t r)
+{
+    RxfParams p;
+    p.L = FT.rxf_len[r];
+    p.anym = FT.rxf_any[r];
+    p.eb = FT.rxf_ext_off[r];
+    p.ee = FT.rxf_ext_off[r + 1];
+    return p;
+}
+
 template <bool TAB256 = false>
 __device__ uint32_t fk_rx_fixed_positions(const FastTables &FT, const DevScratch &GS, const FieldCtx &F, OutCtx &O,
-                                          uint32_t P, uint32_t r, uint64_t *tab, uint8_t *txt)
+                                          uint32_t P, uint32_t r, const RxfParams &prm, uint64_t *tab, uint8_t *txt)
 {
     const int lane = lane_id();
-    const uint32_t L = FT.rxf_len[r];
-    const uint64_t anym = FT.rxf_any[r];
-    const uint32_t eb = FT.rxf_ext_off[r], ee = FT.rxf_ext_off[r + 1];
+    const uint32_t L = prm.L;
+    const uint64_t anym = prm.anym;
+    const uint32_t eb = prm.eb, ee = prm.ee;
     wave_sync();
     tab[lane] = FT.rxf_pm[(size_t)r * 128 + lane];
     tab[lane + 64] = FT.rxf_pm[(size_t)r * 128 + 64 + lane];
@@ -1355,7 +1369,22 @@ __device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTabl
     ++nrx;
     nrx_bt += r < 0;
     nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, rxtab, txt)
+    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, rxf_params(FT, (uint32_t)r),
+                                                              rxtab, txt)
+                                : rx_positions(T, GS, F, O, P);
+    if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
+}
+
+// fk_regex_now with the program's index and parameters already fetched (the regex task kernel's prefetch)
+__device__ __forceinline__ void fk_regex_pre(const FastTables &FT, const DevTables &T, const DevScratch &GS,
+                                             const FieldCtx &F, OutCtx &O, uint32_t P, int32_t r, const RxfParams &prm,
+                                             uint64_t *rxtab, uint8_t *txt, unsigned long long &nrx,
+                                             unsigned long long &nrx_bt, unsigned long long &nrx_rounds)
+{
+    ++nrx;
+    nrx_bt += r < 0;
+    nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
+    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, prm, rxtab, txt)
                                 : rx_positions(T, GS, F, O, P);
     if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
 }
@@ -1993,7 +2022,7 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
 {
     __shared__ uint64_t rxtab_all[RK_WAVES * 256];
     __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
-    __shared__ uint4 rxpre_all[RK_WAVES * WAVE * 3];   // per wave: the next 64 tasks' records, fetched lane-parallel
+    __shared__ uint4 rxpre_all[RK_WAVES * WAVE * 5];   // per wave: the next 64 tasks' records, fetched lane-parallel
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
@@ -2002,7 +2031,7 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
     if (t >= n_regions) return;
     uint64_t *rxtab = rxtab_all + wib * 256;
     uint8_t *txt = (uint8_t *)(rxtxt_all + wib * (RX_TXT / 16));
-    uint4 *pre = rxpre_all + wib * WAVE * 3;
+    uint4 *pre = rxpre_all + wib * WAVE * 5;
     OutCtx O = tout_region(S, t);
     unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
     FieldCtx F;
@@ -2020,15 +2049,19 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
             const uint32_t L = has ? FT.pat_rxl[P] : 0u;
             const uint32_t na = has ? (S.dflags[doc] & (f ? DH_NA1 : DH_NA0)) : 0u;
             const uint2 h = has ? S.hdr[doc] : make_uint2(0u, 0u), nc = has ? S.ncnt[doc] : make_uint2(0u, 0u);
+            const int32_t rr = has ? FT.rxf_idx[P] : -1;   // the field search's program, when it comes to that
+            RxfParams prm = {0u, 0u, 0u, 0ull};
+            if (rr >= 0) prm = rxf_params(FT, (uint32_t)rr);
             wave_sync();
-            pre[3 * lane] = v;
-            pre[3 * lane + 1] = make_uint4(doc, tk.y, na ? 0u : L, h.x + (f ? nc.x : 0u));
-            pre[3 * lane + 2] = make_uint4(f ? nc.y : nc.x, 0u, 0u, 0u);
+            pre[5 * lane] = v;
+            pre[5 * lane + 1] = make_uint4(doc, tk.y, na ? 0u : L, h.x + (f ? nc.x : 0u));
+            pre[5 * lane + 2] = make_uint4(f ? nc.y : nc.x, (uint32_t)rr, prm.L, 0u);
+            pre[5 * lane + 3] = make_uint4(prm.eb, prm.ee, (uint32_t)prm.anym, (uint32_t)(prm.anym >> 32));
             wave_sync();
         }
         const uint32_t nj = min((uint32_t)WAVE, (nx - k0 + (uint32_t)G - 1) / (uint32_t)G);
         for (uint32_t j = 0; j < nj; ++j) {
-            const uint4 vv = pre[3 * j], q = pre[3 * j + 1];
+            const uint4 vv = pre[5 * j], q = pre[5 * j + 1];
             const uint4 v = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)vv.x),
                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)vv.y),
                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)vv.z),
@@ -2048,14 +2081,22 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
             F.field = f;
             // a name with an RXM use in an ASCII field: the probe's RXM items are its matches, no search
             if (L && fk_rx_items(S, GS, F, O, P, L, (uint32_t)__builtin_amdgcn_readfirstlane((int)q.w),
-                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)pre[3 * j + 2].x)))
+                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)pre[5 * j + 2].x)))
                 continue;
 #if defined(RX_TIMING_SKIP) && RX_TIMING_SKIP <= 2   // (timing variants only: 1 skips the backtracking
                                                       // searches, 2 every search, 3 the shift-and loops, 4 all
                                                       // but the mask table load)
             if (RX_TIMING_SKIP == 2 || FT.rxf_idx[P] < 0) continue;
 #endif
-            fk_regex_now(FT, T, GS, F, O, P, rxtab, txt, nrx, nrx_bt, nrx_rounds);
+            const uint4 q2 = pre[5 * j + 2], q3 = pre[5 * j + 3];
+            RxfParams prm;
+            prm.L = (uint32_t)__builtin_amdgcn_readfirstlane((int)q2.z);
+            prm.eb = (uint32_t)__builtin_amdgcn_readfirstlane((int)q3.x);
+            prm.ee = (uint32_t)__builtin_amdgcn_readfirstlane((int)q3.y);
+            prm.anym = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q3.z) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)q3.w) << 32);
+            fk_regex_pre(FT, T, GS, F, O, P, (int32_t)__builtin_amdgcn_readfirstlane((int)q2.y), prm, rxtab, txt, nrx,
+                         nrx_bt, nrx_rounds);
         }
     }
     task_stats(S, 0, 0, 0, nrx, nrx_bt, nrx_rounds);
@@ -2182,7 +2223,7 @@ __device__ __forceinline__ void rk_wave_tail(const FastTables &FT, const DevTabl
         ++C.nrx;
         C.nrx_bt += r < 0;
         C.nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-        const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxtab, RQ.txt)
+        const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions(FT, GS, F, O, P, (uint32_t)r, rxf_params(FT, (uint32_t)r), rxtab, RQ.txt)
                                     : rx_positions(T, GS, F, O, P);
         if (cnt == 0) emit_hits(O, GS, lane == 0, d, P, KW_NOPOS, F.field);
     }
