@@ -1384,8 +1384,12 @@ __device__ __forceinline__ void fk_regex_pre(const FastTables &FT, const DevTabl
     ++nrx;
     nrx_bt += r < 0;
     nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
+#if defined(RX_TIMING_SKIP) && RX_TIMING_SKIP == 5   // (timing variant: no backtracking engine in the kernel)
+    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, prm, rxtab, txt) : 1u;
+#else
     const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, prm, rxtab, txt)
                                 : rx_positions(T, GS, F, O, P);
+#endif
     if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
 }
 
