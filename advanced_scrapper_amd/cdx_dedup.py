@@ -113,6 +113,8 @@ class GpuUrlDedup:
         return hr, urls
 
     def last_ms(self) -> List[float]:
+        """Device times (ms) of the last run: transform + hash + table insert, the byte-serial rows, decide,
+        kept compaction, total (include/kwdedup.h kw_dedup_last_ms)."""
         v = np.zeros(5, dtype=np.float32)
         self._check(_native.lib().kw_dedup_last_ms(self.h, _native.ptr(v), 5))
         return [float(x) for x in v]
