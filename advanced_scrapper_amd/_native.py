@@ -41,8 +41,9 @@ HIT_DTYPE = np.dtype([('doc', '<u4'), ('pattern', '<u4'), ('pos', '<u4'), ('fiel
 EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_last_kernel_ms',
            'kw_last_kernel_times', 'kw_doc_routes', 'kw_last_error', 'kw_destroy',
            'kw_scan_host', 'kw_hits_host', 'kw_device_count', 'kw_device_init',
-           'kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_exchange_plan',
-           'kw_comm_last_error', 'kw_comm_destroy',
+           'kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits',
+           'kw_allgather_hits_planned', 'kw_exchange_plan', 'kw_exchange_caps_ok', 'kw_comm_last_error',
+           'kw_comm_destroy',
            'kw_dedup_create', 'kw_dedup_run', 'kw_dedup_counts', 'kw_dedup_kept_size', 'kw_dedup_kept_copy',
            'kw_dedup_last_ms', 'kw_dedup_last_error', 'kw_dedup_destroy', 'dedup_urls')
 
@@ -116,10 +117,14 @@ def lib() -> ctypes.CDLL:
     L.kw_comm_init.argtypes = [i32, i32, vp, i32, ctypes.POINTER(vp)]
     L.kw_allgather_counts.argtypes = [vp, i64, vp, vp]
     L.kw_allgather_hits.argtypes = [vp, vp, i64, i64, i32, vp, i64, ctypes.POINTER(i64), vp, vp]
+    L.kw_allgather_hits_planned.argtypes = [vp, vp, i64, i64, i32, vp, vp, i64, ctypes.POINTER(i64), vp]
+    L.kw_exchange_caps_ok.argtypes = [i32, i32, vp, vp, ctypes.POINTER(i32)]
+    L.kw_exchange_caps_ok.restype = ctypes.c_int
     L.kw_comm_destroy.argtypes = [vp]
     L.kw_exchange_plan.argtypes = [i32, i32, i32, vp, vp, vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     L.kw_exchange_plan.restype = ctypes.c_int
-    for f in ('kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits', 'kw_comm_destroy'):
+    for f in ('kw_comm_unique_id', 'kw_comm_init', 'kw_allgather_counts', 'kw_allgather_hits',
+              'kw_allgather_hits_planned', 'kw_comm_destroy'):
         getattr(L, f).restype = ctypes.c_int
     L.kw_comm_last_error.argtypes = [vp]
     L.kw_comm_last_error.restype = ctypes.c_char_p
@@ -159,6 +164,17 @@ def exchange_plan(nranks: int, rank: int, root: int, counts):
     if rc != KW_OK:
         raise KwError(rc, 'kw_exchange_plan: bad arguments')
     return off, ops, int(tot.value), int(nrecv.value)
+
+
+def exchange_caps_ok(nranks: int, root: int, counts, caps):
+    """kw_exchange_caps_ok (pure host): (ok, first short receiver or -1)."""
+    cnt = np.ascontiguousarray(counts, dtype=np.int64)
+    cap = np.ascontiguousarray(caps, dtype=np.int64)
+    bad = ctypes.c_int32(-1)
+    rc = lib().kw_exchange_caps_ok(nranks, root, ptr(cnt), ptr(cap), ctypes.byref(bad))
+    if rc not in (KW_OK, KW_EOVERFLOW):
+        raise KwError(rc, 'kw_exchange_caps_ok: bad arguments')
+    return rc == KW_OK, int(bad.value)
 
 
 def check(rc: int, handle=None) -> None:

@@ -95,8 +95,9 @@ class GpuUrlDedup:
         self._check(_native.lib().kw_dedup_counts(self.h, _native.ptr(c)))
         return [int(x) for x in c]
 
-    def kept(self) -> Tuple[np.ndarray, List[str]]:
-        """(source row indices, normalised URLs) of the last run's kept rows, on the host."""
+    def kept_device(self):
+        """(normalised URL bytes, offsets [n_kept + 1], source row indices [n_kept]) of the last run's kept rows,
+        dense and in row order, as device tensors."""
         t = self.torch
         nk, nb = ctypes.c_int64(), ctypes.c_int64()
         self._check(_native.lib().kw_dedup_kept_size(self.h, ctypes.byref(nk), ctypes.byref(nb)))
@@ -108,8 +109,13 @@ class GpuUrlDedup:
         self._check(_native.lib().kw_dedup_kept_copy(self.h, _native.ptr(b), _native.ptr(o), _native.ptr(r),
                                                      ctypes.c_void_p(st.cuda_stream)))
         st.synchronize()
-        hb, ho, hr = b.cpu().numpy().tobytes(), o.cpu().numpy(), r[:nk.value].cpu().numpy()
-        urls = [hb[ho[k]:ho[k + 1]].decode('utf-8', 'surrogatepass') for k in range(nk.value)]
+        return b[:nb.value], o, r[:nk.value]
+
+    def kept(self) -> Tuple[np.ndarray, List[str]]:
+        """(source row indices, normalised URLs) of the last run's kept rows, on the host."""
+        b, o, r = self.kept_device()
+        hb, ho, hr = b.cpu().numpy().tobytes(), o.cpu().numpy(), r.cpu().numpy()
+        urls = [hb[ho[k]:ho[k + 1]].decode('utf-8', 'surrogatepass') for k in range(len(hr))]
         return hr, urls
 
     def last_ms(self) -> List[float]:

@@ -39,6 +39,7 @@
 
 #include "../../include/kwmatch.h"
 #include "../../include/kwdedup.h"
+#include "kwenv.hpp"
 
 namespace dd {
 
@@ -998,7 +999,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     // the transform's grid: its waves' slow lists are sized from the groups of 64 rows each wave takes
     int tbpc = 8;   // transform blocks per CU (KW_DEDUP_TBLOCKS_PER_CU; 4, 5, 8, 16: 130.7-130.8 ms alike)
-    if (const char *e = getenv("KW_DEDUP_TBLOCKS_PER_CU")) tbpc = std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_DEDUP_TBLOCKS_PER_CU")) tbpc = std::max(1, atoi(e));
     const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * tbpc);
     const int64_t n_tw = (int64_t)tgrid * (BLOCK / 64);
     h->S.slow_cap = (uint32_t)(((n + 63) / 64 + n_tw - 1) / n_tw * 64);
@@ -1029,8 +1030,8 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.gnext = S.cnt + 7;
     S.slow = (uint2 *)carve(8 * ((size_t)n_tw * S.slow_cap));
     S.wslow = (uint32_t *)carve(4 * (size_t)n_tw);
-    S.weak = getenv("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
-    S.stats = getenv("KW_DEDUP_STATS") ? 1 : 0;
+    S.weak = kw_env("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
+    S.stats = kw_env("KW_DEDUP_STATS") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
     h->tile_cnt = (unsigned long long *)carve(8 * (size_t)ntiles);
     h->tile_bytes = (unsigned long long *)carve(8 * (size_t)ntiles);

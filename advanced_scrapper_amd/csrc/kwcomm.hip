@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -93,9 +94,11 @@ __global__ void kw_rebase_kernel(const kw_hit *__restrict__ src, kw_hit *__restr
 struct kw_comm {
     int nranks = 1, rank = 0, device = 0;
     ncclComm_t comm = nullptr;
-    int64_t *d_counts = nullptr;   // [nranks + 1]: own count at [nranks], gathered at [0, nranks)
+    int64_t *d_counts = nullptr;   // [2 nranks + 2]: own values at [2 nranks, 2 nranks + 2), gathered at [0, 2 nranks)
     kw_hit *d_stage = nullptr;     // this rank's records, rebased
     size_t stage_cap = 0;
+    kw_hit *d_spill = nullptr;     // a receiver's records when its destination is short (planned exchange)
+    size_t spill_cap = 0;
     std::string err;
 };
 
@@ -136,16 +139,17 @@ extern "C" int kw_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, int
     ncclUniqueId uid;
     memcpy(uid.internal, id, KW_COMM_ID_BYTES);
     NCHK(c, g_rccl.CommInitRank(&c->comm, nranks, uid, rank));
-    CCHK(c, hipMalloc(&c->d_counts, sizeof(int64_t) * (nranks + 1)));
+    CCHK(c, hipMalloc(&c->d_counts, sizeof(int64_t) * (2 * nranks + 2)));
     return KW_OK;
 }
 
-// all-gather one int64 per rank (blocking: the host needs the values)
-static int gather_counts(kw_comm *c, int64_t count, int64_t *counts, hipStream_t st)
+// all-gather k (1 or 2) int64 per rank into out[r * k + j] (blocking: the host needs the values)
+static int gather_values(kw_comm *c, const int64_t *mine, int k, int64_t *out, hipStream_t st)
 {
-    CCHK(c, hipMemcpyAsync(c->d_counts + c->nranks, &count, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    NCHK(c, g_rccl.AllGather(c->d_counts + c->nranks, c->d_counts, 1, nccl_int64, c->comm, st));
-    CCHK(c, hipMemcpyAsync(counts, c->d_counts, sizeof(int64_t) * c->nranks, hipMemcpyDeviceToHost, st));
+    int64_t *own = c->d_counts + 2 * c->nranks;
+    CCHK(c, hipMemcpyAsync(own, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, st));
+    NCHK(c, g_rccl.AllGather(own, c->d_counts, (size_t)k, nccl_int64, c->comm, st));
+    CCHK(c, hipMemcpyAsync(out, c->d_counts, sizeof(int64_t) * k * c->nranks, hipMemcpyDeviceToHost, st));
     CCHK(c, hipStreamSynchronize(st));
     return KW_OK;
 }
@@ -154,7 +158,7 @@ extern "C" int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, v
 {
     if (!c || !counts) return KW_EINVAL;
     CCHK(c, hipSetDevice(c->device));
-    return gather_counts(c, count, counts, (hipStream_t)stream);
+    return gather_values(c, &count, 1, counts, (hipStream_t)stream);
 }
 
 extern "C" int kw_exchange_plan(int32_t nranks, int32_t rank, int32_t root, const int64_t *counts, int64_t *recv_off,
@@ -183,38 +187,39 @@ extern "C" int kw_exchange_plan(int32_t nranks, int32_t rank, int32_t root, cons
     return KW_OK;
 }
 
-extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
-                                 kw_hit *d_out, int64_t cap, int64_t *n_total, int64_t *counts, void *stream)
+extern "C" int kw_exchange_caps_ok(int32_t nranks, int32_t root, const int64_t *counts, const int64_t *caps,
+                                   int32_t *bad_rank)
 {
-    if (!c || !n_total || n < 0 || (n > 0 && !d_local)) return KW_EINVAL;
-    if (root >= c->nranks || doc_base < 0) { c->err = "kw_allgather_hits: bad root or doc_base"; return KW_EINVAL; }
-    hipStream_t st = (hipStream_t)stream;
-    CCHK(c, hipSetDevice(c->device));
-    int rc;
-    std::vector<int64_t> cnt(c->nranks, 0);
-    rc = gather_counts(c, n, cnt.data(), st);
-    if (rc) return rc;
-    std::vector<int64_t> pre(c->nranks + 1, 0);
-    std::vector<int32_t> ops(c->nranks, 0);
-    int64_t n_recv = 0;
-    if (kw_exchange_plan(c->nranks, c->rank, root, cnt.data(), pre.data(), ops.data(), n_total, &n_recv) != KW_OK) {
-        c->err = "kw_allgather_hits: bad exchange plan";
-        return KW_EINVAL;
+    if (nranks < 1 || root >= nranks || !counts || !caps) return KW_EINVAL;
+    int64_t total = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (counts[r] < 0) return KW_EINVAL;
+        total += counts[r];
     }
-    if (counts) memcpy(counts, cnt.data(), sizeof(int64_t) * c->nranks);
-    const bool receive = root < 0 || root == c->rank;
-    if (receive && pre[c->nranks] > cap) { c->err = "kw_allgather_hits: destination too small"; return KW_EINVAL; }
-    if (receive && pre[c->nranks] > 0 && !d_out) { c->err = "kw_allgather_hits: null destination"; return KW_EINVAL; }
-    if (doc_base + n > 0xFFFFFFFFll) { c->err = "kw_allgather_hits: global document ids beyond 2^32"; return KW_EINVAL; }
-    // this rank's records, rebased: straight into its slot of the output when it receives, else into
-    // the staging buffer it sends from
+    for (int r = 0; r < nranks; ++r) {
+        const bool receives = root < 0 || root == r;
+        if (receives && caps[r] < total) {
+            if (bad_rank) *bad_rank = r;
+            return KW_EOVERFLOW;
+        }
+    }
+    if (bad_rank) *bad_rank = -1;
+    return KW_OK;
+}
+
+// rebase this rank's n records (into its slot of dst when it receives, else into the staging buffer) and post
+// the plan's sends and receives (dst = the receiver's output)
+static int post_exchange(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, bool receive,
+                         const int64_t *pre, const int64_t *cnt, const int32_t *ops, kw_hit *dst, hipStream_t st)
+{
     kw_hit *mine = nullptr;
     if (n > 0) {
         if (receive) {
-            mine = d_out + pre[c->rank];
+            mine = dst + pre[c->rank];
         } else {
             if ((size_t)n > c->stage_cap) {
                 if (c->d_stage) (void)hipFree(c->d_stage);
+                c->d_stage = nullptr;
                 c->stage_cap = (size_t)n + (size_t)n / 4 + 1024;
                 CCHK(c, hipMalloc(&c->d_stage, c->stage_cap * sizeof(kw_hit)));
             }
@@ -229,9 +234,86 @@ extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, i
     NCHK(c, g_rccl.GroupStart());
     for (int p = 0; p < c->nranks; ++p) {
         if (ops[p] & KW_PLAN_SEND) NCHK(c, g_rccl.Send(mine, (size_t)n * 4, nccl_uint32, p, c->comm, st));
-        if (ops[p] & KW_PLAN_RECV) NCHK(c, g_rccl.Recv(d_out + pre[p], (size_t)cnt[p] * 4, nccl_uint32, p, c->comm, st));
+        if (ops[p] & KW_PLAN_RECV) NCHK(c, g_rccl.Recv(dst + pre[p], (size_t)cnt[p] * 4, nccl_uint32, p, c->comm, st));
     }
     NCHK(c, g_rccl.GroupEnd());
+    return KW_OK;
+}
+
+extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
+                                 kw_hit *d_out, int64_t cap, int64_t *n_total, int64_t *counts, void *stream)
+{
+    if (!c || !n_total || n < 0 || (n > 0 && !d_local)) return KW_EINVAL;
+    if (root >= c->nranks || doc_base < 0) { c->err = "kw_allgather_hits: bad root or doc_base"; return KW_EINVAL; }
+    hipStream_t st = (hipStream_t)stream;
+    CCHK(c, hipSetDevice(c->device));
+    const bool receive = root < 0 || root == c->rank;
+    // one exchange of (count, receiver capacity) pairs: every rank sees every receiver's room, so a short
+    // destination fails on EVERY rank here, before any record moves (no peer is left waiting in a send)
+    const int64_t mine[2] = {n, receive ? (d_out ? cap : 0) : INT64_MAX};
+    std::vector<int64_t> pairs((size_t)2 * c->nranks);
+    int rc = gather_values(c, mine, 2, pairs.data(), st);
+    if (rc) return rc;
+    std::vector<int64_t> cnt(c->nranks), caps(c->nranks);
+    for (int r = 0; r < c->nranks; ++r) { cnt[r] = pairs[2 * r]; caps[r] = pairs[2 * r + 1]; }
+    std::vector<int64_t> pre(c->nranks + 1, 0);
+    std::vector<int32_t> ops(c->nranks, 0);
+    int64_t n_recv = 0;
+    if (kw_exchange_plan(c->nranks, c->rank, root, cnt.data(), pre.data(), ops.data(), n_total, &n_recv) != KW_OK) {
+        c->err = "kw_allgather_hits: bad exchange plan";
+        return KW_EINVAL;
+    }
+    if (counts) memcpy(counts, cnt.data(), sizeof(int64_t) * c->nranks);
+    int32_t bad = -1;
+    if (kw_exchange_caps_ok(c->nranks, root, cnt.data(), caps.data(), &bad) != KW_OK) {
+        char buf[160];
+        snprintf(buf, sizeof(buf), "kw_allgather_hits: rank %d's destination holds %lld records, the exchange has %lld",
+                 bad, (long long)caps[bad], (long long)*n_total);
+        c->err = buf;
+        return KW_EOVERFLOW;
+    }
+    if (doc_base + n > 0xFFFFFFFFll) { c->err = "kw_allgather_hits: global document ids beyond 2^32"; return KW_EINVAL; }
+    return post_exchange(c, d_local, n, doc_base, receive, pre.data(), cnt.data(), ops.data(), d_out, st);
+}
+
+extern "C" int kw_allgather_hits_planned(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
+                                         const int64_t *counts, kw_hit *d_out, int64_t cap, int64_t *n_total,
+                                         void *stream)
+{
+    if (!c || !n_total || !counts || n < 0 || (n > 0 && !d_local)) return KW_EINVAL;
+    if (root >= c->nranks || doc_base < 0) { c->err = "kw_allgather_hits_planned: bad root or doc_base"; return KW_EINVAL; }
+    if (counts[c->rank] != n) { c->err = "kw_allgather_hits_planned: counts[rank] is not this rank's n"; return KW_EINVAL; }
+    hipStream_t st = (hipStream_t)stream;
+    CCHK(c, hipSetDevice(c->device));
+    std::vector<int64_t> pre(c->nranks + 1, 0);
+    std::vector<int32_t> ops(c->nranks, 0);
+    int64_t n_recv = 0;
+    if (kw_exchange_plan(c->nranks, c->rank, root, counts, pre.data(), ops.data(), n_total, &n_recv) != KW_OK) {
+        c->err = "kw_allgather_hits_planned: bad counts";
+        return KW_EINVAL;
+    }
+    if (doc_base + n > 0xFFFFFFFFll) { c->err = "kw_allgather_hits_planned: global document ids beyond 2^32"; return KW_EINVAL; }
+    const bool receive = root < 0 || root == c->rank;
+    kw_hit *dst = d_out;
+    bool short_dst = false;
+    if (receive && (n_recv > cap || (n_recv > 0 && !d_out))) {
+        // every peer already posts its sends from the same counts: receive into the library's buffer so no one
+        // waits, then report the short destination (the records are dropped)
+        if ((size_t)n_recv > c->spill_cap) {
+            if (c->d_spill) (void)hipFree(c->d_spill);
+            c->d_spill = nullptr;
+            c->spill_cap = (size_t)n_recv;
+            CCHK(c, hipMalloc(&c->d_spill, c->spill_cap * sizeof(kw_hit)));
+        }
+        dst = c->d_spill;
+        short_dst = true;
+    }
+    int rc = post_exchange(c, d_local, n, doc_base, receive, pre.data(), counts, ops.data(), dst, st);
+    if (rc) return rc;
+    if (short_dst) {
+        c->err = "kw_allgather_hits_planned: destination too small (records received into a library buffer and dropped)";
+        return KW_EOVERFLOW;
+    }
     return KW_OK;
 }
 
@@ -247,6 +329,7 @@ extern "C" int kw_comm_destroy(kw_comm *c)
     if (c->comm) (void)g_rccl.CommDestroy(c->comm);
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->d_spill) (void)hipFree(c->d_spill);
     delete c;
     return KW_OK;
 }

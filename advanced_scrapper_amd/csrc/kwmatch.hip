@@ -19,6 +19,7 @@
 #include "kwmatch_kernels.hpp"
 #include "kwmatch_fast_kernel.hpp"
 #include "kwmatch_split.hpp"
+#include "kwenv.hpp"
 
 using namespace kw;
 
@@ -96,6 +97,7 @@ struct kw_handle {
     FastScratch FS{};
     int nk = 0, nr = 0, ng = 0;
     uint32_t defer_cap = 0, item_cap = 0, rx_cap = 0;
+    bool item_clamped = false;          // a scan needed more probe items than 32-bit indexes reach (FS.item_grow)
     ScratchCaps caps;
     uint32_t *out_cnt_all = nullptr;   // counts of every result region (scan, task, resolve, generic)
     kw_hit *out_all = nullptr;
@@ -522,7 +524,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     // open addressing with linear probing: a candidate whose key is absent (most stage-2 survivors of the
     // shorter key lengths) walks to an empty slot, one dependent load per slot; KW_HT_SCALE = slots per key
     uint32_t hs = 1024, hscale = 2;
-    if (const char *e = getenv("KW_HT_SCALE")) hscale = (uint32_t)std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_HT_SCALE")) hscale = (uint32_t)std::max(1, atoi(e));
     while (hs < (size_t)hscale * keys.size()) hs <<= 1;
     B.ht_mask = hs - 1;
     B.ht_key.assign(hs, ~0ull);
@@ -813,7 +815,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
             return a.first != b.first ? a.first > b.first : a.second < b.second;
         });
         size_t nmark = 127;
-        if (const char *e = getenv("KW_TEST_TX_MARKERS")) nmark = std::min<size_t>(127, (size_t)std::max(0, atoi(e)));
+        if (const char *e = kw_env("KW_TEST_TX_MARKERS")) nmark = std::min<size_t>(127, (size_t)std::max(0, atoi(e)));
         std::unordered_map<uint32_t, uint32_t> mk;
         for (size_t k = 0; k < order.size() && k < nmark; ++k) {
             const uint32_t cp = order[k].second, v = 0x81u + (uint32_t)k;
@@ -935,7 +937,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
         int frc = build_fast(FB, Q, n_pat, pat_bytes, pat_off, cps, tcps, pat_info, atoms, rxo, ferr);
         if (frc) return fail(frc, ferr);
     }
-    if (const char *dump = getenv("KW_DUMP_ANCHORS")) {
+    if (const char *dump = kw_env("KW_DUMP_ANCHORS")) {
         // developer aid: one line per anchor use "hex(anchor) pattern kind" (anchor tuning)
         if (FILE *f = fopen(dump, "w")) {
             for (size_t a = 0; a < FB.as_len.size(); ++a)
@@ -1113,7 +1115,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     {
         // KW_SIDE_PRIO=1|2: the side stream (transcoding beside the probe) or
         // side2 (short fields beside verify) at the greatest priority
-        const char *e = getenv("KW_SIDE_PRIO");
+        const char *e = kw_env("KW_SIDE_PRIO");
         int sp = e ? atoi(e) : 0, lo = 0, hi = 0;
         HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, (sp & 1) ? hi : lo));
@@ -1215,7 +1217,7 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.tx_used = (unsigned long long *)(q + 384);    // transcoded-view bytes handed out
     h->FS.res_cnt = (uint32_t *)(q + 392);              // documents left to the resolve kernel
     h->d_total = (unsigned long long *)(q + 400);       // hit records of the scan (kw_offsets_kernel)
-    h->FS.gnext = (uint32_t *)(q + 408);                // 2 x u32: the filter's / epilogue's next group
+    h->FS.gnext = (uint32_t *)(q + 408);                // 2 x u32: the filter's next work unit / the probe's next region
     uint32_t *cnts = (uint32_t *)(q + 1024);
     h->out_cnt_all = cnts;
     h->FS.kout_cnt = cnts;
@@ -1247,11 +1249,18 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     return KW_OK;
 }
 
+// regions x item_cap of the probe's item arrays must index with 32 bits (hdr.x; KW_TEST_ITEM_LIMIT lowers it)
+static uint64_t item_index_limit()
+{
+    if (const char *e = kw_env("KW_TEST_ITEM_LIMIT")) return std::max<uint64_t>(1, (uint64_t)atoll(e));
+    return 0xFFFFFFFFull;
+}
+
 static int launch_scan(kw_handle *h)
 {
     hipStream_t st = h->stream;
     // KW_SERIAL=1 (profiling aid): every kernel on the main stream, so kernel traces show isolated durations
-    static const bool serial = getenv("KW_SERIAL") != nullptr;
+    static const bool serial = kw_env("KW_SERIAL") != nullptr;
     hipStream_t side = serial ? st : h->side, side2 = serial ? st : h->side2;
     const int64_t n_docs = h->n_docs;
     // split scan: filter regions (one wave each, resident at once), probe waves = filter regions,
@@ -1264,21 +1273,21 @@ static int launch_scan(kw_handle *h)
     // (claimed dynamically by the filter waves; one probe wave each)
     const int64_t n_groups_all = (n_docs + FG_DOCS - 1) / FG_DOCS;
     int64_t kchunk = std::max<int64_t>(1, n_groups_all / ((int64_t)nsb * FS_WAVES * 4));
-    if (const char *e = getenv("KW_CHUNK_GROUPS")) kchunk = std::max(1, atoi(e));
-    const bool dyn_groups = getenv("KW_STATIC_GROUPS") == nullptr;   // (A/B: grid-stride, one chunk per wave)
-    if (!dyn_groups && !getenv("KW_CHUNK_GROUPS")) kchunk = (n_groups_all + (int64_t)nsb * FS_WAVES - 1) / ((int64_t)nsb * FS_WAVES);
+    if (const char *e = kw_env("KW_CHUNK_GROUPS")) kchunk = std::max(1, atoi(e));
+    const bool dyn_groups = kw_env("KW_STATIC_GROUPS") == nullptr;   // (A/B: grid-stride, one chunk per wave)
+    if (!dyn_groups && !kw_env("KW_CHUNK_GROUPS")) kchunk = (n_groups_all + (int64_t)nsb * FS_WAVES - 1) / ((int64_t)nsb * FS_WAVES);
     const int n_regions = (int)std::max<int64_t>(1, (n_groups_all + kchunk - 1) / kchunk);
     const int n_epi = neb * EK_WAVES;
     int rmul = 2;   // resolve blocks per resident slot: later blocks balance the uneven documents (measured: 2-3 % faster than 1)
-    if (const char *e = getenv("KW_RESOLVE_MUL")) rmul = std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_RESOLVE_MUL")) rmul = std::max(1, atoi(e));
     int nrb = (int)std::min<int64_t>((n_docs + (int64_t)RK_WAVES * WAVE - 1) / ((int64_t)RK_WAVES * WAVE),
                                      (int64_t)h->cus * h->resolve_blocks_per_cu * rmul);
-    if (const char *e = getenv("KW_RESOLVE_BLOCKS")) nrb = std::min(nrb, std::max(1, atoi(e)));
+    if (const char *e = kw_env("KW_RESOLVE_BLOCKS")) nrb = std::min(nrb, std::max(1, atoi(e)));
     if (nrb < 1) nrb = 1;
     // generic kernel: 4 blocks per CU (one resident, 1 wave / SIMD at 256 VGPRs): the deferred documents'
     // costs vary by orders of magnitude, later blocks take the work of the slow ones
     int gmul = 4;
-    if (const char *e = getenv("KW_GENERIC_BLOCKS_PER_CU")) gmul = std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_GENERIC_BLOCKS_PER_CU")) gmul = std::max(1, atoi(e));
     int ngb = std::max(1, (int)std::min<int64_t>((int64_t)h->cus * gmul, (n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK));
     {   // a generic wave's scratch grows with the largest deferred field: fewer waves then, within a budget
         const size_t per_wave = (size_t)2 * h->caps.gi_cap * 8 + (size_t)h->caps.gc_cap * 4 +
@@ -1296,28 +1305,36 @@ static int launch_scan(kw_handle *h)
     // (regions of a few groups: a 1024 floor; a region that needs more grows every region and rescans)
     w.item_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1024, docs_per_s * 32), (int64_t)1 << 26);
     w.cand_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(1024, docs_per_s * 40), (int64_t)1 << 26);
-    if (const char *e = getenv("KW_TEST_CAND_CAP")) w.cand_cap = w.item_cap = (uint32_t)std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_TEST_CAND_CAP")) w.cand_cap = (uint32_t)std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_TEST_ITEM_CAP")) w.item_cap = (uint32_t)std::max(1, atoi(e));
+    w.item_cap = (uint32_t)std::min<uint64_t>(w.item_cap, item_index_limit() / (uint64_t)n_regions);
     const int64_t docs_per_r = (n_docs + w.nr - 1) / w.nr;
     w.out_cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(4096, std::max(docs_per_r, docs_per_k) * 48),
                                             (int64_t)1 << 26);
     w.rx_cap = (uint32_t)std::min<int64_t>(docs_per_r * 2 + 64, (int64_t)1 << 20);
-    if (const char *e = getenv("KW_TEST_RX_CAP")) w.rx_cap = (uint32_t)std::max(1, atoi(e));   // tests: force the rescan
+    if (const char *e = kw_env("KW_TEST_RX_CAP")) w.rx_cap = (uint32_t)std::max(1, atoi(e));   // tests: force the rescan
     w.hdr_cap = std::max<int64_t>(n_docs, 1);
     w.defer_cap = (uint32_t)std::max<int64_t>(n_docs, 1);
     w.vcap = (uint32_t)std::min<int64_t>(docs_per_k * 8 + 256, (int64_t)1 << 24);
     w.ecap = (uint32_t)std::min<int64_t>(docs_per_k * 2 + 16, (int64_t)1 << 24);
     w.scap = w.ecap;
     w.xcap = (uint32_t)std::min<int64_t>(docs_per_k * 4 + 64, (int64_t)1 << 24);
-    if (const char *e = getenv("KW_TEST_TASK_CAP")) w.vcap = w.ecap = w.scap = w.xcap = (uint32_t)std::max(1, atoi(e));
+    if (const char *e = kw_env("KW_TEST_TASK_CAP")) w.vcap = w.ecap = w.scap = w.xcap = (uint32_t)std::max(1, atoi(e));
     w.dsize = 4096;
     while (w.dsize < (uint64_t)std::max<int64_t>(n_docs, 1) * 16) w.dsize <<= 1;
-    if (const char *e = getenv("KW_TEST_DSET_SIZE")) w.dsize = std::max<uint64_t>(2, (uint64_t)atoll(e));
+    if (const char *e = kw_env("KW_TEST_DSET_SIZE")) w.dsize = std::max<uint64_t>(2, (uint64_t)atoll(e));
     // transcoded view: 768 B per document (~25 % of 2 KB articles non-ASCII), or what the last scan wanted
     w.tx_cap = std::max<uint64_t>((uint64_t)64 << 20, (uint64_t)std::max<int64_t>(n_docs, 1) * 768);
     w.tx_cap = std::max<uint64_t>(w.tx_cap, h->tx_need);
-    if (const char *e = getenv("KW_TEST_TX_CAP")) w.tx_cap = (uint64_t)std::max<long long>(16, atoll(e));
+    if (const char *e = kw_env("KW_TEST_TX_CAP")) w.tx_cap = (uint64_t)std::max<long long>(16, atoll(e));
     int rc = ensure_scratch(h, w);
     if (rc) return rc;
+    {   // the probe's item index (hdr.x) is 32-bit: regions x item_cap stays below 2^32; a larger need than the
+        // clamped capacity defers the overflowing batches' documents to the generic kernel instead of growing
+        const uint64_t icap = std::min<uint64_t>(h->caps.item_cap, item_index_limit() / (uint64_t)n_regions);
+        h->FS.item_cap = (uint32_t)icap;
+        h->FS.item_grow = icap == h->caps.item_cap && !h->item_clamped ? 1u : 0u;
+    }
     h->FS.dyn = dyn_groups ? 1 : 0;
     h->FS.chunk_groups = kchunk;
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
@@ -1336,7 +1353,7 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipEventRecord(h->evf, st));
     // the transcoded view of the documents with a non-ASCII field (the filter flagged them) on the side
     // stream, beside the probe; the epilogue waits for it
-    static const int tx_bpc = getenv("KW_TX_BLOCKS_PER_CU") ? std::max(1, atoi(getenv("KW_TX_BLOCKS_PER_CU"))) : 8;
+    static const int tx_bpc = kw_env("KW_TX_BLOCKS_PER_CU") ? std::max(1, atoi(kw_env("KW_TX_BLOCKS_PER_CU"))) : 8;
     HIPCHK(h, hipStreamWaitEvent(side, h->evf, 0));
     if (n_docs > 0)
         hipLaunchKernelGGL(kw_tx_kernel, dim3(std::max(1, (int)std::min<int64_t>((n_docs + TX_BLOCK - 1) / TX_BLOCK, (int64_t)h->cus * tx_bpc))),
@@ -1351,7 +1368,7 @@ static int launch_scan(kw_handle *h)
     HIPCHK(h, hipStreamWaitEvent(st, h->evx, 0));
     if (n_docs > 0) {
         // the group epilogue (lane = item across 32 documents); KW_EPI_FLAT=0: one wave per document
-        static const bool flat = !getenv("KW_EPI_FLAT") || atoi(getenv("KW_EPI_FLAT")) != 0;
+        static const bool flat = !kw_env("KW_EPI_FLAT") || atoi(kw_env("KW_EPI_FLAT")) != 0;
         if (flat)
             hipLaunchKernelGGL(kw_epi_flat_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off,
                                n_docs, h->FS, h->S);
@@ -1379,7 +1396,7 @@ static int launch_scan(kw_handle *h)
         // flat resolve tasks: verify -> short -> regex (regex decisions of the first two queue up);
         // G[k] waves share each epilogue wave's task region
         int G[4] = {1, 4, 4, 4};   // measured on MI355X (config 2, 2 runs each): 4.98 vs 5.00-5.01 ms for {1, 4, 2, 4} and {1, 4, 8, 4}, 5.00 {2, 4, 4, 4}, 5.17 {1, 4, 6, 6}, 5.34 {1, 4, 4, 8}
-        if (const char *e = getenv("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
+        if (const char *e = kw_env("KW_TASK_G")) sscanf(e, "%d,%d,%d,%d", &G[0], &G[1], &G[2], &G[3]);
         auto task = [&](auto kern, int g, hipStream_t s) {
             g = std::max(1, std::min(g, 16));
             const int nb = (n_epi * g + RK_WAVES - 1) / RK_WAVES;
@@ -1502,7 +1519,7 @@ static int finish(kw_handle *h)
         // transcoded-view bytes (384), record count (400)
         unsigned long long small[51];
         HIPCHK(h, hipMemcpy(small, h->S.status, sizeof(small), hipMemcpyDeviceToHost));
-        if (getenv("KW_DEBUG_TASKS") && h->nk > 0) {   // (developer aid) the task regions' queue lengths
+        if (kw_env("KW_DEBUG_TASKS") && h->nk > 0) {   // (developer aid) the task regions' queue lengths
             std::vector<uint32_t> tc((size_t)4 * h->nk);
             HIPCHK(h, hipMemcpy(tc.data(), h->FS.vcnt, tc.size() * 4, hipMemcpyDeviceToHost));
             for (int q = 0; q < 4; ++q) {
@@ -1571,7 +1588,10 @@ static int finish(kw_handle *h)
                 uint32_t cm[2];
                 HIPCHK(h, hipMemcpy(cm, h->FS.cmax, sizeof(cm), hipMemcpyDeviceToHost));
                 w.cand_cap = std::max(w.cand_cap, cm[0] + cm[0] / 8 + 64);
-                w.item_cap = std::max(w.item_cap, cm[1] + cm[1] / 8 + 64);
+                const uint64_t lim = item_index_limit() / (uint64_t)std::max(1, h->ns);
+                const uint64_t want = (uint64_t)cm[1] + cm[1] / 8 + 64;
+                if (want > lim) h->item_clamped = true;   // from now on: defer, never grow past the index limit
+                w.item_cap = std::max<uint32_t>(w.item_cap, (uint32_t)std::min<uint64_t>(want, lim));
             }
             int rc = ensure_scratch(h, w);
             if (rc) return rc;
@@ -1590,9 +1610,9 @@ static int finish(kw_handle *h)
         h->stats[17] = (unsigned long long)h->rescans;
         {   // the transcoded view: documents it took / left to the resolve kernel; the next scan's capacity
             const unsigned long long used = small[48];
-            if (used > h->caps.tx_cap && !getenv("KW_TEST_TX_CAP")) h->tx_need = used + used / 8;
+            if (used > h->caps.tx_cap && !kw_env("KW_TEST_TX_CAP")) h->tx_need = used + used / 8;
         }
-        if (getenv("KW_DUMP_TIMING")) {   // FK_TIMING builds: resolve-kernel cycles summed over waves
+        if (kw_env("KW_DUMP_TIMING")) {   // FK_TIMING builds: resolve-kernel cycles summed over waves
             fprintf(stderr, "KW_TIMING resolve decode %llu edge %llu items %llu short %llu regex %llu all %llu\n", fst[21],
                     fst[22], fst[23], fst[24], fst[25], fst[26]);
             fprintf(stderr, "KW_TASKS verify %llu edge %llu short %llu regex %llu edge_docs %llu\n", fst[27], fst[28], fst[29],

@@ -159,8 +159,10 @@ struct FastTables {
 };
 
 struct FastScratch {
-    uint64_t *items;            // per scan wave: item_cap items
-    uint32_t item_cap;
+    uint64_t *items;            // per filter region: item_cap items (the probe's), indexed by 32-bit hdr.x
+    uint32_t item_cap;          // regions x item_cap < 2^32 (launch_scan clamps it)
+    uint32_t item_grow;         // 1: a region whose items overflow asks the host for larger regions (rescan);
+                                // 0 (item_cap clamped): its batches' documents only defer to the generic kernel
     uint2 *hdr;                 // per document
     kw_hit *out;                // per resolve wave: out_cap records
     uint32_t *out_cnt;          // per resolve wave
@@ -201,7 +203,8 @@ struct FastScratch {
     uint4 *vrec;                // per document: {text start lo, hi | transcoded << 31, text / title code points}
     uint32_t *res_list;         // documents the epilogue left to the resolve kernel (DH_RESOLVE; defer_cap)
     uint32_t *res_cnt;
-    // dynamic work distribution: [0] the filter's next 32-document group, [1] the epilogue's (zeroed per scan);
+    // dynamic work distribution: [0] the filter's next work unit (chunk of groups), [1] the probe's next region
+    // (zeroed per scan);
     // dyn = 0: grid-stride groups (KW_STATIC_GROUPS=1)
     uint32_t *gnext;
     int dyn;

@@ -1359,23 +1359,8 @@ __device__ __forceinline__ void fk_field_ctx(FieldCtx &F, const uint8_t *arena, 
     F.field = field;
 }
 
-// a decided regex-class name: re.finditer over the field, or `name: []` (rxtab: 256 entries)
-__device__ __forceinline__ void fk_regex_now(const FastTables &FT, const DevTables &T, const DevScratch &GS,
-                                             const FieldCtx &F, OutCtx &O, uint32_t P, uint64_t *rxtab, uint8_t *txt,
-                                             unsigned long long &nrx, unsigned long long &nrx_bt,
-                                             unsigned long long &nrx_rounds)
-{
-    const int32_t r = FT.rxf_idx[P];
-    ++nrx;
-    nrx_bt += r < 0;
-    nrx_rounds += r >= 0 ? (F.n + 2047) / 2048 : 0;
-    const uint32_t cnt = r >= 0 ? fk_rx_fixed_positions<true>(FT, GS, F, O, P, (uint32_t)r, rxf_params(FT, (uint32_t)r),
-                                                              rxtab, txt)
-                                : rx_positions(T, GS, F, O, P);
-    if (cnt == 0) emit_hits(O, GS, lane_id() == 0, F.doc, P, KW_NOPOS, F.field);
-}
-
-// fk_regex_now with the program's index and parameters already fetched (the regex task kernel's prefetch)
+// a decided regex-class name: re.finditer over the field, or `name: []` (rxtab: 256 entries); the program's
+// index and parameters come prefetched (the regex task kernel's records)
 __device__ __forceinline__ void fk_regex_pre(const FastTables &FT, const DevTables &T, const DevScratch &GS,
                                              const FieldCtx &F, OutCtx &O, uint32_t P, int32_t r, const RxfParams &prm,
                                              uint64_t *rxtab, uint8_t *txt, unsigned long long &nrx,

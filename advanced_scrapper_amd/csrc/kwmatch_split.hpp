@@ -603,7 +603,8 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
         int itotal;
         const int iex = wave_excl_scan_dpp((int)nmine, &itotal);
         // the pool dropped items, or the batch's items do not fit the region (the scan is redone with larger
-        // regions, ST_CAND_OVERFLOW): the batch's documents defer, so nothing reads items that were not written
+        // regions, ST_CAND_OVERFLOW, unless S.item_grow is 0): the batch's documents defer, so nothing reads
+        // items that were not written
         const bool ovf = pn > (uint32_t)PK_POOL || icur + (uint32_t)itotal > icap;
         const uint64_t withm = __ballot(nmine > 0);
         if (withm) {
@@ -631,7 +632,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
         scnt[lane] = 0;
         wave_sync();
     }
-    if (lane == 0 && icur > icap) {
+    if (lane == 0 && icur > icap && S.item_grow) {   // (clamped: the deferred documents are the generic kernel's)
         atomicOr(&S.status[0], ST_CAND_OVERFLOW);
         atomicMax(&S.cmax[1], icur);
     }

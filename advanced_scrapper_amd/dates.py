@@ -75,17 +75,22 @@ class Dates:
         return us, ok
 
     def utc_stamps(self, rows):
-        """``int(d.timestamp())`` of the given rows' dates when the process's local time zone is UTC (a naive
-        datetime's timestamp() reads it in local time, match_keywords.py:131-132), else ``None``.  Rows of
-        the dataset's layout take their epoch seconds; the others call timestamp()."""
+        """``(stamps, k, exc)``: ``int(d.timestamp())`` of the given rows' dates when the process's local time
+        zone is UTC (a naive datetime's timestamp() reads it in local time, match_keywords.py:131-132), else
+        ``None``.  Rows of the dataset's layout take their epoch seconds; the others call timestamp(), and the
+        first of them that raises (e.g. a year-1 date) stops there: ``k`` is its index in ``rows`` and ``exc``
+        the exception (``k = len(rows)``, ``exc = None`` when none raises; ``stamps[:k]`` are valid)."""
         import numpy as np
         if not local_zone_is_utc():
             return None
         rows = np.asarray(rows, dtype=np.int64)
         out = self.us[rows] // 1000000
         for j in np.flatnonzero(self.kind[rows] != 1).tolist():
-            out[j] = int(self[int(rows[j])].timestamp())
-        return out
+            try:
+                out[j] = int(self[int(rows[j])].timestamp())
+            except Exception as exc:   # noqa: BLE001 - the reference's append_to_csv raises here (:131-132)
+                return out, j, exc
+        return out, len(rows), None
 
 
 def local_zone_is_utc() -> bool:

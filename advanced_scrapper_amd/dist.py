@@ -113,10 +113,12 @@ class KwComm:
                                     device=torch.device('cuda', self.device))
         out = self._out if receive else None
         nt = ctypes.c_int64()
-        self._n.check_comm(self._n.lib().kw_allgather_hits(
-            self.h, self._n.ptr(hits) if n else None, n, int(doc_base), int(root),
+        cnt = np.asarray(counts, dtype=np.int64)
+        # the counts above are this step's one exchange: the records move without a second one
+        self._n.check_comm(self._n.lib().kw_allgather_hits_planned(
+            self.h, self._n.ptr(hits) if n else None, n, int(doc_base), int(root), self._n.ptr(cnt),
             self._n.ptr(out) if out is not None else None, int(out.shape[0]) if out is not None else 0,
-            ctypes.byref(nt), None, self._sp(stream)), self.h)
+            ctypes.byref(nt), self._sp(stream)), self.h)
         return (out[:total] if receive else None), counts
 
 

@@ -339,7 +339,7 @@ def render_native(chunk, raw_rows, stamps_by_doc, tickers):
     cuts = np.flatnonzero(np.r_[True, ti[1:] != ti[:-1], True]).tolist()
     mv = memoryview(out)
     return [(f'{tickers[ti[a]]}_match.csv', mv[line_off[a]:line_off[b]], rs[a:b], np.diff(line_off[a:b + 1]),
-             flags[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
+             flags[a:b], rd[a:b]) for a, b in zip(cuts[:-1], cuts[1:])]
 
 
 def header_bytes() -> bytes:
@@ -380,6 +380,6 @@ def append_rendered(out_dir: str, rendered, run_files: 'RunFiles' = None, key=(0
         for r in rendered:
             _append_file(os.path.join(out_dir, r[0]), header, r[1])
     if run_files is not None:
-        for name, data, stamps, lens, flags in rendered:
+        for name, data, stamps, lens, flags, _docs in rendered:
             if run_files.owned(name):
                 run_files.add(name, stamps, lens, flags, header, key)

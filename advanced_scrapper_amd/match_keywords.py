@@ -286,7 +286,10 @@ def _native_rows(chunk, matcher, hits, dates, error):
     docs = np.unique(row_doc)
     fast = dates.utc_stamps(docs) if hasattr(dates, 'utc_stamps') else None
     if fast is not None:                       # a UTC process: naive dates' timestamp() = their epoch seconds
-        stamps[docs] = fast
+        st, k, e = fast
+        stamps[docs[:k]] = st[:k]
+        if e is not None:                      # that article's append raises in the reference: rows before it
+            exc, row = e, int(docs[k])
     else:
         for d in docs.tolist():                # time_unix = int(parse(date_time).timestamp()), :131-132
             try:
@@ -596,20 +599,24 @@ def _prefetch(chunks, depth: int = 1):
     stop = threading.Event()
     done = object()
 
+    def put(x) -> bool:
+        """Queue x unless the consumer has left (stop set): never blocks past its exit."""
+        while not stop.is_set():
+            try:
+                q.put(x, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
     def produce():
         try:
             for item in chunks:
-                while not stop.is_set():
-                    try:
-                        q.put((item, None), timeout=0.1)
-                        break
-                    except queue.Full:
-                        continue
-                if stop.is_set():
+                if not put((item, None)):
                     return
-            q.put((done, None))
+            put((done, None))
         except BaseException as exc:   # noqa: BLE001 - re-raised in the consumer, in order
-            q.put((done, exc))
+            put((done, exc))
 
     th = threading.Thread(target=produce, name='kw-ingest', daemon=True)
     th.start()

@@ -162,12 +162,14 @@ def generate(n_docs: int, names: Sequence[str], kinds: Sequence[int], seed: int 
     return Corpus(arena, off, flags, doc_base, seed)
 
 
-def to_dataframe(corpus: Corpus, source: str = 'yahoo'):
+def to_dataframe(corpus: Corpus, source: str = 'yahoo', span_docs: int = None):
     """The article CSV schema the reference reads (match_keywords.py:150-152, :139-143).
 
     NaN flags become missing values (the CSV round trip turns them into NaN,
     which the reference matches as ``"nan"``).  Dates are unique seconds
-    spread over 1980-2025 (naive, ``YYYY-MM-DD HH:MM:SS``).
+    spread over 1980-2025 (naive, ``YYYY-MM-DD HH:MM:SS``); with ``span_docs``
+    the spacing is that of a ``span_docs``-document corpus, so the documents of
+    every slice of it get the same, increasing dates whatever the slicing.
     """
     import pandas as pd
     n = corpus.n_docs
@@ -178,7 +180,7 @@ def to_dataframe(corpus: Corpus, source: str = 'yahoo'):
     start = np.datetime64('1980-01-01T00:00:00')
     span = int((np.datetime64('2025-06-01T00:00:00') - start) / np.timedelta64(1, 's'))
     total = max(n, 1)
-    step = max(span // max(total + corpus.doc_base, 1), 1)
+    step = max(span // max(span_docs if span_docs else total + corpus.doc_base, 1), 1)
     gidx = np.arange(corpus.doc_base, corpus.doc_base + n, dtype=np.int64)
     jitter = (gidx * 2654435761) % step
     stamps = start + (gidx * step + jitter).astype('timedelta64[s]')

@@ -197,14 +197,29 @@ int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, void *stream
  * `root` does (d_out may be NULL elsewhere).  The receiver's d_out (cap
  * records) gets the ranks' records concatenated in rank order = global
  * document order.  *n_total = records over all ranks; counts[nranks] (host,
- * optional) the per-rank counts.  The counts exchange blocks (every rank must
- * call); the records move asynchronously on `stream` (RCCL send/recv over the
- * xGMI mesh), so the next kw_scan can run beside them on another stream.
- * The receiver's cap must hold the total (size d_out from kw_allgather_counts
- * first): a short d_out fails on that rank after the counts exchange and
- * leaves its peers waiting.  Use one stream per communicator. */
+ * optional) the per-rank counts.  One blocking exchange of (count, receiver
+ * capacity) pairs (every rank must call), then the records move asynchronously
+ * on `stream` (RCCL send/recv over the xGMI mesh), so the next kw_scan can run
+ * beside them on another stream.  A receiver whose cap cannot hold the total
+ * makes EVERY rank return KW_EOVERFLOW before any record moves.  Use one
+ * stream per communicator. */
 int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root, kw_hit *d_out,
                       int64_t cap, int64_t *n_total, int64_t *counts, void *stream);
+
+/* kw_allgather_hits with the counts of this step already exchanged
+ * (counts[nranks] from kw_allgather_counts, the same array on every rank, and
+ * counts[rank] == n): no further exchange and no host wait, so one step costs
+ * one blocking counts exchange (the caller sizes d_out from it).  A receiver
+ * whose d_out is short still receives (into a library buffer) so that no peer
+ * waits, and returns KW_EOVERFLOW; the other ranks return KW_OK. */
+int kw_allgather_hits_planned(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
+                              const int64_t *counts, kw_hit *d_out, int64_t cap, int64_t *n_total, void *stream);
+
+/* The capacity rule kw_allgather_hits agrees on (pure host): KW_OK when every
+ * receiving rank r (root < 0: all; else root) has caps[r] >= the sum of
+ * counts; else KW_EOVERFLOW with *bad_rank = the first short receiver.  Given
+ * the same gathered (counts, caps), every rank reaches the same verdict. */
+int kw_exchange_caps_ok(int32_t nranks, int32_t root, const int64_t *counts, const int64_t *caps, int32_t *bad_rank);
 
 /* The exchange plan kw_allgather_hits runs, as a pure host function (no GPU,
  * no RCCL; tests check it against a gloo execution): given every rank's

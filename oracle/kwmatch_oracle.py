@@ -180,6 +180,10 @@ class Oracle:
             tm, ti = {}, {}
             for _attr, names in attrs.items():
                 for name, (start, end) in names.items():
+                    # the period test only decides names that matched a field; skipping it for the others
+                    # changes nothing (it has no side effects and cannot raise on aware/naive datetimes)
+                    if name not in text_r and name not in title_r:
+                        continue
                     if not in_period(article_date, start, end):
                         continue
                     if name in text_r:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of environment knobs on the bench line: bash scripts/gpu_envab.sh "VAR=a" "VAR=b" ... (each: 2 runs)
 cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
+export TMPDIR=/tmp KW_DEV=1
 mkdir -p gpurun_out
 i=0
 for kv in "$@"; do

@@ -1,0 +1,236 @@
+"""Pin north_star's hit CSV at 10M articles: the per-ticker output rows of config 3's corpus, oracle-made.
+
+Input: documents 0..9 999 999 of bench.py's generator (csrc/synth.c, seed 20250905, the reference KB
+tests/golden/kb_processed.json.gz), written as the reference's article CSV 20 000 rows at a time (the
+reference's chunksize, match_keywords.py:227) by ``synth.to_dataframe(corpus, span_docs=10M).to_csv()``
+(unique, increasing dates over the whole 10M) and read back by ``pd.read_csv`` as its chunk reader does.
+
+For every article: the reference's field prep (:150-152), ``ticker_matches`` from the CPU oracle
+(oracle/kwmatch_oracle.py ``Oracle.ticker_matches``, :153-187 restated; pinned against the reference's own
+``process_chunk`` by matches.jsonl.gz and per document over 10M by c2_digests / c3_blocks), and for each
+matched ticker the row ``append_to_csv`` writes (:128-146): the same dict, rendered by pandas'
+``DataFrame([row]).to_csv(header=False, index=False)``, ``time_unix = int(parser.parse(date).timestamp())``
+in a UTC process.
+
+Committed:
+* tests/golden/c3_csv.npz — per 1000-document block: the wrapping sum of tests/bytes_digest.line_values over
+  the block's rows (row bytes, file = KB ticker position, article) and the row count (10 000 blocks);
+* tests/golden/c3_csv.json — per ticker file: sha256 and size of the appended file (header + rows in
+  append order) and of the file after the reference's own ``sort_matched_csv`` (:195-217, imported from
+  /root/reference with rapidfuzz stubbed, as make_c2_slice.py does); the chained sha256 of the 500 chunk
+  CSVs (the GPU test regenerates them and must produce the same bytes).
+
+tests/test_gpu_c3.py::test_c3_csv_rows_ten_million renders the same chunks through the drop-in's native
+path (ingest -> kw_scan -> kwrows -> kwcsv_emit) on the GPU box and compares every block and file.
+
+    python tests/golden/make_n1_digests.py [--procs 6] [--docs 10000000]
+
+Runs in the build container on CPU (~2.5 h on 6 cores), never on GPU minutes.  The appended files are
+written to tests/golden/_local/n1/ for the sort pass and deleted at the end.
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import hashlib
+import io
+import json
+import multiprocessing as mp
+import os
+import shutil
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+sys.path.insert(0, REPO)
+
+SEED = 20250905
+CHUNK = 20000
+DBLOCK = 1000
+SPAN_DOCS = 10_000_000
+COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source', 'source_url',
+           'article_text')
+_W = {}
+
+
+def chunk_csv_bytes(lo: int, n: int = CHUNK, names_kinds=None) -> bytes:
+    """The article CSV of documents [lo, lo + n) (also used by the GPU test)."""
+    from advanced_scrapper_amd import synth
+    if names_kinds is None:
+        from advanced_scrapper_amd.kb import compile_kb
+        from tests import golden_data
+        names_kinds = synth.injectable_names(compile_kb(golden_data.kb_processed()))
+    names, kinds = names_kinds
+    corpus = synth.generate(n, names, kinds, seed=SEED, doc_base=lo)
+    return synth.to_dataframe(corpus, span_docs=SPAN_DOCS).to_csv(index=False).encode('utf-8')
+
+
+def _init():
+    os.environ['TZ'] = 'UTC'
+    time.tzset()
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from oracle import kwmatch_oracle as orc
+    from tests import golden_data
+    processed = golden_data.kb_processed()
+    _W['nk'] = synth.injectable_names(compile_kb(processed))
+    _W['oracle'] = orc.Oracle(processed)
+    _W['tickers'] = {t: i for i, t in enumerate(processed)}
+    _W['names'] = list(processed)
+
+
+_MARK = 'QZXJROWQZXJ'
+
+
+def _render(recs):
+    """Each dict's ``pd.DataFrame([d]).to_csv(index=False, header=False)`` line (append_to_csv, :144-146).
+
+    For speed the rows are rendered as one frame with a marker column in front (the csv writer renders every
+    cell on its own, and the columns' dtypes are those of the one-row frames: int time_unix, text or NaN
+    cells), split at the markers; a sample of rows is rendered one frame per row and must agree."""
+    import pandas as pd
+    if not recs:
+        return []
+    frame = pd.DataFrame(recs)
+    frame.insert(0, '_m', _MARK)
+    text = frame.to_csv(index=False, header=False).encode('utf-8')
+    mark = (_MARK + ',').encode()
+    assert text.startswith(mark)
+    parts = text[len(mark):].split(b'\n' + mark)
+    lines = [p + b'\n' for p in parts[:-1]] + [parts[-1]]
+    assert len(lines) == len(recs) and lines[-1].endswith(b'\n')
+    rng = np.random.default_rng(len(recs))
+    for j in set(range(min(50, len(recs)))) | set(rng.integers(0, len(recs), 50).tolist()):
+        one = pd.DataFrame([recs[j]]).to_csv(index=False, header=False).encode('utf-8')
+        assert one == lines[j], (j, one[:200], lines[j][:200])
+    return lines
+
+
+def _chunk(lo):
+    import pandas as pd
+    from dateutil import parser
+    from tests import bytes_digest as bd
+    csv = chunk_csv_bytes(lo, CHUNK, _W['nk'])
+    df = pd.read_csv(io.BytesIO(csv))
+    O, tix = _W['oracle'], _W['tickers']
+    recs, docs, tis = [], [], []
+    for i, (_idx, row) in enumerate(df.iterrows()):                       # :149
+        text = str(row['article_text']) if row['article_text'] else ''    # :150
+        title = str(row['title']) if row['title'] else ''                 # :151
+        date = parser.parse(str(row['date_time'])) if pd.notna(row['date_time']) else None   # :152
+        tm = O.ticker_matches(text, title, date)                          # :153-187
+        if not tm:
+            continue
+        stamp = int(parser.parse(row['date_time']).timestamp())           # :131-132 (the same for each ticker)
+        for ticker, m in tm.items():                                      # :189-192
+            recs.append({'time_unix': stamp, 'date_time': row['date_time'],               # :134-143
+                         'text_matches': json.dumps(m['text']), 'title_matches': json.dumps(m['title']),
+                         'title': row['title'], 'url': row['url'], 'source': row['source'],
+                         'source_url': row['source_url'], 'article_text': row['article_text']})
+            docs.append(lo + i)
+            tis.append(tix[ticker])
+    lines = _render(recs)
+    per_ticker = {}
+    for line, t in zip(lines, tis):
+        per_ticker.setdefault(t, []).append(line)
+    lens = np.fromiter((len(x) for x in lines), dtype=np.int64, count=len(lines))
+    off = np.zeros(len(lines) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    bh = bd.bytehash_np(np.frombuffer(b''.join(lines), dtype=np.uint8), off) if lines else np.zeros(0, np.uint64)
+    vals = bd.line_values(bh, lens, np.asarray(tis, np.int64), np.asarray(docs, np.int64))
+    dig, cnt = bd.block_sums(vals, np.asarray(docs, np.int64), lo, CHUNK // DBLOCK, DBLOCK)
+    return lo, hashlib.sha256(csv).hexdigest(), dig, cnt, {_W['names'][t]: b''.join(v) for t, v in per_ticker.items()}
+
+
+def _sort_one(path):
+    """The reference's sort_matched_csv (:195-217) on one file; (sha256, bytes) after it."""
+    os.environ['TZ'] = 'UTC'
+    time.tzset()
+    from tests.golden.make_golden import _stub_rapidfuzz
+    _stub_rapidfuzz()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import match_keywords as ref      # the reference, imported (not copied)
+    with contextlib.redirect_stdout(io.StringIO()):
+        ref.sort_matched_csv(path)
+    data = open(path, 'rb').read()
+    return os.path.basename(path), hashlib.sha256(data).hexdigest(), len(data)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--procs', type=int, default=6)
+    ap.add_argument('--docs', type=int, default=SPAN_DOCS)
+    ap.add_argument('--out', default=os.path.join(HERE, 'c3_csv'))
+    args = ap.parse_args()
+    os.environ['TZ'] = 'UTC'
+    time.tzset()
+    from tests import golden_data
+    n = args.docs
+    assert n % CHUNK == 0
+    tickers = list(golden_data.kb_processed())
+    work = os.path.join(HERE, '_local', 'n1')
+    shutil.rmtree(work, ignore_errors=True)
+    os.makedirs(work)
+    header = (','.join(COLUMNS) + '\n').encode()        # pandas' header line of the :144 frame
+    nb = n // DBLOCK
+    dig = np.zeros(nb, np.uint64)
+    cnt = np.zeros(nb, np.int64)
+    chain = hashlib.sha256()
+    sha = {}
+    size = {}
+    rows = {}
+    t0 = time.time()
+    with mp.get_context('spawn').Pool(args.procs, initializer=_init) as pool:
+        for k, (lo, csv_sha, d, c, per) in enumerate(pool.imap(_chunk, range(0, n, CHUNK))):   # document order
+            b = lo // DBLOCK
+            dig[b:b + len(d)] = d
+            cnt[b:b + len(c)] = c
+            chain.update(bytes.fromhex(csv_sha))
+            for t in tickers:                                   # KB order: files are distinct, order is immaterial
+                data = per.get(t)
+                if data is None:
+                    continue
+                path = os.path.join(work, f'{t}_match.csv')
+                if t not in sha:
+                    sha[t] = hashlib.sha256(header)
+                    size[t] = len(header)
+                    rows[t] = 0
+                    with open(path, 'wb') as fh:
+                        fh.write(header)
+                with open(path, 'ab') as fh:
+                    fh.write(data)
+                sha[t].update(data)
+                size[t] += len(data)
+                rows[t] += data.count(b'\n')     # informational only (article text may hold newlines)
+            if k % 25 == 0:
+                print(f'{k + 1}/{n // CHUNK} chunks, {time.time() - t0:.0f} s', flush=True)
+    t1 = time.time()
+    files = {f'{t}_match.csv': {'appended_sha256': sha[t].hexdigest(), 'appended_bytes': size[t]} for t in sha}
+    with mp.get_context('spawn').Pool(min(args.procs, 4)) as pool:
+        for name, s, nbytes in pool.imap_unordered(_sort_one, [os.path.join(work, f) for f in files]):
+            files[name]['sorted_sha256'] = s
+            files[name]['sorted_bytes'] = nbytes
+    shutil.rmtree(work, ignore_errors=True)
+    np.savez_compressed(args.out + '.npz', digest=dig, count=cnt.astype(np.uint32))
+    with np.errstate(over='ignore'):
+        total = f'{int(dig.sum(dtype=np.uint64)):016x}'
+    meta = {'generator': 'tests/golden/make_n1_digests.py (CPU oracle ticker_matches + append_to_csv rows by '
+                         'pandas; sort by the reference sort_matched_csv)',
+            'seed': SEED, 'n_docs': n, 'chunk_rows': CHUNK, 'docs_per_block': DBLOCK, 'span_docs': SPAN_DOCS,
+            'kb': 'tests/golden/kb_processed.json.gz', 'csv_chain_sha256': chain.hexdigest(),
+            'total_rows': int(cnt.sum()), 'rows_digest': total, 'n_files': len(files),
+            'files_sorted_unchanged': sum(f['sorted_sha256'] == f['appended_sha256'] for f in files.values()),
+            'oracle_seconds': round(t1 - t0, 1), 'sort_seconds': round(time.time() - t1, 1), 'procs': args.procs,
+            'files': dict(sorted(files.items()))}
+    with open(args.out + '.json', 'w') as fh:
+        json.dump(meta, fh, indent=1)
+    print(json.dumps({k: v for k, v in meta.items() if k != 'files'}, indent=1))
+
+
+if __name__ == '__main__':
+    main()

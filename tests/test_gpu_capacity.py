@@ -1,0 +1,91 @@
+"""GPU parity at the scan's capacity boundaries, forced small through the library's test overrides.
+
+Each scratch region of a scan (csrc/kwmatch.hip launch_scan) has a capacity sized from the corpus; when a
+region overflows, the scan either grows it and rescans, or defers the affected documents to the generic kernel.
+The golden and the adversarial corpora rarely reach these paths, so here each capacity is set tiny
+(KW_TEST_* overrides, honoured under KW_TEST_HOOKS=1, tests/conftest.py) on a fresh handle, and the results
+must still equal the CPU oracle (match_keywords.py:155-180 per field) while the statistics show that the path
+ran:
+
+* KW_TEST_CAND_CAP   the filter's candidate regions overflow -> ST_CAND_OVERFLOW -> larger regions, rescan
+* KW_TEST_ITEM_CAP   the probe's item regions overflow: the batches that do not fit defer their documents
+                     (nothing reads items that were not written), then larger regions, rescan
+* KW_TEST_ITEM_LIMIT the item index limit (2^32 in production) reached: no growth, the overflowing batches'
+                     documents go to the generic kernel in the same scan
+* KW_TEST_TASK_CAP   the verify / short / regex task queues overflow -> ST_TASK_OVERFLOW -> rescan
+* KW_TEST_DSET_SIZE  the decided (doc, field, name) set fills -> ST_DSET_FULL -> rescan
+"""
+import pytest
+
+from tests.test_gpu_parity import _adversarial_strings, _compare, _golden_rows, _gpu_maps, _many_item_docs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def corpus(golden):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    processed = golden.kb_processed()
+    ckb = compile_kb(processed)
+    texts, titles, _ = _golden_rows(golden)
+    a_t, a_i = _adversarial_strings(ckb)
+    m_t, m_i = _many_item_docs(ckb)
+    names, kinds = synth.injectable_names(ckb)
+    c = synth.generate(600, names, kinds, seed=31, doc_base=7000)
+    return {'processed': processed, 'ckb': ckb,
+            'texts': texts + a_t + m_t + c.texts(), 'titles': titles + a_i + m_i + c.titles()}
+
+
+def _run(corpus, monkeypatch, **env):
+    from advanced_scrapper_amd.matcher import GpuMatcher
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    m = GpuMatcher(corpus['ckb'])            # a fresh handle: its regions start at the forced sizes
+    got = _gpu_maps(m, corpus['texts'], corpus['titles'])
+    bad = _compare(corpus['processed'], corpus['texts'], corpus['titles'], got)
+    st = m.stats()
+    assert not bad, f"{env}: GPU differs from the oracle on docs {bad[:20]} (stats {st})"
+    return st
+
+
+def test_baseline_no_overrides(corpus, monkeypatch):
+    st = _run(corpus, monkeypatch)
+    assert st['rescans'] == 0
+
+
+def test_candidate_region_overflow_rescans(corpus, monkeypatch):
+    st = _run(corpus, monkeypatch, KW_TEST_CAND_CAP=16)
+    assert st['rescans'] >= 1
+
+
+def test_item_region_overflow_defers_then_grows(corpus, monkeypatch):
+    st = _run(corpus, monkeypatch, KW_TEST_ITEM_CAP=8)
+    assert st['rescans'] >= 1
+
+
+def test_item_index_limit_defers_to_generic(corpus, monkeypatch):
+    """No growth past the item index limit: the documents of every batch that did not fit its region are
+    finished by the generic kernel in the same scan (results exact, deferred_docs > 0)."""
+    st = _run(corpus, monkeypatch, KW_TEST_ITEM_LIMIT=1024)
+    assert st['deferred_docs'] > 0
+
+
+def test_task_queue_overflow_rescans(corpus, monkeypatch):
+    st = _run(corpus, monkeypatch, KW_TEST_TASK_CAP=2)
+    assert st['rescans'] >= 1
+
+
+def test_decided_set_full_rescans(corpus, monkeypatch):
+    st = _run(corpus, monkeypatch, KW_TEST_DSET_SIZE=4)
+    assert st['rescans'] >= 1
+
+
+def test_overrides_ignored_without_the_gate(corpus, monkeypatch):
+    """A production process (no KW_TEST_HOOKS) ignores the overrides: no rescans."""
+    monkeypatch.delenv('KW_TEST_HOOKS', raising=False)
+    st = _run(corpus, monkeypatch, KW_TEST_CAND_CAP=16, KW_TEST_TASK_CAP=2)
+    assert st['rescans'] == 0

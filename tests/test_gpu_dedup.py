@@ -159,3 +159,57 @@ def test_scale_determinism_and_sample_parity(gpu):
     want = np.array([1 if i in kept else (0 if keys[i] is None and dd._HTML.search(urls[i]) is None
                                           else (2 if keys[i] is None else 3)) for i in range(u.n)], dtype=np.uint8)
     assert np.array_equal(c1, want)
+
+
+def test_c5_500m_rows_vs_oracle_digest(gpu):
+    """Config 5 at its stated size (BASELINE.json configs[4]): bench.py's 500M synthetic CDX rows, one kw_dedup_run.
+
+    Pinned by tests/golden/c5_digest.json (make_c5_digest.py: the CPU oracle's url_transform + keep-first over
+    the same 500M rows, hash-partitioned in the build container): the four row counts, the kept bytes and the
+    order-independent digests of the kept row indices and of the kept normalised URL bytes
+    (tests/bytes_digest.py).  Properties at full size: a second run gives the same codes, the kept rows come in
+    row order, and the kept normalised URLs are pairwise distinct (device sort of their byte hashes; equal
+    hashes are compared byte for byte)."""
+    import torch
+    from advanced_scrapper_amd import synth
+    from tests import bytes_digest as bd
+    meta = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'c5_digest.json')))
+    n = meta['rows']
+    u = synth.generate_urls(n, seed=meta['seed'], n_articles=meta['n_articles'])
+    d_a, d_o = gpu.upload(u.arena, u.off)
+    del u
+    c1 = gpu.run(d_a, d_o, n)
+    counts = gpu.counts()
+    want = meta['counts']
+    assert counts == [want['no_html'], want['kept'], want['filtered'], want['duplicate']], (counts, want)
+    b, o, r = gpu.kept_device()
+    assert len(r) == want['kept'] and len(b) == meta['kept_bytes']
+    assert bool((r[1:] > r[:-1]).all())
+    rows = r.cpu().numpy()
+    assert f'{bd.row_digest(rows):016x}' == meta['row_digest']
+    del rows
+    w = torch.from_numpy(bd.weights().view(np.int64)).to(b.device)
+    step = 4_000_000
+    bh = torch.empty(len(r), dtype=torch.int64, device=b.device)
+    for lo in range(0, len(r), step):
+        hi = min(lo + step, len(r))
+        bh[lo:hi] = bd.bytehash_torch(b, o, lo, hi, w)
+    lens = (o[1:] - o[:-1]).cpu().numpy()
+    bh_h = bh.cpu().numpy().view(np.uint64)
+    assert f'{bd.bytes_digest(bh_h, lens):016x}' == meta['bytes_digest']
+    # distinct kept URLs: equal (hash, length) pairs must differ in their bytes
+    key = torch.from_numpy(bd.row_value(bh_h, lens).view(np.int64)).to(b.device)
+    del bh_h, lens
+    sk, perm = torch.sort(key)
+    same = torch.nonzero(sk[1:] == sk[:-1]).flatten()
+    oh = o.cpu()
+    for i in same.cpu().tolist()[:1000]:
+        x, y = int(perm[i]), int(perm[i + 1])
+        bx = bytes(b[oh[x]:oh[x + 1]].cpu().numpy())
+        by = bytes(b[oh[y]:oh[y + 1]].cpu().numpy())
+        assert bx != by, f'kept rows {int(r[x])} and {int(r[y])} have the same normalised URL'
+    assert len(same) <= 1000
+    del sk, perm, key, bh, b, o, r
+    c2 = gpu.run(d_a, d_o, n)
+    assert torch.equal(c1, c2)
+    assert gpu.counts() == counts

@@ -184,7 +184,7 @@ def test_native_dates_equal_parse_date(monkeypatch):
     assert ok.tolist() == [d is not None for d in want]
     assert [int(u) for u, d in zip(us, want) if d is not None] == [epoch_us(d) for d in want if d is not None]
     rows_ = [i for i, d in enumerate(want) if d is not None]
-    assert got.utc_stamps(rows_).tolist() == [int(want[i].timestamp()) for i in rows_]
+    assert got.utc_stamps(rows_)[0].tolist() == [int(want[i].timestamp()) for i in rows_]
     monkeypatch.setenv('TZ', 'America/New_York')
     time.tzset()
     try:
