@@ -186,8 +186,9 @@ def test_c4_whole_corpus_vs_oracle_digests():
 def test_c4_ten_million_vs_oracle():
     """Config 4 at its stated size: the ~52k-name KB against 10M articles in ONE kw_scan (~22.9 GB resident).
     Documents 0..999 999 per document against tests/golden/c4_digests.npz, and the strided 1000-document
-    blocks beyond 1M that tests/golden/c4_blocks.npz pins (make_c2_digests.py --config 4 --strided 10
-    --lo 1000000 --docs 10000000 --blocks c4_blocks, CPU oracle in the build container)."""
+    blocks beyond 1M that tests/golden/c4_blocks.npz pins (make_c2_digests.py --config 4 --strided 200
+    --lo 1000000 --docs 10000000 --blocks c4_blocks, CPU oracle in the build container: 208 blocks, 2.3 % of
+    the documents beyond 1M)."""
     import time
     import numpy as np
     import torch
@@ -223,7 +224,7 @@ def test_c4_ten_million_vs_oracle():
     bcnt = cnt.reshape(-1, blk).sum(axis=1)
     sel = z['block'].astype(np.int64)
     beyond = sel[sel >= 1_000_000 // blk]
-    assert len(beyond) >= 10
+    assert len(beyond) >= 200
     badb = np.flatnonzero((bdig[sel] != z['digest']) | (bcnt[sel] != z['count'].astype(np.int64)))
     if len(badb):
         lo = int(sel[badb[0]]) * blk
