@@ -50,7 +50,10 @@ EXPORTS = ('kw_compile', 'kw_scan', 'kw_hits', 'kw_hits_copy', 'kw_stats', 'kw_l
 # KW_URL_* row codes (include/kwdedup.h)
 KW_URL_NO_HTML, KW_URL_KEPT, KW_URL_FILTERED, KW_URL_DUPLICATE = 0, 1, 2, 3
 KW_DEDUP_NORMALIZE = 1
-KW_N_STATS = 20
+KW_N_STATS = 21
+# KW_RESCAN_* bits of stats[20] (include/kwmatch.h)
+KW_RESCAN_GENERIC_ITEMS, KW_RESCAN_RESULTS, KW_RESCAN_GENERIC_CPS = 1, 2, 4
+KW_RESCAN_REGEX_QUEUE, KW_RESCAN_TASK_QUEUES, KW_RESCAN_DECIDED_SET, KW_RESCAN_REGIONS = 16, 32, 64, 128
 KW_COMM_ID_BYTES = 128
 KW_ROUTE_SCAN, KW_ROUTE_RESOLVE, KW_ROUTE_GENERIC, KW_ROUTE_TRANSCODE = 0, 1, 2, 3
 KW_PLAN_SEND, KW_PLAN_RECV = 1, 2

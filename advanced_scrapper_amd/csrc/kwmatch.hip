@@ -86,6 +86,7 @@ struct kw_handle {
     int64_t n_hits = 0;
     unsigned long long stats[KW_N_STATS] = {0};
     int rescans = 0;   // scans of the last kw_scan's batch redone after growing a buffer
+    uint32_t rescan_causes = 0;   // the ST_* overflow bits that made them (= the KW_RESCAN_* bits)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     int cus = 256;
     int blocks_per_cu = 2;
@@ -1451,6 +1452,7 @@ extern "C" int kw_scan(kw_handle *h, const uint8_t *d_arena, const int64_t *d_do
     h->scanned = true;
     h->fetched = false;
     h->rescans = 0;
+    h->rescan_causes = 0;
     return launch_scan(h);
 }
 
@@ -1560,6 +1562,7 @@ static int finish(kw_handle *h)
             int rc = ensure_scratch(h, w);
             if (rc) return rc;
             ++h->rescans;
+            h->rescan_causes |= status[0] & ~ST_FIELD_TOO_LONG;
             rc = launch_scan(h);
             if (rc) return rc;
             continue;
@@ -1596,6 +1599,7 @@ static int finish(kw_handle *h)
             int rc = ensure_scratch(h, w);
             if (rc) return rc;
             ++h->rescans;
+            h->rescan_causes |= status[0] & ~ST_FIELD_TOO_LONG;
             rc = launch_scan(h);
             if (rc) return rc;
             continue;
@@ -1608,6 +1612,7 @@ static int finish(kw_handle *h)
         h->stats[3] = fst[3];
         for (int i = 4; i < KW_N_STATS; ++i) h->stats[i] = fst[i];
         h->stats[17] = (unsigned long long)h->rescans;
+        h->stats[20] = (unsigned long long)h->rescan_causes;
         {   // the transcoded view: documents it took / left to the resolve kernel; the next scan's capacity
             const unsigned long long used = small[48];
             if (used > h->caps.tx_cap && !kw_env("KW_TEST_TX_CAP")) h->tx_need = used + used / 8;

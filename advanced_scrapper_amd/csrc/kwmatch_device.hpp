@@ -109,6 +109,9 @@ constexpr uint32_t ST_FIELD_TOO_LONG = 8u;
 constexpr uint32_t ST_RX_OVERFLOW = 16u;     // a resolve wave queued more regex searches than rx_cap
 constexpr uint32_t ST_TASK_OVERFLOW = 32u;   // a scan wave made more tasks than a task region holds
 constexpr uint32_t ST_DSET_FULL = 64u;       // the decided-name set is full
+static_assert(KW_RESCAN_GENERIC_ITEMS == 1 && KW_RESCAN_RESULTS == 2 && KW_RESCAN_GENERIC_CPS == 4 &&
+              KW_RESCAN_REGEX_QUEUE == 16 && KW_RESCAN_TASK_QUEUES == 32 && KW_RESCAN_DECIDED_SET == 64 &&
+              KW_RESCAN_REGIONS == 128, "the public rescan bits are the ST_* overflow bits");
 constexpr uint32_t ST_CAND_OVERFLOW = 128u;  // a filter region held more candidates, or a probe region more items, than fit
 
 }  // namespace kw

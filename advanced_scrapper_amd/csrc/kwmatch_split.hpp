@@ -33,6 +33,11 @@ namespace kw {
 #ifndef FS_MINW
 #define FS_MINW 1
 #endif
+#ifndef FS_KEY_REGS
+#define FS_KEY_REGS 0    // 1: stage-2 keys queued from the owner lanes' registers instead of a global load in
+                         // the round: filter 1.44 vs 1.35 ms on MI355X (the key selection's VALU costs more than
+                         // the load's wait: the filter is issue-bound, not latency-bound)
+#endif
 #ifndef FS_AHEAD
 #define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
 #endif
@@ -68,7 +73,23 @@ struct __attribute__((aligned(16))) FilterLds {
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
     uint32_t spos[FS_WAVES][2 * WAVE];        // stage 2: the queue of survivors' group-relative positions (a ring)
+#if FS_KEY_REGS
+    uint32_t skey[FS_WAVES][2 * WAVE];        // ... and their 4-byte keys (from the owner lane's registers)
+#endif
 };
+
+// the 4 bytes at position j (0..15) of a lane's 16 (+4) bytes W[0..4]: the stage-2 key of a survivor, taken
+// from registers when it is queued (a global load in the round would make the wave wait for every tile load
+// in flight: vmcnt counts in order)
+// (two-level selects on the words as values: an indexed W[q] would go through scratch)
+__device__ __forceinline__ uint32_t fk_key_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
+                                              uint32_t j)
+{
+    const bool odd = (j & 4u) != 0, high = (j & 8u) != 0;
+    const uint32_t lo = high ? (odd ? w3 : w2) : (odd ? w1 : w0);
+    const uint32_t hi = high ? (odd ? w4 : w3) : (odd ? w2 : w1);
+    return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
+}
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
 __device__ __forceinline__ uint32_t fg_doc(const uint32_t *dstart, uint32_t nd, uint32_t r)
@@ -178,6 +199,9 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const uint32_t *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
     uint32_t *spos = L.spos[wib];
+#if FS_KEY_REGS
+    uint32_t *skey = L.skey[wib];
+#endif
     uint32_t *cand = S.cand + (size_t)region * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const uint32_t t3on = FT.has_t3 ? 1u : 0u;
@@ -219,9 +243,16 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const bool act = (uint32_t)lane < n;
             const uint32_t slot = (qh + (uint32_t)lane) & (2u * WAVE - 1u);
             const uint32_t r = spos[slot];
+#if FS_KEY_REGS
+            // the 4-byte key at the position (bytes past the group end may differ from the arena's: clamped
+            // loads; no anchor that fits its field reads them, and the 3- and 2-byte filters use the low bytes)
+            const uint32_t key = act ? skey[slot] : 0u;
+            wave_sync();
+#else
             wave_sync();
             // the 4-byte key at the position (the group's bytes were just streamed: a cache hit)
             const uint32_t key = act ? ld_u32_unaligned(arena, gb + (int64_t)r) : 0u;
+#endif
             qh = (qh + n) & (2u * WAVE - 1u);
             qn -= n;
             const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
@@ -308,8 +339,14 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                     int rk = sx;
                     for (uint32_t hm = smp; hm; hm &= hm - 1u) {
                         if (rk >= c0 + take) break;
-                        if (rk >= c0)
-                            spos[(qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u)] = rel + (uint32_t)(__ffs(hm) - 1);
+                        if (rk >= c0) {
+                            const uint32_t j = (uint32_t)(__ffs(hm) - 1);
+                            const uint32_t sl = (qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u);
+                            spos[sl] = rel + j;
+#if FS_KEY_REGS
+                            skey[sl] = fk_key_at(W[0], W[1], W[2], W[3], W[4], j);
+#endif
+                        }
                         ++rk;
                     }
                 }
@@ -321,7 +358,10 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         uint4 v[FS_AHEAD];
         uint32_t w[FS_AHEAD];
 #pragma unroll
-        for (int k = 0; k < FS_AHEAD; ++k) load(v[k], w[k], blk + 1024 * k);
+        for (int k = 0; k < FS_AHEAD; ++k) {   // in tile order: the first tile's wait then leaves the others in flight
+            load(v[k], w[k], blk + 1024 * k);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         for (bool more = true; more;) {
 #pragma unroll
             for (int k = 0; k < FS_AHEAD; ++k) {   // (unrolled: each tile in flight keeps its own registers)

@@ -169,7 +169,7 @@ class GpuMatcher:
     STAT_KEYS = ('candidates', 'anchor_hits', 'lcs_windows', 'verifications', 'deferred_docs', 'deferred_items',
                  'deferred_long_nonascii', 'edge_items', 'candidates_stage2', 'resolved_docs', 'regex_searches',
                  'regex_backtracking', 'regex_rounds', 'deferred_long_run', 'deferred_item_caps', 'deferred_flagged',
-                 'big_docs', 'rescans', 'transcoded_docs', 'resolve_fallback_docs')
+                 'big_docs', 'rescans', 'transcoded_docs', 'resolve_fallback_docs', 'rescan_causes')
 
     def stats(self) -> Dict[str, int]:
         v = np.zeros(_native.KW_N_STATS, dtype=np.int64)

@@ -120,8 +120,17 @@ int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void
  * the batch was scanned again after a device buffer grew (0 once the buffers
  * fit the workload: growth persists across kw_scan calls); documents with a
  * non-ASCII field that [18] the epilogue finished on their transcoded view (one
- * byte per code point) or [19] it left to the resolve kernel. */
-#define KW_N_STATS 20
+ * byte per code point) or [19] it left to the resolve kernel; [20] why the
+ * batch was scanned again: the KW_RESCAN_* bits of every buffer that overflowed
+ * in a scan that was redone. */
+#define KW_N_STATS 21
+#define KW_RESCAN_GENERIC_ITEMS 1   /* the generic kernel's items per field */
+#define KW_RESCAN_RESULTS 2         /* a wave's result region */
+#define KW_RESCAN_GENERIC_CPS 4     /* the generic kernel's code points per field */
+#define KW_RESCAN_REGEX_QUEUE 16    /* a resolve wave's regex-search queue */
+#define KW_RESCAN_TASK_QUEUES 32    /* a scan wave's verify / short / regex task queues */
+#define KW_RESCAN_DECIDED_SET 64    /* the decided (doc, field, name) set */
+#define KW_RESCAN_REGIONS 128       /* a filter region's candidates or a probe region's items */
 int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
 /* Device times (ms) of the last kw_scan, from HIP events on the scan's stream

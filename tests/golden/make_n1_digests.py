@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import functools
 import hashlib
 import io
 import json
@@ -57,13 +58,19 @@ COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', '
 _W = {}
 
 
+@functools.lru_cache(maxsize=1)
+def _names_kinds():
+    from advanced_scrapper_amd import synth
+    from advanced_scrapper_amd.kb import compile_kb
+    from tests import golden_data
+    return synth.injectable_names(compile_kb(golden_data.kb_processed()))
+
+
 def chunk_csv_bytes(lo: int, n: int = CHUNK, names_kinds=None) -> bytes:
     """The article CSV of documents [lo, lo + n) (also used by the GPU test)."""
     from advanced_scrapper_amd import synth
     if names_kinds is None:
-        from advanced_scrapper_amd.kb import compile_kb
-        from tests import golden_data
-        names_kinds = synth.injectable_names(compile_kb(golden_data.kb_processed()))
+        names_kinds = _names_kinds()
     names, kinds = names_kinds
     corpus = synth.generate(n, names, kinds, seed=SEED, doc_base=lo)
     return synth.to_dataframe(corpus, span_docs=SPAN_DOCS).to_csv(index=False).encode('utf-8')

@@ -17,6 +17,8 @@ ran:
 """
 import pytest
 
+from advanced_scrapper_amd import _native
+
 from tests.test_gpu_parity import _adversarial_strings, _compare, _golden_rows, _gpu_maps, _many_item_docs
 
 pytestmark = pytest.mark.gpu
@@ -52,40 +54,52 @@ def _run(corpus, monkeypatch, **env):
     return st
 
 
-def test_baseline_no_overrides(corpus, monkeypatch):
-    st = _run(corpus, monkeypatch)
-    assert st['rescans'] == 0
+@pytest.fixture(scope='module')
+def baseline(corpus):
+    """The corpus without overrides (its many-item documents already grow the generic kernel's buffers once)."""
+    mp = pytest.MonkeyPatch()
+    try:
+        return _run(corpus, mp)
+    finally:
+        mp.undo()
 
 
-def test_candidate_region_overflow_rescans(corpus, monkeypatch):
+def test_baseline_no_overrides(baseline):
+    assert baseline['deferred_docs'] > 0 and baseline['big_docs'] > 0
+    # the corpus alone grows only other buffers: each override below must add its own cause
+    assert not baseline['rescan_causes'] & (_native.KW_RESCAN_REGIONS | _native.KW_RESCAN_TASK_QUEUES |
+                                            _native.KW_RESCAN_DECIDED_SET), baseline
+
+
+def test_candidate_region_overflow_rescans(corpus, baseline, monkeypatch):
     st = _run(corpus, monkeypatch, KW_TEST_CAND_CAP=16)
-    assert st['rescans'] >= 1
+    assert st['rescan_causes'] & _native.KW_RESCAN_REGIONS
 
 
-def test_item_region_overflow_defers_then_grows(corpus, monkeypatch):
+def test_item_region_overflow_defers_then_grows(corpus, baseline, monkeypatch):
     st = _run(corpus, monkeypatch, KW_TEST_ITEM_CAP=8)
-    assert st['rescans'] >= 1
+    assert st['rescan_causes'] & _native.KW_RESCAN_REGIONS
 
 
-def test_item_index_limit_defers_to_generic(corpus, monkeypatch):
+def test_item_index_limit_defers_to_generic(corpus, baseline, monkeypatch):
     """No growth past the item index limit: the documents of every batch that did not fit its region are
     finished by the generic kernel in the same scan (results exact, deferred_docs > 0)."""
     st = _run(corpus, monkeypatch, KW_TEST_ITEM_LIMIT=1024)
-    assert st['deferred_docs'] > 0
+    assert st['deferred_docs'] > baseline['deferred_docs']
 
 
-def test_task_queue_overflow_rescans(corpus, monkeypatch):
+def test_task_queue_overflow_rescans(corpus, baseline, monkeypatch):
     st = _run(corpus, monkeypatch, KW_TEST_TASK_CAP=2)
-    assert st['rescans'] >= 1
+    assert st['rescan_causes'] & _native.KW_RESCAN_TASK_QUEUES
 
 
-def test_decided_set_full_rescans(corpus, monkeypatch):
+def test_decided_set_full_rescans(corpus, baseline, monkeypatch):
     st = _run(corpus, monkeypatch, KW_TEST_DSET_SIZE=4)
-    assert st['rescans'] >= 1
+    assert st['rescan_causes'] & _native.KW_RESCAN_DECIDED_SET
 
 
-def test_overrides_ignored_without_the_gate(corpus, monkeypatch):
-    """A production process (no KW_TEST_HOOKS) ignores the overrides: no rescans."""
+def test_overrides_ignored_without_the_gate(corpus, baseline, monkeypatch):
+    """A production process (no KW_TEST_HOOKS) ignores the overrides: the baseline's statistics."""
     monkeypatch.delenv('KW_TEST_HOOKS', raising=False)
     st = _run(corpus, monkeypatch, KW_TEST_CAND_CAP=16, KW_TEST_TASK_CAP=2)
-    assert st['rescans'] == 0
+    assert st == baseline
