@@ -4,29 +4,36 @@
 // restated in oracle/dedup_oracle.py.  One pass per row (lane per row):
 //
 //   dd_transform_kernel  find the cut (first "html" after a code point that is
-//                        not '\n'), rewrite the prefix (':80' removed, 'http:'
-//                        -> 'https:'), append ".html", flag 'news/%' / "news/'",
-//                        write the normalised URL into a sparse 8-aligned arena
-//                        and hash it (one 64-bit word hash: tag and slot).
-//                        Rows whose only extra ':' is at most one ':80' take a
-//                        word-wide copy; the rest run the byte-serial rewrite.
-//                        Waves claim groups of 64 rows in row order.  Each
-//                        kept row is inserted at once (table_insert):
-//                        open-addressing slots {tag, position}, the first
-//                        inserter claims a slot by CAS, an earlier row
-//                        displaces the holder by atomicMin (keep='first'); a
-//                        row that finds an earlier holder keeps its position
-//                        as its hint, a displaced holder gets a `moved` bit.
+//                        not '\n'), plan the rewrite of the prefix (':80'
+//                        removed, 'http:' -> 'https:', ".html" appended), flag
+//                        'news/%' / "news/'", and hash the normalised URL's
+//                        words (one 64-bit word hash: tag and slot).  Nothing
+//                        of the normalised URL is stored: a row keeps its PLAN
+//                        (the cut, the 's' insertion, the one ':80' gap), from
+//                        which any later kernel regenerates its words from the
+//                        raw bytes (RowGen).  Rows whose only extra ':' is at
+//                        most one ':80' take the word-wide plan; the rest run
+//                        the byte-serial rewrite (dd_slow_kernel), whose bytes
+//                        go to a small slow-row arena.  Waves claim groups of
+//                        64 rows in row order.  Each kept row is inserted at
+//                        once (table_insert): open-addressing slots {tag, row},
+//                        the first inserter claims a slot by CAS, an earlier
+//                        row displaces the holder by atomicMin (keep='first');
+//                        a row that finds an earlier holder keeps that row as
+//                        its hint, a displaced holder gets a `moved` bit.
 //   dd_decide_kernel     a row with a hint is a duplicate iff its normalised
-//                        bytes equal the hinted row's (length, then every
-//                        word); a moved row or a differing one is compared
-//                        with its tag's first row from the table.  Rows that
-//                        share a tag with a different URL are resolved
-//                        exactly on the host.
+//                        bytes equal the hinted row's (length, then every word,
+//                        both regenerated); a moved row or a differing one is
+//                        compared with its tag's first row from the table.
+//                        Rows that share a tag with a different URL are
+//                        resolved exactly on the host.
 //   dd_count / dd_scan / dd_place / dd_copy
-//                        dense offsets, source rows and bytes of the kept rows.
+//                        dense offsets, source rows and bytes of the kept rows
+//                        (the copy regenerates each kept row's words).
 //
-// All byte/integer work: the roofline is HBM bandwidth.
+// All byte/integer work: the roofline is HBM bandwidth.  Round 5: the sparse
+// normalised arena of earlier rounds (73 GB at 500M rows, written by the
+// transform and read back by decide and the copy) is gone.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -51,16 +58,11 @@ constexpr uint32_t NEWS4 = 0x7377656Eu;            // "news"
 constexpr uint64_t DOTHTML = 0x6C6D74682Eull;      // ".html"
 constexpr uint8_t CODE_COLLIDE = 4;                // internal: tag shared with a different URL
 
-// sparse output arena: row i's normalised URL starts at obase(off[i], i) (8-aligned, room for
-// len + len/5 + 16 bytes: at most one extra 's' per 5 input bytes, ".html", word padding), after an 8-byte
-// header word holding its length (a duplicate's compare reads the rep's length with its first bytes)
-__host__ __device__ __forceinline__ int64_t obase(int64_t off_i, int64_t i)
-{
-    return ((off_i + off_i / 5 + 32 * i + 7) & ~(int64_t)7) + 8;
-}
-constexpr uint64_t NO_HINT = ~0ull;
-constexpr int POS_BITS = 35;                        // a table slot: hash tag (29 bits) | sparse position / 8
-constexpr uint64_t POS_MASK = (1ull << POS_BITS) - 1;
+constexpr uint32_t NO_HINT = 0xFFFFFFFFu;         // a kept row that took its tag's slot
+constexpr uint32_t SLOW_ROW = 0xFFFFFFFFu;        // plan.x of a byte-serial row (plan.y: its slow-arena word)
+constexpr uint32_t NO_GAP = 0x7FFFFFFFu;          // plan.y bits 0..30 without a ':80' gap
+constexpr uint32_t LEN_BIG = 0xFFFFFFu;           // rowd's 24-bit length field of a longer row (len3 holds it)
+// a table slot: the hash's high 32 bits (tag) | the row + 1 (0: empty)
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *__restrict__ a, int64_t p)
 {
@@ -101,20 +103,23 @@ __host__ __device__ __forceinline__ uint64_t fmix(uint64_t h)
 }
 
 struct Scratch {
-    uint8_t *out;            // sparse normalised URLs
+    uint4 *rowd;             // per kept row, what RowGen needs in one 16-byte load: x, y[7:0] = the raw start
+                             //   (40 bits), y[31:8] = the normalised length (LEN_BIG: see len3); z, w = the plan:
+                             //   z = the cut j (raw: the length; SLOW_ROW), w = 's' insertion << 31 | the ':80'
+                             //   gap's raw position (NO_GAP) (a slow row: its slow-arena word)
     uint32_t *len3;          // per row: normalised length
     unsigned long long *table;
-    uint64_t *hint;          // per kept row: the sparse position of an earlier row with its tag, or NO_HINT
-    uint32_t *moved;         // bit per sparse 8-byte word: the row starting there lost its slot to an earlier row
+    uint32_t *hint;          // per kept row: an earlier row with its tag, or NO_HINT
+    uint32_t *moved;         // bit per row: the row lost its slot to an earlier row
     uint64_t mask;
     unsigned long long *cnt;   // [0..4] per code
     unsigned long long *gnext;   // the transform's next group of 64 rows
     int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
     int stats;               // KW_DEDUP_STATS: count the rows decide looks up in the table (cnt[5] moved, [6] other)
     int normalize;           // KW_DEDUP_NORMALIZE: apply :63-76; else keep-first over the raw strings
-    uint2 *slow;             // rows (index, cut) for the byte-serial rewrite: slow_cap per transform wave
-    uint32_t *wslow;         // per transform wave: its slow rows (no shared counter: one address for every
-    uint32_t slow_cap;       //   wave's atomic serialised the transform)
+    uint2 *slow;             // rows (index, cut) for the byte-serial rewrite (capacity: every row)
+    unsigned long long *nslow;   // [0] slow rows listed, [1] slow-arena words they may need, [2] words handed out
+    uint64_t *sarena;        // the slow rows' normalised words (sized after the transform from nslow[1])
 };
 
 // byte-serial writer of the normalised URL: 8-byte words to the sparse arena + hashes + filter window
@@ -216,35 +221,35 @@ struct LdsSrc {
     }
 };
 
-// Open-addressing table of 64-bit slots {tag, position}: the first inserter of a tag claims a slot by CAS, an
-// earlier row (smaller position: obase grows with the row) displaces the holder by atomicMin, so the slot ends
-// with the tag's first row (keep='first').  Every kept row writes its own hint: the position of the earlier
-// holder it found, or NO_HINT when it took the slot; a row that displaces the holder sets the holder's bit in
-// `moved` (each row leaves its slot at most once).  The plain load is only a hint of the slot (a slot's tag
-// never changes once claimed; its position only decreases).  Nothing another row wrote in this kernel is read
-// (no cross-XCD visibility is assumed): decide reads the hints, bits and bytes after the kernel boundary.
-__device__ __forceinline__ void table_insert(const Scratch &S, uint64_t h, int64_t i, int64_t pos)
+// Open-addressing table of 64-bit slots {tag, row}: the first inserter of a tag claims a slot by CAS, an earlier
+// row (smaller index) displaces the holder by atomicMin, so the slot ends with the tag's first row
+// (keep='first').  Every kept row writes its own hint: the earlier holder it found, or NO_HINT when it took the
+// slot; a row that displaces the holder sets the holder's bit in `moved` (each row leaves its slot at most once).
+// The plain load is only a hint of the slot (a slot's tag never changes once claimed; its row only decreases).
+// Nothing another row wrote in this kernel is read (no cross-XCD visibility is assumed): decide reads the
+// hints, bits and plans after the kernel boundary.
+__device__ __forceinline__ void table_insert(const Scratch &S, uint64_t h, int64_t i)
 {
-    const unsigned long long key = ((h >> POS_BITS) << POS_BITS) | ((uint64_t)pos >> 3);
+    const unsigned long long key = ((h >> 32) << 32) | (uint64_t)((uint32_t)i + 1u);   // (row + 1: 0 is empty)
     uint64_t slot = (h ^ (h >> 29)) & S.mask;
     unsigned long long cur = S.table[slot];
-    uint64_t hint = NO_HINT;
+    uint32_t hint = NO_HINT;
     for (;;) {
         if (cur == 0ull) {
             cur = atomicCAS(&S.table[slot], 0ull, key);
             if (cur == 0ull) break;
             continue;   // claimed meanwhile: look at the claimer
         }
-        if ((cur >> POS_BITS) == (key >> POS_BITS)) {
+        if ((cur >> 32) == (key >> 32)) {
             if (cur > key) {
                 cur = atomicMin(&S.table[slot], key);
                 if (cur > key) {   // displaced the holder
-                    const uint64_t q = cur & POS_MASK;
-                    atomicOr(&S.moved[q >> 5], 1u << (uint32_t)(q & 31));
+                    const uint32_t q = (uint32_t)cur - 1u;
+                    atomicOr(&S.moved[q >> 5], 1u << (q & 31u));
                     break;
                 }
             }
-            hint = (cur & POS_MASK) << 3;
+            hint = (uint32_t)cur - 1u;
             break;
         }
         slot = (slot + 1) & S.mask;
@@ -253,26 +258,31 @@ __device__ __forceinline__ void table_insert(const Scratch &S, uint64_t h, int64
     S.hint[i] = hint;
 }
 
-// finish a row: hashes, length (also in the header word before its bytes at out), code; a kept row goes into
-// the table
+// finish a row: hash, length, code; a kept row goes into the table
 __device__ __forceinline__ void finish_row(uint64_t h1, int64_t len3, bool bad, int64_t i,
-                                           uint8_t *__restrict__ code, const Scratch &S, uint8_t *out)
+                                           uint8_t *__restrict__ code, const Scratch &S, int64_t b, uint2 pl)
 {
     h1 = fmix(h1 ^ (uint64_t)len3);
     if (S.weak) h1 &= 0xFull;
     S.len3[i] = (uint32_t)len3;
-    *(uint64_t *)(out - 8) = (uint64_t)len3;
+    const uint32_t l24 = len3 < (int64_t)LEN_BIG ? (uint32_t)len3 : LEN_BIG;
+    S.rowd[i] = make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32) | (l24 << 8), pl.x, pl.y);
     code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
-    if (!bad) table_insert(S, h1, i, out - S.out);
+    if (!bad) table_insert(S, h1, i);
 }
 
-// the general rewrite of the cut prefix u[0, j), byte by byte (rows with ':80' or a second 'http:')
+// slow-arena words a byte-serial row of cut j may need (one extra 's' per 5 bytes, ".html", a partial word)
+__host__ __device__ __forceinline__ uint64_t slow_words(int64_t j) { return (uint64_t)((j + j / 5 + 5 + 7) / 8 + 1); }
+
+// the general rewrite of the cut prefix u[0, j), byte by byte (rows with ':80' or a second 'http:'), into the
+// slow arena
 __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j, int64_t i,
                          uint8_t *__restrict__ code, const Scratch &S)
 {
+    const unsigned long long w0 = atomicAdd(&S.nslow[2], (unsigned long long)slow_words(j));
     Emit Em;
     Em.w = 0; Em.win = 0; Em.h1 = 0x243F6A8885A308D3ull;
-    Em.pos = 0; Em.len = 0; Em.nb = 0; Em.bad = false; Em.out = S.out + obase(b, i);
+    Em.pos = 0; Em.len = 0; Em.nb = 0; Em.bad = false; Em.out = (uint8_t *)(S.sarena + w0);
     Rewrite R;
     R.P = 0; R.np = 0; R.Q = 0; R.nq = 0;
     for (int64_t t = 0; t < j; t += 4) {
@@ -283,13 +293,85 @@ __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j
     R.flush(Em);
     Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
     Em.finish();
-    finish_row(Em.h1, Em.len, Em.bad, i, code, S, Em.out);
+    finish_row(Em.h1, Em.len, Em.bad, i, code, S, b, make_uint2(SLOW_ROW, (uint32_t)w0));
 }
+
+// The normalised words of a row of the fast path, from its raw bytes and its plan: the prefix u[0, j) with
+// "https" for a leading "http:" (ins), minus at most one ':80' (the gap G, in normalised coordinates), then
+// ".html" at E.  Used by the transform (to hash) and by decide / the copy / the host's exact pass (to compare
+// and write): one definition of the normalised bytes.
+template <class Src>
+struct FastWords {
+    const Src &src;
+    int64_t b, G, E;
+    int ins;
+    __device__ __forceinline__ uint64_t body(int64_t x) const   // bytes [x, x + 8) of the prefix, x < E, x % 8 == 0
+    {
+        uint64_t w = (ins && x == 0) ? 0x7370747468ull | (src.ld64(b + 4) << 40)   // "https" + u[4..7)
+                                     : src.ld64(b + x - ins + (x >= G ? 3 : 0));
+        if (x < G && G < x + 8) {
+            const int k = (int)(G - x) * 8;
+            w = (w & ((1ull << k) - 1)) | (src.ld64(b + G - ins + 3) << k);
+        }
+        return w;
+    }
+    __device__ __forceinline__ uint64_t splice(uint64_t w, int64_t x) const   // ".html" at E, zeros after it
+    {
+        if (E < x + 8) {
+            if (E >= x) {
+                const int sh = (int)(E - x) * 8;
+                w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
+            } else {
+                const int64_t d = x - E;
+                w = d < 8 ? DOTHTML >> (8 * d) : 0ull;
+            }
+        }
+        return w;
+    }
+    __device__ __forceinline__ uint64_t word(int64_t x) const { return splice(x < E ? body(x) : 0ull, x); }
+};
+
+// Any kept row's normalised words, regenerated (RowGen::word: 8-aligned x; zeros past the length)
+struct RowGen {
+    const uint8_t *a;
+    const uint64_t *sw;   // a slow row's words
+    int64_t b, G, E;
+    uint32_t len;
+    int ins, raw;
+    __device__ __forceinline__ void init(const Scratch &S, const uint8_t *arena, uint4 r, int64_t i)
+    {
+        const uint2 pl = make_uint2(r.z, r.w);
+        a = arena;
+        b = (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x);
+        len = r.y >> 8;
+        if (len == LEN_BIG) len = S.len3[i];
+        raw = !S.normalize;
+        sw = (!raw && pl.x == SLOW_ROW) ? S.sarena + pl.y : nullptr;
+        ins = (int)(pl.y >> 31);
+        const uint32_t ec = pl.y & NO_GAP;
+        const bool gap = ec != NO_GAP;
+        G = gap ? (int64_t)ec + ins : INT64_MAX / 2;
+        E = (int64_t)pl.x + ins - (gap ? 3 : 0);
+    }
+    __device__ __forceinline__ uint64_t word(int64_t x) const
+    {
+        if (x >= (int64_t)len) return 0ull;
+        if (sw) return sw[x >> 3];
+        if (raw) {
+            const uint64_t w = ld64(a, b + x);
+            return len - x >= 8 ? w : w & ((1ull << (8 * (len - x))) - 1);
+        }
+        const GlobalSrc src{a};
+        const FastWords<GlobalSrc> F{src, b, G, E, ins};
+        return F.word(x);
+    }
+    __device__ __forceinline__ uint32_t byte(int64_t y) const { return (uint32_t)(word(y & ~(int64_t)7) >> (8 * (y & 7))) & 0xFFu; }
+};
 
 // one row: returns -1 when done, or the cut j of a row that needs slow_row
 template <class Src>
 __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int64_t L, int64_t i,
-                                                 uint8_t *__restrict__ code, const Scratch &S, uint8_t *out)
+                                                 uint8_t *__restrict__ code, const Scratch &S)
 {
     if (!S.normalize) {
         // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
@@ -297,10 +379,9 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
         for (int64_t x0 = 0; x0 < L; x0 += 8) {
             uint64_t w = src.ld64(b + x0);
             if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
-            *(uint64_t *)(out + x0) = w;
             h1 = mix1(h1, w);
         }
-        finish_row(h1, L, false, i, code, S, out);
+        finish_row(h1, L, false, i, code, S, b, make_uint2((uint32_t)L, NO_GAP));
         return -1;
     }
     // ---- pass 1: the cut j, the first two extra ':' and the first 'news/%' | "news/'" end, one 4-byte word a
@@ -364,77 +445,50 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
         S.len3[i] = 0;
         return -1;
     }
-    uint64_t h1 = 0x243F6A8885A308D3ull;
-    int64_t len3;
-    bool bad;
     const bool gap = ec < j;
-    if (!gap || (ec2 >= j && ec > 5 && ec + 3 <= j && (src.ld32(b + ec) & 0xFFFFFFu) == 0x30383Au)) {
-        // ---- fast path: the prefix u[0, j) minus at most one ':80' after the scheme (a splice with one gap at
-        // G; with no other extra ':' left neither a new ':80' nor a new 'http:' can form), 'http:' -> 'https:'
-        // at the scheme, ".html" at E.  Every lane runs the same word loop; only the filter window across the
-        // gap is extra work for the gap rows
-        const int ins = (scheme_http && j > 4) ? 1 : 0;
-        const int64_t G = gap ? ec + ins : INT64_MAX / 2, E = j + ins - (gap ? 3 : 0);
-        len3 = E + 5;
-        auto body = [&](int64_t x) -> uint64_t {   // bytes [x, x + 8) of the normalised prefix, x < E, x % 8 == 0
-            uint64_t w = (ins && x == 0) ? 0x7370747468ull | (src.ld64(b + 4) << 40)   // "https" + u[4..7)
-                                         : src.ld64(b + x - ins + (x >= G ? 3 : 0));
-            if (x < G && G < x + 8) {
-                const int k = (int)(G - x) * 8;
-                w = (w & ((1ull << k) - 1)) | (src.ld64(b + G - ins + 3) << k);
-            }
-            return w;
-        };
-        auto splice = [&](uint64_t w, int64_t x) -> uint64_t {   // ".html" at E, zeros after it
-            if (E < x + 8) {
-                if (E >= x) {
-                    const int sh = (int)(E - x) * 8;
-                    w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
-                } else {
-                    const int64_t d = x - E;
-                    w = d < 8 ? DOTHTML >> (8 * d) : 0ull;
-                }
-            }
-            return w;
-        };
-        bool jn = false;
-        if (gap) {
-            // 'news/%' | "news/'" across the gap: windows starting at G - 5 .. G - 1 (G >= 6)
-            auto seg1 = [&](int64_t x) -> uint64_t {   // bytes [x, x + 8) of u[0, ec) after the 's' insertion
-                if (!ins) return src.ld64(b + x);
-                if (x >= 5) return src.ld64(b + x - 1);
-                const uint64_t h0 = 0x7370747468ull | (src.ld64(b + 4) << 40);
-                return x ? (h0 >> (8 * x)) | (src.ld64(b + 7) << (64 - 8 * x)) : h0;
-            };
-            auto nword = [&](int64_t x) -> uint64_t {
-                uint64_t w = 0;
-                if (x < E) {
-                    if (x + 8 <= G) w = seg1(x);
-                    else if (x >= G) w = src.ld64(b + x - ins + 3);
-                    else {
-                        const int k = (int)(G - x) * 8;
-                        w = (seg1(x) & ((1ull << k) - 1)) | (src.ld64(b + G - ins + 3) << k);
-                    }
-                }
-                return splice(w, x);
-            };
-            const uint64_t lo = nword(G - 5), hi = nword(G + 3);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const uint64_t win = ((lo >> (8 * k)) | (k ? hi << (64 - 8 * k) : 0ull)) & 0xFFFFFFFFFFFFull;
-                jn |= win == 0x252F7377656Eull || win == 0x272F7377656Eull;
-            }
-        }
-        bad = kf < j || jn;
-        for (int64_t x0 = 0; x0 < len3; x0 += 8) {
-            const uint64_t w = splice(x0 < E ? body(x0) : 0ull, x0);
-            *(uint64_t *)(out + x0) = w;
-            h1 = mix1(h1, w);
-        }
-    } else {
+    if (gap && !(ec2 >= j && ec > 5 && ec + 3 <= j && (src.ld32(b + ec) & 0xFFFFFFu) == 0x30383Au))
         return j;   // the byte-serial rewrite runs in dd_slow_kernel, off the divergent path
+    // ---- fast path: the prefix u[0, j) minus at most one ':80' after the scheme (a splice with one gap at
+    // G; with no other extra ':' left neither a new ':80' nor a new 'http:' can form), 'http:' -> 'https:'
+    // at the scheme, ".html" at E.  Every lane runs the same word loop; only the filter window across the
+    // gap is extra work for the gap rows
+    const int ins = (scheme_http && j > 4) ? 1 : 0;
+    const int64_t G = gap ? ec + ins : INT64_MAX / 2, E = j + ins - (gap ? 3 : 0);
+    const int64_t len3 = E + 5;
+    const FastWords<Src> F{src, b, G, E, ins};
+    bool jn = false;
+    if (gap) {
+        // 'news/%' | "news/'" across the gap: windows starting at G - 5 .. G - 1 (G >= 6)
+        auto seg1 = [&](int64_t x) -> uint64_t {   // bytes [x, x + 8) of u[0, ec) after the 's' insertion
+            if (!ins) return src.ld64(b + x);
+            if (x >= 5) return src.ld64(b + x - 1);
+            const uint64_t h0 = 0x7370747468ull | (src.ld64(b + 4) << 40);
+            return x ? (h0 >> (8 * x)) | (src.ld64(b + 7) << (64 - 8 * x)) : h0;
+        };
+        auto nword = [&](int64_t x) -> uint64_t {
+            uint64_t w = 0;
+            if (x < E) {
+                if (x + 8 <= G) w = seg1(x);
+                else if (x >= G) w = src.ld64(b + x - ins + 3);
+                else {
+                    const int k = (int)(G - x) * 8;
+                    w = (seg1(x) & ((1ull << k) - 1)) | (src.ld64(b + G - ins + 3) << k);
+                }
+            }
+            return F.splice(w, x);
+        };
+        const uint64_t lo = nword(G - 5), hi = nword(G + 3);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint64_t win = ((lo >> (8 * k)) | (k ? hi << (64 - 8 * k) : 0ull)) & 0xFFFFFFFFFFFFull;
+            jn |= win == 0x252F7377656Eull || win == 0x272F7377656Eull;
+        }
     }
-    finish_row(h1, len3, bad, i, code, S, out);
+    const bool bad = kf < j || jn;
+    uint64_t h1 = 0x243F6A8885A308D3ull;
+    for (int64_t x0 = 0; x0 < len3; x0 += 8) h1 = mix1(h1, F.word(x0));
+    finish_row(h1, len3, bad, i, code, S, b,
+               make_uint2((uint32_t)j, ((uint32_t)ins << 31) | (gap ? (uint32_t)ec : NO_GAP)));
     return -1;
 }
 
@@ -451,9 +505,6 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
     const int wib = threadIdx.x >> 6;
     uint4 *stage = stage_all + wib * (STAGE_BYTES / 16);
     const int64_t n_groups = (n + 63) / 64;
-    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + wib;
-    uint32_t ns = 0;   // this wave's rows for the byte-serial rewrite (wave-uniform)
-    uint2 *wsl = S.slow + (size_t)wave * S.slow_cap;
     // groups of 64 rows claimed from a counter in row order: rows enter the table in about row order, so few
     // earlier duplicates displace a later row already there (grid-stride let waves drift apart: 16-26 % of the
     // duplicates were displaced rows, which decide looks up in the table again)
@@ -481,73 +532,69 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             LdsSrc src{(const uint32_t *)stage, base};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
+            if (i < n) jslow = transform_row(src, b, L, i, code, S);
         } else {
             GlobalSrc src{arena};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S, S.out + obase(b, i));
+            if (i < n) jslow = transform_row(src, b, L, i, code, S);
         }
-        // rows for the byte-serial rewrite -> the wave's slow list
+        // rows for the byte-serial rewrite -> the global slow list (rare rows: one atomic per wave that has any)
         const uint64_t sm = __ballot(jslow >= 0);
-        if (sm && ns + (uint32_t)__popcll(sm) > S.slow_cap) {   // (a wave that claimed more than its share)
-            if (jslow >= 0) slow_row(arena, b, jslow, i, code, S);
-        } else if (sm) {
+        if (sm) {
+            unsigned long long base_k = 0;
+            if (lane == 0) base_k = atomicAdd(&S.nslow[0], (unsigned long long)__popcll(sm));
+            base_k = (unsigned long long)__builtin_amdgcn_readfirstlane((int)(uint32_t)base_k) |
+                     ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base_k >> 32)) << 32);
             if (jslow >= 0) {
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                wsl[ns + r] = make_uint2((uint32_t)i, (uint32_t)jslow);
+                S.slow[base_k + r] = make_uint2((uint32_t)i, (uint32_t)jslow);
+                atomicAdd(&S.nslow[1], (unsigned long long)slow_words(jslow));
             }
-            ns += (uint32_t)__popcll(sm);
         }
     }
-    if (lane == 0) S.wslow[wave] = ns;
 }
 
 __global__ __launch_bounds__(BLOCK) void dd_slow_kernel(const uint8_t *__restrict__ arena,
                                                         const int64_t *__restrict__ off, uint8_t *__restrict__ code,
-                                                        Scratch S)
+                                                        Scratch S, uint64_t ns)
 {
-    // wave w takes transform wave w's list (the same grid)
-    const int64_t wave = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-    const uint32_t ns = S.wslow[wave];
-    const uint2 *wsl = S.slow + (size_t)wave * S.slow_cap;
-    for (uint32_t k = threadIdx.x & 63u; k < ns; k += 64u) {
-        const uint2 e = wsl[k];
+    for (uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; k < ns; k += (uint64_t)gridDim.x * BLOCK) {
+        const uint2 e = S.slow[k];
         slow_row(arena, off[e.x], (int64_t)e.y, (int64_t)e.x, code, S);
     }
 }
 
-// the normalised bytes of rows a and b are equal (their header words, i.e. lengths, first): 16 word pairs in
-// flight per round, so a URL of up to 120 bytes takes one memory round trip (8 per round: 33.2 ms decide)
-constexpr int SAME_U = 16;
-__device__ __forceinline__ bool same_url(const Scratch &S, int64_t oa, int64_t ob, uint32_t len)
+// a row's regenerator (its descriptor: one 16-byte load)
+__device__ __forceinline__ RowGen row_gen(const Scratch &S, const uint8_t *arena, int64_t i)
 {
-    const uint64_t *x = (const uint64_t *)(S.out + oa) - 1;
-    const uint64_t *y = (const uint64_t *)(S.out + ob) - 1;
-    const uint32_t nw = (len + 7) / 8 + 1;
-    for (uint32_t w = 0; w < nw; w += SAME_U) {
+    RowGen g;
+    g.init(S, arena, S.rowd[i], i);
+    return g;
+}
+
+// the normalised bytes of rows a and b are equal (same length len, both regenerated): SAME_U word pairs in flight
+// per round
+constexpr int SAME_U = 8;
+__device__ __forceinline__ bool same_url(const RowGen &x, const RowGen &y)
+{
+    if (x.len != y.len) return false;
+    const int64_t nw = ((int64_t)x.len + 7) / 8;
+    for (int64_t w = 0; w < nw; w += SAME_U) {
         uint64_t d = 0;
 #pragma unroll
         for (int q = 0; q < SAME_U; ++q)
-            if (w + q < nw) d |= x[w + q] ^ y[w + q];
+            if (w + q < nw) d |= x.word(8 * (w + q)) ^ y.word(8 * (w + q));
         if (d) return false;
     }
     return true;
 }
 
-// a row's hash again from its normalised words (as the transform made it), 8 loads in flight per round
-__device__ __forceinline__ uint64_t row_hash(const Scratch &S, int64_t o, uint32_t len)
+// a row's hash again from its regenerated words (as the transform made it)
+__device__ __forceinline__ uint64_t row_hash(const Scratch &S, const RowGen &g)
 {
-    const uint64_t *x = (const uint64_t *)(S.out + o);
     uint64_t h = 0x243F6A8885A308D3ull;
-    const uint32_t nw = (len + 7) / 8;
-    for (uint32_t w = 0; w < nw; w += 8) {
-        uint64_t v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = w + q < nw ? x[w + q] : 0ull;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (w + q < nw) h = mix1(h, v[q]);
-    }
-    h = fmix(h ^ (uint64_t)len);
+    const int64_t nw = ((int64_t)g.len + 7) / 8;
+    for (int64_t w = 0; w < nw; ++w) h = mix1(h, g.word(8 * w));
+    h = fmix(h ^ (uint64_t)g.len);
     return S.weak ? h & 0xFull : h;
 }
 
@@ -556,30 +603,30 @@ __device__ __forceinline__ uint64_t row_hash(const Scratch &S, int64_t o, uint32
 // its tag's first row from the table (a tag shared by different URLs: rare): equal -> duplicate, else
 // CODE_COLLIDE, which the host resolves exactly among those rows (every row of a URL other than the first
 // row's gets it, so their keep-first is complete)
-__global__ __launch_bounds__(BLOCK) void dd_decide_kernel(int64_t n, uint8_t *__restrict__ code, Scratch S,
+__global__ __launch_bounds__(BLOCK) void dd_decide_kernel(const uint8_t *__restrict__ arena, int64_t n,
+                                                          uint8_t *__restrict__ code, Scratch S,
                                                           const int64_t *__restrict__ off)
 {
     unsigned long long c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
         uint8_t k = code[i];
         if (k == KW_URL_KEPT) {
-            const uint64_t hp = S.hint[i];
-            const int64_t oi = obase(off[i], i);
-            const uint64_t q = (uint64_t)oi >> 3;
-            if (hp != NO_HINT || ((S.moved[q >> 5] >> (uint32_t)(q & 31)) & 1u)) {
-                const uint32_t len = S.len3[i];
-                bool eq = hp != NO_HINT && same_url(S, oi, (int64_t)hp, len);
+            const uint32_t hp = S.hint[i];
+            if (hp != NO_HINT || ((S.moved[i >> 5] >> (uint32_t)(i & 31)) & 1u)) {
+                const RowGen gi = row_gen(S, arena, i);
+                bool eq = hp != NO_HINT && same_url(gi, row_gen(S, arena, hp));
                 if (!eq) {
                     if (S.stats) atomicAdd(&S.cnt[hp == NO_HINT ? 5 : 6], 1ull);
-                    const uint64_t h = row_hash(S, oi, len);
+                    const uint64_t h = row_hash(S, gi);
                     uint64_t slot = (h ^ (h >> 29)) & S.mask;
                     unsigned long long cur;
                     for (;;) {
                         cur = S.table[slot];
-                        if ((cur >> POS_BITS) == (h >> POS_BITS)) break;
+                        if ((cur >> 32) == (h >> 32)) break;
                         slot = (slot + 1) & S.mask;
                     }
-                    eq = same_url(S, oi, (int64_t)((cur & POS_MASK) << 3), len);
+                    const uint32_t r0 = (uint32_t)cur - 1u;   // (an empty slot: weak test hashes only; no row)
+                    eq = cur != 0ull && r0 != (uint32_t)i && same_url(gi, row_gen(S, arena, r0));
                 }
                 k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
                 code[i] = k;
@@ -745,6 +792,7 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
 // offset is <= it (binary search over shuffles).
 __device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                          const int64_t *__restrict__ kept_row,
+                                                         const uint8_t *__restrict__ arena,
                                                          const int64_t *__restrict__ off, const Scratch &S,
                                                          uint8_t *__restrict__ dst)
 {
@@ -753,11 +801,10 @@ __device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_
         const int64_t kk = k0 + lane;
         const int64_t kend = k0 + 64 < n_kept ? k0 + 64 : n_kept;
         const int64_t D1 = kept_off[kend];
-        int64_t d0 = D1, src = 0;   // lanes past the end hold the range end
+        int64_t d0 = D1, row = 0;   // lanes past the end hold the range end
         if (kk < n_kept) {
-            const int64_t row = kept_row[kk];
+            row = kept_row[kk];
             d0 = kept_off[kk];
-            src = obase(off[row], row);
         }
         const int64_t D0 = __shfl(d0, 0, 64);
         for (int64_t x0 = (D0 & ~(int64_t)7) + 8 * (int64_t)lane; x0 - 8 * (int64_t)lane < D1; x0 += 64 * 8) {
@@ -770,12 +817,18 @@ __device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_
                 const int64_t dc = __shfl(d0, c & 63, 64);
                 if (c < 64 && dc <= xs) o = c;
             }
-            const int64_t od = __shfl(d0, o, 64), os = __shfl(src, o, 64);
+            const int64_t od = __shfl(d0, o, 64), orow = __shfl(row, o, 64);
             int64_t nd = __shfl(d0, (o + 1) & 63, 64);
             if (o == 63) nd = D1;
             const bool inner = live && xs == x0 && xe == x0 + 8;   // the whole chunk is this group's
             const bool full = inner && x0 + 8 <= nd;
-            if (full) *(uint64_t *)(dst + x0) = ld64(S.out, os + (x0 - od));
+            if (full) {   // bytes [p, p + 8) of row o
+                const RowGen g = row_gen(S, arena, orow);
+                const int64_t p = x0 - od, pa = p & ~(int64_t)7;
+                const int sh = (int)(p - pa) * 8;
+                const uint64_t w0 = g.word(pa);
+                *(uint64_t *)(dst + x0) = sh ? (w0 >> sh) | (g.word(pa + 8) << (64 - sh)) : w0;
+            }
             const bool edge = live && !full;
             if (__ballot(edge)) {
                 uint64_t w = 0;
@@ -783,15 +836,18 @@ __device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_
                 for (int r = 0; r < 8; ++r) {
                     const int idx = o + r;
                     // every lane runs every shuffle (a lane that skips one would not serve its value)
-                    const int64_t sd = __shfl(d0, idx & 63, 64), rs = __shfl(src, idx & 63, 64);
+                    const int64_t sd = __shfl(d0, idx & 63, 64), rr = __shfl(row, idx & 63, 64);
                     const int64_t sn = __shfl(d0, (idx + 1) & 63, 64);
                     const int64_t rd = idx < 64 ? sd : D1, rn = idx + 1 < 64 ? sn : D1;
                     if (edge) {
                         const int64_t y0 = xs > rd ? xs : rd, y1 = xe < rn ? xe : rn;
-                        for (int64_t y = y0; y < y1; ++y) {
-                            const uint32_t c = S.out[rs + (y - rd)];
-                            if (inner) w |= (uint64_t)c << (8 * (y - x0));
-                            else dst[y] = (uint8_t)c;   // a chunk shared with the neighbouring group
+                        if (y0 < y1) {
+                            const RowGen g = row_gen(S, arena, rr);
+                            for (int64_t y = y0; y < y1; ++y) {
+                                const uint32_t c = g.byte(y - rd);
+                                if (inner) w |= (uint64_t)c << (8 * (y - x0));
+                                else dst[y] = (uint8_t)c;   // a chunk shared with the neighbouring group
+                            }
                         }
                     }
                 }
@@ -810,6 +866,7 @@ __device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_
 constexpr int CP_STAGE = 8192;   // bytes of LDS per wave
 __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                         const int64_t *__restrict__ kept_row,
+                                                        const uint8_t *__restrict__ arena,
                                                         const int64_t *__restrict__ off, Scratch S,
                                                         uint8_t *__restrict__ dst)
 {
@@ -827,15 +884,14 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
         const int64_t D0 = kept_off[k0], D1 = kept_off[kend];
         const int64_t A = D0 & ~(int64_t)15;
         if (D1 - A > CP_STAGE) {   // (wave-uniform)
-            copy_group_shfl(k0, n_kept, kept_off, kept_row, off, S, dst);
+            copy_group_shfl(k0, n_kept, kept_off, kept_row, arena, off, S, dst);
             continue;
         }
-        int64_t d0 = 0, len = 0, src = 0;
+        int64_t d0 = 0, len = 0, row = 0;
         if (kk < n_kept) {
-            const int64_t row = kept_row[kk];
+            row = kept_row[kk];
             d0 = kept_off[kk];
             len = kept_off[kk + 1] - d0;
-            src = obase(off[row], row);
         }
         const int nz = (int)((D1 - A + 15) >> 4);
         __builtin_amdgcn_wave_barrier();
@@ -844,21 +900,24 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (len > 0) {
-            // the row's bytes are zero past its end within its last 8-byte word of the sparse arena (8-aligned):
-            // 16 source dwords per round from 8 loads in flight, each destination dword the shifted pair of
-            // source dwords; the first and last destination dwords may hold a neighbour's bytes (ds_or), the
-            // rest are this row's alone (plain stores into the zeroed stage)
+            // the row's regenerated words are zero past its end: 16 source dwords per round from 8 words in
+            // flight, each destination dword the shifted pair of source dwords; the first and last destination
+            // dwords may hold a neighbour's bytes (ds_or), the rest are this row's alone (plain stores into the
+            // zeroed stage)
             const int64_t o = d0 - A;
             const uint32_t sh = (uint32_t)(o & 3) * 8u;
             uint32_t *dw = st32 + (o >> 2);
-            const uint2 *sw = (const uint2 *)(S.out + src);
+            const RowGen g = row_gen(S, arena, row);
             const int nw8 = (int)((len + 7) >> 3);
             const int K = (int)(((o & 3) + len + 3) >> 2);
             uint32_t prev = 0;
             for (int k0 = 0; k0 < K; k0 += 16) {
                 uint2 v[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = (k0 >> 1) + q < nw8 ? sw[(k0 >> 1) + q] : make_uint2(0u, 0u);
+                for (int q = 0; q < 8; ++q) {
+                    const uint64_t wq = (k0 >> 1) + q < nw8 ? g.word(8 * (int64_t)((k0 >> 1) + q)) : 0ull;
+                    v[q] = make_uint2((uint32_t)wq, (uint32_t)(wq >> 32));
+                }
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     const uint32_t cur = (j & 1) ? v[j >> 1].y : v[j >> 1].x;
@@ -887,6 +946,25 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
     }
 }
 
+// the lengths of listed rows, then their normalised bytes (8-aligned slots at boff[k]): the host's exact pass
+__global__ __launch_bounds__(BLOCK) void dd_gather_len_kernel(const uint32_t *__restrict__ rows, uint32_t m, Scratch S,
+                                                              uint32_t *__restrict__ out)
+{
+    for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < m; k += gridDim.x * BLOCK) out[k] = S.len3[rows[k]];
+}
+
+__global__ __launch_bounds__(BLOCK) void dd_materialize_kernel(const uint8_t *__restrict__ arena,
+                                                               const int64_t *__restrict__ off, Scratch S,
+                                                               const uint32_t *__restrict__ rows, uint32_t m,
+                                                               const uint64_t *__restrict__ boff, uint8_t *__restrict__ buf)
+{
+    for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < m; k += gridDim.x * BLOCK) {
+        const uint32_t r = rows[k];
+        const RowGen g = row_gen(S, arena, r);
+        for (int64_t x = 0; x < (int64_t)g.len; x += 8) *(uint64_t *)(buf + boff[k] + x) = g.word(x);
+    }
+}
+
 }  // namespace dd
 
 using namespace dd;
@@ -904,6 +982,8 @@ struct kw_dedup {
     size_t kept_bytes_cap = 0;
     void *d_kept = nullptr;
     void *d_collide = nullptr;   // count + list of the CODE_COLLIDE rows
+    void *d_sarena = nullptr;    // the slow rows' normalised words
+    size_t sarena_bytes = 0;
     int64_t n = 0, n_kept = 0, n_kept_bytes = 0;
     int64_t counts[4] = {0, 0, 0, 0};
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -935,11 +1015,13 @@ extern "C" int kw_dedup_create(int32_t device, kw_dedup **out)
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// exact keep-first over the rows that share a hash tag with a different URL (in row order)
-static int resolve_collisions(kw_dedup *h, const int64_t *d_off, int64_t n, uint8_t *d_code, hipStream_t st)
+// exact keep-first over the rows that share a hash tag with a different URL (in row order): their normalised
+// bytes regenerated on the device, compared on the host
+static int resolve_collisions(kw_dedup *h, const uint8_t *d_arena, const int64_t *d_off, int64_t n, uint8_t *d_code,
+                              hipStream_t st)
 {
     constexpr uint32_t CAP = 1u << 16;
-    std::vector<int64_t> rows;
+    std::vector<uint32_t> rows;
     if (!h->d_collide) DDCHK(h, hipMalloc(&h->d_collide, 8 + 4 * (size_t)CAP));
     unsigned long long *d_cnt = (unsigned long long *)h->d_collide;
     DDCHK(h, hipMemsetAsync(d_cnt, 0, 8, st));
@@ -951,29 +1033,64 @@ static int resolve_collisions(kw_dedup *h, const int64_t *d_off, int64_t n, uint
     DDCHK(h, hipMemcpyAsync(&m, d_cnt, 8, hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
     if (m <= CAP) {
-        std::vector<uint32_t> l(m);
-        if (m) DDCHK(h, hipMemcpy(l.data(), d_cnt + 1, 4 * m, hipMemcpyDeviceToHost));
-        rows.assign(l.begin(), l.end());
+        rows.resize(m);
+        if (m) DDCHK(h, hipMemcpy(rows.data(), d_cnt + 1, 4 * m, hipMemcpyDeviceToHost));
         std::sort(rows.begin(), rows.end());
     } else {
         std::vector<uint8_t> code(n);
         DDCHK(h, hipMemcpy(code.data(), d_code, n, hipMemcpyDeviceToHost));
         for (int64_t i = 0; i < n; ++i)
-            if (code[i] == CODE_COLLIDE) rows.push_back(i);
+            if (code[i] == CODE_COLLIDE) rows.push_back((uint32_t)i);
     }
-    std::unordered_set<std::string> seen;
-    std::vector<int64_t> offs(2);
-    std::vector<uint32_t> len(1);
-    for (const int64_t i : rows) {
-        DDCHK(h, hipMemcpy(offs.data(), d_off + i, 8, hipMemcpyDeviceToHost));
-        DDCHK(h, hipMemcpy(len.data(), h->S.len3 + i, 4, hipMemcpyDeviceToHost));
-        std::string s(len[0], '\0');
-        if (len[0]) DDCHK(h, hipMemcpy(&s[0], h->S.out + obase(offs[0], i), len[0], hipMemcpyDeviceToHost));
-        const uint8_t k = seen.insert(s).second ? (uint8_t)KW_URL_KEPT : (uint8_t)KW_URL_DUPLICATE;
-        DDCHK(h, hipMemcpy(d_code + i, &k, 1, hipMemcpyHostToDevice));
-        ++h->counts[k];
+    const uint32_t k = (uint32_t)rows.size();
+    if (k == 0) return KW_OK;
+    uint32_t *d_rows = nullptr, *d_len = nullptr;
+    uint64_t *d_boff = nullptr;
+    uint8_t *d_buf = nullptr;
+    std::vector<uint32_t> len(k);
+    std::vector<uint64_t> boff(k + 1, 0);
+    int rc = KW_OK;
+    auto fail = [&](hipError_t e, const char *what) {
+        h->err = std::string("HIP error ") + hipGetErrorString(e) + " at " + what;
+        rc = KW_EHIP;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&d_rows, 4 * (size_t)k)) != hipSuccess) fail(e, "collide rows");
+    if (!rc && (e = hipMalloc(&d_len, 4 * (size_t)k)) != hipSuccess) fail(e, "collide lengths");
+    if (!rc && (e = hipMemcpy(d_rows, rows.data(), 4 * (size_t)k, hipMemcpyHostToDevice)) != hipSuccess) fail(e, "rows");
+    const int g2 = (int)std::min<uint32_t>((k + BLOCK - 1) / BLOCK, 1024u);
+    if (!rc) {
+        hipLaunchKernelGGL(dd_gather_len_kernel, dim3(g2), dim3(BLOCK), 0, st, (const uint32_t *)d_rows, k, h->S, d_len);
+        if ((e = hipMemcpyAsync(len.data(), d_len, 4 * (size_t)k, hipMemcpyDeviceToHost, st)) != hipSuccess) fail(e, "lengths");
+        if (!rc && (e = hipStreamSynchronize(st)) != hipSuccess) fail(e, "sync");
     }
-    return KW_OK;
+    for (uint32_t q = 0; q < k; ++q) boff[q + 1] = boff[q] + ((len[q] + 7) & ~7u);
+    if (!rc && (e = hipMalloc(&d_boff, 8 * ((size_t)k + 1))) != hipSuccess) fail(e, "offsets");
+    if (!rc && (e = hipMalloc(&d_buf, boff[k] + 8)) != hipSuccess) fail(e, "bytes");
+    std::vector<uint8_t> buf(boff[k] + 8);
+    if (!rc && (e = hipMemcpy(d_boff, boff.data(), 8 * ((size_t)k + 1), hipMemcpyHostToDevice)) != hipSuccess) fail(e, "boff");
+    if (!rc) {
+        hipLaunchKernelGGL(dd_materialize_kernel, dim3(g2), dim3(BLOCK), 0, st, d_arena, d_off, h->S,
+                           (const uint32_t *)d_rows, k, (const uint64_t *)d_boff, d_buf);
+        if ((e = hipMemcpyAsync(buf.data(), d_buf, boff[k], hipMemcpyDeviceToHost, st)) != hipSuccess) fail(e, "bytes back");
+        if (!rc && (e = hipStreamSynchronize(st)) != hipSuccess) fail(e, "sync");
+    }
+    std::vector<uint8_t> codes(k);
+    if (!rc) {
+        std::unordered_set<std::string> seen;
+        for (uint32_t q = 0; q < k; ++q) {
+            const std::string s((const char *)buf.data() + boff[q], len[q]);
+            codes[q] = seen.insert(s).second ? (uint8_t)KW_URL_KEPT : (uint8_t)KW_URL_DUPLICATE;
+            ++h->counts[codes[q]];
+        }
+        for (uint32_t q = 0; q < k && !rc; ++q)
+            if ((e = hipMemcpy(d_code + rows[q], &codes[q], 1, hipMemcpyHostToDevice)) != hipSuccess) fail(e, "code");
+    }
+    if (d_rows) (void)hipFree(d_rows);
+    if (d_len) (void)hipFree(d_len);
+    if (d_boff) (void)hipFree(d_boff);
+    if (d_buf) (void)hipFree(d_buf);
+    return rc;
 }
 
 extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *d_off, int64_t n, int32_t flags,
@@ -990,26 +1107,17 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     for (int k = 0; k < 4; ++k) h->counts[k] = 0;
     h->n_kept = h->n_kept_bytes = 0;
     if (n == 0) return KW_OK;
-    int64_t arena_end = 0;
-    DDCHK(h, hipMemcpyAsync(&arena_end, d_off + n, 8, hipMemcpyDeviceToHost, st));
-    DDCHK(h, hipStreamSynchronize(st));
     // ---- scratch (grown on demand)
     uint64_t tsize = 1024;
     while (tsize < 2 * (uint64_t)n) tsize <<= 1;
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-    // the transform's grid: its waves' slow lists are sized from the groups of 64 rows each wave takes
-    int tbpc = 8;   // transform blocks per CU (KW_DEDUP_TBLOCKS_PER_CU; 4, 5, 8, 16: 130.7-130.8 ms alike)
+    int tbpc = 8;   // transform blocks per CU (KW_DEDUP_TBLOCKS_PER_CU; 4, 5, 8, 16: 130.7-130.8 ms alike in round 4)
     if (const char *e = kw_env("KW_DEDUP_TBLOCKS_PER_CU")) tbpc = std::max(1, atoi(e));
     const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * tbpc);
-    const int64_t n_tw = (int64_t)tgrid * (BLOCK / 64);
-    h->S.slow_cap = (uint32_t)(((n + 63) / 64 + n_tw - 1) / n_tw * 64);
-    const size_t out_bytes = align256((size_t)obase(arena_end, n) + 64);
-    if (out_bytes >> (POS_BITS + 3)) { h->err = "kw_dedup_run: URL bytes beyond the table's 35-bit positions"; return KW_EUNSUPPORTED; }
-    const size_t need = out_bytes + align256(8 * (size_t)n) + align256(8 * (size_t)n_tw * h->S.slow_cap) +
-                        align256(4 * (size_t)n_tw) + align256(4 * (size_t)n) + align256(8 * tsize) +
-                        align256(out_bytes / 64 + 4) +
-                        align256(8 * 8) + 2 * align256(8 * (size_t)ntiles) + align256(16) +
-                        2 * align256(8 * ((size_t)n + 1));
+    const size_t need = align256(16 * (size_t)n) + align256(4 * (size_t)n) + align256(8 * tsize) +
+                        align256(4 * (size_t)n) + align256(((size_t)n + 31) / 32 * 4) + align256(8 * 8) +
+                        align256(8 * 4) + align256(8 * (size_t)n) + 2 * align256(8 * (size_t)ntiles) +
+                        align256(16) + 2 * align256(8 * ((size_t)n + 1));
     if (need > h->buf_bytes) {
         if (h->d_buf) (void)hipFree(h->d_buf);
         h->d_buf = nullptr;
@@ -1020,16 +1128,18 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     uint8_t *p = (uint8_t *)h->d_buf;
     auto carve = [&](size_t bytes) { uint8_t *r = p; p += align256(bytes); return r; };
     Scratch &S = h->S;
-    S.out = carve(out_bytes);
+    S.rowd = (uint4 *)carve(16 * (size_t)n);
     S.len3 = (uint32_t *)carve(4 * (size_t)n);
     S.table = (unsigned long long *)carve(8 * tsize);
-    S.hint = (uint64_t *)carve(8 * (size_t)n);
-    S.moved = (uint32_t *)carve(out_bytes / 64 + 4);
+    S.hint = (uint32_t *)carve(4 * (size_t)n);
+    const size_t moved_bytes = ((size_t)n + 31) / 32 * 4;
+    S.moved = (uint32_t *)carve(moved_bytes);
     S.mask = tsize - 1;
     S.cnt = (unsigned long long *)carve(8 * 8);
     S.gnext = S.cnt + 7;
-    S.slow = (uint2 *)carve(8 * ((size_t)n_tw * S.slow_cap));
-    S.wslow = (uint32_t *)carve(4 * (size_t)n_tw);
+    S.nslow = (unsigned long long *)carve(8 * 4);
+    S.slow = (uint2 *)carve(8 * (size_t)n);
+    S.sarena = (uint64_t *)h->d_sarena;
     S.weak = kw_env("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
     S.stats = kw_env("KW_DEDUP_STATS") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
@@ -1039,16 +1149,34 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->kept_off = (int64_t *)carve(8 * ((size_t)n + 1));
     h->kept_row = (int64_t *)carve(8 * ((size_t)n + 1));
     DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
+    DDCHK(h, hipMemsetAsync(S.nslow, 0, 32, st));
     const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
     DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
-    DDCHK(h, hipMemsetAsync(S.moved, 0, out_bytes / 64 + 4, st));
+    DDCHK(h, hipMemsetAsync(S.moved, 0, moved_bytes, st));
     DDCHK(h, hipEventRecord(h->ev[0], st));
     hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
-    DDCHK(h, hipEventRecord(h->ev[1], st));
-    hipLaunchKernelGGL(dd_slow_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S);
     DDCHK(h, hipGetLastError());
+    DDCHK(h, hipEventRecord(h->ev[1], st));
+    // the byte-serial rows (rare): their slow-arena words are sized from the transform's count
+    unsigned long long ns2[2];
+    DDCHK(h, hipMemcpyAsync(ns2, S.nslow, sizeof(ns2), hipMemcpyDeviceToHost, st));
+    DDCHK(h, hipStreamSynchronize(st));
+    if (ns2[0]) {
+        const size_t sbytes = 8 * (size_t)ns2[1] + 64;
+        if (sbytes > h->sarena_bytes) {
+            if (h->d_sarena) (void)hipFree(h->d_sarena);
+            h->d_sarena = nullptr;
+            h->sarena_bytes = 0;
+            DDCHK(h, hipMalloc(&h->d_sarena, sbytes + sbytes / 4));
+            h->sarena_bytes = sbytes + sbytes / 4;
+        }
+        S.sarena = (uint64_t *)h->d_sarena;
+        const int sgrid = (int)std::min<uint64_t>((ns2[0] + BLOCK - 1) / BLOCK, (uint64_t)h->cus * 16);
+        hipLaunchKernelGGL(dd_slow_kernel, dim3(sgrid), dim3(BLOCK), 0, st, d_arena, d_off, d_code, S, (uint64_t)ns2[0]);
+        DDCHK(h, hipGetLastError());
+    }
     DDCHK(h, hipEventRecord(h->ev[2], st));
-    hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, n, d_code, S, d_off);
+    hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, n, d_code, S, d_off);
     DDCHK(h, hipGetLastError());
     unsigned long long cnt[7];
     DDCHK(h, hipMemcpyAsync(cnt, S.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
@@ -1056,7 +1184,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     if (S.stats) fprintf(stderr, "kw_dedup: table lookups in decide: %llu moved, %llu hint mismatches\n", cnt[5], cnt[6]);
     for (int k = 0; k < 4; ++k) h->counts[k] = (int64_t)cnt[k];
     if (cnt[CODE_COLLIDE]) {
-        int rc = resolve_collisions(h, d_off, n, d_code, st);
+        int rc = resolve_collisions(h, d_arena, d_off, n, d_code, st);
         if (rc) return rc;
     }
     DDCHK(h, hipEventRecord(h->ev[3], st));
@@ -1083,7 +1211,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     if (h->n_kept > 0) {
         const int cgrid = (int)std::min<int64_t>((h->n_kept + 63) / 64 * 64 / BLOCK + 1, (int64_t)h->cus * 8);
         hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, h->n_kept, (const int64_t *)h->kept_off,
-                           (const int64_t *)h->kept_row, d_off, S, h->kept_bytes);
+                           (const int64_t *)h->kept_row, d_arena, d_off, S, h->kept_bytes);
         DDCHK(h, hipGetLastError());
     }
     DDCHK(h, hipEventRecord(h->ev[4], st));
@@ -1143,6 +1271,7 @@ extern "C" int kw_dedup_destroy(kw_dedup *h)
     if (h->d_buf) (void)hipFree(h->d_buf);
     if (h->d_kept) (void)hipFree(h->d_kept);
     if (h->d_collide) (void)hipFree(h->d_collide);
+    if (h->d_sarena) (void)hipFree(h->d_sarena);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     delete h;
