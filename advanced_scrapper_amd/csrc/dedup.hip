@@ -19,14 +19,16 @@
 //                        once (table_insert): open-addressing slots {tag, row},
 //                        the first inserter claims a slot by CAS, an earlier
 //                        row displaces the holder by atomicMin (keep='first');
-//                        a row that finds an earlier holder keeps that row as
-//                        its hint, a displaced holder gets a `moved` bit.
-//   dd_decide_kernel     a row with a hint is a duplicate iff its normalised
-//                        bytes equal the hinted row's (length, then every word,
-//                        both regenerated); a moved row or a differing one is
-//                        compared with its tag's first row from the table.
-//                        Rows that share a tag with a different URL are
-//                        resolved exactly on the host.
+//                        a row that finds an earlier holder lists the pair
+//                        (row, holder), a row that displaces the holder lists
+//                        (holder, row).
+//   dd_pairs_kernel      a listed row is a duplicate iff its normalised bytes
+//                        equal the holder's (length, then every word, both
+//                        regenerated; 8 lanes a pair).  A differing pair's
+//                        later row is compared with its tag's first row
+//                        from the table (dd_recheck_kernel).  Rows that share
+//                        a tag with a different URL are resolved exactly on
+//                        the host.
 //   dd_count / dd_scan / dd_place / dd_copy
 //                        dense offsets, source rows and bytes of the kept rows
 //                        (the copy regenerates each kept row's words).
@@ -109,13 +111,16 @@ struct Scratch {
                              //   gap's raw position (NO_GAP) (a slow row: its slow-arena word)
     uint32_t *len3;          // per row: normalised length
     unsigned long long *table;
-    uint32_t *hint;          // per kept row: an earlier row with its tag, or NO_HINT
-    uint32_t *moved;         // bit per row: the row lost its slot to an earlier row
+    uint2 *pairs;            // (row, an earlier row with its tag) of every kept row that found one, listed per
+                             //   claim of TCLAIM groups: claim c's pairs at [c * 64 * TCLAIM, + pcount[c])
+    uint32_t *pcount;        // pairs per claim
+    uint32_t *recheck;       // rows compared with their tag's first row from the table (cnt[5] listed)
     uint64_t mask;
-    unsigned long long *cnt;   // [0..4] per code
-    unsigned long long *gnext;   // the transform's next group of 64 rows
+    unsigned long long *cnt;   // [0], [2], [3], [4]: rows per code but KEPT; [5] differing pairs;
+                               // [7] the transform's next group of 64 rows
+    unsigned long long *gnext;   // &cnt[7]
     int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
-    int stats;               // KW_DEDUP_STATS: count the rows decide looks up in the table (cnt[5] moved, [6] other)
+    int stats;               // KW_DEDUP_STATS: print the differing pairs (rows looked up in the table)
     int normalize;           // KW_DEDUP_NORMALIZE: apply :63-76; else keep-first over the raw strings
     uint2 *slow;             // rows (index, cut) for the byte-serial rewrite (capacity: every row)
     unsigned long long *nslow;   // [0] slow rows listed, [1] slow-arena words they may need, [2] words handed out
@@ -223,17 +228,19 @@ struct LdsSrc {
 
 // Open-addressing table of 64-bit slots {tag, row}: the first inserter of a tag claims a slot by CAS, an earlier
 // row (smaller index) displaces the holder by atomicMin, so the slot ends with the tag's first row
-// (keep='first').  Every kept row writes its own hint: the earlier holder it found, or NO_HINT when it took the
-// slot; a row that displaces the holder sets the holder's bit in `moved` (each row leaves its slot at most once).
+// (keep='first').  Every kept row returns at most one pair (later row, earlier row) of its tag to compare: (row,
+// the earlier holder it found), or (the holder, row) when it displaced the holder (each row leaves its slot at
+// most once, so every row that took a slot and is not its tag's first row gets exactly one such pair);
+// (row, NO_HINT) when it took an empty slot.
 // The plain load is only a hint of the slot (a slot's tag never changes once claimed; its row only decreases).
-// Nothing another row wrote in this kernel is read (no cross-XCD visibility is assumed): decide reads the
-// hints, bits and plans after the kernel boundary.
-__device__ __forceinline__ void table_insert(const Scratch &S, uint64_t h, int64_t i)
+// Nothing another row wrote in this kernel is read (no cross-XCD visibility is assumed): the pair and recheck
+// kernels read the pairs, bits and plans after the kernel boundary.
+__device__ __forceinline__ uint2 table_insert(const Scratch &S, uint64_t h, int64_t i)
 {
     const unsigned long long key = ((h >> 32) << 32) | (uint64_t)((uint32_t)i + 1u);   // (row + 1: 0 is empty)
     uint64_t slot = (h ^ (h >> 29)) & S.mask;
     unsigned long long cur = S.table[slot];
-    uint32_t hint = NO_HINT;
+    uint2 pr = make_uint2((uint32_t)i, NO_HINT);
     for (;;) {
         if (cur == 0ull) {
             cur = atomicCAS(&S.table[slot], 0ull, key);
@@ -244,23 +251,22 @@ __device__ __forceinline__ void table_insert(const Scratch &S, uint64_t h, int64
             if (cur > key) {
                 cur = atomicMin(&S.table[slot], key);
                 if (cur > key) {   // displaced the holder
-                    const uint32_t q = (uint32_t)cur - 1u;
-                    atomicOr(&S.moved[q >> 5], 1u << (q & 31u));
+                    pr = make_uint2((uint32_t)cur - 1u, (uint32_t)i);
                     break;
                 }
             }
-            hint = (uint32_t)cur - 1u;
+            pr.y = (uint32_t)cur - 1u;
             break;
         }
         slot = (slot + 1) & S.mask;
         cur = S.table[slot];
     }
-    S.hint[i] = hint;
+    return pr;
 }
 
-// finish a row: hash, length, code; a kept row goes into the table
-__device__ __forceinline__ void finish_row(uint64_t h1, int64_t len3, bool bad, int64_t i,
-                                           uint8_t *__restrict__ code, const Scratch &S, int64_t b, uint2 pl)
+// finish a row: hash, length, code; a kept row goes into the table (returns its pair)
+__device__ __forceinline__ uint2 finish_row(uint64_t h1, int64_t len3, bool bad, int64_t i,
+                                               uint8_t *__restrict__ code, const Scratch &S, int64_t b, uint2 pl)
 {
     h1 = fmix(h1 ^ (uint64_t)len3);
     if (S.weak) h1 &= 0xFull;
@@ -268,7 +274,7 @@ __device__ __forceinline__ void finish_row(uint64_t h1, int64_t len3, bool bad, 
     const uint32_t l24 = len3 < (int64_t)LEN_BIG ? (uint32_t)len3 : LEN_BIG;
     S.rowd[i] = make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32) | (l24 << 8), pl.x, pl.y);
     code[i] = bad ? (uint8_t)KW_URL_FILTERED : (uint8_t)KW_URL_KEPT;
-    if (!bad) table_insert(S, h1, i);
+    return bad ? make_uint2((uint32_t)i, NO_HINT) : table_insert(S, h1, i);
 }
 
 // slow-arena words a byte-serial row of cut j may need (one extra 's' per 5 bytes, ".html", a partial word)
@@ -276,8 +282,8 @@ __host__ __device__ __forceinline__ uint64_t slow_words(int64_t j) { return (uin
 
 // the general rewrite of the cut prefix u[0, j), byte by byte (rows with ':80' or a second 'http:'), into the
 // slow arena
-__device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j, int64_t i,
-                         uint8_t *__restrict__ code, const Scratch &S)
+__device__ uint2 slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j, int64_t i,
+                             uint8_t *__restrict__ code, const Scratch &S)
 {
     const unsigned long long w0 = atomicAdd(&S.nslow[2], (unsigned long long)slow_words(j));
     Emit Em;
@@ -293,7 +299,9 @@ __device__ void slow_row(const uint8_t *__restrict__ arena, int64_t b, int64_t j
     R.flush(Em);
     Em.put('.'); Em.put('h'); Em.put('t'); Em.put('m'); Em.put('l');
     Em.finish();
-    finish_row(Em.h1, Em.len, Em.bad, i, code, S, b, make_uint2(SLOW_ROW, (uint32_t)w0));
+    const uint2 pr = finish_row(Em.h1, Em.len, Em.bad, i, code, S, b, make_uint2(SLOW_ROW, (uint32_t)w0));
+    if (Em.bad) atomicAdd(&S.cnt[KW_URL_FILTERED], 1ull);   // (rare rows: one atomic each)
+    return pr;
 }
 
 // The normalised words of a row of the fast path, from its raw bytes and its plan: the prefix u[0, j) with
@@ -340,11 +348,17 @@ struct RowGen {
     int ins, raw;
     __device__ __forceinline__ void init(const Scratch &S, const uint8_t *arena, uint4 r, int64_t i)
     {
+        uint32_t l = r.y >> 8;
+        if (l == LEN_BIG) l = S.len3[i];
+        init_len(S, arena, r, l);
+    }
+    // from the descriptor and the resolved length (descriptors handed between lanes)
+    __device__ __forceinline__ void init_len(const Scratch &S, const uint8_t *arena, uint4 r, uint32_t l)
+    {
         const uint2 pl = make_uint2(r.z, r.w);
         a = arena;
         b = (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x);
-        len = r.y >> 8;
-        if (len == LEN_BIG) len = S.len3[i];
+        len = l;
         raw = !S.normalize;
         sw = (!raw && pl.x == SLOW_ROW) ? S.sarena + pl.y : nullptr;
         ins = (int)(pl.y >> 31);
@@ -368,10 +382,10 @@ struct RowGen {
     __device__ __forceinline__ uint32_t byte(int64_t y) const { return (uint32_t)(word(y & ~(int64_t)7) >> (8 * (y & 7))) & 0xFFu; }
 };
 
-// one row: returns -1 when done, or the cut j of a row that needs slow_row
+// one row: returns -1 when done, or the cut j of a row that needs slow_row; `pair` gets finish_row's
 template <class Src>
 __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int64_t L, int64_t i,
-                                                 uint8_t *__restrict__ code, const Scratch &S)
+                                                 uint8_t *__restrict__ code, const Scratch &S, uint2 &pair)
 {
     if (!S.normalize) {
         // raw keep-first (the merge step :174 over already normalised rows): the key is the string itself
@@ -381,7 +395,7 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
             if (L - x0 < 8) w &= (1ull << (8 * (L - x0))) - 1;
             h1 = mix1(h1, w);
         }
-        finish_row(h1, L, false, i, code, S, b, make_uint2((uint32_t)L, NO_GAP));
+        pair = finish_row(h1, L, false, i, code, S, b, make_uint2((uint32_t)L, NO_GAP));
         return -1;
     }
     // ---- pass 1: the cut j, the first two extra ':' and the first 'news/%' | "news/'" end, one 4-byte word a
@@ -487,8 +501,8 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
     const bool bad = kf < j || jn;
     uint64_t h1 = 0x243F6A8885A308D3ull;
     for (int64_t x0 = 0; x0 < len3; x0 += 8) h1 = mix1(h1, F.word(x0));
-    finish_row(h1, len3, bad, i, code, S, b,
-               make_uint2((uint32_t)j, ((uint32_t)ins << 31) | (gap ? (uint32_t)ec : NO_GAP)));
+    pair = finish_row(h1, len3, bad, i, code, S, b,
+                      make_uint2((uint32_t)j, ((uint32_t)ins << 31) | (gap ? (uint32_t)ec : NO_GAP)));
     return -1;
 }
 
@@ -508,15 +522,20 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
     // groups of 64 rows claimed from a counter in row order: rows enter the table in about row order, so few
     // earlier duplicates displace a later row already there (grid-stride let waves drift apart: 16-26 % of the
     // duplicates were displaced rows, which decide looks up in the table again)
-    // (TCLAIM groups per claim: one counter address for every group serialised the transform, 98 vs 68 ms)
+    // (TCLAIM groups per claim: one counter address for every group serialised the transform, 98 vs 68 ms; so
+    // a claim's pairs go to its own segment, counted by the wave)
     auto claim = [&]() -> int64_t {
         uint64_t g = 0;
         if (lane == 0) g = atomicAdd(S.gnext, (unsigned long long)TCLAIM);
         return (int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g) |
                ((int64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32);
     };
-    int64_t g = claim(), gend = g + TCLAIM;
-    for (; g < n_groups; g = (g + 1 < gend) ? g + 1 : (gend = claim() + TCLAIM) - TCLAIM) {
+    uint32_t n_nohtml = 0, n_filtered = 0;   // this lane's rows per code (one atomic per wave at the end)
+    for (int64_t gc = claim(); gc < n_groups; gc = claim()) {
+      const int64_t gce = gc + TCLAIM < n_groups ? gc + TCLAIM : n_groups;
+      uint2 *const seg = S.pairs + gc * 64;   // this claim's pairs (a wave-uniform count: no shared counter)
+      uint32_t pc = 0;
+      for (int64_t g = gc; g < gce; ++g) {
         const int64_t i0 = g * 64, i1 = i0 + 64 < n ? i0 + 64 : n;
         const int64_t A0 = off[i0], A1 = off[i1];
         const int64_t base = A0 & ~(int64_t)15;
@@ -525,6 +544,7 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
         int64_t b = 0, L = 0;
         if (i < n) { b = off[i]; L = off[i + 1] - b; }
         int64_t jslow = -1;
+        uint2 pair = make_uint2(0u, NO_HINT);
         if (nch * 16 + 16 <= STAGE_BYTES) {
             __builtin_amdgcn_wave_barrier();
             for (int64_t c = lane; c < nch; c += 64) stage[c] = *(const uint4 *)(arena + base + 16 * c);
@@ -532,11 +552,23 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             LdsSrc src{(const uint32_t *)stage, base};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S);
+            if (i < n) jslow = transform_row(src, b, L, i, code, S, pair);
         } else {
             GlobalSrc src{arena};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S);
+            if (i < n) jslow = transform_row(src, b, L, i, code, S, pair);
         }
+        if (i < n && jslow < 0) {
+            const uint8_t k = code[i];   // (this lane's own store)
+            n_nohtml += k == KW_URL_NO_HTML;
+            n_filtered += k == KW_URL_FILTERED;
+        }
+        // pairs to compare -> the claim's segment (at most one per row: the segment holds the claim's rows)
+        const uint64_t pm = __ballot(pair.y != NO_HINT);
+        if (pair.y != NO_HINT) {
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+            seg[pc + r] = pair;
+        }
+        pc += (uint32_t)__popcll(pm);
         // rows for the byte-serial rewrite -> the global slow list (rare rows: one atomic per wave that has any)
         const uint64_t sm = __ballot(jslow >= 0);
         if (sm) {
@@ -550,6 +582,16 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
                 atomicAdd(&S.nslow[1], (unsigned long long)slow_words(jslow));
             }
         }
+      }
+      if (lane == 0) S.pcount[gc / TCLAIM] = pc;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        n_nohtml += __shfl_xor(n_nohtml, d, 64);
+        n_filtered += __shfl_xor(n_filtered, d, 64);
+    }
+    if (lane == 0) {
+        if (n_nohtml) atomicAdd(&S.cnt[KW_URL_NO_HTML], (unsigned long long)n_nohtml);
+        if (n_filtered) atomicAdd(&S.cnt[KW_URL_FILTERED], (unsigned long long)n_filtered);
     }
 }
 
@@ -559,7 +601,8 @@ __global__ __launch_bounds__(BLOCK) void dd_slow_kernel(const uint8_t *__restric
 {
     for (uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; k < ns; k += (uint64_t)gridDim.x * BLOCK) {
         const uint2 e = S.slow[k];
-        slow_row(arena, off[e.x], (int64_t)e.y, (int64_t)e.x, code, S);
+        // the entry becomes the row's pair (or (row, NO_HINT)), compared with the claims' pairs
+        S.slow[k] = slow_row(arena, off[e.x], (int64_t)e.y, (int64_t)e.x, code, S);
     }
 }
 
@@ -598,52 +641,132 @@ __device__ __forceinline__ uint64_t row_hash(const Scratch &S, const RowGen &g)
     return S.weak ? h & 0xFull : h;
 }
 
-// A kept row with a hint is a duplicate iff its bytes equal the hinted (earlier) row's; a row without one is
-// kept unless it lost its slot (its `moved` bit).  A hinted row that differs, or a moved row, is compared with
-// its tag's first row from the table (a tag shared by different URLs: rare): equal -> duplicate, else
+// A pair's later row is a duplicate iff its bytes equal the earlier row's; a kept row in no pair is its tag's
+// first row.  A pair that differs has its later row compared with its tag's first row from the table (a tag shared by different URLs: rare): equal -> duplicate, else
 // CODE_COLLIDE, which the host resolves exactly among those rows (every row of a URL other than the first
-// row's gets it, so their keep-first is complete)
-__global__ __launch_bounds__(BLOCK) void dd_decide_kernel(const uint8_t *__restrict__ arena, int64_t n,
-                                                          uint8_t *__restrict__ code, Scratch S,
-                                                          const int64_t *__restrict__ off)
+// row's gets it, so their keep-first is complete).
+//
+// dd_pairs_kernel: 8 lanes a pair, lane s comparing words s, s + 8, ... of the two regenerated rows, so each load
+// instruction touches a few lines of 8 rows (lane = row made every load touch 64 rows' lines: 37.8 ms at 500M
+// rows, 123M pairs)
+constexpr int PAIR_LANES = 8;
+
+// a row's descriptor and resolved length, loaded by one lane (handed to the lanes that use it by shuffles)
+struct Desc {
+    uint4 r;
+    uint32_t len;
+};
+__device__ __forceinline__ Desc load_desc(const Scratch &S, int64_t i)
 {
-    unsigned long long c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
-        uint8_t k = code[i];
-        if (k == KW_URL_KEPT) {
-            const uint32_t hp = S.hint[i];
-            if (hp != NO_HINT || ((S.moved[i >> 5] >> (uint32_t)(i & 31)) & 1u)) {
-                const RowGen gi = row_gen(S, arena, i);
-                bool eq = hp != NO_HINT && same_url(gi, row_gen(S, arena, hp));
-                if (!eq) {
-                    if (S.stats) atomicAdd(&S.cnt[hp == NO_HINT ? 5 : 6], 1ull);
-                    const uint64_t h = row_hash(S, gi);
-                    uint64_t slot = (h ^ (h >> 29)) & S.mask;
-                    unsigned long long cur;
-                    for (;;) {
-                        cur = S.table[slot];
-                        if ((cur >> 32) == (h >> 32)) break;
-                        slot = (slot + 1) & S.mask;
-                    }
-                    const uint32_t r0 = (uint32_t)cur - 1u;   // (an empty slot: weak test hashes only; no row)
-                    eq = cur != 0ull && r0 != (uint32_t)i && same_url(gi, row_gen(S, arena, r0));
-                }
-                k = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
-                code[i] = k;
+    Desc d;
+    d.r = S.rowd[i];
+    d.len = d.r.y >> 8;
+    if (d.len == LEN_BIG) d.len = S.len3[i];
+    return d;
+}
+__device__ __forceinline__ Desc shfl_desc(const Desc &d, int src)
+{
+    Desc o;
+    o.r.x = (uint32_t)__shfl((int)d.r.x, src, 64);
+    o.r.y = (uint32_t)__shfl((int)d.r.y, src, 64);
+    o.r.z = (uint32_t)__shfl((int)d.r.z, src, 64);
+    o.r.w = (uint32_t)__shfl((int)d.r.w, src, 64);
+    o.len = (uint32_t)__shfl((int)d.len, src, 64);
+    return o;
+}
+
+// pairs e[0, m) (m <= 64, wave-uniform): lane t loads pair t's two descriptors, then 8 rounds of 8 pairs, lane s
+// of a pair's group comparing words s, s + 8, ... of the two regenerated rows (each load instruction touches a
+// few lines of 8 rows; the descriptors' dependent loads are paid once per 64 pairs)
+__device__ __forceinline__ void compare_pairs(const uint8_t *__restrict__ arena, uint8_t *__restrict__ code,
+                                              const Scratch &S, const uint2 *__restrict__ e, uint32_t m,
+                                              uint32_t &n_dup)
+{
+    const int lane = threadIdx.x & 63, grp = lane / PAIR_LANES, s = lane & (PAIR_LANES - 1);
+    uint2 pr = make_uint2(0u, NO_HINT);
+    if ((uint32_t)lane < m) pr = e[lane];
+    const bool live = pr.y != NO_HINT;   // (the slow list's entries without a pair)
+    Desc dx{}, dy{};
+    if (live) {
+        dx = load_desc(S, pr.x);
+        dy = load_desc(S, pr.y);
+    }
+    const uint64_t lm = __ballot(live);
+    for (uint32_t r0 = 0; r0 < m; r0 += 64 / PAIR_LANES) {
+        const int src = (int)r0 + grp;
+        const Desc x = shfl_desc(dx, src), y = shfl_desc(dy, src);
+        const uint32_t row = (uint32_t)__shfl((int)pr.x, src, 64);
+        const bool act = (uint32_t)src < m && ((lm >> src) & 1ull);
+        uint64_t d = 0;
+        if (act) {
+            RowGen gx, gy;
+            gx.init_len(S, arena, x.r, x.len);
+            gy.init_len(S, arena, y.r, y.len);
+            d = gx.len != gy.len;
+            if (!d) {
+                const int64_t nw = ((int64_t)gx.len + 7) / 8;
+                for (int64_t w = s; w < nw; w += PAIR_LANES) d |= gx.word(8 * w) ^ gy.word(8 * w);
             }
         }
-        c0 += k == 0;
-        c1 += k == 1;
-        c2 += k == 2;
-        c3 += k == 3;
-        c4 += k == CODE_COLLIDE;
+        const uint64_t bm = __ballot(d != 0);
+        const bool eq = ((bm >> (lane & ~(PAIR_LANES - 1))) & ((1ull << PAIR_LANES) - 1)) == 0;
+        if (act && s == 0) {
+            if (eq) {
+                code[row] = (uint8_t)KW_URL_DUPLICATE;
+                ++n_dup;
+            } else {
+                S.recheck[atomicAdd(&S.cnt[5], 1ull)] = row;   // (rare)
+            }
+        }
     }
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        unsigned long long v = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : c4;
-        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&S.cnt[q], v);
+}
+
+// a wave per claim: its pairs 64 at a time; then the slow rows' entries, 64 at a time
+__global__ __launch_bounds__(BLOCK) void dd_pairs_kernel(const uint8_t *__restrict__ arena, uint8_t *__restrict__ code,
+                                                         Scratch S, int64_t n_claims, uint64_t ns)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * BLOCK) >> 6;
+    uint32_t n_dup = 0;
+    for (int64_t c = wave; c < n_claims; c += n_waves) {
+        const uint32_t pc = S.pcount[c];
+        const uint2 *seg = S.pairs + c * 64 * TCLAIM;
+        for (uint32_t k = 0; k < pc; k += 64) compare_pairs(arena, code, S, seg + k, pc - k < 64 ? pc - k : 64, n_dup);
     }
+    for (uint64_t k = (uint64_t)wave * 64; k < ns; k += (uint64_t)n_waves * 64)
+        compare_pairs(arena, code, S, S.slow + k, (uint32_t)(ns - k < 64 ? ns - k : 64), n_dup);
+    for (int d = 32; d >= 1; d >>= 1) n_dup += __shfl_xor(n_dup, d, 64);
+    if (lane == 0 && n_dup) atomicAdd(&S.cnt[KW_URL_DUPLICATE], (unsigned long long)n_dup);
+}
+
+// a row against its tag's first row from the table (lane = row; rare rows): duplicate or CODE_COLLIDE
+__device__ __forceinline__ void recheck_row(const uint8_t *__restrict__ arena, uint8_t *__restrict__ code,
+                                            const Scratch &S, uint32_t i)
+{
+    const RowGen gi = row_gen(S, arena, i);
+    const uint64_t h = row_hash(S, gi);
+    uint64_t slot = (h ^ (h >> 29)) & S.mask;
+    unsigned long long cur;
+    for (;;) {
+        cur = S.table[slot];
+        if ((cur >> 32) == (h >> 32)) break;
+        slot = (slot + 1) & S.mask;
+    }
+    const uint32_t r0 = (uint32_t)cur - 1u;   // (an empty slot: weak test hashes only; no row)
+    const bool eq = cur != 0ull && r0 != i && same_url(gi, row_gen(S, arena, r0));
+    code[i] = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
+    atomicAdd(&S.cnt[eq ? KW_URL_DUPLICATE : CODE_COLLIDE], 1ull);
+}
+
+// the later rows of the pairs that differed (the list)
+__global__ __launch_bounds__(BLOCK) void dd_recheck_kernel(const uint8_t *__restrict__ arena,
+                                                           uint8_t *__restrict__ code, Scratch S)
+{
+    const unsigned long long nr = S.cnt[5];
+    for (unsigned long long k = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x; k < nr;
+         k += (unsigned long long)gridDim.x * BLOCK)
+        recheck_row(arena, code, S, S.recheck[k]);
 }
 
 // the CODE_COLLIDE rows (rare: a 32-bit tag shared by two URLs in one probe run), listed for the host's exact pass
@@ -784,76 +907,23 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
     }
 }
 
-// (groups whose dense range exceeds a wave's LDS stage) dense kept rows: a wave owns kept rows [k0, k0 + 64) whose dense bytes are one contiguous range
-// [D0, D1).  Lane l handles the 8-aligned destination chunks D0 & ~7 + 8 (l + 64 t): a chunk inside
-// one row is one unaligned 8-byte load from the sparse arena and one aligned 8-byte store; a chunk
-// with a row boundary (or a range edge) is written byte by byte from up to 8 rows, whose offsets all
-// lanes fetch with the same shuffles.  The owner row of a byte is the last of the 64 whose dense
-// offset is <= it (binary search over shuffles).
-__device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_kept, const int64_t *__restrict__ kept_off,
+// (groups whose dense range exceeds a wave's LDS stage: rows of 128 bytes on average or more) lane = row: the
+// row's regenerated words written byte by byte at its dense offset (every byte has one writer)
+__device__ __attribute__((noinline)) void copy_group_rows(int64_t k0, int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                          const int64_t *__restrict__ kept_row,
-                                                         const uint8_t *__restrict__ arena,
-                                                         const int64_t *__restrict__ off, const Scratch &S,
+                                                         const uint8_t *__restrict__ arena, const Scratch &S,
                                                          uint8_t *__restrict__ dst)
 {
-    const int lane = threadIdx.x & 63;
-    {
-        const int64_t kk = k0 + lane;
-        const int64_t kend = k0 + 64 < n_kept ? k0 + 64 : n_kept;
-        const int64_t D1 = kept_off[kend];
-        int64_t d0 = D1, row = 0;   // lanes past the end hold the range end
-        if (kk < n_kept) {
-            row = kept_row[kk];
-            d0 = kept_off[kk];
-        }
-        const int64_t D0 = __shfl(d0, 0, 64);
-        for (int64_t x0 = (D0 & ~(int64_t)7) + 8 * (int64_t)lane; x0 - 8 * (int64_t)lane < D1; x0 += 64 * 8) {
-            const bool live = x0 < D1;
-            const int64_t xs = x0 > D0 ? x0 : D0, xe = x0 + 8 < D1 ? x0 + 8 : D1;
-            int o = 0;
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-                const int c = o + step;
-                const int64_t dc = __shfl(d0, c & 63, 64);
-                if (c < 64 && dc <= xs) o = c;
-            }
-            const int64_t od = __shfl(d0, o, 64), orow = __shfl(row, o, 64);
-            int64_t nd = __shfl(d0, (o + 1) & 63, 64);
-            if (o == 63) nd = D1;
-            const bool inner = live && xs == x0 && xe == x0 + 8;   // the whole chunk is this group's
-            const bool full = inner && x0 + 8 <= nd;
-            if (full) {   // bytes [p, p + 8) of row o
-                const RowGen g = row_gen(S, arena, orow);
-                const int64_t p = x0 - od, pa = p & ~(int64_t)7;
-                const int sh = (int)(p - pa) * 8;
-                const uint64_t w0 = g.word(pa);
-                *(uint64_t *)(dst + x0) = sh ? (w0 >> sh) | (g.word(pa + 8) << (64 - sh)) : w0;
-            }
-            const bool edge = live && !full;
-            if (__ballot(edge)) {
-                uint64_t w = 0;
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const int idx = o + r;
-                    // every lane runs every shuffle (a lane that skips one would not serve its value)
-                    const int64_t sd = __shfl(d0, idx & 63, 64), rr = __shfl(row, idx & 63, 64);
-                    const int64_t sn = __shfl(d0, (idx + 1) & 63, 64);
-                    const int64_t rd = idx < 64 ? sd : D1, rn = idx + 1 < 64 ? sn : D1;
-                    if (edge) {
-                        const int64_t y0 = xs > rd ? xs : rd, y1 = xe < rn ? xe : rn;
-                        if (y0 < y1) {
-                            const RowGen g = row_gen(S, arena, rr);
-                            for (int64_t y = y0; y < y1; ++y) {
-                                const uint32_t c = g.byte(y - rd);
-                                if (inner) w |= (uint64_t)c << (8 * (y - x0));
-                                else dst[y] = (uint8_t)c;   // a chunk shared with the neighbouring group
-                            }
-                        }
-                    }
-                }
-                if (edge && inner) *(uint64_t *)(dst + x0) = w;   // assembled from several rows: one full store
-            }
-        }
+    const int64_t kk = k0 + (threadIdx.x & 63);
+    if (kk >= n_kept) return;
+    const int64_t d0 = kept_off[kk], len = kept_off[kk + 1] - d0;
+    const RowGen g = row_gen(S, arena, kept_row[kk]);
+#pragma unroll 1
+    for (int64_t x = 0; x < len; x += 8) {
+        const uint64_t w = g.word(x);
+        const int m = len - x < 8 ? (int)(len - x) : 8;
+#pragma unroll 1
+        for (int k = 0; k < m; ++k) dst[d0 + x + k] = (uint8_t)(w >> (8 * k));
     }
 }
 
@@ -862,12 +932,11 @@ __device__ __attribute__((noinline)) void copy_group_shfl(int64_t k0, int64_t n_
 // The range is staged in the wave's LDS (zeroed, then every lane ORs its row's dwords in at the row's dense
 // offset: the partial dwords two rows share merge by ds_or_b32) and written out with aligned 16-byte stores,
 // the two partial 16-byte chunks it may share with the neighbouring groups byte by byte.  A group whose range
-// exceeds the stage takes copy_group_shfl.
+// exceeds the stage takes copy_group_rows.
 constexpr int CP_STAGE = 8192;   // bytes of LDS per wave
 __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                         const int64_t *__restrict__ kept_row,
-                                                        const uint8_t *__restrict__ arena,
-                                                        const int64_t *__restrict__ off, Scratch S,
+                                                        const uint8_t *__restrict__ arena, Scratch S,
                                                         uint8_t *__restrict__ dst)
 {
     __shared__ uint4 stage_all[(BLOCK / 64) * (CP_STAGE / 16)];
@@ -884,12 +953,13 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
         const int64_t D0 = kept_off[k0], D1 = kept_off[kend];
         const int64_t A = D0 & ~(int64_t)15;
         if (D1 - A > CP_STAGE) {   // (wave-uniform)
-            copy_group_shfl(k0, n_kept, kept_off, kept_row, arena, off, S, dst);
+            copy_group_rows(k0, n_kept, kept_off, kept_row, arena, S, dst);
             continue;
         }
-        int64_t d0 = 0, len = 0, row = 0;
+        int64_t d0 = 0, len = 0;
+        uint32_t row = 0;
         if (kk < n_kept) {
-            row = kept_row[kk];
+            row = (uint32_t)kept_row[kk];
             d0 = kept_off[kk];
             len = kept_off[kk + 1] - d0;
         }
@@ -907,7 +977,8 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
             const int64_t o = d0 - A;
             const uint32_t sh = (uint32_t)(o & 3) * 8u;
             uint32_t *dw = st32 + (o >> 2);
-            const RowGen g = row_gen(S, arena, row);
+            RowGen g;
+            g.init_len(S, arena, S.rowd[row], (uint32_t)len);   // (the length: the dense range's)
             const int nw8 = (int)((len + 7) >> 3);
             const int K = (int)(((o & 3) + len + 3) >> 2);
             uint32_t prev = 0;
@@ -1111,11 +1182,14 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     uint64_t tsize = 1024;
     while (tsize < 2 * (uint64_t)n) tsize <<= 1;
     const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const int64_t n_claims = ((n + 63) / 64 + TCLAIM - 1) / TCLAIM;
     int tbpc = 8;   // transform blocks per CU (KW_DEDUP_TBLOCKS_PER_CU; 4, 5, 8, 16: 130.7-130.8 ms alike in round 4)
     if (const char *e = kw_env("KW_DEDUP_TBLOCKS_PER_CU")) tbpc = std::max(1, atoi(e));
     const int tgrid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * tbpc);
     const size_t need = align256(16 * (size_t)n) + align256(4 * (size_t)n) + align256(8 * tsize) +
-                        align256(4 * (size_t)n) + align256(((size_t)n + 31) / 32 * 4) + align256(8 * 8) +
+                        align256(8 * ((size_t)n_claims * 64 * TCLAIM)) + align256(4 * (size_t)n_claims) +
+                        align256(4 * (size_t)n) +
+                        align256(8 * 16) +
                         align256(8 * 4) + align256(8 * (size_t)n) + 2 * align256(8 * (size_t)ntiles) +
                         align256(16) + 2 * align256(8 * ((size_t)n + 1));
     if (need > h->buf_bytes) {
@@ -1131,11 +1205,11 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.rowd = (uint4 *)carve(16 * (size_t)n);
     S.len3 = (uint32_t *)carve(4 * (size_t)n);
     S.table = (unsigned long long *)carve(8 * tsize);
-    S.hint = (uint32_t *)carve(4 * (size_t)n);
-    const size_t moved_bytes = ((size_t)n + 31) / 32 * 4;
-    S.moved = (uint32_t *)carve(moved_bytes);
+    S.pairs = (uint2 *)carve(8 * ((size_t)n_claims * 64 * TCLAIM));
+    S.pcount = (uint32_t *)carve(4 * (size_t)n_claims);
+    S.recheck = (uint32_t *)carve(4 * (size_t)n);
     S.mask = tsize - 1;
-    S.cnt = (unsigned long long *)carve(8 * 8);
+    S.cnt = (unsigned long long *)carve(8 * 16);
     S.gnext = S.cnt + 7;
     S.nslow = (unsigned long long *)carve(8 * 4);
     S.slow = (uint2 *)carve(8 * (size_t)n);
@@ -1148,11 +1222,9 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->totals = (unsigned long long *)carve(16);
     h->kept_off = (int64_t *)carve(8 * ((size_t)n + 1));
     h->kept_row = (int64_t *)carve(8 * ((size_t)n + 1));
-    DDCHK(h, hipMemsetAsync(S.cnt, 0, 64, st));
+    DDCHK(h, hipMemsetAsync(S.cnt, 0, 128, st));
     DDCHK(h, hipMemsetAsync(S.nslow, 0, 32, st));
-    const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
     DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
-    DDCHK(h, hipMemsetAsync(S.moved, 0, moved_bytes, st));
     DDCHK(h, hipEventRecord(h->ev[0], st));
     hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
     DDCHK(h, hipGetLastError());
@@ -1176,13 +1248,22 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
         DDCHK(h, hipGetLastError());
     }
     DDCHK(h, hipEventRecord(h->ev[2], st));
-    hipLaunchKernelGGL(dd_decide_kernel, dim3(grid), dim3(BLOCK), 0, st, d_arena, n, d_code, S, d_off);
+    // decide: the pairs compared (8 lanes a pair), then the later rows of the differing ones against the table
+    hipLaunchKernelGGL(dd_pairs_kernel, dim3((int)std::min<int64_t>((n_claims + 3) / 4, (int64_t)h->cus * 16)),
+                       dim3(BLOCK), 0, st, d_arena, d_code, S, n_claims, (uint64_t)ns2[0]);
+    hipLaunchKernelGGL(dd_recheck_kernel, dim3(h->cus * 4), dim3(BLOCK), 0, st, d_arena, d_code, S);
     DDCHK(h, hipGetLastError());
     unsigned long long cnt[7];
     DDCHK(h, hipMemcpyAsync(cnt, S.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
-    if (S.stats) fprintf(stderr, "kw_dedup: table lookups in decide: %llu moved, %llu hint mismatches\n", cnt[5], cnt[6]);
-    for (int k = 0; k < 4; ++k) h->counts[k] = (int64_t)cnt[k];
+    if (S.stats)
+        fprintf(stderr, "kw_dedup: table lookups: %llu differing pairs\n", cnt[5]);
+    // per code (the CODE_COLLIDE rows are added by resolve_collisions); KEPT: the rest
+    h->counts[KW_URL_NO_HTML] = (int64_t)cnt[KW_URL_NO_HTML];
+    h->counts[KW_URL_FILTERED] = (int64_t)cnt[KW_URL_FILTERED];
+    h->counts[KW_URL_DUPLICATE] = (int64_t)cnt[KW_URL_DUPLICATE];
+    h->counts[KW_URL_KEPT] = n - (int64_t)(cnt[KW_URL_NO_HTML] + cnt[KW_URL_FILTERED] + cnt[KW_URL_DUPLICATE] +
+                                           cnt[CODE_COLLIDE]);
     if (cnt[CODE_COLLIDE]) {
         int rc = resolve_collisions(h, d_arena, d_off, n, d_code, st);
         if (rc) return rc;
@@ -1211,7 +1292,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     if (h->n_kept > 0) {
         const int cgrid = (int)std::min<int64_t>((h->n_kept + 63) / 64 * 64 / BLOCK + 1, (int64_t)h->cus * 8);
         hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, h->n_kept, (const int64_t *)h->kept_off,
-                           (const int64_t *)h->kept_row, d_arena, d_off, S, h->kept_bytes);
+                           (const int64_t *)h->kept_row, d_arena, S, h->kept_bytes);
         DDCHK(h, hipGetLastError());
     }
     DDCHK(h, hipEventRecord(h->ev[4], st));
