@@ -507,6 +507,178 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
 }
 
 constexpr int STAGE_BYTES = 8192;   // per-wave LDS copy of the wave's 64 rows
+
+// A row in the wave's LDS stage, addressed from its start with 32-bit offsets: the row starts at byte s of stage
+// dword k0 (dw(k) = the row's k-th aligned dword)
+struct LdsRow {
+    const uint32_t *w;
+    int k0;
+    uint32_t s;
+    __device__ __forceinline__ uint32_t dw(int k) const { return w[k0 + k]; }
+    __device__ __forceinline__ uint32_t ld32(int p) const
+    {
+        const int q = p + (int)s, k = k0 + (q >> 2);
+        return __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)(q & 3));
+    }
+    __device__ __forceinline__ uint64_t ld64(int p) const
+    {
+        const int q = p + (int)s, k = k0 + (q >> 2);
+        const uint32_t sh = (uint32_t)(q & 3), x0 = w[k], x1 = w[k + 1], x2 = w[k + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
+    }
+};
+
+// transform_row for a staged row (normalising runs; the common case), with 32-bit offsets: the same plan, hash
+// and codes.  Pass 1 reads one aligned dword a step (the rolling pair of dwords gives the unaligned window) and
+// masks nothing by the row's end but the "html" candidates: an extra ':' or a 'news/%' end found at or past the
+// end lies past any cut (j < L), where it changes nothing (gap needs ec < j, the filter kf < j; ec2 only matters
+// as ec2 >= j).  The hash reads each normalised word with one 3-dword LDS window.
+__device__ __forceinline__ int64_t transform_row_lds(const LdsRow &R, int L, int64_t i, int64_t b,
+                                                     uint8_t *__restrict__ code, const Scratch &S, uint2 &pair)
+{
+    constexpr int NONE = 0x7FFFFFFF;
+    int j = -1, ec = NONE, ec2 = NONE, kf = NONE;
+    bool scheme_http = false;
+    uint32_t excl = 0;   // the scheme's ':' (as transform_row)
+    if (L >= 5 && R.ld32(0) == 0x70747468u) {
+        const uint32_t w4 = R.ld32(4);
+        if ((w4 & 0xFFu) == 0x3Au && !(L >= 7 && (w4 & 0xFFFFFFu) == 0x30383Au)) { scheme_http = true; excl = 0x80u; }
+        if (L >= 6 && (w4 & 0xFFFFu) == 0x3A73u && !(L >= 8 && (w4 >> 8) == 0x30383Au)) excl = 0x8000u;
+    }
+    // the scan stops at any "html" at q in [t, t + 4); the candidates are validated out of the loop (q >= 1,
+    // q + 4 <= L, no '\n' before q), and a step without a valid one resumes the scan
+    // (d1, d2: the aligned dwords k - 1, k under y; dword k + 1 is read a step ahead)
+    uint32_t d1 = R.dw(1), d2 = R.dw(2);
+    uint32_t x = __builtin_amdgcn_alignbyte(d1, R.dw(0), R.s), xp = 0, y = 0;
+    int t = 0, k = 2;
+    for (;;) {
+        for (; t < L; t += 4, ++k) {
+            const uint32_t dn = R.dw(k + 1);
+            y = __builtin_amdgcn_alignbyte(d2, d1, R.s);
+            d1 = d2;
+            d2 = dn;
+            uint32_t cm = eq_bytes(x, 0x3A3A3A3Au);
+            if (t == 4) cm &= ~excl;
+            if (cm) {
+                const uint32_t cm1 = cm & (cm - 1u);
+                const int c0 = t + (__builtin_ctz(cm) >> 3);
+                const int c1 = cm1 ? t + (__builtin_ctz(cm1) >> 3) : NONE;
+                ec2 = ec == NONE ? c1 : (ec2 == NONE ? c0 : ec2);
+                ec = ec == NONE ? c0 : ec;
+            }
+            uint32_t pm = eq_bytes(x | 0x02020202u, 0x27272727u);
+            while (pm) {
+                const int p = t + (__builtin_ctz(pm) >> 3);
+                pm &= pm - 1u;
+                if (p >= 5 && p < kf && R.ld32(p - 5) == NEWS4 && (R.ld32(p - 1) & 0xFFu) == 0x2Fu) kf = p;
+            }
+            if ((x == HTML4) | (__builtin_amdgcn_alignbyte(y, x, 1) == HTML4) |
+                (__builtin_amdgcn_alignbyte(y, x, 2) == HTML4) | (__builtin_amdgcn_alignbyte(y, x, 3) == HTML4))
+                break;
+            xp = x;
+            x = y;
+        }
+        if (t >= L) break;   // no cut
+        uint32_t hm = (x == HTML4 ? 0x80u : 0u) | (__builtin_amdgcn_alignbyte(y, x, 1) == HTML4 ? 0x8000u : 0u) |
+                      (__builtin_amdgcn_alignbyte(y, x, 2) == HTML4 ? 0x800000u : 0u) |
+                      (__builtin_amdgcn_alignbyte(y, x, 3) == HTML4 ? 0x80000000u : 0u);
+        const int r3 = L - t - 3;   // candidates q = t + k with q + 4 <= L
+        hm &= r3 >= 4 ? 0x80808080u : (r3 <= 0 ? 0u : 0x80808080u & ((1u << (8 * r3)) - 1u));
+        hm &= ~eq_bytes(__builtin_amdgcn_alignbyte(x, xp, 3), 0x0A0A0A0Au);
+        if (t == 0) hm &= ~0x80u;
+        if (hm) {
+            const int q = t + (__builtin_ctz(hm) >> 3);
+            int sp = q - 1;
+            if ((R.ld32(sp) & 0xFFu) >= 0x80u) {
+                while (sp > 0 && (R.ld32(sp) & 0xC0u) == 0x80u && q - sp < 4) --sp;
+            }
+            j = sp;
+            break;
+        }
+        xp = x;   // no valid candidate in this step: on with the next
+        x = y;
+        t += 4;
+        ++k;
+    }
+    if (j < 0) {
+        code[i] = KW_URL_NO_HTML;
+        S.len3[i] = 0;
+        return -1;
+    }
+    const bool gap = ec < j;
+    if (gap && !(ec2 >= j && ec > 5 && ec + 3 <= j && (R.ld32(ec) & 0xFFFFFFu) == 0x30383Au))
+        return j;   // the byte-serial rewrite (dd_slow_kernel)
+    const int ins = (scheme_http && j > 4) ? 1 : 0;
+    const int G = gap ? ec + ins : NONE, E = j + ins - (gap ? 3 : 0);
+    const int len3 = E + 5;
+    // the normalised word at x (x % 8 == 0, x < len3): as FastWords, with 32-bit offsets
+    auto splice = [&](uint64_t w, int x) -> uint64_t {
+        if (E < x + 8) {
+            if (E >= x) {
+                const int sh = (E - x) * 8;
+                w = (sh ? (w & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
+            } else {
+                const int d = x - E;
+                w = d < 8 ? DOTHTML >> (8 * d) : 0ull;
+            }
+        }
+        return w;
+    };
+    auto body = [&](int x) -> uint64_t {
+        uint64_t w = (ins && x == 0) ? 0x7370747468ull | (R.ld64(4) << 40) : R.ld64(x - ins + (x >= G ? 3 : 0));
+        if (x < G && G < x + 8) {
+            const int k = (G - x) * 8;
+            w = (w & ((1ull << k) - 1)) | (R.ld64(G - ins + 3) << k);
+        }
+        return w;
+    };
+    bool jn = false;
+    if (gap) {
+        // 'news/%' | "news/'" across the gap: windows starting at G - 5 .. G - 1 (as transform_row)
+        auto seg1 = [&](int x) -> uint64_t {
+            if (!ins) return R.ld64(x);
+            if (x >= 5) return R.ld64(x - 1);
+            const uint64_t h0 = 0x7370747468ull | (R.ld64(4) << 40);
+            return x ? (h0 >> (8 * x)) | (R.ld64(7) << (64 - 8 * x)) : h0;
+        };
+        auto nword = [&](int x) -> uint64_t {
+            uint64_t w = 0;
+            if (x < E) {
+                if (x + 8 <= G) w = seg1(x);
+                else if (x >= G) w = R.ld64(x - ins + 3);
+                else {
+                    const int k = (G - x) * 8;
+                    w = (seg1(x) & ((1ull << k) - 1)) | (R.ld64(G - ins + 3) << k);
+                }
+            }
+            return splice(w, x);
+        };
+        const uint64_t lo = nword(G - 5), hi = nword(G + 3);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint64_t win = ((lo >> (8 * k)) | (k ? hi << (64 - 8 * k) : 0ull)) & 0xFFFFFFFFFFFFull;
+            jn |= win == 0x252F7377656Eull || win == 0x272F7377656Eull;
+        }
+    }
+    const bool bad = kf < j || jn;
+    // the hash over the words: word 0 (the 's' insertion) and the last words (".html" at E) in general form, the
+    // words between as plain windows (the ':80' gap's straddling word merged)
+    uint64_t h1 = 0x243F6A8885A308D3ull;
+    const int nfull = E >> 3;   // words x with x + 8 <= E: no splice
+    if (nfull > 0) h1 = mix1(h1, body(0));
+    for (int x = 8; x < 8 * nfull; x += 8) {
+        uint64_t w = R.ld64(x - ins + (x >= G ? 3 : 0));
+        if (x < G && G < x + 8) {
+            const int k = (G - x) * 8;
+            w = (w & ((1ull << k) - 1)) | (R.ld64(G - ins + 3) << k);
+        }
+        h1 = mix1(h1, w);
+    }
+    for (int x = 8 * nfull; x < len3; x += 8) h1 = mix1(h1, splice(x < E ? body(x) : 0ull, x));
+    pair = finish_row(h1, len3, bad, i, code, S, b,
+                      make_uint2((uint32_t)j, ((uint32_t)ins << 31) | (gap ? (uint32_t)ec : NO_GAP)));
+    return -1;
+}
 constexpr int TCLAIM = 8;           // groups of 64 rows a transform wave claims at once
 
 // lane = row; the wave's 64 rows are staged into LDS with coalesced 16-byte loads when they fit
@@ -551,8 +723,16 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            LdsSrc src{(const uint32_t *)stage, base};
-            if (i < n) jslow = transform_row(src, b, L, i, code, S, pair);
+            if (i < n) {
+                if (S.normalize) {
+                    const int o = (int)(b - base);
+                    const LdsRow R{(const uint32_t *)stage, o >> 2, (uint32_t)(o & 3)};
+                    jslow = transform_row_lds(R, (int)L, i, b, code, S, pair);
+                } else {
+                    LdsSrc src{(const uint32_t *)stage, base};
+                    jslow = transform_row(src, b, L, i, code, S, pair);
+                }
+            }
         } else {
             GlobalSrc src{arena};
             if (i < n) jslow = transform_row(src, b, L, i, code, S, pair);
