@@ -32,7 +32,7 @@ ARENA_PAD = 64
 
 
 def pack_urls(urls: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
-    """UTF-8 arena (padded, readable 16 B past the end) + int64 offsets (n + 1)."""
+    """UTF-8 arena (padded: readable 64 B past the end, kw_dedup_run needs 32) + int64 offsets (n + 1)."""
     enc = [u.encode('utf-8', 'surrogatepass') for u in urls]
     off = np.zeros(len(enc) + 1, dtype=np.int64)
     if enc:

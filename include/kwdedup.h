@@ -15,7 +15,7 @@
  * in glob order) gives the final yfin_urls.csv rows.
  *
  * Rows are UTF-8 URL strings in a caller-owned device arena: row i is
- * d_arena[d_off[i], d_off[i+1]); the arena must be readable 16 bytes past
+ * d_arena[d_off[i], d_off[i+1]); the arena must be readable 32 bytes past
  * d_off[n].  Every function returns 0 or a negative KW_E* code (kwmatch.h);
  * kw_dedup_last_error gives the message.  A handle is not thread-safe.
  */
