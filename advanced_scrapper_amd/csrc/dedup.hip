@@ -1092,10 +1092,11 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
 __device__ __attribute__((noinline)) void copy_group_rows(int64_t k0, int64_t n_kept, const int64_t *__restrict__ kept_off,
                                                          const int64_t *__restrict__ kept_row,
                                                          const uint8_t *__restrict__ arena, const Scratch &S,
-                                                         uint8_t *__restrict__ dst)
+                                                         uint8_t *__restrict__ dst, int nrows = 64)
 {
-    const int64_t kk = k0 + (threadIdx.x & 63);
-    if (kk >= n_kept) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t kk = k0 + lane;
+    if (lane >= nrows || kk >= n_kept) return;
     const int64_t d0 = kept_off[kk], len = kept_off[kk + 1] - d0;
     const RowGen g = row_gen(S, arena, kept_row[kk]);
 #pragma unroll 1
@@ -1197,6 +1198,140 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
     }
 }
 
+// A kept row's normalised words regenerated from the wave's LDS copy of the raw bytes (RowGen's cases: a slow
+// row's words from the slow arena, the raw strings without normalising, else FastWords)
+struct RowGenL {
+    LdsSrc src;
+    const uint64_t *sw;
+    int64_t b, G, E;
+    uint32_t len;
+    int ins, raw;
+    __device__ __forceinline__ void init(const Scratch &S, const uint32_t *stage, int64_t base, uint4 r, uint32_t l)
+    {
+        src = LdsSrc{stage, base};
+        b = (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x);
+        len = l;
+        raw = !S.normalize;
+        sw = (!raw && r.z == SLOW_ROW) ? S.sarena + r.w : nullptr;
+        ins = (int)(r.w >> 31);
+        const uint32_t ec = r.w & NO_GAP;
+        const bool gap = ec != NO_GAP;
+        G = gap ? (int64_t)ec + ins : INT64_MAX / 2;
+        E = (int64_t)r.z + ins - (gap ? 3 : 0);
+    }
+    __device__ __forceinline__ uint64_t word(int64_t x) const
+    {
+        if (x >= (int64_t)len) return 0ull;
+        if (sw) return sw[x >> 3];
+        if (raw) {
+            const uint64_t w = src.ld64(b + x);
+            return len - x >= 8 ? w : w & ((1ull << (8 * (len - x))) - 1);
+        }
+        const FastWords<LdsSrc> F{src, b, G, E, ins};
+        return F.word(x);
+    }
+};
+
+// The dense copy with staged input: a wave owns 32 kept rows (two lanes a row: the first and second half of its
+// words), stages the raw bytes they are made from with coalesced 16-byte loads (the rows are consecutive in the
+// arena but for the dropped rows between them), regenerates the words from LDS into the zeroed output stage,
+// and writes the dense range out as dd_copy_kernel does.  The lane-per-row copy regenerated each word from
+// global memory: a load instruction touched a line of each of 64 rows, and with 20 waves' rows per CU the L1
+// held none of them between a row's words (every word a new trip to L2).  A task whose raw span or dense range
+// exceeds its stage takes copy_group_rows.
+constexpr int CPS_ROWS = 32;
+constexpr int CPS_IN = 6144, CPS_OUT = 4096;   // LDS bytes per wave (one wave a block)
+__global__ __launch_bounds__(64) void dd_copy_staged_kernel(int64_t n_kept, const int64_t *__restrict__ kept_off,
+                                                            const int64_t *__restrict__ kept_row,
+                                                            const uint8_t *__restrict__ arena, Scratch S,
+                                                            uint8_t *__restrict__ dst)
+{
+    __shared__ uint4 in16[CPS_IN / 16];
+    __shared__ uint4 out16[CPS_OUT / 16];
+    uint32_t *out32 = (uint32_t *)out16;
+    const uint8_t *out8 = (const uint8_t *)out16;
+    const int lane = threadIdx.x & 63, r = lane & (CPS_ROWS - 1), half = lane / CPS_ROWS;
+    const int64_t n_tasks = (n_kept + CPS_ROWS - 1) / CPS_ROWS;
+    for (int64_t tk = blockIdx.x; tk < n_tasks; tk += gridDim.x) {
+        const int64_t k0 = tk * CPS_ROWS, kk = k0 + r;
+        const int nr = (int)(n_kept - k0 < CPS_ROWS ? n_kept - k0 : CPS_ROWS);
+        int64_t d0 = 0, len = 0, row = 0, need = 0;
+        uint4 rd = make_uint4(0u, 0u, 0u, 0u);
+        if (r < nr) {
+            row = kept_row[kk];
+            d0 = kept_off[kk];
+            len = kept_off[kk + 1] - d0;
+            rd = S.rowd[row];
+        }
+        const int64_t b = (int64_t)(((uint64_t)(rd.y & 0xFFu) << 32) | rd.x);
+        // the raw bytes a row's words read: below its cut + 16 (the 8-byte windows past a ':80' gap), its whole
+        // length when not normalising, none for a slow row; the last row's end bounds every row's
+        need = b + 16 + (!S.normalize ? len : (rd.z == SLOW_ROW ? 0 : (int64_t)rd.z));
+        const int64_t D0 = __shfl(d0, 0, 64), D1 = __shfl(d0 + len, nr - 1, 64);
+        const int64_t B0 = __shfl(b, 0, 64) & ~(int64_t)15, B1 = __shfl(need, nr - 1, 64);
+        const int64_t OA = D0 & ~(int64_t)15;
+        if (B1 - B0 > CPS_IN || D1 - OA > CPS_OUT) {   // (wave-uniform)
+            copy_group_rows(k0, n_kept, kept_off, kept_row, arena, S, dst, nr);
+            continue;
+        }
+        const int nin = (int)((B1 - B0 + 15) >> 4), nz = (int)((D1 - OA + 15) >> 4);
+        __builtin_amdgcn_wave_barrier();
+        for (int c = lane; c < nin; c += 64) in16[c] = *(const uint4 *)(arena + B0 + 16 * (int64_t)c);
+        for (int c = lane; c < nz; c += 64) out16[c] = make_uint4(0u, 0u, 0u, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (r < nr && len > 0) {
+            RowGenL g;
+            g.init(S, (const uint32_t *)in16, B0, rd, (uint32_t)len);
+            const int nw = (int)((len + 7) >> 3), nwh = (nw + 1) >> 1;
+            const int w0 = half ? nwh : 0, nwl = half ? nw - nwh : nwh;   // this lane's words [w0, w0 + nwl)
+            if (nwl > 0) {
+                const int64_t o = d0 - OA + 8 * (int64_t)w0;
+                // (the first half's words end inside the row, or at its end when it holds them all)
+                const int64_t rest = len - 8 * (int64_t)w0;
+                const int64_t bytes = half || rest < 8 * (int64_t)nwl ? rest : 8 * (int64_t)nwl;
+                const uint32_t sh = (uint32_t)(o & 3) * 8u;
+                uint32_t *dw = out32 + (o >> 2);
+                const int K = (int)(((o & 3) + bytes + 3) >> 2);
+                uint32_t prev = 0;
+                for (int k0w = 0; k0w < K; k0w += 8) {
+                    uint2 v[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int wi = (k0w >> 1) + q;
+                        const uint64_t wq = wi < nwl ? g.word(8 * (int64_t)(w0 + wi)) : 0ull;
+                        v[q] = make_uint2((uint32_t)wq, (uint32_t)(wq >> 32));
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const uint32_t cur = (jj & 1) ? v[jj >> 1].y : v[jj >> 1].x;
+                        const uint32_t out = sh ? (cur << sh) | (prev >> (32u - sh)) : cur;
+                        prev = cur;
+                        const int k = k0w + jj;
+                        if (k < K) {
+                            if (k == 0 || k == K - 1) atomicOr(&dw[k], out);
+                            else dw[k] = out;
+                        }
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t a0 = (D0 + 15) & ~(int64_t)15, a1 = D1 & ~(int64_t)15;
+        if (a0 >= a1) {
+            for (int64_t x = D0 + lane; x < D1; x += 64) dst[x] = out8[x - OA];
+        } else {
+            if (D0 + lane < a0) dst[D0 + lane] = out8[D0 + lane - OA];
+            if (a1 + lane < D1) dst[a1 + lane] = out8[a1 + lane - OA];
+            for (int64_t q = a0 + 16 * (int64_t)lane; q < a1; q += 16 * 64)
+                *(uint4 *)(dst + q) = out16[(q - OA) >> 4];
+        }
+    }
+}
+
 // the lengths of listed rows, then their normalised bytes (8-aligned slots at boff[k]): the host's exact pass
 __global__ __launch_bounds__(BLOCK) void dd_gather_len_kernel(const uint32_t *__restrict__ rows, uint32_t m, Scratch S,
                                                               uint32_t *__restrict__ out)
@@ -1223,6 +1358,8 @@ using namespace dd;
 struct kw_dedup {
     int device = 0;
     int cus = 256;
+    int copy_bpc = 4, pairs_bpc = 4, copys_bpc = 16;   // resident blocks per CU of the statically divided kernels (one round of
+                                       // blocks: a second partial round left CUs idle at the end)
     std::string err;
     void *d_buf = nullptr;
     size_t buf_bytes = 0;
@@ -1260,6 +1397,12 @@ extern "C" int kw_dedup_create(int32_t device, kw_dedup **out)
     hipDeviceProp_t prop;
     DDCHK(h, hipGetDeviceProperties(&prop, device));
     h->cus = prop.multiProcessorCount;
+    DDCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&h->copy_bpc, dd_copy_kernel, BLOCK, 0));
+    DDCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&h->pairs_bpc, dd_pairs_kernel, BLOCK, 0));
+    DDCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&h->copys_bpc, dd_copy_staged_kernel, 64, 0));
+    h->copy_bpc = std::max(1, h->copy_bpc);
+    h->copys_bpc = std::max(1, h->copys_bpc);
+    h->pairs_bpc = std::max(1, h->pairs_bpc);
     for (auto &e : h->ev) DDCHK(h, hipEventCreate(&e));
     return KW_OK;
 }
@@ -1429,7 +1572,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     }
     DDCHK(h, hipEventRecord(h->ev[2], st));
     // decide: the pairs compared (8 lanes a pair), then the later rows of the differing ones against the table
-    hipLaunchKernelGGL(dd_pairs_kernel, dim3((int)std::min<int64_t>((n_claims + 3) / 4, (int64_t)h->cus * 16)),
+    hipLaunchKernelGGL(dd_pairs_kernel, dim3((int)std::min<int64_t>((n_claims + 3) / 4, (int64_t)h->cus * h->pairs_bpc)),
                        dim3(BLOCK), 0, st, d_arena, d_code, S, n_claims, (uint64_t)ns2[0]);
     hipLaunchKernelGGL(dd_recheck_kernel, dim3(h->cus * 4), dim3(BLOCK), 0, st, d_arena, d_code, S);
     DDCHK(h, hipGetLastError());
@@ -1471,8 +1614,14 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->kept_bytes = (uint8_t *)h->d_kept;
     if (h->n_kept > 0) {
         const int cgrid = (int)std::min<int64_t>((h->n_kept + 63) / 64 * 64 / BLOCK + 1, (int64_t)h->cus * 8);
-        hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, h->n_kept, (const int64_t *)h->kept_off,
-                           (const int64_t *)h->kept_row, d_arena, S, h->kept_bytes);
+        if (kw_env("KW_DEDUP_COPY_LANE_ROW"))   // (A/B: the lane-per-row copy from global memory)
+            hipLaunchKernelGGL(dd_copy_kernel, dim3(cgrid), dim3(BLOCK), 0, st, h->n_kept, (const int64_t *)h->kept_off,
+                               (const int64_t *)h->kept_row, d_arena, S, h->kept_bytes);
+        else
+            hipLaunchKernelGGL(dd_copy_staged_kernel, dim3((int)std::min<int64_t>((h->n_kept + CPS_ROWS - 1) / CPS_ROWS,
+                                                                                (int64_t)h->cus * h->copys_bpc)),
+                               dim3(64), 0, st, h->n_kept, (const int64_t *)h->kept_off, (const int64_t *)h->kept_row,
+                               d_arena, S, h->kept_bytes);
         DDCHK(h, hipGetLastError());
     }
     DDCHK(h, hipEventRecord(h->ev[4], st));
