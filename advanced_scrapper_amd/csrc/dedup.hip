@@ -508,6 +508,23 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
 
 constexpr int STAGE_BYTES = 8192;   // per-wave LDS copy of the wave's 64 rows
 
+// A wave's 16-byte chunks [0, nch) of src into its LDS stage by LDS-DMA (global_load_lds_dwordx4: 64 chunks
+// an instruction, every instruction issued before the one wait; no VGPRs).  A loop of load-then-store waited
+// for each of its ~6 loads in turn, and staging through registers all at once spilled.  Lanes past nch re-read
+// the last chunk (their LDS bytes lie inside the stage, past what is read).
+typedef __attribute__((address_space(1))) const void gmem_void;
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void stage_dma(uint4 *stage, const uint8_t *__restrict__ src, int nch)
+{
+    const int lane = threadIdx.x & 63;
+    for (int u = 0; 64 * u < nch; ++u) {
+        const int c = 64 * u + lane;
+        const int cc = c < nch ? c : nch - 1;
+        __builtin_amdgcn_global_load_lds((gmem_void *)(src + 16 * (int64_t)cc), (lds_void *)(stage + 64 * u), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // A row in the wave's LDS stage, addressed from its start with 32-bit offsets: the row starts at byte s of stage
 // dword k0 (dw(k) = the row's k-th aligned dword)
 struct LdsRow {
@@ -719,7 +736,7 @@ __global__ __launch_bounds__(BLOCK) void dd_transform_kernel(const uint8_t *__re
         uint2 pair = make_uint2(0u, NO_HINT);
         if (nch * 16 + 16 <= STAGE_BYTES) {
             __builtin_amdgcn_wave_barrier();
-            for (int64_t c = lane; c < nch; c += 64) stage[c] = *(const uint4 *)(arena + base + 16 * c);
+            stage_dma(stage, arena + base, (int)nch);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1276,7 +1293,7 @@ __global__ __launch_bounds__(64) void dd_copy_staged_kernel(int64_t n_kept, cons
         }
         const int nin = (int)((B1 - B0 + 15) >> 4), nz = (int)((D1 - OA + 15) >> 4);
         __builtin_amdgcn_wave_barrier();
-        for (int c = lane; c < nin; c += 64) in16[c] = *(const uint4 *)(arena + B0 + 16 * (int64_t)c);
+        stage_dma(in16, arena + B0, nin);
         for (int c = lane; c < nz; c += 64) out16[c] = make_uint4(0u, 0u, 0u, 0u);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
