@@ -846,7 +846,14 @@ __device__ __forceinline__ uint64_t row_hash(const Scratch &S, const RowGen &g)
 // dd_pairs_kernel: 8 lanes a pair, lane s comparing words s, s + 8, ... of the two regenerated rows, so each load
 // instruction touches a few lines of 8 rows (lane = row made every load touch 64 rows' lines: 37.8 ms at 500M
 // rows, 123M pairs)
-constexpr int PAIR_LANES = 8;
+#ifndef DD_PAIR_LANES
+#define DD_PAIR_LANES 4
+#endif
+#ifndef DD_PAIR_UNROLL
+#define DD_PAIR_UNROLL 4
+#endif
+constexpr int PAIR_LANES = DD_PAIR_LANES;    // lanes a pair
+constexpr int PAIR_UNROLL = DD_PAIR_UNROLL;  // words a lane has in flight per row
 
 // a row's descriptor and resolved length, loaded by one lane (handed to the lanes that use it by shuffles)
 struct Desc {
@@ -872,6 +879,52 @@ __device__ __forceinline__ Desc shfl_desc(const Desc &d, int src)
     return o;
 }
 
+// A row's normalised words for the pair compare with 32-bit offsets (RowGen's cases; rows shorter than 2^31
+// bytes): one raw window a word, the 's' insertion taken from the same window (u[4..7) is its bytes 4..6)
+struct PairRow {
+    const uint8_t *a;       // the row's raw start
+    const uint64_t *sw;     // a slow row's words
+    int G, E, len, ins;
+    __device__ __forceinline__ void init(const Scratch &S, const uint8_t *arena, uint4 r, uint32_t l)
+    {
+        a = arena + (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x);
+        len = (int)l;
+        sw = (S.normalize && r.z == SLOW_ROW) ? S.sarena + r.w : nullptr;
+        ins = (int)(r.w >> 31);
+        const uint32_t ec = r.w & NO_GAP;
+        const bool gap = ec != NO_GAP;
+        G = gap ? (int)ec + ins : 0x7FFFFFFF;
+        E = (int)r.z + ins - (gap ? 3 : 0);
+    }
+    __device__ __forceinline__ uint64_t word(int x, bool normalize) const   // x < len, x % 8 == 0
+    {
+        if (!normalize) {
+            const uint64_t w = ld64(a, x);
+            return len - x >= 8 ? w : w & ((1ull << (8 * (len - x))) - 1);
+        }
+        if (sw) return sw[x >> 3];
+        int p = x - ins + (x >= G ? 3 : 0);
+        p = p < 0 ? 0 : p;
+        uint64_t v = ld64(a, p);
+        if (ins & (x == 0)) v = 0x7370747468ull | ((v >> 32) << 40);
+        if (x < G && G < x + 8) {
+            const int k = (G - x) * 8;
+            v = (v & ((1ull << k) - 1)) | (ld64(a, G - ins + 3) << k);
+        }
+        v = x < E ? v : 0ull;
+        if (E < x + 8) {
+            if (E >= x) {
+                const int sh = (E - x) * 8;
+                v = (sh ? (v & ((1ull << sh) - 1)) : 0ull) | (DOTHTML << sh);
+            } else {
+                const int d = x - E;
+                v = d < 8 ? DOTHTML >> (8 * d) : 0ull;
+            }
+        }
+        return v;
+    }
+};
+
 // pairs e[0, m) (m <= 64, wave-uniform): lane t loads pair t's two descriptors, then 8 rounds of 8 pairs, lane s
 // of a pair's group comparing words s, s + 8, ... of the two regenerated rows (each load instruction touches a
 // few lines of 8 rows; the descriptors' dependent loads are paid once per 64 pairs)
@@ -896,13 +949,25 @@ __device__ __forceinline__ void compare_pairs(const uint8_t *__restrict__ arena,
         const bool act = (uint32_t)src < m && ((lm >> src) & 1ull);
         uint64_t d = 0;
         if (act) {
-            RowGen gx, gy;
-            gx.init_len(S, arena, x.r, x.len);
-            gy.init_len(S, arena, y.r, y.len);
-            d = gx.len != gy.len;
+            // (rows of 2 GiB and more count as differing: the recheck compares them with 64-bit offsets)
+            d = x.len != y.len || x.len >= 0x80000000u;
             if (!d) {
-                const int64_t nw = ((int64_t)gx.len + 7) / 8;
-                for (int64_t w = s; w < nw; w += PAIR_LANES) d |= gx.word(8 * w) ^ gy.word(8 * w);
+                PairRow gx, gy;
+                gx.init(S, arena, x.r, x.len);
+                gy.init(S, arena, y.r, y.len);
+                const int nw = (gx.len + 7) >> 3;
+                const bool nz = S.normalize != 0;
+                for (int w0 = s; w0 < nw; w0 += PAIR_LANES * PAIR_UNROLL) {
+                    uint64_t xa[PAIR_UNROLL], ya[PAIR_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < PAIR_UNROLL; ++u) {
+                        const int w = w0 + u * PAIR_LANES;
+                        xa[u] = w < nw ? gx.word(8 * w, nz) : 0ull;
+                        ya[u] = w < nw ? gy.word(8 * w, nz) : 0ull;
+                    }
+#pragma unroll
+                    for (int u = 0; u < PAIR_UNROLL; ++u) d |= xa[u] ^ ya[u];
+                }
             }
         }
         const uint64_t bm = __ballot(d != 0);
