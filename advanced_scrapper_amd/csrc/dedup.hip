@@ -879,15 +879,31 @@ __device__ __forceinline__ Desc shfl_desc(const Desc &d, int src)
     return o;
 }
 
-// A row's normalised words for the pair compare with 32-bit offsets (RowGen's cases; rows shorter than 2^31
-// bytes): one raw window a word, the 's' insertion taken from the same window (u[4..7) is its bytes 4..6)
-struct PairRow {
-    const uint8_t *a;       // the row's raw start
+// A row's normalised words with 32-bit offsets from its raw start (RowGen's cases; rows shorter than 2^31
+// bytes): one raw window a word, the 's' insertion taken from the same window (u[4..7) is its bytes 4..6).
+// Src::ld64(p) = the 8 raw bytes at p: GRow from global memory (the pair compare), LRow from the wave's LDS
+// stage (the copy).
+struct GRow {
+    const uint8_t *a;   // the row's raw start
+    __device__ __forceinline__ uint64_t ld64(int p) const { return dd::ld64(a, p); }
+};
+struct LRow {
+    const uint32_t *w;  // the stage's words; the row starts at stage byte o
+    int o;
+    __device__ __forceinline__ uint64_t ld64(int p) const
+    {
+        const int q = o + p, k = q >> 2;
+        const uint32_t sh = (uint32_t)(q & 3), x0 = w[k], x1 = w[k + 1], x2 = w[k + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
+    }
+};
+template <class Src>
+struct NormRow {
+    Src src;
     const uint64_t *sw;     // a slow row's words
     int G, E, len, ins;
-    __device__ __forceinline__ void init(const Scratch &S, const uint8_t *arena, uint4 r, uint32_t l)
+    __device__ __forceinline__ void plan(const Scratch &S, uint4 r, uint32_t l)
     {
-        a = arena + (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x);
         len = (int)l;
         sw = (S.normalize && r.z == SLOW_ROW) ? S.sarena + r.w : nullptr;
         ins = (int)(r.w >> 31);
@@ -899,17 +915,17 @@ struct PairRow {
     __device__ __forceinline__ uint64_t word(int x, bool normalize) const   // x < len, x % 8 == 0
     {
         if (!normalize) {
-            const uint64_t w = ld64(a, x);
+            const uint64_t w = src.ld64(x);
             return len - x >= 8 ? w : w & ((1ull << (8 * (len - x))) - 1);
         }
         if (sw) return sw[x >> 3];
         int p = x - ins + (x >= G ? 3 : 0);
         p = p < 0 ? 0 : p;
-        uint64_t v = ld64(a, p);
+        uint64_t v = src.ld64(p);
         if (ins & (x == 0)) v = 0x7370747468ull | ((v >> 32) << 40);
         if (x < G && G < x + 8) {
             const int k = (G - x) * 8;
-            v = (v & ((1ull << k) - 1)) | (ld64(a, G - ins + 3) << k);
+            v = (v & ((1ull << k) - 1)) | (src.ld64(G - ins + 3) << k);
         }
         v = x < E ? v : 0ull;
         if (E < x + 8) {
@@ -924,6 +940,7 @@ struct PairRow {
         return v;
     }
 };
+__device__ __forceinline__ int64_t desc_start(uint4 r) { return (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x); }
 
 // pairs e[0, m) (m <= 64, wave-uniform): lane t loads pair t's two descriptors, then 8 rounds of 8 pairs, lane s
 // of a pair's group comparing words s, s + 8, ... of the two regenerated rows (each load instruction touches a
@@ -952,9 +969,11 @@ __device__ __forceinline__ void compare_pairs(const uint8_t *__restrict__ arena,
             // (rows of 2 GiB and more count as differing: the recheck compares them with 64-bit offsets)
             d = x.len != y.len || x.len >= 0x80000000u;
             if (!d) {
-                PairRow gx, gy;
-                gx.init(S, arena, x.r, x.len);
-                gy.init(S, arena, y.r, y.len);
+                NormRow<GRow> gx, gy;
+                gx.src = GRow{arena + desc_start(x.r)};
+                gx.plan(S, x.r, x.len);
+                gy.src = GRow{arena + desc_start(y.r)};
+                gy.plan(S, y.r, y.len);
                 const int nw = (gx.len + 7) >> 3;
                 const bool nz = S.normalize != 0;
                 for (int w0 = s; w0 < nw; w0 += PAIR_LANES * PAIR_UNROLL) {
@@ -1280,40 +1299,6 @@ __global__ __launch_bounds__(BLOCK) void dd_copy_kernel(int64_t n_kept, const in
     }
 }
 
-// A kept row's normalised words regenerated from the wave's LDS copy of the raw bytes (RowGen's cases: a slow
-// row's words from the slow arena, the raw strings without normalising, else FastWords)
-struct RowGenL {
-    LdsSrc src;
-    const uint64_t *sw;
-    int64_t b, G, E;
-    uint32_t len;
-    int ins, raw;
-    __device__ __forceinline__ void init(const Scratch &S, const uint32_t *stage, int64_t base, uint4 r, uint32_t l)
-    {
-        src = LdsSrc{stage, base};
-        b = (int64_t)(((uint64_t)(r.y & 0xFFu) << 32) | r.x);
-        len = l;
-        raw = !S.normalize;
-        sw = (!raw && r.z == SLOW_ROW) ? S.sarena + r.w : nullptr;
-        ins = (int)(r.w >> 31);
-        const uint32_t ec = r.w & NO_GAP;
-        const bool gap = ec != NO_GAP;
-        G = gap ? (int64_t)ec + ins : INT64_MAX / 2;
-        E = (int64_t)r.z + ins - (gap ? 3 : 0);
-    }
-    __device__ __forceinline__ uint64_t word(int64_t x) const
-    {
-        if (x >= (int64_t)len) return 0ull;
-        if (sw) return sw[x >> 3];
-        if (raw) {
-            const uint64_t w = src.ld64(b + x);
-            return len - x >= 8 ? w : w & ((1ull << (8 * (len - x))) - 1);
-        }
-        const FastWords<LdsSrc> F{src, b, G, E, ins};
-        return F.word(x);
-    }
-};
-
 // The dense copy with staged input: a wave owns 32 kept rows (two lanes a row: the first and second half of its
 // words), stages the raw bytes they are made from with coalesced 16-byte loads (the rows are consecutive in the
 // arena but for the dropped rows between them), regenerates the words from LDS into the zeroed output stage,
@@ -1364,8 +1349,10 @@ __global__ __launch_bounds__(64) void dd_copy_staged_kernel(int64_t n_kept, cons
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (r < nr && len > 0) {
-            RowGenL g;
-            g.init(S, (const uint32_t *)in16, B0, rd, (uint32_t)len);
+            NormRow<LRow> g;
+            g.src = LRow{(const uint32_t *)in16, (int)(b - B0)};
+            g.plan(S, rd, (uint32_t)len);
+            const bool nz = S.normalize != 0;
             const int nw = (int)((len + 7) >> 3), nwh = (nw + 1) >> 1;
             const int w0 = half ? nwh : 0, nwl = half ? nw - nwh : nwh;   // this lane's words [w0, w0 + nwl)
             if (nwl > 0) {
@@ -1382,7 +1369,7 @@ __global__ __launch_bounds__(64) void dd_copy_staged_kernel(int64_t n_kept, cons
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int wi = (k0w >> 1) + q;
-                        const uint64_t wq = wi < nwl ? g.word(8 * (int64_t)(w0 + wi)) : 0ull;
+                        const uint64_t wq = wi < nwl ? g.word(8 * (w0 + wi), nz) : 0ull;
                         v[q] = make_uint2((uint32_t)wq, (uint32_t)(wq >> 32));
                     }
 #pragma unroll
