@@ -42,9 +42,16 @@ def corpus(golden):
             'texts': texts + a_t + m_t + c.texts(), 'titles': titles + a_i + m_i + c.titles()}
 
 
-def _run(corpus, monkeypatch, **env):
+# Every capacity large (a scan of this corpus grows none of them): the reference point of each test below,
+# which makes one capacity small and keeps the others large, so the statistics show that capacity's path alone
+LARGE = {'KW_TEST_CAND_CAP': 1 << 20, 'KW_TEST_ITEM_CAP': 1 << 20, 'KW_TEST_TASK_CAP': 1 << 13,
+         'KW_TEST_DSET_SIZE': 1 << 22}
+CAUSES = _native.KW_RESCAN_REGIONS | _native.KW_RESCAN_TASK_QUEUES | _native.KW_RESCAN_DECIDED_SET
+
+
+def _run(corpus, monkeypatch, large=True, **env):
     from advanced_scrapper_amd.matcher import GpuMatcher
-    for k, v in env.items():
+    for k, v in {**(LARGE if large else {}), **env}.items():
         monkeypatch.setenv(k, str(v))
     m = GpuMatcher(corpus['ckb'])            # a fresh handle: its regions start at the forced sizes
     got = _gpu_maps(m, corpus['texts'], corpus['titles'])
@@ -55,8 +62,18 @@ def _run(corpus, monkeypatch, **env):
 
 
 @pytest.fixture(scope='module')
+def natural(corpus):
+    """The corpus with the library's own sizing (no overrides): its many-item documents grow buffers."""
+    mp = pytest.MonkeyPatch()
+    try:
+        return _run(corpus, mp, large=False)
+    finally:
+        mp.undo()
+
+
+@pytest.fixture(scope='module')
 def baseline(corpus):
-    """The corpus without overrides (its many-item documents already grow the generic kernel's buffers once)."""
+    """Every capacity large: no region, task queue or decided set overflows."""
     mp = pytest.MonkeyPatch()
     try:
         return _run(corpus, mp)
@@ -64,11 +81,10 @@ def baseline(corpus):
         mp.undo()
 
 
-def test_baseline_no_overrides(baseline):
-    assert baseline['deferred_docs'] > 0 and baseline['big_docs'] > 0
-    # the corpus alone grows only other buffers: each override below must add its own cause
-    assert not baseline['rescan_causes'] & (_native.KW_RESCAN_REGIONS | _native.KW_RESCAN_TASK_QUEUES |
-                                            _native.KW_RESCAN_DECIDED_SET), baseline
+def test_baseline_no_overrides(baseline, natural):
+    assert natural['deferred_docs'] > 0 and natural['big_docs'] > 0
+    # with every capacity large nothing overflows: each test below must add its own cause
+    assert not baseline['rescan_causes'] & CAUSES, baseline
 
 
 def test_candidate_region_overflow_rescans(corpus, baseline, monkeypatch):
@@ -98,8 +114,8 @@ def test_decided_set_full_rescans(corpus, baseline, monkeypatch):
     assert st['rescan_causes'] & _native.KW_RESCAN_DECIDED_SET
 
 
-def test_overrides_ignored_without_the_gate(corpus, baseline, monkeypatch):
-    """A production process (no KW_TEST_HOOKS) ignores the overrides: the baseline's statistics."""
+def test_overrides_ignored_without_the_gate(corpus, natural, monkeypatch):
+    """A production process (no KW_TEST_HOOKS) ignores the overrides: the library's own sizing's statistics."""
     monkeypatch.delenv('KW_TEST_HOOKS', raising=False)
-    st = _run(corpus, monkeypatch, KW_TEST_CAND_CAP=16, KW_TEST_TASK_CAP=2)
-    assert st == baseline
+    st = _run(corpus, monkeypatch, large=False, KW_TEST_CAND_CAP=16, KW_TEST_TASK_CAP=2)
+    assert st == natural
