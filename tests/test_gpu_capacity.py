@@ -44,7 +44,7 @@ def corpus(golden):
 
 # Every capacity large (a scan of this corpus grows none of them): the reference point of each test below,
 # which makes one capacity small and keeps the others large, so the statistics show that capacity's path alone
-LARGE = {'KW_TEST_CAND_CAP': 1 << 20, 'KW_TEST_ITEM_CAP': 1 << 20, 'KW_TEST_TASK_CAP': 1 << 13,
+LARGE = {'KW_TEST_CAND_CAP': 1 << 20, 'KW_TEST_ITEM_CAP': 1 << 20, 'KW_TEST_TASK_CAP': 1 << 16,
          'KW_TEST_DSET_SIZE': 1 << 22}
 CAUSES = _native.KW_RESCAN_REGIONS | _native.KW_RESCAN_TASK_QUEUES | _native.KW_RESCAN_DECIDED_SET
 
