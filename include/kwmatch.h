@@ -133,18 +133,19 @@ int kw_hits_copy(kw_handle *h, kw_hit *d_dst, int64_t cap, int64_t *n_hits, void
 #define KW_RESCAN_REGIONS 128       /* a filter region's candidates or a probe region's items */
 int kw_stats(kw_handle *h, int64_t *stats, int32_t n_stats);
 
-/* Device times (ms) of the last kw_scan, from HIP events on the scan's stream
- * (valid after kw_hits): the fast path (scan + resolve kernels), the generic
- * kernel that redoes deferred documents, and everything including result
- * compaction. */
+/* Device times (ms) of the last kw_scan, from HIP events on the scan's streams
+ * (valid after kw_hits): the fast path up to the generic kernel's start (scan +
+ * resolve kernels), the generic kernel that redoes deferred documents, and
+ * everything including result compaction. */
 int kw_last_kernel_ms(kw_handle *h, float *fast_ms, float *generic_ms, float *total_ms);
 
 /* Per-kernel device times (ms) of the last kw_scan, up to 10 values: [0] scan
- * (filter + probe + epilogue kernels), [1] resolve phase (the task kernels,
- * then the wait for the resolve kernel, which starts after the probe on a
- * side stream), [2] generic, [3] result compaction, [4] total, [5] filter
- * kernel, [6] probe kernel, [7] epilogue kernel, [8] resolve kernel (side
- * stream), [9] task kernels. */
+ * (filter + probe + epilogue kernels), [1] resolve phase (the resolve kernels
+ * on the side stream, from the epilogue's end to the generic kernel's start),
+ * [2] generic (side stream, beside the task kernels), [3] result compaction
+ * and any wait for the task kernels, [4] total, [5] filter kernel, [6] probe
+ * kernel, [7] epilogue kernel, [8] resolve kernel (side stream), [9] task
+ * kernels (from the epilogue's end). */
 int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 
 /* Which kernel finished each document of the last scan (after kw_hits):
