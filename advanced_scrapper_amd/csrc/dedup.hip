@@ -1168,25 +1168,39 @@ __global__ __launch_bounds__(BLOCK) void dd_place_kernel(const uint8_t *__restri
                                                          const unsigned long long *__restrict__ tile_bytes,
                                                          int64_t *__restrict__ kept_off, int64_t *__restrict__ kept_row)
 {
+    // the tile's kept entries assembled in LDS, then written as two contiguous runs (each thread writing its
+    // own rows' entries in place wrote every line in 3-entry pieces: 12 GB of writes for 5.6 GB of entries)
     __shared__ uint64_t sh[2 * BLOCK / 64];
+    __shared__ int64_t soff[SCAN_TILE], srow[SCAN_TILE];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ROWS;
+    uint8_t k[SCAN_ROWS];
+    uint32_t l[SCAN_ROWS];
     uint64_t c = 0, by = 0;
+#pragma unroll
     for (int r = 0; r < SCAN_ROWS; ++r) {
         const int64_t i = base + r;
-        if (i < n && code[i] == KW_URL_KEPT) { ++c; by += S.len3[i]; }
+        k[r] = i < n ? code[i] : (uint8_t)0xFF;
+        l[r] = k[r] == KW_URL_KEPT ? S.len3[i] : 0u;
+        c += k[r] == KW_URL_KEPT;
+        by += l[r];
     }
     uint64_t ta, tb;
-    block_excl_scan2(c, by, sh, ta, tb);
-    c += tile_cnt[blockIdx.x];
-    by += tile_bytes[blockIdx.x];
+    block_excl_scan2(c, by, sh, ta, tb);   // (c, by): this thread's first entry within the tile, its offset
+    const uint64_t c0 = tile_cnt[blockIdx.x], b0 = tile_bytes[blockIdx.x];
+    uint32_t q = (uint32_t)c;
+#pragma unroll
     for (int r = 0; r < SCAN_ROWS; ++r) {
-        const int64_t i = base + r;
-        if (i < n && code[i] == KW_URL_KEPT) {
-            kept_off[c] = (int64_t)by;
-            kept_row[c] = i;
-            ++c;
-            by += S.len3[i];
+        if (k[r] == KW_URL_KEPT) {
+            soff[q] = (int64_t)(b0 + by);
+            srow[q] = base + r;
+            ++q;
+            by += l[r];
         }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < (uint32_t)ta; e += BLOCK) {
+        kept_off[c0 + e] = soff[e];
+        kept_row[c0 + e] = srow[e];
     }
 }
 
