@@ -64,7 +64,7 @@ constexpr uint32_t NO_HINT = 0xFFFFFFFFu;         // a kept row that took its ta
 constexpr uint32_t SLOW_ROW = 0xFFFFFFFFu;        // plan.x of a byte-serial row (plan.y: its slow-arena word)
 constexpr uint32_t NO_GAP = 0x7FFFFFFFu;          // plan.y bits 0..30 without a ':80' gap
 constexpr uint32_t LEN_BIG = 0xFFFFFFu;           // rowd's 24-bit length field of a longer row (len3 holds it)
-// a table slot: the hash's high 32 bits (tag) | the row + 1 (0: empty)
+// a table slot: the hash's high 24 bits (tag) | the run's epoch (8 bits; another epoch: empty) | the row + 1
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *__restrict__ a, int64_t p)
 {
@@ -116,6 +116,8 @@ struct Scratch {
     uint32_t *pcount;        // pairs per claim
     uint32_t *recheck;       // rows compared with their tag's first row from the table (cnt[5] listed)
     uint64_t mask;
+    uint32_t epoch;          // this run's table epoch (1..255): a slot of another epoch is empty, so the table is
+                             //   cleared only when it moves, grows or the epoch wraps (the memset cost 1.4 ms a run)
     unsigned long long *cnt;   // [0], [2], [3], [4]: rows per code but KEPT; [5] differing pairs;
                                // [7] the transform's next group of 64 rows
     unsigned long long *gnext;   // &cnt[7]
@@ -226,7 +228,7 @@ struct LdsSrc {
     }
 };
 
-// Open-addressing table of 64-bit slots {tag, row}: the first inserter of a tag claims a slot by CAS, an earlier
+// Open-addressing table of 64-bit slots {tag, epoch, row}: the first inserter of a tag claims a slot by CAS, an earlier
 // row (smaller index) displaces the holder by atomicMin, so the slot ends with the tag's first row
 // (keep='first').  Every kept row returns at most one pair (later row, earlier row) of its tag to compare: (row,
 // the earlier holder it found), or (the holder, row) when it displaced the holder (each row leaves its slot at
@@ -239,14 +241,16 @@ struct LdsSrc {
 // kernels read the pairs, bits and plans after the kernel boundary.
 __device__ __forceinline__ uint2 table_insert(const Scratch &S, uint64_t h, int64_t i)
 {
-    const unsigned long long key = ((h >> 32) << 32) | (uint64_t)((uint32_t)i + 1u);   // (row + 1: 0 is empty)
+    // slot = the hash's high 24 bits (tag) | the epoch (8 bits) | the row + 1
+    const unsigned long long key = ((h >> 40) << 40) | ((uint64_t)S.epoch << 32) | (uint64_t)((uint32_t)i + 1u);
     uint64_t slot = (h ^ (h >> 29)) & S.mask;
     unsigned long long cur = S.table[slot];
     uint2 pr = make_uint2((uint32_t)i, NO_HINT);
     for (;;) {
-        if (cur == 0ull) {
-            cur = atomicCAS(&S.table[slot], 0ull, key);
-            if (cur == 0ull) break;
+        if (((cur >> 32) & 0xFFu) != S.epoch) {   // empty (another run's or never written)
+            const unsigned long long got = atomicCAS(&S.table[slot], cur, key);
+            if (got == cur) break;
+            cur = got;
             continue;   // claimed meanwhile: look at the claimer
         }
         if ((cur >> 32) == (key >> 32)) {
@@ -1031,13 +1035,14 @@ __device__ __forceinline__ void recheck_row(const uint8_t *__restrict__ arena, u
     const uint64_t h = row_hash(S, gi);
     uint64_t slot = (h ^ (h >> 29)) & S.mask;
     unsigned long long cur;
-    for (;;) {
+    const uint32_t want = (uint32_t)((h >> 40) << 8) | S.epoch;   // its tag and this run's epoch
+    for (;;) {   // (the row's own insert left its tag on this probe path)
         cur = S.table[slot];
-        if ((cur >> 32) == (h >> 32)) break;
+        if ((uint32_t)(cur >> 32) == want) break;
         slot = (slot + 1) & S.mask;
     }
-    const uint32_t r0 = (uint32_t)cur - 1u;   // (an empty slot: weak test hashes only; no row)
-    const bool eq = cur != 0ull && r0 != i && same_url(gi, row_gen(S, arena, r0));
+    const uint32_t r0 = (uint32_t)cur - 1u;
+    const bool eq = r0 != i && same_url(gi, row_gen(S, arena, r0));
     code[i] = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
     atomicAdd(&S.cnt[eq ? KW_URL_DUPLICATE : CODE_COLLIDE], 1ull);
 }
@@ -1458,6 +1463,9 @@ struct kw_dedup {
     void *d_sarena = nullptr;    // the slow rows' normalised words
     size_t sarena_bytes = 0;
     int64_t n = 0, n_kept = 0, n_kept_bytes = 0;
+    void *table_at = nullptr;   // where the table was last cleared, its slots, the epoch of the last run
+    uint64_t table_slots = 0;
+    uint32_t epoch = 0;
     int64_t counts[4] = {0, 0, 0, 0};
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool have_run = false;
@@ -1632,7 +1640,14 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->kept_row = (int64_t *)carve(8 * ((size_t)n + 1));
     DDCHK(h, hipMemsetAsync(S.cnt, 0, 128, st));
     DDCHK(h, hipMemsetAsync(S.nslow, 0, 32, st));
-    DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
+    // the table is cleared when it moved or grew, or when the epoch wraps; else this run's epoch marks its slots
+    if ((void *)S.table != h->table_at || tsize != h->table_slots || h->epoch >= 255) {
+        DDCHK(h, hipMemsetAsync(S.table, 0, 8 * tsize, st));
+        h->table_at = (void *)S.table;
+        h->table_slots = tsize;
+        h->epoch = 0;
+    }
+    S.epoch = ++h->epoch;
     DDCHK(h, hipEventRecord(h->ev[0], st));
     hipLaunchKernelGGL(dd_transform_kernel, dim3(tgrid), dim3(BLOCK), 0, st, d_arena, d_off, n, d_code, S);
     DDCHK(h, hipGetLastError());
