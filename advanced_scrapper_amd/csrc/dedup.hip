@@ -60,6 +60,7 @@ constexpr uint32_t HTML4 = 0x6C6D7468u;            // "html"
 constexpr uint32_t NEWS4 = 0x7377656Eu;            // "news"
 constexpr uint64_t DOTHTML = 0x6C6D74682Eull;      // ".html"
 constexpr uint8_t CODE_COLLIDE = 4;                // internal: tag shared with a different URL
+constexpr uint32_t COLLIDE_CAP = 1u << 16;         // CODE_COLLIDE rows listed by the recheck kernel
 
 constexpr uint32_t NO_HINT = 0xFFFFFFFFu;         // a kept row that took its tag's slot
 constexpr uint32_t SLOW_ROW = 0xFFFFFFFFu;        // plan.x of a byte-serial row (plan.y: its slow-arena word)
@@ -116,11 +117,13 @@ struct Scratch {
                              //   claim of TCLAIM groups: claim c's pairs at [c * 64 * TCLAIM, + pcount[c])
     uint32_t *pcount;        // pairs per claim
     uint32_t *recheck;       // rows compared with their tag's first row from the table (cnt[5] listed)
+    uint32_t *collide;       // the CODE_COLLIDE rows (cnt[9] listed; a list longer than COLLIDE_CAP: the host
+                             //   finds them by a scan of the codes)
     uint64_t mask;
     uint32_t epoch;          // this run's table epoch (1..255): a slot of another epoch is empty, so the table is
                              //   cleared only when it moves, grows or the epoch wraps (the memset cost 1.4 ms a run)
     unsigned long long *cnt;   // [0], [2], [3], [4]: rows per code but KEPT; [5] differing pairs;
-                               // [7] the transform's next group of 64 rows
+                               // [7] the transform's next group of 64 rows; [9] CODE_COLLIDE rows listed
     unsigned long long *gnext;   // &cnt[7]
     int weak;                // tests: hash h1 down to 4 bits (forces the collision path)
     int stats;               // KW_DEDUP_STATS: print the differing pairs (rows looked up in the table)
@@ -1046,6 +1049,10 @@ __device__ __forceinline__ void recheck_row(const uint8_t *__restrict__ arena, u
     const bool eq = r0 != i && same_url(gi, row_gen(S, arena, r0));
     code[i] = eq ? (uint8_t)KW_URL_DUPLICATE : CODE_COLLIDE;
     atomicAdd(&S.cnt[eq ? KW_URL_DUPLICATE : CODE_COLLIDE], 1ull);
+    if (!eq) {
+        const unsigned long long k = atomicAdd(&S.cnt[9], 1ull);
+        if (k < COLLIDE_CAP) S.collide[k] = i;
+    }
 }
 
 // the later rows of the pairs that differed (the list)
@@ -1542,20 +1549,21 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // exact keep-first over the rows that share a hash tag with a different URL (in row order): their normalised
 // bytes regenerated on the device, compared on the host
 static int resolve_collisions(kw_dedup *h, const uint8_t *d_arena, const int64_t *d_off, int64_t n, uint8_t *d_code,
-                              hipStream_t st)
+                              hipStream_t st, unsigned long long listed)
 {
-    constexpr uint32_t CAP = 1u << 16;
+    constexpr uint32_t CAP = COLLIDE_CAP;
     std::vector<uint32_t> rows;
-    if (!h->d_collide) DDCHK(h, hipMalloc(&h->d_collide, 8 + 4 * (size_t)CAP));
     unsigned long long *d_cnt = (unsigned long long *)h->d_collide;
-    DDCHK(h, hipMemsetAsync(d_cnt, 0, 8, st));
-    const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
-    hipLaunchKernelGGL(dd_collect_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, d_cnt,
-                       (uint32_t *)(d_cnt + 1), CAP);
-    DDCHK(h, hipGetLastError());
-    unsigned long long m = 0;
-    DDCHK(h, hipMemcpyAsync(&m, d_cnt, 8, hipMemcpyDeviceToHost, st));
-    DDCHK(h, hipStreamSynchronize(st));
+    unsigned long long m = listed;   // the recheck kernel's list (its rows: the CODE_COLLIDE rows)
+    if (m > CAP) {   // (a longer list: the codes scanned again, by the kernel up to CAP, then on the host)
+        DDCHK(h, hipMemsetAsync(d_cnt, 0, 8, st));
+        const int grid = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, (int64_t)h->cus * 16);
+        hipLaunchKernelGGL(dd_collect_kernel, dim3(grid), dim3(BLOCK), 0, st, (const uint8_t *)d_code, n, d_cnt,
+                           (uint32_t *)(d_cnt + 1), CAP);
+        DDCHK(h, hipGetLastError());
+        DDCHK(h, hipMemcpyAsync(&m, d_cnt, 8, hipMemcpyDeviceToHost, st));
+        DDCHK(h, hipStreamSynchronize(st));
+    }
     if (m <= CAP) {
         rows.resize(m);
         if (m) DDCHK(h, hipMemcpy(rows.data(), d_cnt + 1, 4 * m, hipMemcpyDeviceToHost));
@@ -1667,6 +1675,8 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     S.nslow = (unsigned long long *)carve(8 * 4);
     S.slow = (uint2 *)carve(8 * (size_t)n);
     S.sarena = (uint64_t *)h->d_sarena;
+    if (!h->d_collide) DDCHK(h, hipMalloc(&h->d_collide, 8 + 4 * (size_t)COLLIDE_CAP));
+    S.collide = (uint32_t *)((unsigned long long *)h->d_collide + 1);
     S.weak = kw_env("KW_TEST_DEDUP_WEAK_HASH") ? 1 : 0;
     S.stats = kw_env("KW_DEDUP_STATS") ? 1 : 0;
     S.normalize = (flags & KW_DEDUP_NORMALIZE) ? 1 : 0;
@@ -1715,7 +1725,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
                        dim3(BLOCK), 0, st, d_arena, d_code, S, n_claims, (uint64_t)ns2[0]);
     hipLaunchKernelGGL(dd_recheck_kernel, dim3(h->cus * 4), dim3(BLOCK), 0, st, d_arena, d_code, S);
     DDCHK(h, hipGetLastError());
-    unsigned long long cnt[7];
+    unsigned long long cnt[10];
     DDCHK(h, hipMemcpyAsync(cnt, S.cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
     DDCHK(h, hipStreamSynchronize(st));
     if (S.stats)
@@ -1727,7 +1737,7 @@ extern "C" int kw_dedup_run(kw_dedup *h, const uint8_t *d_arena, const int64_t *
     h->counts[KW_URL_KEPT] = n - (int64_t)(cnt[KW_URL_NO_HTML] + cnt[KW_URL_FILTERED] + cnt[KW_URL_DUPLICATE] +
                                            cnt[CODE_COLLIDE]);
     if (cnt[CODE_COLLIDE]) {
-        int rc = resolve_collisions(h, d_arena, d_off, n, d_code, st);
+        int rc = resolve_collisions(h, d_arena, d_off, n, d_code, st, cnt[9]);
         if (rc) return rc;
     }
     DDCHK(h, hipEventRecord(h->ev[3], st));
