@@ -517,6 +517,9 @@ __device__ __forceinline__ int64_t transform_row(const Src &src, int64_t b, int6
 }
 
 constexpr int STAGE_BYTES = 8192;   // per-wave LDS copy of the wave's 64 rows
+#ifndef DD_STEP8
+#define DD_STEP8 1                  // transform_row_lds's scan: 8 bytes a step (0: 4)
+#endif
 
 // A wave's 16-byte chunks [0, nch) of src into its LDS stage by LDS-DMA (global_load_lds_dwordx4: 64 chunks
 // an instruction, every instruction issued before the one wait; no VGPRs).  A loop of load-then-store waited
@@ -572,6 +575,87 @@ __device__ __forceinline__ int64_t transform_row_lds(const LdsRow &R, int L, int
         if ((w4 & 0xFFu) == 0x3Au && !(L >= 7 && (w4 & 0xFFFFFFu) == 0x30383Au)) { scheme_http = true; excl = 0x80u; }
         if (L >= 6 && (w4 & 0xFFFFu) == 0x3A73u && !(L >= 8 && (w4 >> 8) == 0x30383Au)) excl = 0x8000u;
     }
+#if DD_STEP8
+    // 8 bytes a step (x = bytes [t, t + 4), x2 = [t + 4, t + 8), y = [t + 8, t + 12)): the loop's control, its
+    // branches' tests and the dword reads (two a step, read a step ahead) are paid once per 8 bytes.  The scan
+    // stops at any "html" at q in [t, t + 8); the candidates are validated out of the loop (q >= 1, q + 4 <= L,
+    // no '\n' before q), first those in [t, t + 4), and a step without a valid one resumes the scan
+    uint32_t d1 = R.dw(1), d2 = R.dw(2);   // the aligned dwords under x2 (and y) at a step's start
+    uint32_t x = __builtin_amdgcn_alignbyte(d1, R.dw(0), R.s), xp = 0, x2 = 0, y = 0;
+    int t = 0, k = 3;
+    auto colons = [&](uint32_t cm, int tt) {
+        const uint32_t cm1 = cm & (cm - 1u);
+        const int c0 = tt + (__builtin_ctz(cm) >> 3);
+        const int c1 = cm1 ? tt + (__builtin_ctz(cm1) >> 3) : NONE;
+        ec2 = ec == NONE ? c1 : (ec2 == NONE ? c0 : ec2);
+        ec = ec == NONE ? c0 : ec;
+    };
+    auto filt = [&](uint32_t pm, int tt) {
+        while (pm) {
+            const int p = tt + (__builtin_ctz(pm) >> 3);
+            pm &= pm - 1u;
+            if (p >= 5 && p < kf && R.ld32(p - 5) == NEWS4 && (R.ld32(p - 1) & 0xFFu) == 0x2Fu) kf = p;
+        }
+    };
+    auto any_html = [&](uint32_t lo, uint32_t hi) -> bool {
+        return (lo == HTML4) | (__builtin_amdgcn_alignbyte(hi, lo, 1) == HTML4) |
+               (__builtin_amdgcn_alignbyte(hi, lo, 2) == HTML4) | (__builtin_amdgcn_alignbyte(hi, lo, 3) == HTML4);
+    };
+    // valid candidates among q = tt + 0..3 (lo = bytes [tt, tt + 4), hi the next 4, prev the 4 before)
+    auto valid_html = [&](uint32_t lo, uint32_t hi, uint32_t prev, int tt) -> uint32_t {
+        uint32_t hm = (lo == HTML4 ? 0x80u : 0u) | (__builtin_amdgcn_alignbyte(hi, lo, 1) == HTML4 ? 0x8000u : 0u) |
+                      (__builtin_amdgcn_alignbyte(hi, lo, 2) == HTML4 ? 0x800000u : 0u) |
+                      (__builtin_amdgcn_alignbyte(hi, lo, 3) == HTML4 ? 0x80000000u : 0u);
+        const int r3 = L - tt - 3;   // q + 4 <= L
+        hm &= r3 >= 4 ? 0x80808080u : (r3 <= 0 ? 0u : 0x80808080u & ((1u << (8 * r3)) - 1u));
+        hm &= ~eq_bytes(__builtin_amdgcn_alignbyte(lo, prev, 3), 0x0A0A0A0Au);
+        if (tt == 0) hm &= ~0x80u;
+        return hm;
+    };
+    for (;;) {
+        for (; t < L; t += 8, k += 2) {
+            const uint32_t d3 = R.dw(k), d4 = R.dw(k + 1);
+            x2 = __builtin_amdgcn_alignbyte(d2, d1, R.s);
+            y = __builtin_amdgcn_alignbyte(d3, d2, R.s);
+            d1 = d3;
+            d2 = d4;
+            const uint32_t cmA = eq_bytes(x, 0x3A3A3A3Au);
+            const uint32_t cmB = eq_bytes(x2, 0x3A3A3A3Au) & (t == 0 ? ~excl : ~0u);
+            if (cmA | cmB) {
+                if (cmA) colons(cmA, t);
+                if (cmB) colons(cmB, t + 4);
+            }
+            const uint32_t pmA = eq_bytes(x | 0x02020202u, 0x27272727u), pmB = eq_bytes(x2 | 0x02020202u, 0x27272727u);
+            if (pmA | pmB) {
+                filt(pmA, t);
+                filt(pmB, t + 4);
+            }
+            if ((int)any_html(x, x2) | (int)any_html(x2, y)) break;   // (no short circuit: one test)
+            xp = x2;
+            x = y;
+        }
+        if (t >= L) break;   // no cut
+        uint32_t hm = valid_html(x, x2, xp, t);
+        int tq = t;
+        if (!hm) {
+            hm = valid_html(x2, y, x, t + 4);
+            tq = t + 4;
+        }
+        if (hm) {
+            const int q = tq + (__builtin_ctz(hm) >> 3);
+            int sp = q - 1;
+            if ((R.ld32(sp) & 0xFFu) >= 0x80u) {
+                while (sp > 0 && (R.ld32(sp) & 0xC0u) == 0x80u && q - sp < 4) --sp;
+            }
+            j = sp;
+            break;
+        }
+        xp = x2;   // no valid candidate in this step: on with the next
+        x = y;
+        t += 8;
+        k += 2;
+    }
+#else
     // the scan stops at any "html" at q in [t, t + 4); the candidates are validated out of the loop (q >= 1,
     // q + 4 <= L, no '\n' before q), and a step without a valid one resumes the scan
     // (d1, d2: the aligned dwords k - 1, k under y; dword k + 1 is read a step ahead)
@@ -627,6 +711,7 @@ __device__ __forceinline__ int64_t transform_row_lds(const LdsRow &R, int L, int
         t += 4;
         ++k;
     }
+#endif
     if (j < 0) {
         code[i] = KW_URL_NO_HTML;
         S.len3[i] = 0;
@@ -1013,7 +1098,10 @@ __device__ __forceinline__ void compare_pairs(const uint8_t *__restrict__ arena,
 }
 
 // a wave per claim: its pairs 64 at a time; then the slow rows' entries, 64 at a time
-__global__ __launch_bounds__(BLOCK) void dd_pairs_kernel(const uint8_t *__restrict__ arena, uint8_t *__restrict__ code,
+#ifndef DD_PAIRS_MINB
+#define DD_PAIRS_MINB 1   // (A/B: blocks per CU the compiler must fit)
+#endif
+__global__ __launch_bounds__(BLOCK, DD_PAIRS_MINB) void dd_pairs_kernel(const uint8_t *__restrict__ arena, uint8_t *__restrict__ code,
                                                          Scratch S, int64_t n_claims, uint64_t ns)
 {
     const int lane = threadIdx.x & 63;
