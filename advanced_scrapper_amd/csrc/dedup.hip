@@ -1,41 +1,45 @@
 // libkwmatch: CDX link-row normalise + keep-first dedup (include/kwdedup.h).
 //
 // Reference: yahoo_links_selenium.py:63-79 (per part) and :160-174 (merge);
-// restated in oracle/dedup_oracle.py.  One pass per row (lane per row):
+// restated in oracle/dedup_oracle.py.
 //
-//   dd_transform_kernel  find the cut (first "html" after a code point that is
-//                        not '\n'), plan the rewrite of the prefix (':80'
-//                        removed, 'http:' -> 'https:', ".html" appended), flag
-//                        'news/%' / "news/'", and hash the normalised URL's
-//                        words (one 64-bit word hash: tag and slot).  Nothing
-//                        of the normalised URL is stored: a row keeps its PLAN
-//                        (the cut, the 's' insertion, the one ':80' gap), from
-//                        which any later kernel regenerates its words from the
-//                        raw bytes (RowGen).  Rows whose only extra ':' is at
-//                        most one ':80' take the word-wide plan; the rest run
-//                        the byte-serial rewrite (dd_slow_kernel), whose bytes
-//                        go to a small slow-row arena.  Waves claim groups of
-//                        64 rows in row order.  Each kept row is inserted at
-//                        once (table_insert): open-addressing slots {tag, row},
-//                        the first inserter claims a slot by CAS, an earlier
-//                        row displaces the holder by atomicMin (keep='first');
-//                        a row that finds an earlier holder lists the pair
-//                        (row, holder), a row that displaces the holder lists
-//                        (holder, row).
-//   dd_pairs_kernel      a listed row is a duplicate iff its normalised bytes
-//                        equal the holder's (length, then every word, both
-//                        regenerated; 8 lanes a pair).  A differing pair's
-//                        later row is compared with its tag's first row
-//                        from the table (dd_recheck_kernel).  Rows that share
-//                        a tag with a different URL are resolved exactly on
-//                        the host.
-//   dd_count / dd_scan / dd_place / dd_copy
-//                        dense offsets, source rows and bytes of the kept rows
-//                        (the copy regenerates each kept row's words).
+//   dd_transform_kernel  lane = row over the wave's 64 rows, staged in LDS by
+//                        LDS-DMA; groups of 64 rows claimed 8 at a time, so
+//                        rows enter the table in about row order.  Finds the
+//                        cut (first "html" after a code point that is not
+//                        '\n'; a staged row scanned 8 bytes a step with 32-bit
+//                        offsets), plans the rewrite of the prefix (':80'
+//                        removed, 'http:' -> 'https:', ".html" appended),
+//                        flags 'news/%' / "news/'", and hashes the normalised
+//                        words (one 64-bit hash: tag and slot).  Nothing of
+//                        the normalised URL is stored: a row keeps a 16-byte
+//                        descriptor (raw start, length, cut, 's' insertion,
+//                        the one ':80' gap) from which later kernels
+//                        regenerate its words from the raw bytes (NormRow,
+//                        RowGen).  Rows with other extra ':' run the
+//                        byte-serial rewrite (dd_slow_kernel) into a small
+//                        slow-row arena.  Each kept row is inserted at once
+//                        (table_insert): slots {24-bit tag, 8-bit run epoch,
+//                        row}, the first inserter claims a slot by CAS, an
+//                        earlier row displaces the holder by atomicMin
+//                        (keep='first'); a row that finds an earlier holder
+//                        lists the pair (row, holder), a displacing row lists
+//                        (holder, row), in its claim's own segment.
+//   dd_pairs_kernel      a pair's later row is a duplicate iff its normalised
+//                        bytes equal the earlier row's (4 lanes a pair, the
+//                        descriptors handed out by shuffles).  A differing
+//                        pair's later row is compared with its tag's first row
+//                        from the table (dd_recheck_kernel); rows that share a
+//                        tag with a different URL are listed and resolved
+//                        exactly on the host.
+//   dd_count / dd_tile_sums / dd_scan_tiles / dd_place / dd_copy_staged
+//                        dense offsets (a two-level tile scan), source rows
+//                        and bytes of the kept rows (32 kept rows a wave, their
+//                        raw span staged by LDS-DMA, words regenerated from
+//                        LDS into an output stage, aligned 16-byte stores).
 //
-// All byte/integer work: the roofline is HBM bandwidth.  Round 5: the sparse
-// normalised arena of earlier rounds (73 GB at 500M rows, written by the
-// transform and read back by decide and the copy) is gone.
+// All byte/integer work: the roofline is HBM bandwidth; the table's random
+// atomics bound the insert.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
