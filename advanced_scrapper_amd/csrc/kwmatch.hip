@@ -470,7 +470,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
         const uint8_t *p = (const uint8_t *)st.data();
         if (st.size() >= 4) {
             const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-            const uint32_t h1 = fk_s1_hash(k4, k4 >> 8);
+            const uint32_t h1 = fk_s1_hash(k4);
             B.s1[fk_s1_word(h1)] |= 1u << (h1 & 31);
             B.l2[fk_l2_index(k4) >> 5] |= 1u << (fk_l2_index(k4) & 31);
             keys[(4ull << 32) | k4].push_back(a);
@@ -485,7 +485,7 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
             if (st.size() == 3 && !upper_only && s1_ext < FK_S1_EXT_MAX) {
                 for (uint32_t x = 0; x < 256; ++x) {
                     const uint32_t k4 = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (x << 24);
-                    const uint32_t h1 = fk_s1_hash(k4, k4 >> 8);
+                    const uint32_t h1 = fk_s1_hash(k4);
                     B.s1[fk_s1_word(h1)] |= 1u << (h1 & 31);
                 }
                 s1_ext += 256;
@@ -513,6 +513,12 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     // the box as SWAR range constants per byte: bytes < 0x80 in [lo, hi] by two additions, bytes >= 0x80 all
     // in (one flag) when the range reaches them
     if (B.has_short) {
+#if FK_GATE_UNION
+        // one range for both bytes (a superset: the exact pair table decides in stage 2), so the filter
+        // computes each word's byte flags once (fk_stage1<2>)
+        box[0] = box[2] = std::min(box[0], box[2]);
+        box[1] = box[3] = std::max(box[1], box[3]);
+#endif
         for (int r = 0; r < 2; ++r) {
             const uint32_t lo = box[2 * r], hi = box[2 * r + 1];
             const uint32_t alo = std::min(lo, 0x80u), ahi = std::min(hi, 0x7Fu);

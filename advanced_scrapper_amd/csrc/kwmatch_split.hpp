@@ -38,6 +38,10 @@ namespace kw {
                          // the round: filter 1.44 vs 1.35 ms on MI355X (the key selection's VALU costs more than
                          // the load's wait: the filter is issue-bound, not latency-bound)
 #endif
+#ifndef FK_PLACE_ASM
+#define FK_PLACE_ASM 0   // 1: stage 1's bits placed by v_lshl_or_b32 in inline asm (fewer VALU, but the compiler then
+                         // issues all 16 lookups together and waits on them at once)
+#endif
 #ifndef FS_AHEAD
 #define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
 #endif
@@ -144,12 +148,22 @@ __device__ __forceinline__ uint32_t fk_in_box(uint32_t x, uint32_t A, uint32_t B
     return (((t + A) & ~(t + B) & ~x) | (x & N)) & 0x80808080u;
 }
 
+// (a << S) | c as one v_lshl_or_b32 (left to itself the compiler shifts each bit and ORs them three at a time:
+// 1.5 instructions per bit instead of 1)
+template <int S>
+__device__ __forceinline__ uint32_t fk_lshl_or(uint32_t a, uint32_t c)
+{
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "I"(S), "v"(c));
+    return r;
+}
+
 // Stage 1 of one lane's 16 bytes W[0..3] (+ W[4]): `hit` = positions where an anchor of >= 4 bytes may start
 // (its first four bytes' bit in the 4-gram table; also the fuzzy 3-byte anchors' 4-grams), `gate` = positions
-// whose first two bytes lie in the pair box of the other 2-3 byte anchors (SWAR, no lookup); transposed bit
-// order (fk_tbit).  The 4-gram hash of position j reuses position j + 1's key (fk_s1_hash): one
-// v_mul_u32_u24 and one v_mad_u32_u24 per position.
-template <bool SHORT>
+// whose first two bytes lie in the pair box of the other 2-3 byte anchors (SWAR, no lookup; SH = 2: one box
+// for both bytes, the byte flags of each word computed once; SH = 3: two ranges below 0x80); transposed bit order (fk_tbit).  Per position:
+// one v_mad_u32_u24 (fk_s1_hash; FK_S1_ONE), the address, the lookup, v_bfe_u32 and v_lshl_or_b32.
+template <int SH>
 __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds &L, const uint32_t (&W)[5],
                                           uint32_t &hit, uint32_t &gate)
 {
@@ -160,11 +174,15 @@ __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds 
     uint32_t hh[16], sw[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
+#if FK_S1_ONE
+        hh[j] = __umul24(k[j], FK_S1_M1) + k[j];
+#else
         hh[j] = __umul24(k[j], FK_S1_M1) + __umul24(k[j + 1], FK_S1_M2);
+#endif
         sw[j] = lds_word_at(L.s1, (hh[j] >> 16) & (4u * FK_S1_WORDS - 4u));
     }
     uint32_t g = 0;
-    if (SHORT) {
+    if (SH == 1) {
         uint32_t f0[4], f1[5];
 #pragma unroll
         for (int q = 0; q < 4; ++q) f0[q] = fk_in_box(W[q], FT.gate[0], FT.gate[1], FT.gate[2]);
@@ -175,10 +193,45 @@ __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds 
             const uint32_t pr = f0[q] & __builtin_amdgcn_alignbyte(f1[q + 1], f1[q], 1);   // byte i: b[i], b[i+1]
             g |= pr >> (7 - q);
         }
+    } else if (SH == 3) {
+        // both ranges below 0x80 (no N term): a byte >= 0x80 may be flagged too (a superset; the exact pair
+        // table decides in stage 2), so each flag is two additions and one v_bitop3_b32
+        uint32_t t[5], f1[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) t[q] = W[q] & 0x7F7F7F7Fu;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) f1[q] = (t[q] + FT.gate[3]) & ~(t[q] + FT.gate[4]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t f0 = (t[q] + FT.gate[0]) & ~(t[q] + FT.gate[1]);
+            const uint32_t pr = f0 & __builtin_amdgcn_alignbyte(f1[q + 1], f1[q], 1) & 0x80808080u;
+            g |= pr >> (7 - q);
+        }
+    } else if (SH == 2) {
+        uint32_t f[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) f[q] = fk_in_box(W[q], FT.gate[0], FT.gate[1], FT.gate[2]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pr = f[q] & __builtin_amdgcn_alignbyte(f[q + 1], f[q], 1);
+            g |= pr >> (7 - q);
+        }
     }
     uint32_t h = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) h |= __builtin_amdgcn_ubfe(sw[j], hh[j], 1) << fk_tbit(j);
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t b = __builtin_amdgcn_ubfe(sw[j], hh[j], 1);
+        if (!FK_PLACE_ASM) {
+            h |= b << fk_tbit(j);
+            continue;
+        }
+        switch (fk_tbit(j)) {   // (a constant per unrolled j: the shift is the instruction's inline operand)
+#define FK_PLACE(t) case t: h = fk_lshl_or<t>(b, h); break;
+            FK_PLACE(0) FK_PLACE(1) FK_PLACE(2) FK_PLACE(3) FK_PLACE(8) FK_PLACE(9) FK_PLACE(10) FK_PLACE(11)
+            FK_PLACE(16) FK_PLACE(17) FK_PLACE(18) FK_PLACE(19) FK_PLACE(24) FK_PLACE(25) FK_PLACE(26) FK_PLACE(27)
+#undef FK_PLACE
+        }
+    }
     hit = h;
     gate = g;
 }
@@ -189,7 +242,7 @@ __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds 
 // set-up.  Keys that run over a field or document end are kept (a superset): the probe checks every
 // anchor against its field.  Non-ASCII bytes mark their field in dflags (rare: an LDS lookup of the
 // document, one atomic per field).
-template <bool SHORT>
+template <int SH>
 __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds &L, const uint8_t *__restrict__ arena,
                                                  const int64_t *__restrict__ off, int64_t n_docs, const FastScratch &S,
                                                  int64_t region, int64_t g_lo, int64_t g_hi, int wib, uint32_t &ncand,
@@ -220,7 +273,11 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         if (lane <= nd) dstart[lane] = (uint32_t)(o0 - gb);
         if (lane < nd) dtitle[lane] = (uint32_t)(o1 - gb);
         wave_sync();
-        int64_t blk = gb & ~(int64_t)15;
+        // byte offsets below are 32-bit, from the group's first 16-byte block gbase (groups are < 2^31 bytes):
+        // the loads take the SGPR base and a VGPR offset, no 64-bit address arithmetic per tile
+        const uint8_t *gbase = arena + (gb & ~(int64_t)15);
+        const uint32_t g0 = (uint32_t)(gb & 15), gl = (uint32_t)(ge - (gb & ~(int64_t)15));
+        uint32_t blk = 0;   // the tile's offset from gbase
         uint32_t kdoc = 0;   // document of the current stage-2 round's first survivor (candidate emission)
         bool ghdr = true;    // the group's header record is not written yet
         uint32_t qh = 0, qn = 0;   // the survivor queue's head and length (wave-uniform)
@@ -228,11 +285,11 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         // register copy waits for a load).  Loads are unconditional: an address past the group's last
         // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
         // comes with the word after it (lane 63's fifth word).
-        const int64_t glast = (ge - 1) & ~(int64_t)15;
-        auto load = [&](uint4 &v, uint32_t &w, int64_t tb) {
-            const int64_t a = tb + 16 * (int64_t)lane, e = tb + 1024;
-            v = *(const uint4 *)(arena + (a < glast ? a : glast));
-            w = *(const uint32_t *)(arena + (e < glast ? e : glast));
+        const uint32_t glast = (gl - 1u) & ~15u;
+        auto load = [&](uint4 &v, uint32_t &w, uint32_t tb) {
+            const uint32_t a = tb + 16u * (uint32_t)lane, e = tb + 1024u;
+            v = *(const uint4 *)(gbase + (a < glast ? a : glast));
+            w = *(const uint32_t *)(gbase + (e < glast ? e : glast));
         };
         // Stage 2, one round: the queue's first n (<= 64) survivors, lane = survivor, in position order; the
         // three second filters (every key length's: a superset of what the stage-1 family asked for, the short
@@ -286,8 +343,8 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             ccur += np;
             ncand2 += (lane == 0) ? np : 0u;
         };
-        auto tile = [&](const uint4 &v, uint32_t w4, int64_t tb) {
-            const int64_t lp = tb + 16 * (int64_t)lane;
+        auto tile = [&](const uint4 &v, uint32_t w4, uint32_t tb) {
+            const uint32_t lp = tb + 16u * (uint32_t)lane;
             uint32_t W[5];
             W[0] = v.x;
             W[1] = v.y;
@@ -297,12 +354,15 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 const uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1, WAVE);
                 W[4] = lane == WAVE - 1 ? w4 : nx;
             }
-            const int32_t rlo = (int32_t)(gb - lp), rhi = (int32_t)(ge - lp);   // |.| < 2^31: groups are
-            const int jlo = rlo <= 0 ? 0 : (rlo >= 16 ? 16 : rlo);                // capped at 2^31 bytes
-            const int jhi = rhi <= 0 ? 0 : (rhi >= 16 ? 16 : rhi);
-            const uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
-            const uint32_t rel = (uint32_t)(lp - gb);   // group-relative byte of this lane's position 0 (wraps
-                                                        // below the group start: only valid positions are used)
+            uint32_t valid = 0xFFFFu;
+            if (tb < g0 || tb + 1024u > gl) {   // (uniform: only a group's first and last tiles)
+                const int32_t rlo = (int32_t)(g0 - lp), rhi = (int32_t)(gl - lp);
+                const int jlo = rlo <= 0 ? 0 : (rlo >= 16 ? 16 : rlo);
+                const int jhi = rhi <= 0 ? 0 : (rhi >= 16 ? 16 : rhi);
+                valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
+            }
+            const uint32_t rel = lp - g0;   // group-relative byte of this lane's position 0 (wraps below the
+                                            // group start: only valid positions are used)
             if ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) {
                 uint32_t hb = 0;
 #pragma unroll
@@ -318,12 +378,12 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                     const bool title = r >= tb2;
                     atomicOr(&S.dflags[d0 + k], title ? DH_NA1 : DH_NA0);
                     const uint32_t fend = title ? dstart[k + 1] : tb2;   // group-relative end of that field
-                    const int64_t skip = (int64_t)fend - (lp - gb);
+                    const int64_t skip = (int64_t)fend - (int64_t)(int32_t)rel;
                     hb &= skip >= 16 ? 0u : ~((1u << (uint32_t)skip) - 1u);
                 }
             }
             uint32_t hit, gate;
-            fk_stage1<SHORT>(FT, L, W, hit, gate);
+            fk_stage1<SH>(FT, L, W, hit, gate);
             const uint32_t tvalid = valid == 0xFFFFu ? 0x0F0F0F0Fu : fk_transpose16(valid);
             const uint32_t sm = (hit | gate) & tvalid;
             ncand += (uint32_t)__popc(sm);
@@ -365,7 +425,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         for (bool more = true; more;) {
 #pragma unroll
             for (int k = 0; k < FS_AHEAD; ++k) {   // (unrolled: each tile in flight keeps its own registers)
-                if (blk >= ge) { more = false; break; }
+                if (blk >= gl) { more = false; break; }
                 tile(v[k], w[k], blk);
                 load(v[k], w[k], blk + 1024 * FS_AHEAD);
                 blk += 1024;
@@ -401,14 +461,19 @@ __global__ __launch_bounds__(FS_BLOCK, FS_MINW) void kw_filter_kernel(FastTables
     const int64_t n_groups = (n_docs + FG_DOCS - 1) / FG_DOCS;
     const int64_t K = S.chunk_groups;
     const int64_t n_chunks = (n_groups + K - 1) / K;
+    const bool gate_one = FT.gate[0] == FT.gate[3] && FT.gate[1] == FT.gate[4] && FT.gate[2] == FT.gate[5];
     for (int64_t c = S.dyn ? fk_next_group(S.gnext, true, 0, 0) : wave; c < n_chunks;
          c = fk_next_group(S.gnext, S.dyn, c, n_waves)) {
         uint32_t ccur = 0;
         const int64_t g_lo = c * K, g_hi = g_lo + K < n_groups ? g_lo + K : n_groups;
-        if (FT.has_short)
-            fk_filter_groups<true>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
+        if (!FT.has_short)
+            fk_filter_groups<0>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
+        else if (gate_one)
+            fk_filter_groups<2>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
+        else if (FT.gate[2] == 0u && FT.gate[5] == 0u)
+            fk_filter_groups<3>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
         else
-            fk_filter_groups<false>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
+            fk_filter_groups<1>(FT, L, arena, off, n_docs, S, c, g_lo, g_hi, wib, ncand, ncand2, ccur);
         if (lane == 0) {
             S.ccnt[c] = ccur;
             if (ccur > S.cand_cap) {

@@ -13,7 +13,7 @@ for tag in "$@"; do
   if [ "$tag" = default ]; then V=""; else V="--lib-variant $tag"; fi
   for rep in 1 2; do
     timeout -k 10 240 python bench.py --steps 30 --warmup 3 --cpu-sample 0 $V $BENCH_ARGS > gpurun_out/libab_${tag}_${rep}.log 2>&1 || exit $?
-    echo "$tag rep$rep $(grep '^{' gpurun_out/libab_${tag}_${rep}.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['roofline']['kernels_ms_avg']; print(d['ms_per_step'], d['value'], d['config'].get('hits_digest'), ' '.join(f'{a} {b:.3f}' for a, b in k.items()))")" >> gpurun_out/libab.txt
+    echo "$tag rep$rep $(grep '^{' gpurun_out/libab_${tag}_${rep}.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['roofline']['kernels_ms_avg']; print(d['ms_per_step'], d['value'], d['config'].get('hits_digest'), 'cand', d['scan_stats']['candidates'], d['scan_stats']['candidates_stage2'], ' '.join(f'{a} {b:.3f}' for a, b in k.items()))")" >> gpurun_out/libab.txt
   done
 done
 cat gpurun_out/libab.txt
