@@ -23,6 +23,12 @@
 
 using namespace kw;
 
+// The regex tasks the epilogue queued run beside the verify / short kernels (instead of after them) for KBs of
+// at most this many patterns: config 2 (3074) 4.85 -> 4.79 ms; config 4 (52k names, verify-heavy) 9.15 -> 9.37.
+#ifndef RX_SPLIT_MAX_PAT
+#define RX_SPLIT_MAX_PAT 16384
+#endif
+
 // Scratch sizes of one launch configuration (every field only grows over a handle's life).
 struct ScratchCaps {
     int nk = 0, nr = 0, ng = 0;            // epilogue, resolve and generic waves (task waves = nk)
@@ -109,6 +115,8 @@ struct kw_handle {
     hipEvent_t evf = nullptr, evp = nullptr;   // after the filter / probe kernels
     hipStream_t side = nullptr;                // the resolve kernel's stream (beside epilogue + tasks)
     hipStream_t side2 = nullptr;               // the short-field task kernel's stream (beside verify)
+    hipStream_t side3 = nullptr;               // the epilogue's regex tasks (beside verify / short; KW_RX_SPLIT)
+    hipEvent_t evrx = nullptr;                 // after them (side3)
     hipEvent_t eve = nullptr, evq = nullptr;   // after the epilogue (main); after the short kernel (side2)
     hipEvent_t evs0 = nullptr, evs1 = nullptr, evt = nullptr;   // resolve start / end (side), tasks end
     int n_anchor_fast = 0;
@@ -1127,9 +1135,11 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
         HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, (sp & 1) ? hi : lo));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side2, hipStreamNonBlocking, (sp & 2) ? hi : lo));
+        HIPCHK(h, hipStreamCreateWithPriority(&h->side3, hipStreamNonBlocking, lo));
     }
     HIPCHK(h, hipEventCreateWithFlags(&h->eve, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->evq, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->evrx, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->evx, hipEventDisableTiming));
     HIPCHK(h, hipEventCreate(&h->evs0));
     HIPCHK(h, hipEventCreate(&h->evs1));
@@ -1199,11 +1209,12 @@ static int ensure_scratch(kw_handle *h, const ScratchCaps &want)
     h->FS.ecap = c.ecap;
     h->FS.scap = c.scap;
     h->FS.xcap = c.xcap;
-    uint32_t *tcnt = (uint32_t *)carve((size_t)c.nk * 16);
+    uint32_t *tcnt = (uint32_t *)carve((size_t)c.nk * 20);
     h->FS.vcnt = tcnt;
     h->FS.ecnt = tcnt + c.nk;
     h->FS.scnt = tcnt + 2 * (size_t)c.nk;
     h->FS.xcnt = tcnt + 3 * (size_t)c.nk;
+    h->FS.xmark = tcnt + 4 * (size_t)c.nk;
     h->FS.dset = (unsigned long long *)carve(c.dsize * 8);
     h->FS.dmask = c.dsize - 1;
     h->FS.vrec = (uint4 *)carve((size_t)c.hdr_cap * 16);
@@ -1268,7 +1279,7 @@ static int launch_scan(kw_handle *h)
     hipStream_t st = h->stream;
     // KW_SERIAL=1 (profiling aid): every kernel on the main stream, so kernel traces show isolated durations
     static const bool serial = kw_env("KW_SERIAL") != nullptr;
-    hipStream_t side = serial ? st : h->side, side2 = serial ? st : h->side2;
+    hipStream_t side = serial ? st : h->side, side2 = serial ? st : h->side2, side3 = serial ? st : h->side3;
     const int64_t n_docs = h->n_docs;
     // split scan: filter regions (one wave each, resident at once), probe waves = filter regions,
     // epilogue waves = task regions
@@ -1366,9 +1377,10 @@ static int launch_scan(kw_handle *h)
         hipLaunchKernelGGL(kw_tx_kernel, dim3(std::max(1, (int)std::min<int64_t>((n_docs + TX_BLOCK - 1) / TX_BLOCK, (int64_t)h->cus * tx_bpc))),
                            dim3(TX_BLOCK), 0, side, h->FT, h->arena, h->doc_off, n_docs, h->FS);
     HIPCHK(h, hipEventRecord(h->evx, side));
+    // probe waves: the filter's wave count (each claims regions until none are left); KW_PROBE_WAVES (dev) sets it
+    static const int probe_waves = kw_env("KW_PROBE_WAVES") ? std::max(1, atoi(kw_env("KW_PROBE_WAVES"))) : 0;
     if (n_docs > 0)
-        // probe waves: at most the filter's wave count (each claims regions until none are left)
-        hipLaunchKernelGGL(kw_probe_kernel, dim3((std::min(n_regions, nsb * FS_WAVES) + PK_WAVES - 1) / PK_WAVES),
+        hipLaunchKernelGGL(kw_probe_kernel, dim3((std::min(n_regions, probe_waves ? probe_waves : nsb * FS_WAVES) + PK_WAVES - 1) / PK_WAVES),
                            dim3(PK_BLOCK), 0, st, h->FT,
                            h->T, h->arena, h->doc_off, n_regions, h->FS);
     HIPCHK(h, hipEventRecord(h->evp, st));
@@ -1410,15 +1422,34 @@ static int launch_scan(kw_handle *h)
             hipLaunchKernelGGL(kern, dim3(nb), dim3(RK_BLOCK), 0, s, h->FT, h->T, h->arena, h->doc_off,
                                n_epi, g, h->FS, h->S);
         };
+        // the early regex tasks at 2 waves per region (config 2: 4.68 ms vs 4.78 at G[3] = 4, 4.70 at 1)
+        static const int g_early = kw_env("KW_RX_EARLY_G") ? atoi(kw_env("KW_RX_EARLY_G")) : 2;
+        auto rx_task = [&](int phase, hipStream_t s) {
+            const int g = std::max(1, std::min(phase == 1 && g_early > 0 ? g_early : G[3], 16));
+            const int nb = (n_epi * g + RK_WAVES - 1) / RK_WAVES;
+            hipLaunchKernelGGL(kw_rx_task_kernel, dim3(nb), dim3(RK_BLOCK), 0, s, h->FT, h->T, h->arena, h->doc_off,
+                               n_epi, g, h->FS, h->S, phase);
+        };
         // verify and short-field tasks are independent (both only append decisions): side by side; the
-        // regex tasks they (and the epilogue) queued run after both
+        // regex tasks they queued run after both.  The regex tasks the epilogue queued (counted into xmark
+        // when it ends) run beside them on side3 (KW_RX_SPLIT=0: all regex tasks after verify and short)
+        static const int rx_split_env = kw_env("KW_RX_SPLIT") ? atoi(kw_env("KW_RX_SPLIT")) : -1;
+        const bool rx_split = rx_split_env >= 0 ? rx_split_env != 0 : h->n_pat <= RX_SPLIT_MAX_PAT;
+        if (rx_split)
+            HIPCHK(h, hipMemcpyAsync(h->FS.xmark, h->FS.xcnt, (size_t)n_epi * 4, hipMemcpyDeviceToDevice, st));
         HIPCHK(h, hipEventRecord(h->eve, st));
+        if (rx_split) {
+            HIPCHK(h, hipStreamWaitEvent(side3, h->eve, 0));
+            rx_task(1, side3);
+            HIPCHK(h, hipEventRecord(h->evrx, side3));
+        }
         HIPCHK(h, hipStreamWaitEvent(side2, h->eve, 0));
         task(kw_short_kernel, G[2], side2);
         HIPCHK(h, hipEventRecord(h->evq, side2));
         task(kw_verify_kernel, G[0], st);
         HIPCHK(h, hipStreamWaitEvent(st, h->evq, 0));
-        task(kw_rx_task_kernel, G[3], st);
+        rx_task(rx_split ? 2 : 0, st);
+        if (rx_split) HIPCHK(h, hipStreamWaitEvent(st, h->evrx, 0));
         HIPCHK(h, hipGetLastError());
     }
     HIPCHK(h, hipEventRecord(h->evt, st));
@@ -1744,11 +1775,13 @@ extern "C" int kw_destroy(kw_handle *h)
     if (h->evt) (void)hipEventDestroy(h->evt);
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
+    if (h->side3) (void)hipStreamDestroy(h->side3);
     if (h->own) (void)hipStreamDestroy(h->own);
     if (h->h_arena) (void)hipFree(h->h_arena);
     if (h->h_off) (void)hipFree(h->h_off);
     if (h->eve) (void)hipEventDestroy(h->eve);
     if (h->evq) (void)hipEventDestroy(h->evq);
+    if (h->evrx) (void)hipEventDestroy(h->evrx);
     if (h->evx) (void)hipEventDestroy(h->evx);
     if (h->evp) (void)hipEventDestroy(h->evp);
     delete h;

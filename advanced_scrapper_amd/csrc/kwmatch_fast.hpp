@@ -199,6 +199,7 @@ struct FastScratch {
     uint4 *vq, *eq, *sq, *xq;   // per scan wave: verify / edge / short / regex task regions
     uint32_t vcap, ecap, scap, xcap;
     uint32_t *vcnt, *ecnt, *scnt, *xcnt;   // per scan wave
+    uint32_t *xmark;            // per scan wave: the regex tasks the epilogue queued (xcnt after it; KW_RX_SPLIT)
     uint32_t *tmax;             // [4] largest task count a wave needed (rescan sizing)
     unsigned long long *dset;   // decided (doc, field, pattern) set: open addressing, 0 = empty
     unsigned long long dmask;

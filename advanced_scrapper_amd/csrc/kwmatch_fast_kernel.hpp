@@ -2004,10 +2004,12 @@ __device__ bool fk_rx_items(const FastScratch &S, const DevScratch &GS, const Fi
     return true;
 }
 
-// Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.
+// Regex-class names decided (by the scan or the task kernels): re.finditer positions or `name: []`.  phase 0:
+// every task of the region; 1: the tasks the epilogue queued (xmark, beside the verify / short kernels); 2: the
+// ones the verify / short kernels queued after them.
 __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTables FT, DevTables T, const uint8_t *__restrict__ arena,
                                                               const int64_t *__restrict__ off, int n_regions, int G,
-                                                              FastScratch S, DevScratch GS)
+                                                              FastScratch S, DevScratch GS, int phase)
 {
     __shared__ uint64_t rxtab_all[RK_WAVES * 256];
     __shared__ uint4 rxtxt_all[RK_WAVES * (RX_TXT / 16)];
@@ -2024,8 +2026,9 @@ __global__ __launch_bounds__(RK_BLOCK, RX_MINW) void kw_rx_task_kernel(FastTable
     OutCtx O = tout_region(S, t);
     unsigned long long nrx = 0, nrx_bt = 0, nrx_rounds = 0;
     FieldCtx F;
-    const uint32_t nx = min(S.xcnt[t], S.xcap);
-    const uint4 *xq = S.xq + (size_t)t * S.xcap;
+    const uint32_t xall = min(S.xcnt[t], S.xcap), xm = phase ? min(S.xmark[t], xall) : 0u;
+    const uint32_t x0 = phase == 2 ? xm : 0u, nx = (phase == 1 ? xm : xall) - x0;
+    const uint4 *xq = S.xq + (size_t)t * S.xcap + x0;
     for (uint32_t k0 = sub; k0 < nx; k0 += (uint32_t)G * WAVE) {
         // lane j fetches task k0 + j G and its document's view record, flags and item range (one dependent
         // round for all 64 instead of two per task)
