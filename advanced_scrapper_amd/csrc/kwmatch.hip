@@ -1128,10 +1128,11 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (const void *)kw_epi_kernel, EK_BLOCK, 0));
     h->epi_blocks_per_cu = bpc > 0 ? bpc : 1;
     {
-        // KW_SIDE_PRIO=1|2: the side stream (transcoding beside the probe) or
-        // side2 (short fields beside verify) at the greatest priority
+        // KW_SIDE_PRIO=0..3 (bit 0: the side stream, transcoding beside the probe; bit 1: side2, the short
+        // fields beside verify and the epilogue's regex tasks) at the greatest priority.  Default 2 (config 2:
+        // 4.64-4.67 vs 4.68-4.69 ms; config 4 unchanged)
         const char *e = kw_env("KW_SIDE_PRIO");
-        int sp = e ? atoi(e) : 0, lo = 0, hi = 0;
+        int sp = e ? atoi(e) : 2, lo = 0, hi = 0;
         HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, (sp & 1) ? hi : lo));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side2, hipStreamNonBlocking, (sp & 2) ? hi : lo));
@@ -1358,7 +1359,7 @@ static int launch_scan(kw_handle *h)
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
     HIPCHK(h, hipMemsetAsync(h->S.status, 0, 416, st));   // status .. stats, tx_used, res_cnt, total, gnext
     HIPCHK(h, hipMemsetAsync(h->out_cnt_all, 0, ((size_t)2 * nk + h->nr + h->ng) * 4, st));
-    HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 16, st));
+    HIPCHK(h, hipMemsetAsync(h->FS.vcnt, 0, (size_t)nk * 20, st));   // vcnt, ecnt, scnt, xcnt, xmark
     HIPCHK(h, hipMemsetAsync(h->FS.dset, 0, (h->FS.dmask + 1) * 8, st));
     if (n_docs > 0) {
         HIPCHK(h, hipMemsetAsync(h->FS.ncnt, 0, (size_t)n_docs * 8, st));
@@ -1431,12 +1432,10 @@ static int launch_scan(kw_handle *h)
                                n_epi, g, h->FS, h->S, phase);
         };
         // verify and short-field tasks are independent (both only append decisions): side by side; the
-        // regex tasks they queued run after both.  The regex tasks the epilogue queued (counted into xmark
-        // when it ends) run beside them on side3 (KW_RX_SPLIT=0: all regex tasks after verify and short)
+        // regex tasks they queued run after both.  The regex tasks the epilogue queued (its waves write their
+        // count into xmark too) run beside them on side3 (KW_RX_SPLIT=0: all regex tasks after verify and short)
         static const int rx_split_env = kw_env("KW_RX_SPLIT") ? atoi(kw_env("KW_RX_SPLIT")) : -1;
         const bool rx_split = rx_split_env >= 0 ? rx_split_env != 0 : h->n_pat <= RX_SPLIT_MAX_PAT;
-        if (rx_split)
-            HIPCHK(h, hipMemcpyAsync(h->FS.xmark, h->FS.xcnt, (size_t)n_epi * 4, hipMemcpyDeviceToDevice, st));
         HIPCHK(h, hipEventRecord(h->eve, st));
         if (rx_split) {
             HIPCHK(h, hipStreamWaitEvent(side3, h->eve, 0));

@@ -1412,6 +1412,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);
         S.scnt[wave] = TC.s;
         S.xcnt[wave] = TC.x;
+        S.xmark[wave] = TC.x;   // (the regex tasks the epilogue queued: KW_RX_SPLIT's early phase)
         if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
             atomicOr(&S.status[0], ST_TASK_OVERFLOW);
             atomicMax(&S.tmax[0], TC.v);
@@ -1788,6 +1789,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         if (TC.e) atomicAdd(&S.stats[7], (unsigned long long)TC.e);
         S.scnt[wave] = TC.s;
         S.xcnt[wave] = TC.x;
+        S.xmark[wave] = TC.x;   // (the regex tasks the epilogue queued: KW_RX_SPLIT's early phase)
         if (TC.v > S.vcap || TC.s > S.scap || TC.x > S.xcap) {
             atomicOr(&S.status[0], ST_TASK_OVERFLOW);
             atomicMax(&S.tmax[0], TC.v);
