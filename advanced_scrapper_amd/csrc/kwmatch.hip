@@ -1129,7 +1129,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
     h->epi_blocks_per_cu = bpc > 0 ? bpc : 1;
     {
         // KW_SIDE_PRIO=0..3 (bit 0: the side stream, transcoding beside the probe; bit 1: side2, the short
-        // fields beside verify and the epilogue's regex tasks) at the greatest priority.  Default 2 (config 2:
+        // fields beside verify) at the greatest priority.  Default 2 (config 2:
         // 4.64-4.67 vs 4.68-4.69 ms; config 4 unchanged)
         const char *e = kw_env("KW_SIDE_PRIO");
         int sp = e ? atoi(e) : 2, lo = 0, hi = 0;
@@ -1424,7 +1424,7 @@ static int launch_scan(kw_handle *h)
                                n_epi, g, h->FS, h->S);
         };
         // the early regex tasks at 2 waves per region (config 2: 4.68 ms vs 4.78 at G[3] = 4, 4.70 at 1)
-        static const int g_early = kw_env("KW_RX_EARLY_G") ? atoi(kw_env("KW_RX_EARLY_G")) : 2;
+        const int g_early = kw_env("KW_RX_EARLY_G") ? atoi(kw_env("KW_RX_EARLY_G")) : 2;
         auto rx_task = [&](int phase, hipStream_t s) {
             const int g = std::max(1, std::min(phase == 1 && g_early > 0 ? g_early : G[3], 16));
             const int nb = (n_epi * g + RK_WAVES - 1) / RK_WAVES;
@@ -1434,7 +1434,7 @@ static int launch_scan(kw_handle *h)
         // verify and short-field tasks are independent (both only append decisions): side by side; the
         // regex tasks they queued run after both.  The regex tasks the epilogue queued (its waves write their
         // count into xmark too) run beside them on side3 (KW_RX_SPLIT=0: all regex tasks after verify and short)
-        static const int rx_split_env = kw_env("KW_RX_SPLIT") ? atoi(kw_env("KW_RX_SPLIT")) : -1;
+        const int rx_split_env = kw_env("KW_RX_SPLIT") ? atoi(kw_env("KW_RX_SPLIT")) : -1;   // (read per scan: tests)
         const bool rx_split = rx_split_env >= 0 ? rx_split_env != 0 : h->n_pat <= RX_SPLIT_MAX_PAT;
         HIPCHK(h, hipEventRecord(h->eve, st));
         if (rx_split) {

@@ -14,6 +14,9 @@ ran:
                      documents go to the generic kernel in the same scan
 * KW_TEST_TASK_CAP   the verify / short / regex task queues overflow -> ST_TASK_OVERFLOW -> rescan
 * KW_TEST_DSET_SIZE  the decided (doc, field, name) set fills -> ST_DSET_FULL -> rescan
+
+and the scheduling knobs (KW_DEV=1) leave the results unchanged: the epilogue's regex tasks beside the verify /
+short kernels or after them (KW_RX_SPLIT), at 1 or 4 waves a region, the side streams' priorities.
 """
 import pytest
 
@@ -119,3 +122,13 @@ def test_overrides_ignored_without_the_gate(corpus, natural, monkeypatch):
     monkeypatch.delenv('KW_TEST_HOOKS', raising=False)
     st = _run(corpus, monkeypatch, large=False, KW_TEST_CAND_CAP=16, KW_TEST_TASK_CAP=2)
     assert st == natural
+
+
+@pytest.mark.parametrize('env', [{'KW_RX_SPLIT': 0}, {'KW_RX_SPLIT': 1, 'KW_RX_EARLY_G': 1, 'KW_SIDE_PRIO': 0},
+                                 {'KW_RX_SPLIT': 1, 'KW_RX_EARLY_G': 4, 'KW_SIDE_PRIO': 3}])
+def test_regex_task_split_and_stream_priorities(corpus, natural, monkeypatch, env):
+    """The regex tasks the epilogue queued run beside the verify / short kernels (phase 1, up to the count each
+    epilogue wave wrote) or after them with the rest (phase 2 / 0): every task exactly once either way."""
+    monkeypatch.setenv('KW_DEV', '1')
+    st = _run(corpus, monkeypatch, large=False, **env)
+    assert st['regex_searches'] == natural['regex_searches'] and st['deferred_docs'] == natural['deferred_docs']
