@@ -24,8 +24,8 @@
 // fk_s1_hash) into a 2^19-bit table of the anchors' first four bytes; anchors
 // of 2-3 bytes: their first two bytes in an exact 64K-bit pair table.  Only the
 // survivors (~1 % of the positions) run stage 2, each in its own lane: an
-// independent hash of the 4-byte key (2^17 bits), of the 3-byte key (2^14 bits)
-// or of the 2-byte key (2^14 bits) must hit before the global anchor hash
+// independent hash of the 4-byte key (2^18 bits), of the 3-byte key (2^16 bits)
+// or of the 2-byte key (2^16 bits) must hit before the global anchor hash
 // table is probed.  Field edges: the first / last four bytes of a field are
 // tested against the prefix / suffix keys of the one-deletion variants
 // (2 x 2^15 bits); only flagged fields run the edge check.
@@ -36,9 +36,22 @@ namespace kw {
 
 constexpr int FK_S1_BITS = 19;                  // stage 1: 2^19 bits = 64 KB
 constexpr int FK_P2_WORDS = 2048;               // stage 1, 2-3 byte anchors: exact pair table, 8 KB
-constexpr int FK_L2_BITS = 17;                  // stage 2, 4-byte keys: 16 KB
-constexpr int FK_T3_BITS = 14;                  // stage 2, 3-byte keys: 2 KB
-constexpr int FK_B2_BITS = 14;                  // stage 2, 2-byte keys: 2 KB
+// Stage-2 table sizes (filter LDS 132 KiB with them; 17 / 14 / 14 before: config 4's 52k-name KB filled the
+// 4-byte table, stage-2 survivors 24.6M -> 18.8M, probe 2.04 -> 1.77 ms, config 4 9.21 -> 8.91 ms, config 2
+// unchanged; r05_stage2_tables_ab.txt)
+#ifndef FK_L2_BITS_CFG
+#define FK_L2_BITS_CFG 18
+#endif
+#ifndef FK_T3_BITS_CFG
+#define FK_T3_BITS_CFG 16
+#endif
+#ifndef FK_B2_BITS_CFG
+#define FK_B2_BITS_CFG 16
+#endif
+constexpr int FK_L2_BITS = FK_L2_BITS_CFG;      // stage 2, 4-byte keys: 32 KB
+constexpr int FK_T3_BITS = FK_T3_BITS_CFG;      // stage 2, 3-byte keys: 8 KB
+constexpr int FK_B2_BITS = FK_B2_BITS_CFG;      // stage 2, 2-byte keys: 8 KB (<= 16: fk_b2h_index)
+static_assert(FK_B2_BITS <= 16, "fk_b2h_index takes the high bits of a 16-bit index");
 constexpr int FK_EDGE_BITS = 20;                // edge prefix / suffix 8-byte keys: 2 x 128 KB (global, L2)
 constexpr int FK_ITEMS0 = 512;                  // items of field 0 (text) on the fast path (power of 2: LDS sort)
 constexpr int FK_ITEMS1 = 64;                   // items of field 1 (title)

@@ -5,7 +5,7 @@
 //                     stage-2 survivors ("candidates", 4 bytes: position in the document << 8 | document
 //                     in its group << 3 | key lengths to probe, after a header record per group) go to the
 //                     wave's region in HBM in document and position order, with the document's flags (non-ASCII fields, edge prefilter, field
-//                     too long) in its header.  96 KiB of LDS: one 16-wave workgroup per CU.
+//                     too long) in its header.  132 KiB of LDS: one 16-wave workgroup per CU.
 //   kw_probe_kernel   one wave per filter region: the region's candidates 64 at a time, whatever document
 //                     they belong to (a document averages ~13 candidates, so per-document batches left most
 //                     lanes idle): anchor hash probe, head compare, then the (candidate, use) pairs spread
