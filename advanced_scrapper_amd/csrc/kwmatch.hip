@@ -538,7 +538,9 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     }
     // open addressing with linear probing: a candidate whose key is absent (most stage-2 survivors of the
     // shorter key lengths) walks to an empty slot, one dependent load per slot; KW_HT_SCALE = slots per key
-    uint32_t hs = 1024, hscale = 2;
+    // (4: config 2 4.64-4.67 -> 4.60-4.62 ms, probe 1.11 -> 1.08; config 4 probe 1.78 -> 1.74; 8 is no better for
+    // config 2 and doubles the table's L2 footprint; r05_ht_scale_ab.txt)
+    uint32_t hs = 1024, hscale = 4;
     if (const char *e = kw_env("KW_HT_SCALE")) hscale = (uint32_t)std::max(1, atoi(e));
     while (hs < (size_t)hscale * keys.size()) hs <<= 1;
     B.ht_mask = hs - 1;
