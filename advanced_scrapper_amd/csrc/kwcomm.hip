@@ -248,14 +248,27 @@ extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, i
     hipStream_t st = (hipStream_t)stream;
     CCHK(c, hipSetDevice(c->device));
     const bool receive = root < 0 || root == c->rank;
-    // one exchange of (count, receiver capacity) pairs: every rank sees every receiver's room, so a short
-    // destination fails on EVERY rank here, before any record moves (no peer is left waiting in a send)
-    const int64_t mine[2] = {n, receive ? (d_out ? cap : 0) : INT64_MAX};
-    std::vector<int64_t> pairs((size_t)2 * c->nranks);
-    int rc = gather_values(c, mine, 2, pairs.data(), st);
+    // one exchange of (count, receiver capacity, error) triples: every rank sees every receiver's room and every
+    // rank's local verdict, so a short destination or a rank whose global document ids overflow 32 bits fails on
+    // EVERY rank here, before any record moves (no peer is left waiting in a send)
+    const int64_t bad_ids = doc_base + n > 0xFFFFFFFFll ? 1 : 0;
+    const int64_t mine[3] = {n, receive ? (d_out ? cap : 0) : INT64_MAX, bad_ids};
+    std::vector<int64_t> trip((size_t)3 * c->nranks);
+    int rc = gather_values(c, mine, 3, trip.data(), st);
     if (rc) return rc;
     std::vector<int64_t> cnt(c->nranks), caps(c->nranks);
-    for (int r = 0; r < c->nranks; ++r) { cnt[r] = pairs[2 * r]; caps[r] = pairs[2 * r + 1]; }
+    for (int r = 0; r < c->nranks; ++r) {
+        cnt[r] = trip[3 * r];
+        caps[r] = trip[3 * r + 1];
+    }
+    for (int r = 0; r < c->nranks; ++r) {
+        if (trip[3 * r + 2]) {
+            char buf[160];
+            snprintf(buf, sizeof(buf), "kw_allgather_hits: rank %d's global document ids go beyond 2^32", r);
+            c->err = buf;
+            return KW_EINVAL;
+        }
+    }
     std::vector<int64_t> pre(c->nranks + 1, 0);
     std::vector<int32_t> ops(c->nranks, 0);
     int64_t n_recv = 0;
@@ -272,7 +285,6 @@ extern "C" int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, i
         c->err = buf;
         return KW_EOVERFLOW;
     }
-    if (doc_base + n > 0xFFFFFFFFll) { c->err = "kw_allgather_hits: global document ids beyond 2^32"; return KW_EINVAL; }
     return post_exchange(c, d_local, n, doc_base, receive, pre.data(), cnt.data(), ops.data(), d_out, st);
 }
 
@@ -282,17 +294,44 @@ extern "C" int kw_allgather_hits_planned(kw_comm *c, const kw_hit *d_local, int6
 {
     if (!c || !n_total || !counts || n < 0 || (n > 0 && !d_local)) return KW_EINVAL;
     if (root >= c->nranks || doc_base < 0) { c->err = "kw_allgather_hits_planned: bad root or doc_base"; return KW_EINVAL; }
-    if (counts[c->rank] != n) { c->err = "kw_allgather_hits_planned: counts[rank] is not this rank's n"; return KW_EINVAL; }
     hipStream_t st = (hipStream_t)stream;
     CCHK(c, hipSetDevice(c->device));
     std::vector<int64_t> pre(c->nranks + 1, 0);
     std::vector<int32_t> ops(c->nranks, 0);
     int64_t n_recv = 0;
+    // (the same counts on every rank: a negative count -- kw_allgather_counts' error flag -- fails every rank here,
+    // before anything is posted)
     if (kw_exchange_plan(c->nranks, c->rank, root, counts, pre.data(), ops.data(), n_total, &n_recv) != KW_OK) {
-        c->err = "kw_allgather_hits_planned: bad counts";
+        c->err = "kw_allgather_hits_planned: bad counts (a rank flagged an error with a negative count)";
         return KW_EINVAL;
     }
-    if (doc_base + n > 0xFFFFFFFFll) { c->err = "kw_allgather_hits_planned: global document ids beyond 2^32"; return KW_EINVAL; }
+    const char *local_err = nullptr;
+    if (counts[c->rank] != n) local_err = "kw_allgather_hits_planned: counts[rank] is not this rank's n";
+    else if (doc_base + n > 0xFFFFFFFFll) local_err = "kw_allgather_hits_planned: global document ids beyond 2^32";
+    if (local_err) {
+        // the peers already post their halves from `counts`: post this rank's matching sends and receives (zero
+        // records of the agreed size from / into the library's buffer) so no one waits, then fail this rank
+        const int64_t need = std::max<int64_t>(counts[c->rank], n_recv);
+        if ((size_t)need > c->spill_cap) {
+            if (c->d_spill) (void)hipFree(c->d_spill);
+            c->d_spill = nullptr;
+            c->spill_cap = (size_t)need;
+            CCHK(c, hipMalloc(&c->d_spill, c->spill_cap * sizeof(kw_hit)));
+        }
+        if (need > 0) CCHK(c, hipMemsetAsync(c->d_spill, 0, (size_t)need * sizeof(kw_hit), st));
+        if (c->nranks > 1) {
+            NCHK(c, g_rccl.GroupStart());
+            for (int p = 0; p < c->nranks; ++p) {
+                if (ops[p] & KW_PLAN_SEND)
+                    NCHK(c, g_rccl.Send(c->d_spill, (size_t)counts[c->rank] * 4, nccl_uint32, p, c->comm, st));
+                if (ops[p] & KW_PLAN_RECV)
+                    NCHK(c, g_rccl.Recv(c->d_spill, (size_t)counts[p] * 4, nccl_uint32, p, c->comm, st));
+            }
+            NCHK(c, g_rccl.GroupEnd());
+        }
+        c->err = local_err;
+        return KW_EINVAL;
+    }
     const bool receive = root < 0 || root == c->rank;
     kw_hit *dst = d_out;
     bool short_dst = false;

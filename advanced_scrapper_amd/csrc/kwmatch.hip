@@ -104,7 +104,8 @@ struct kw_handle {
     FastScratch FS{};
     int nk = 0, nr = 0, ng = 0;
     uint32_t defer_cap = 0, item_cap = 0, rx_cap = 0;
-    bool item_clamped = false;          // a scan needed more probe items than 32-bit indexes reach (FS.item_grow)
+    bool item_clamped = false;          // this batch's rescans needed more probe items than 32-bit indexes reach
+                                        // (FS.item_grow = 0 for its remaining rescans; reset by every kw_scan)
     ScratchCaps caps;
     uint32_t *out_cnt_all = nullptr;   // counts of every result region (scan, task, resolve, generic)
     kw_hit *out_all = nullptr;
@@ -521,12 +522,6 @@ int build_fast(FastBuild &B, const QStats &Q, int n_pat, const uint8_t *pat_byte
     // the box as SWAR range constants per byte: bytes < 0x80 in [lo, hi] by two additions, bytes >= 0x80 all
     // in (one flag) when the range reaches them
     if (B.has_short) {
-#if FK_GATE_UNION
-        // one range for both bytes (a superset: the exact pair table decides in stage 2), so the filter
-        // computes each word's byte flags once (fk_stage1<2>)
-        box[0] = box[2] = std::min(box[0], box[2]);
-        box[1] = box[3] = std::max(box[1], box[3]);
-#endif
         for (int r = 0; r < 2; ++r) {
             const uint32_t lo = box[2 * r], hi = box[2 * r + 1];
             const uint32_t alo = std::min(lo, 0x80u), ahi = std::min(hi, 0x7Fu);
@@ -1494,6 +1489,7 @@ extern "C" int kw_scan(kw_handle *h, const uint8_t *d_arena, const int64_t *d_do
     h->fetched = false;
     h->rescans = 0;
     h->rescan_causes = 0;
+    h->item_clamped = false;   // (per batch: a later batch with fewer regions may grow its item regions again)
     return launch_scan(h);
 }
 
@@ -1634,7 +1630,7 @@ static int finish(kw_handle *h)
                 w.cand_cap = std::max(w.cand_cap, cm[0] + cm[0] / 8 + 64);
                 const uint64_t lim = item_index_limit() / (uint64_t)std::max(1, h->ns);
                 const uint64_t want = (uint64_t)cm[1] + cm[1] / 8 + 64;
-                if (want > lim) h->item_clamped = true;   // from now on: defer, never grow past the index limit
+                if (want > lim) h->item_clamped = true;   // this batch: defer, never grow past the index limit
                 w.item_cap = std::max<uint32_t>(w.item_cap, (uint32_t)std::min<uint64_t>(want, lim));
             }
             int rc = ensure_scratch(h, w);

@@ -67,20 +67,7 @@ constexpr uint32_t FK_MUL3 = 0xC2B2AE35u;
 constexpr uint32_t FK_MUL4 = 0x27D4EB2Fu;
 
 constexpr int FK_S1_WORDS = 1 << (FK_S1_BITS - 5);
-#ifndef FK_S1_ONE
-#define FK_S1_ONE 0     // 1: stage-1 hash in one v_mad_u32_u24 per position (fk_s1_hash): 16 fewer VALU per 1 KiB
-                        // tile, but its bit index takes only b0's low 5 bits (~27 values in text): config 2's
-                        // stage-1 survivors 59.9M -> 72.0M and the filter unchanged (1.40 vs 1.39 ms)
-#endif
-#ifndef FK_GATE_UNION
-#define FK_GATE_UNION 0 // 1: one pair-box range for both bytes of a 2-3 byte anchor (kw_compile; fk_stage1<2>):
-                        // config 2's stage-1 survivors 72.0M -> 95.0M, filter 1.40 -> 1.50 ms
-#endif
-#if FK_S1_ONE
-constexpr uint32_t FK_S1_M1 = 0xD2511Eu;       // stage-1 hash multiplier (24 bits, even: fk_s1_hash)
-#else
 constexpr uint32_t FK_S1_M1 = 0xD2511Fu;        // stage-1 hash multipliers (24 bits: v_mul_u32_u24 / v_mad_u32_u24)
-#endif
 constexpr uint32_t FK_S1_M2 = 0x9E3779u;
 constexpr uint32_t FK_S1_EXT_MAX = 16384;       // stage-1 4-grams of the fuzzy 3-byte anchors (256 each)
 constexpr int FK_L2_WORDS = 1 << (FK_L2_BITS - 5);
@@ -249,17 +236,12 @@ __device__ __forceinline__ int64_t fk_next_group(uint32_t *ctr, bool dyn, int64_
 }
 
 // host + device hashes of the LDS tables
-// stage 1: the 4-gram b0..b3 at a position as k4 = b0 | b1 << 8 | b2 << 16 | b3 << 24.  FK_S1_ONE: h = (k4 mod
-// 2^24) * M1 + k4, one v_mad_u32_u24 per position; M1 is even, so the bit index h & 31 = (b0 * (M1 + 1)) & 31
-// takes all of b0's low 5 bits, and b3 moves the word by b3 << 6.  Else h = (b0..b2) * M1 + (b1..b3) * M2 (a
-// v_mul_u32_u24 and a v_mad_u32_u24).  Word h >> 18 of the table, bit h & 31.
+// stage 1: the 4-gram b0..b3 at a position as k4 = b0 | b1 << 8 | b2 << 16 | b3 << 24; h = (b0..b2) * M1 +
+// (b1..b3) * M2 (a v_mul_u32_u24 and a v_mad_u32_u24; the one-multiply form h = (k4 mod 2^24) * M1 + k4 was
+// measured in round 5 and dropped: its bit index sees only b0's low 5 bits).  Word h >> 18 of the table, bit h & 31.
 __host__ __device__ __forceinline__ uint32_t fk_s1_hash(uint32_t k4)
 {
-#if FK_S1_ONE
-    return (k4 & 0xFFFFFFu) * FK_S1_M1 + k4;
-#else
     return (k4 & 0xFFFFFFu) * FK_S1_M1 + ((k4 >> 8) & 0xFFFFFFu) * FK_S1_M2;
-#endif
 }
 __host__ __device__ __forceinline__ uint32_t fk_s1_word(uint32_t h) { return h >> (32 - FK_S1_BITS + 5); }
 __device__ __forceinline__ uint32_t lds_word_at(const uint32_t *t, uint32_t byte_off)

@@ -33,15 +33,6 @@ namespace kw {
 #ifndef FS_MINW
 #define FS_MINW 1
 #endif
-#ifndef FS_KEY_REGS
-#define FS_KEY_REGS 0    // 1: stage-2 keys queued from the owner lanes' registers instead of a global load in
-                         // the round: filter 1.44 vs 1.35 ms on MI355X (the key selection's VALU costs more than
-                         // the load's wait: the filter is issue-bound, not latency-bound)
-#endif
-#ifndef FK_PLACE_ASM
-#define FK_PLACE_ASM 0   // 1: stage 1's bits placed by v_lshl_or_b32 in inline asm (fewer VALU, but the compiler then
-                         // issues all 16 lookups together and waits on them at once)
-#endif
 #ifndef FS_AHEAD
 #define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
 #endif
@@ -77,23 +68,7 @@ struct __attribute__((aligned(16))) FilterLds {
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
     uint32_t spos[FS_WAVES][2 * WAVE];        // stage 2: the queue of survivors' group-relative positions (a ring)
-#if FS_KEY_REGS
-    uint32_t skey[FS_WAVES][2 * WAVE];        // ... and their 4-byte keys (from the owner lane's registers)
-#endif
 };
-
-// the 4 bytes at position j (0..15) of a lane's 16 (+4) bytes W[0..4]: the stage-2 key of a survivor, taken
-// from registers when it is queued (a global load in the round would make the wave wait for every tile load
-// in flight: vmcnt counts in order)
-// (two-level selects on the words as values: an indexed W[q] would go through scratch)
-__device__ __forceinline__ uint32_t fk_key_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
-                                              uint32_t j)
-{
-    const bool odd = (j & 4u) != 0, high = (j & 8u) != 0;
-    const uint32_t lo = high ? (odd ? w3 : w2) : (odd ? w1 : w0);
-    const uint32_t hi = high ? (odd ? w4 : w3) : (odd ? w2 : w1);
-    return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
-}
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
 __device__ __forceinline__ uint32_t fg_doc(const uint32_t *dstart, uint32_t nd, uint32_t r)
@@ -148,21 +123,11 @@ __device__ __forceinline__ uint32_t fk_in_box(uint32_t x, uint32_t A, uint32_t B
     return (((t + A) & ~(t + B) & ~x) | (x & N)) & 0x80808080u;
 }
 
-// (a << S) | c as one v_lshl_or_b32 (left to itself the compiler shifts each bit and ORs them three at a time:
-// 1.5 instructions per bit instead of 1)
-template <int S>
-__device__ __forceinline__ uint32_t fk_lshl_or(uint32_t a, uint32_t c)
-{
-    uint32_t r;
-    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "I"(S), "v"(c));
-    return r;
-}
-
 // Stage 1 of one lane's 16 bytes W[0..3] (+ W[4]): `hit` = positions where an anchor of >= 4 bytes may start
 // (its first four bytes' bit in the 4-gram table; also the fuzzy 3-byte anchors' 4-grams), `gate` = positions
 // whose first two bytes lie in the pair box of the other 2-3 byte anchors (SWAR, no lookup; SH = 2: one box
 // for both bytes, the byte flags of each word computed once; SH = 3: two ranges below 0x80); transposed bit order (fk_tbit).  Per position:
-// one v_mad_u32_u24 (fk_s1_hash; FK_S1_ONE), the address, the lookup, v_bfe_u32 and v_lshl_or_b32.
+// one v_mad_u32_u24 (fk_s1_hash), the address, the lookup, v_bfe_u32 and v_lshl_or_b32.
 template <int SH>
 __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds &L, const uint32_t (&W)[5],
                                           uint32_t &hit, uint32_t &gate)
@@ -174,11 +139,7 @@ __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds 
     uint32_t hh[16], sw[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-#if FK_S1_ONE
-        hh[j] = __umul24(k[j], FK_S1_M1) + k[j];
-#else
         hh[j] = __umul24(k[j], FK_S1_M1) + __umul24(k[j + 1], FK_S1_M2);
-#endif
         sw[j] = lds_word_at(L.s1, (hh[j] >> 16) & (4u * FK_S1_WORDS - 4u));
     }
     uint32_t g = 0;
@@ -221,16 +182,7 @@ __device__ __forceinline__ void fk_stage1(const FastTables &FT, const FilterLds 
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t b = __builtin_amdgcn_ubfe(sw[j], hh[j], 1);
-        if (!FK_PLACE_ASM) {
-            h |= b << fk_tbit(j);
-            continue;
-        }
-        switch (fk_tbit(j)) {   // (a constant per unrolled j: the shift is the instruction's inline operand)
-#define FK_PLACE(t) case t: h = fk_lshl_or<t>(b, h); break;
-            FK_PLACE(0) FK_PLACE(1) FK_PLACE(2) FK_PLACE(3) FK_PLACE(8) FK_PLACE(9) FK_PLACE(10) FK_PLACE(11)
-            FK_PLACE(16) FK_PLACE(17) FK_PLACE(18) FK_PLACE(19) FK_PLACE(24) FK_PLACE(25) FK_PLACE(26) FK_PLACE(27)
-#undef FK_PLACE
-        }
+        h |= b << fk_tbit(j);
     }
     hit = h;
     gate = g;
@@ -252,9 +204,6 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
     const uint32_t *l2 = L.l2, *t3 = L.t3, *b2 = L.b2;
     uint32_t *dstart = L.dstart[wib], *dtitle = L.dtitle[wib];
     uint32_t *spos = L.spos[wib];
-#if FS_KEY_REGS
-    uint32_t *skey = L.skey[wib];
-#endif
     uint32_t *cand = S.cand + (size_t)region * S.cand_cap;
     const uint32_t ccap = S.cand_cap;
     const uint32_t t3on = FT.has_t3 ? 1u : 0u;
@@ -300,16 +249,10 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const bool act = (uint32_t)lane < n;
             const uint32_t slot = (qh + (uint32_t)lane) & (2u * WAVE - 1u);
             const uint32_t r = spos[slot];
-#if FS_KEY_REGS
-            // the 4-byte key at the position (bytes past the group end may differ from the arena's: clamped
-            // loads; no anchor that fits its field reads them, and the 3- and 2-byte filters use the low bytes)
-            const uint32_t key = act ? skey[slot] : 0u;
             wave_sync();
-#else
-            wave_sync();
-            // the 4-byte key at the position (the group's bytes were just streamed: a cache hit)
+            // the 4-byte key at the position (the group's bytes were just streamed: a cache hit; taking it from
+            // the owner lane's registers when queued was measured slower in round 5: the selects cost more VALU)
             const uint32_t key = act ? ld_u32_unaligned(arena, gb + (int64_t)r) : 0u;
-#endif
             qh = (qh + n) & (2u * WAVE - 1u);
             qn -= n;
             const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
@@ -403,9 +346,6 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                             const uint32_t j = (uint32_t)(__ffs(hm) - 1);
                             const uint32_t sl = (qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u);
                             spos[sl] = rel + j;
-#if FS_KEY_REGS
-                            skey[sl] = fk_key_at(W[0], W[1], W[2], W[3], W[4], j);
-#endif
                         }
                         ++rk;
                     }

@@ -105,8 +105,10 @@ class KwComm:
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
         n = int(hits.shape[0])
-        counts = self.allgather_counts(n, stream)
-        total = sum(counts)
+        # a shard whose global document ids overflow the records' 32 bits sends the error flag (a negative count)
+        # in the counts exchange: every rank's planned exchange then fails before anything is posted
+        counts = self.allgather_counts(-1 if int(doc_base) + n > 0xFFFFFFFF else n, stream)
+        total = sum(c for c in counts if c > 0)
         receive = root < 0 or root == self.rank
         if receive and (self._out is None or self._out.shape[0] < max(total, 1)):
             self._out = torch.empty((max(total + total // 4, 1), 4), dtype=torch.int32,

@@ -297,8 +297,9 @@ def _emit_buffer(cap: int) -> np.ndarray:
 
 def render_native(chunk, raw_rows, stamps_by_doc, tickers):
     """The rows of a native chunk (``raw_rows`` = rows.assemble_json_raw's arrays, document order, KB ticker
-    order) rendered by the C emitter into one buffer, grouped by ticker file: a list of (file name, line
-    bytes, time_unix[], line lengths[], cell flags[]) in KB ticker order, rows in article order within each.
+    order) rendered by the C emitter into one buffer, grouped by ticker file: a list of 6-tuples (file name,
+    line bytes, time_unix[], line lengths[], cell flags[], document ids[]) in KB ticker order, rows in article
+    order within each (document ids[] = each row's article in the chunk).
     ``stamps_by_doc[d]`` = article d's time_unix.  ``None`` when the emitter cannot reproduce the writer (a
     NUL cell, a platform line end other than "\n"): the caller takes the per-row path."""
     from .ingest import _p

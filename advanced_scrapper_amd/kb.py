@@ -170,16 +170,16 @@ def read_and_process_json_files(folder_path, _listdir=None):
         try:
             merged.update(_load_kb_file(path, 'utf-8'))
         except UnicodeDecodeError:
-            print(f"UTF-8 decoding failed, retrying other encodings: {filename}")
+            print(f"UTF-8解码失败，尝试其他编码读取文件: {filename}")   # ref :104
             try:
                 merged.update(_load_kb_file(path, 'gbk'))
             except UnicodeDecodeError:
                 try:
                     merged.update(_load_kb_file(path, 'latin1'))
                 except Exception as exc:  # noqa: BLE001 - mirrors the reference
-                    print(f"cannot read file {filename}: {exc}")
+                    print(f"无法读取文件 {filename}: {exc}")   # ref :117
         except Exception as exc:  # noqa: BLE001 - mirrors the reference
-            print(f"error while processing file {filename}: {exc}")
+            print(f"处理文件 {filename} 时出错: {exc}")   # ref :119
     return merged
 
 

@@ -305,6 +305,8 @@ def main():
     if rank != 0:
         return
     kavg = {k: float(np.mean([t[k] for t in ktimes])) for k in ktimes[0]}
+    lib_id = _native.lib_identity()
+    lib_sha = lib_id['sha256']
     scan_avg = kavg['filter']         # the kernel that streams every article byte (HIP events on its stream)
     achieved = local_bytes / (scan_avg * 1e-3) / 1e9
     cpu = None
@@ -352,10 +354,18 @@ def main():
         'roofline': {
             'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4),
-            'traffic': (pmc_traffic(args.traffic_json or TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=n_local, seed=args.seed)
+            'traffic': (pmc_traffic(args.traffic_json or TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=n_local,
+                                    seed=args.seed, library_sha256=lib_sha)
                         if args.workload == 'match' else
                         pmc_traffic(args.traffic_json or TRAFFIC_C4, 'kw_filter_kernel', docs_per_gpu=n_local,
-                                    seed=args.seed, workload='kb50k')),
+                                    seed=args.seed, workload='kb50k', library_sha256=lib_sha)),
+            'step_traffic': pmc_step_traffic(args.traffic_json or (TRAFFIC_KW if args.workload == 'match'
+                                                                    else TRAFFIC_C4),
+                                             docs_per_gpu=n_local, seed=args.seed, library_sha256=lib_sha,
+                                             **({} if args.workload == 'match' else {'workload': 'kb50k'})),
+            # the metric's own "% of HBM peak": the whole step's article bytes per second (value) over 8 TB/s;
+            # frac above prices the filter kernel alone
+            'step_frac': round(value / HBM_PEAK_GBS, 4),
             'algorithmic_bytes_per_launch': local_bytes,
             'kernel': 'kw::kw_filter_kernel', 'kernel_ms_avg': round(scan_avg, 4),
             'kernels_ms_avg': {k: round(v, 4) for k, v in kavg.items()},
@@ -363,7 +373,7 @@ def main():
         },
         'cpu_baseline': cpu,
         'scan_stats': st,
-        'library': _native.lib_identity(),
+        'library': lib_id,
         'host': {'kb_load_compile_s': round(t_kb, 3), 'generate_s': round(t_gen, 2), 'h2d_s': round(t_up, 3),
                  'h2d_GBps_pcie_inclusive': round(local_bytes / t_up / 1e9, 2) if t_up > 0 else None,
                  **host_cpus()},
@@ -420,6 +430,7 @@ def bench_dedup(args):
     names = ('transform_insert', 'slow_rows', 'decide', 'compact', 'total')
     kms = {a: round(float(b), 4) for a, b in zip(names, k)}
     transform_gbs = rows.n_bytes / (kms['transform_insert'] * 1e-3) / 1e9
+    lib_id = _native.lib_identity()
     cpu = None
     if world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline_dedup(rows, min(n, 2_000_000))
@@ -436,11 +447,15 @@ def bench_dedup(args):
         'roofline': {'bound': 'hbm', 'achieved': round(transform_gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(transform_gbs / HBM_PEAK_GBS, 4),
                      'traffic': pmc_traffic(args.traffic_json or TRAFFIC_DEDUP, 'dd_transform_kernel', rows_per_gpu=n,
-                                            seed=args.seed),
+                                            seed=args.seed, library_sha256=lib_id['sha256']),
+                     'step_traffic': pmc_step_traffic(args.traffic_json or TRAFFIC_DEDUP, rows_per_gpu=n,
+                                                      seed=args.seed, library_sha256=lib_id['sha256'],
+                                                      prefix='dd_'),
+                     'step_frac': round(float(nb.item()) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                      'algorithmic_bytes_per_launch': rows.n_bytes, 'kernel': 'dd::dd_transform_kernel',
                      'kernel_ms_avg': kms['transform_insert'], 'kernels_ms_avg': kms},
         'cpu_baseline': cpu,
-        'library': _native.lib_identity(),
+        'library': lib_id,
         'host': {'generate_s': round(t_gen, 2)},
     }
     print(json.dumps(out), flush=True)
@@ -466,15 +481,16 @@ def cpu_baseline_dedup(rows, n_sample: int):
                       f'(yahoo_links_selenium.py:63-79), one process, {secs:.2f} s', 'kept': int(len(df))}
 
 
-TRAFFIC_KW = os.path.join(REPO, 'profiles', 'traffic_r04.json')
-TRAFFIC_DEDUP = os.path.join(REPO, 'profiles', 'traffic_dedup_r04.json')
-TRAFFIC_C4 = os.path.join(REPO, 'profiles', 'traffic_c4_r04.json')
+# this round's PMC passes (scripts/gpu_profile.sh); each file's workload key carries the sha256 of the library it
+# profiled, so a file left from an older build prices nothing (traffic = None) instead of an old kernel's bytes
+TRAFFIC_KW = os.path.join(REPO, 'profiles', 'traffic_r06.json')
+TRAFFIC_DEDUP = os.path.join(REPO, 'profiles', 'traffic_dedup_r06.json')
+TRAFFIC_C4 = os.path.join(REPO, 'profiles', 'traffic_c4_r06.json')
 
 
-def pmc_traffic(path: str, kernel: str, **workload):
-    """HBM bytes per launch of `kernel` measured by the PMC passes of the same
-    workload (every given key equal; FETCH_SIZE x2 + WRITE_SIZE, see
-    profiles/pmc_traffic.py), or None."""
+def _traffic_file(path: str, workload: dict):
+    """The PMC traffic JSON at `path` if it was measured on this workload with this library (every given key
+    equal, the library's sha256 included), else None."""
     if not path or path == 'none':
         return None
     try:
@@ -484,10 +500,34 @@ def pmc_traffic(path: str, kernel: str, **workload):
     w = j.get('workload', {})
     if any(str(w.get(k)) != str(v) for k, v in workload.items()):
         return None
+    return j
+
+
+def pmc_traffic(path: str, kernel: str, **workload):
+    """HBM bytes per launch of `kernel` measured by the PMC passes of the same
+    workload and library (FETCH_SIZE x2 + WRITE_SIZE, see profiles/pmc_traffic.py), or None."""
+    j = _traffic_file(path, workload)
+    if j is None:
+        return None
     for k, v in j.get('kernels', {}).items():
         if kernel in k:
             return int(v['hbm_bytes_per_launch'])
     return None
+
+
+def pmc_step_traffic(path: str, prefix: str = 'kw', **workload):
+    """HBM bytes per step of the library's own kernels (names starting with `prefix`; the runtime's copy / fill
+    kernels and torch's digest kernels outside the timed region are left out), or None."""
+    j = _traffic_file(path, workload)
+    if j is None:
+        return None
+    tot = 0.0
+    for k, v in j.get('kernels', {}).items():
+        name = k.split('(')[0]
+        if name.startswith(prefix) or name.startswith(prefix.rstrip('_') + '::'):
+            # a kernel launched twice a step (the regex tasks' two phases) counts twice
+            tot += v['hbm_bytes_per_launch'] * v.get('launches_per_step', 1)
+    return int(tot)
 
 
 def cpu_baseline(processed, corpus, n_sample: int, procs: int):

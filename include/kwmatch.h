@@ -198,7 +198,11 @@ int kw_comm_unique_id(uint8_t *id_out /* KW_COMM_ID_BYTES */);
 /* Join the communicator `id` as `rank` of `nranks` on HIP device `device`. */
 int kw_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, int32_t device, kw_comm **out);
 
-/* All-gather one count per rank into counts[nranks] (host).  Blocking. */
+/* All-gather one count per rank into counts[nranks] (host).  Blocking.  A rank
+ * that cannot take part in the step's record exchange (e.g. its global
+ * document ids would pass 2^32) sends count = -1: every rank's
+ * kw_allgather_hits_planned on those counts then returns KW_EINVAL before
+ * anything is posted. */
 int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, void *stream);
 
 /* Exchange hit records (e.g. a kw_hits_copy of this rank's last scan: d_local,
@@ -208,11 +212,12 @@ int kw_allgather_counts(kw_comm *c, int64_t count, int64_t *counts, void *stream
  * records) gets the ranks' records concatenated in rank order = global
  * document order.  *n_total = records over all ranks; counts[nranks] (host,
  * optional) the per-rank counts.  One blocking exchange of (count, receiver
- * capacity) pairs (every rank must call), then the records move asynchronously
- * on `stream` (RCCL send/recv over the xGMI mesh), so the next kw_scan can run
- * beside them on another stream.  A receiver whose cap cannot hold the total
- * makes EVERY rank return KW_EOVERFLOW before any record moves.  Use one
- * stream per communicator. */
+ * capacity, error flag) triples (every rank must call), then the records move
+ * asynchronously on `stream` (RCCL send/recv over the xGMI mesh), so the next
+ * kw_scan can run beside them on another stream.  A receiver whose cap cannot
+ * hold the total makes EVERY rank return KW_EOVERFLOW, and a rank whose global
+ * document ids pass 2^32 makes every rank return KW_EINVAL, before any record
+ * moves.  Use one stream per communicator. */
 int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root, kw_hit *d_out,
                       int64_t cap, int64_t *n_total, int64_t *counts, void *stream);
 
@@ -221,7 +226,11 @@ int kw_allgather_hits(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_
  * counts[rank] == n): no further exchange and no host wait, so one step costs
  * one blocking counts exchange (the caller sizes d_out from it).  A receiver
  * whose d_out is short still receives (into a library buffer) so that no peer
- * waits, and returns KW_EOVERFLOW; the other ranks return KW_OK. */
+ * waits, and returns KW_EOVERFLOW; the other ranks return KW_OK.  Counts with
+ * a negative entry fail every rank (KW_EINVAL) before anything is posted.  A
+ * rank whose own arguments disagree with them (counts[rank] != n, ids past
+ * 2^32) still posts its matching sends / receives (zero records of the
+ * agreed sizes) so no peer waits, and returns KW_EINVAL. */
 int kw_allgather_hits_planned(kw_comm *c, const kw_hit *d_local, int64_t n, int64_t doc_base, int32_t root,
                               const int64_t *counts, kw_hit *d_out, int64_t cap, int64_t *n_total, void *stream);
 

@@ -1,18 +1,41 @@
 """bench.py's roofline `traffic` comes from the committed PMC profiles: the default files must exist, name
-the bench's own default workloads, and hold the dominant kernel of each line (CPU only: JSON lookups)."""
+the bench's own default workloads and the library they profiled, and hold the dominant kernel of each line
+(CPU only: JSON lookups)."""
+import json
+
 import bench
 
 
+def _sha(path):
+    return json.load(open(path))['workload']['library_sha256']
+
+
 def test_default_traffic_profiles_resolve():
-    kw = bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=20250905)
-    dd = bench.pmc_traffic(bench.TRAFFIC_DEDUP, 'dd_transform_kernel', rows_per_gpu=500_000_000, seed=20250905)
+    kw_sha, dd_sha = _sha(bench.TRAFFIC_KW), _sha(bench.TRAFFIC_DEDUP)
+    kw = bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=20250905,
+                           library_sha256=kw_sha)
+    dd = bench.pmc_traffic(bench.TRAFFIC_DEDUP, 'dd_transform_kernel', rows_per_gpu=500_000_000, seed=20250905,
+                           library_sha256=dd_sha)
     assert kw and kw > 2_000_000_000
     assert dd and dd > 40_000_000_000
+    step = bench.pmc_step_traffic(bench.TRAFFIC_KW, docs_per_gpu=1_000_000, seed=20250905, library_sha256=kw_sha)
+    assert step and step > kw
+    c4 = bench.pmc_traffic(bench.TRAFFIC_C4, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=20250905,
+                           workload='kb50k', library_sha256=_sha(bench.TRAFFIC_C4))
+    assert c4 and c4 > 2_000_000_000
 
 
-def test_traffic_lookup_refuses_other_workloads():
-    assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=10_000, seed=20250905) is None
-    assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=1) is None
+def test_traffic_lookup_refuses_other_workloads_and_libraries():
+    sha = _sha(bench.TRAFFIC_KW)
+    assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=10_000, seed=20250905,
+                             library_sha256=sha) is None
+    assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=1,
+                             library_sha256=sha) is None
+    # a profile of another build prices nothing
+    assert bench.pmc_traffic(bench.TRAFFIC_KW, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=20250905,
+                             library_sha256='0' * 64) is None
+    assert bench.pmc_step_traffic(bench.TRAFFIC_KW, docs_per_gpu=1_000_000, seed=20250905,
+                                  library_sha256='0' * 64) is None
     assert bench.pmc_traffic('none', 'kw_filter_kernel') is None
 
 

@@ -42,3 +42,49 @@ def test_one_rank_exchange_all_roots(comm):
 def test_one_rank_counts(comm):
     assert comm.allgather_counts(42) == [42]
     assert comm.allgather_counts(0) == [0]
+
+
+def test_one_rank_short_destination_and_errors(comm):
+    """the receiver-capacity verdict of both exchange calls on the hardware (KW_EOVERFLOW), the
+    planned call's local argument errors (KW_EINVAL after posting its matching half), the negative-count error
+    flag -- and the communicator still works for a following good exchange."""
+    import ctypes
+    import torch
+    from advanced_scrapper_amd import _native
+    L, h = _native.lib(), comm.h
+    n = 100
+    src = torch.arange(n * 4, dtype=torch.int32, device='cuda').reshape(n, 4)
+    short = torch.zeros((n - 1, 4), dtype=torch.int32, device='cuda')
+    nt = ctypes.c_int64()
+    cnt = np.zeros(1, dtype=np.int64)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = L.kw_allgather_hits(h, _native.ptr(src), n, 0, 0, _native.ptr(short), n - 1, ctypes.byref(nt),
+                             _native.ptr(cnt), sp)
+    assert rc == _native.KW_EOVERFLOW and b'destination holds' in L.kw_comm_last_error(h)
+    counts = np.array([n], dtype=np.int64)
+    rc = L.kw_allgather_hits_planned(h, _native.ptr(src), n, 0, -1, _native.ptr(counts), _native.ptr(short), n - 1,
+                                     ctypes.byref(nt), sp)
+    assert rc == _native.KW_EOVERFLOW and b'too small' in L.kw_comm_last_error(h)
+    # ids past 2^32: the self-contained call agrees on the error before any record moves
+    rc = L.kw_allgather_hits(h, _native.ptr(src), n, 0xFFFFFFFF - 10, 0, _native.ptr(src), n, ctypes.byref(nt),
+                             _native.ptr(cnt), sp)
+    assert rc == _native.KW_EINVAL and b'beyond 2^32' in L.kw_comm_last_error(h)
+    # the planned call: counts that disagree with n, and the negative-count flag
+    wrong = np.array([n + 5], dtype=np.int64)
+    big = torch.zeros((n + 5, 4), dtype=torch.int32, device='cuda')
+    rc = L.kw_allgather_hits_planned(h, _native.ptr(src), n, 0, -1, _native.ptr(wrong), _native.ptr(big), n + 5,
+                                     ctypes.byref(nt), sp)
+    assert rc == _native.KW_EINVAL and b'counts[rank]' in L.kw_comm_last_error(h)
+    neg = np.array([-1], dtype=np.int64)
+    rc = L.kw_allgather_hits_planned(h, _native.ptr(src), n, 0, -1, _native.ptr(neg), _native.ptr(big), n + 5,
+                                     ctypes.byref(nt), sp)
+    assert rc == _native.KW_EINVAL and b'negative count' in L.kw_comm_last_error(h)
+    with pytest.raises(Exception):
+        comm.gather_hits(src, doc_base=0xFFFFFFFF - 10, root=0)
+    torch.cuda.synchronize()
+    # a good exchange after all of them
+    out, counts = comm.gather_hits(src, doc_base=7, root=0)
+    torch.cuda.synchronize()
+    want = src.cpu().numpy().copy()
+    want[:, 0] += 7
+    assert counts == [n] and np.array_equal(out.cpu().numpy(), want)

@@ -36,6 +36,10 @@ def test_kb_loader_error_paths(tmp_path, capsys):
     got = kb.read_and_process_json_files(str(d), _listdir=lambda p: sorted(os.listdir(p)))
     assert list(got) == ['AAA', 'DDD']
     assert 'Aaa Corp' in got['AAA']['aliases']
+    # the reference's own messages (match_keywords.py:104,119): the KeyError file, then the utf-8 retry
+    out = capsys.readouterr().out.splitlines()
+    assert out[-2] == "处理文件 B_info.json 时出错: 'country'"
+    assert out[-1] == 'UTF-8解码失败，尝试其他编码读取文件: C_info.json'
 
 
 def test_extract_time_periods_rules():
