@@ -36,6 +36,7 @@ namespace kw {
 #ifndef FS_AHEAD
 #define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
 #endif
+
 constexpr int FS_WAVES = FS_WAVES_CFG;   // waves per filter workgroup
 constexpr int FS_BLOCK = FS_WAVES * WAVE;
 constexpr int PK_WAVES = 4;              // waves per probe workgroup
@@ -67,7 +68,9 @@ struct __attribute__((aligned(16))) FilterLds {
     uint32_t b2[FK_B2_WORDS];
     uint32_t dstart[FS_WAVES][FG_DOCS + 1];   // group-relative document starts (+ the group end)
     uint32_t dtitle[FS_WAVES][FG_DOCS];       // group-relative title starts
-    uint32_t spos[FS_WAVES][2 * WAVE];        // stage 2: the queue of survivors' group-relative positions (a ring)
+    uint2 sent[FS_WAVES][2 * WAVE];           // stage 2: the queue of entries {group-relative byte of the lane's
+                                              // position 0, transposed survivor mask} (a ring)
+    uint32_t spos[FS_WAVES][WAVE];            // a round's survivors' group-relative positions
 };
 
 // the group document holding group-relative byte r (dstart[0] = 0 <= r < dstart[nd])
@@ -229,7 +232,6 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         uint32_t blk = 0;   // the tile's offset from gbase
         uint32_t kdoc = 0;   // document of the current stage-2 round's first survivor (candidate emission)
         bool ghdr = true;    // the group's header record is not written yet
-        uint32_t qh = 0, qn = 0;   // the survivor queue's head and length (wave-uniform)
         // FS_AHEAD tiles in flight per wave, each in its own registers (the loop is unrolled by FS_AHEAD, so no
         // register copy waits for a load).  Loads are unconditional: an address past the group's last
         // 16-byte block is clamped to it (the arena is padded; such lanes' positions are masked).  A tile
@@ -244,17 +246,12 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         // three second filters (every key length's: a superset of what the stage-1 family asked for, the short
         // keys behind the exact pair table); the final survivors ("candidates") ranked by ballot and written
         // with their document
-        auto round = [&](uint32_t n) {
-            wave_sync();
+        // (r: the lane's survivor position, lanes < n)
+        auto round_at = [&](uint32_t n, uint32_t r) {
             const bool act = (uint32_t)lane < n;
-            const uint32_t slot = (qh + (uint32_t)lane) & (2u * WAVE - 1u);
-            const uint32_t r = spos[slot];
-            wave_sync();
             // the 4-byte key at the position (the group's bytes were just streamed: a cache hit; taking it from
             // the owner lane's registers when queued was measured slower in round 5: the selects cost more VALU)
             const uint32_t key = act ? ld_u32_unaligned(arena, gb + (int64_t)r) : 0u;
-            qh = (qh + n) & (2u * WAVE - 1u);
-            qn -= n;
             const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
             const uint32_t pr = (uint32_t)lds_bit(L.p2, fk_b2_index(key));
             const uint32_t b3 = pr & t3on & (uint32_t)lds_bit(t3, fk_t3_index(key));
@@ -285,6 +282,35 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const uint32_t np = (uint32_t)__popcll(pm);
             ccur += np;
             ncand2 += (lane == 0) ? np : 0u;
+        };
+        uint2 *sent = L.sent[wib];
+        uint32_t eh = 0, en = 0;   // the entry ring's head and length (wave-uniform)
+        // one round: lane = entry, the ring's first E entries whose survivors add up to <= 64 (E >= 1: an entry
+        // holds <= 16); each expands its survivors in position order into spos at its rank, then lane = survivor
+        auto round = [&]() {
+            wave_sync();
+            const bool ein = (uint32_t)lane < en;
+            const uint2 ent = ein ? sent[(eh + (uint32_t)lane) & (2u * WAVE - 1u)] : make_uint2(0u, 0u);
+            const int c = __popc(ent.y);
+            int tot;
+            const int ex = wave_excl_scan_dpp(c, &tot);
+            const uint64_t tm = __ballot(ein && ex + c <= WAVE);
+            const int E = __popcll(tm);
+            if ((tm >> lane) & 1ull) {
+                uint32_t m = fk_untranspose(ent.y);
+                uint32_t o = (uint32_t)ex;
+                while (m) {
+                    spos[o++] = ent.x + (uint32_t)(__ffs(m) - 1);
+                    m &= m - 1u;
+                }
+            }
+            const uint32_t n = (uint32_t)__shfl(ex + c, E - 1, WAVE);
+            eh = (eh + (uint32_t)E) & (2u * WAVE - 1u);
+            en -= (uint32_t)E;
+            wave_sync();
+            const uint32_t r = spos[lane];
+            wave_sync();
+            round_at(n, r);
         };
         auto tile = [&](const uint4 &v, uint32_t w4, uint32_t tb) {
             const uint32_t lp = tb + 16u * (uint32_t)lane;
@@ -330,30 +356,14 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const uint32_t tvalid = valid == 0xFFFFu ? 0x0F0F0F0Fu : fk_transpose16(valid);
             const uint32_t sm = (hit | gate) & tvalid;
             ncand += (uint32_t)__popc(sm);
-            // the tile's survivors join the wave's queue in position order (each written by the lane that owns
-            // it: its group-relative position); stage 2 runs on full rounds of 64
-            int ts;
-            const int sx = wave_excl_scan_dpp(__popc(sm), &ts);
-            if (ts == 0) return;
-            const uint32_t smp = fk_untranspose(sm);   // position order: the candidates' order
-            for (int c0 = 0; c0 < ts;) {
-                const int take = min((int)(2u * WAVE - qn), ts - c0);
-                {
-                    int rk = sx;
-                    for (uint32_t hm = smp; hm; hm &= hm - 1u) {
-                        if (rk >= c0 + take) break;
-                        if (rk >= c0) {
-                            const uint32_t j = (uint32_t)(__ffs(hm) - 1);
-                            const uint32_t sl = (qh + qn + (uint32_t)(rk - c0)) & (2u * WAVE - 1u);
-                            spos[sl] = rel + j;
-                        }
-                        ++rk;
-                    }
-                }
-                qn += (uint32_t)take;
-                c0 += take;
-                while (qn >= (uint32_t)WAVE) round(WAVE);
-            }
+            // the lanes with survivors join the entry ring in lane (= position) order: no per-survivor work here
+            // (the per-lane survivor loop, the DPP scan and the untranspose were ~60 VALU a tile); stage 2 runs
+            // whenever 64 entries (>= 64 survivors) are queued (en < 64 before: the ring of 128 never overflows)
+            const uint64_t em = __ballot(sm != 0u);
+            if (!em) return;
+            if (sm != 0u) sent[(eh + en + mbcnt(em)) & (2u * WAVE - 1u)] = make_uint2(rel, sm);
+            en += (uint32_t)__popcll(em);
+            while (en >= (uint32_t)WAVE) round();
         };
         uint4 v[FS_AHEAD];
         uint32_t w[FS_AHEAD];
@@ -371,7 +381,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
                 blk += 1024;
             }
         }
-        while (qn) round(qn < (uint32_t)WAVE ? qn : (uint32_t)WAVE);   // the group's last survivors
+        while (en) round();   // the group's last survivors
     }
 }
 

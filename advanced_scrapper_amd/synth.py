@@ -162,7 +162,7 @@ def generate(n_docs: int, names: Sequence[str], kinds: Sequence[int], seed: int 
     return Corpus(arena, off, flags, doc_base, seed)
 
 
-def to_dataframe(corpus: Corpus, source: str = 'yahoo', span_docs: int = None):
+def to_dataframe(corpus: Corpus, source: str = 'yahoo', span_docs: int = None, date_perm=None):
     """The article CSV schema the reference reads (match_keywords.py:150-152, :139-143).
 
     NaN flags become missing values (the CSV round trip turns them into NaN,
@@ -170,6 +170,9 @@ def to_dataframe(corpus: Corpus, source: str = 'yahoo', span_docs: int = None):
     spread over 1980-2025 (naive, ``YYYY-MM-DD HH:MM:SS``); with ``span_docs``
     the spacing is that of a ``span_docs``-document corpus, so the documents of
     every slice of it get the same, increasing dates whatever the slicing.
+    ``date_perm = (a, b)`` (with ``span_docs``; gcd(a, span_docs) = 1): document g
+    gets the date of slot (a g + b) mod span_docs instead -- the same unique dates,
+    in an order that is not the documents' (the output sort then has work to do).
     """
     import pandas as pd
     n = corpus.n_docs
@@ -182,8 +185,14 @@ def to_dataframe(corpus: Corpus, source: str = 'yahoo', span_docs: int = None):
     total = max(n, 1)
     step = max(span // max(span_docs if span_docs else total + corpus.doc_base, 1), 1)
     gidx = np.arange(corpus.doc_base, corpus.doc_base + n, dtype=np.int64)
-    jitter = (gidx * 2654435761) % step
-    stamps = start + (gidx * step + jitter).astype('timedelta64[s]')
+    didx = gidx
+    if date_perm is not None:
+        import math
+        a, b = date_perm
+        assert span_docs and math.gcd(a, span_docs) == 1 and corpus.doc_base + n <= span_docs
+        didx = (gidx * a + b) % span_docs
+    jitter = (didx * 2654435761) % step
+    stamps = start + (didx * step + jitter).astype('timedelta64[s]')
     dates = [str(s).replace('T', ' ') for s in stamps]
     urls = [f"https://finance.yahoo.com/news/synthetic-{corpus.seed}-{g}.html" for g in gidx]
     return pd.DataFrame({

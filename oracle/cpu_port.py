@@ -101,15 +101,29 @@ def _cleanup(_):
     return 0
 
 
-def time_port(processed, rows: Sequence[Tuple[str, str, str]], procs: int) -> Tuple[float, int]:
-    """Wall seconds to match `rows` ((text, title, date string)) with `procs` worker processes."""
+def _reset(_):
+    """Empty the worker's scratch directory between timed runs (the next run appends from scratch)."""
+    d = _STATE.get('dir', '')
+    shutil.rmtree(d, ignore_errors=True)
+    os.makedirs(d, exist_ok=True)
+    return 0
+
+
+def time_port(processed, rows: Sequence[Tuple[str, str, str]], procs: int, runs: int = 1):
+    """Wall seconds to match `rows` ((text, title, date string)) with `procs` worker processes: (seconds, rows
+    done) for runs = 1, else (the `runs` wall times, rows done) -- every run over the same rows in the same
+    warm pool."""
     ctx = mp.get_context('spawn')
     with ctx.Pool(procs, initializer=_init, initargs=(processed,)) as pool:
         pool.map(_run, [[] for _ in range(procs)])           # warm the workers (imports, KB)
         parts = [list(p) for p in np.array_split(np.arange(len(rows)), procs)]
         subs = [[rows[i] for i in p] for p in parts]
-        t0 = time.perf_counter()
-        done = sum(pool.map(_run, subs))
-        secs = time.perf_counter() - t0
+        times = []
+        for r in range(max(1, runs)):
+            if r:
+                pool.map(_reset, range(procs))
+            t0 = time.perf_counter()
+            done = sum(pool.map(_run, subs))
+            times.append(time.perf_counter() - t0)
         pool.map(_cleanup, range(procs))
-        return secs, done
+        return (times[0] if runs == 1 else times), done

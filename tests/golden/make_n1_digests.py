@@ -23,7 +23,13 @@ Committed:
 tests/test_gpu_c3.py::test_c3_csv_rows_ten_million renders the same chunks through the drop-in's native
 path (ingest -> kw_scan -> kwrows -> kwcsv_emit) on the GPU box and compares every block and file.
 
-    python tests/golden/make_n1_digests.py [--procs 6] [--docs 10000000]
+``--perm`` (-> tests/golden/c3_csv_perm.*): the same documents with their dates permuted
+(synth.to_dataframe ``date_perm=DATE_PERM``: document g gets the date slot (a g + b) mod 10M, the same unique
+dates out of article order), so the reference's ``sort_matched_csv`` reorders the files; tests/
+test_gpu_sort_scale.py runs ``match_keywords.main`` on those articles (its RunFiles sort) and compares every
+final file with the reference's sorted bytes.
+
+    python tests/golden/make_n1_digests.py [--procs 6] [--docs 10000000] [--perm --docs 400000]
 
 Runs in the build container on CPU (~2.5 h on 6 cores), never on GPU minutes.  The appended files are
 written to tests/golden/_local/n1/ for the sort pass and deleted at the end.
@@ -53,6 +59,7 @@ SEED = 20250905
 CHUNK = 20000
 DBLOCK = 1000
 SPAN_DOCS = 10_000_000
+DATE_PERM = (3_000_017, 123_457)      # --perm: a bijection of the 10M date slots (gcd(a, 10M) = 1)
 COLUMNS = ('time_unix', 'date_time', 'text_matches', 'title_matches', 'title', 'url', 'source', 'source_url',
            'article_text')
 _W = {}
@@ -66,17 +73,19 @@ def _names_kinds():
     return synth.injectable_names(compile_kb(golden_data.kb_processed()))
 
 
-def chunk_csv_bytes(lo: int, n: int = CHUNK, names_kinds=None) -> bytes:
-    """The article CSV of documents [lo, lo + n) (also used by the GPU test)."""
+def chunk_csv_bytes(lo: int, n: int = CHUNK, names_kinds=None, perm: bool = False) -> bytes:
+    """The article CSV of documents [lo, lo + n) (also used by the GPU tests); perm: DATE_PERM's dates."""
     from advanced_scrapper_amd import synth
     if names_kinds is None:
         names_kinds = _names_kinds()
     names, kinds = names_kinds
     corpus = synth.generate(n, names, kinds, seed=SEED, doc_base=lo)
-    return synth.to_dataframe(corpus, span_docs=SPAN_DOCS).to_csv(index=False).encode('utf-8')
+    return synth.to_dataframe(corpus, span_docs=SPAN_DOCS,
+                              date_perm=DATE_PERM if perm else None).to_csv(index=False).encode('utf-8')
 
 
-def _init():
+def _init(perm=False):
+    _W['perm'] = perm
     os.environ['TZ'] = 'UTC'
     time.tzset()
     from advanced_scrapper_amd import synth
@@ -121,7 +130,7 @@ def _chunk(lo):
     import pandas as pd
     from dateutil import parser
     from tests import bytes_digest as bd
-    csv = chunk_csv_bytes(lo, CHUNK, _W['nk'])
+    csv = chunk_csv_bytes(lo, CHUNK, _W['nk'], _W['perm'])
     df = pd.read_csv(io.BytesIO(csv))
     O, tix = _W['oracle'], _W['tickers']
     recs, docs, tis = [], [], []
@@ -172,8 +181,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--procs', type=int, default=6)
     ap.add_argument('--docs', type=int, default=SPAN_DOCS)
-    ap.add_argument('--out', default=os.path.join(HERE, 'c3_csv'))
+    ap.add_argument('--out', default=None)
+    ap.add_argument('--perm', action='store_true', help='dates permuted over the documents (DATE_PERM)')
     args = ap.parse_args()
+    if args.out is None:
+        args.out = os.path.join(HERE, 'c3_csv_perm' if args.perm else 'c3_csv')
     os.environ['TZ'] = 'UTC'
     time.tzset()
     from tests import golden_data
@@ -192,7 +204,7 @@ def main():
     size = {}
     rows = {}
     t0 = time.time()
-    with mp.get_context('spawn').Pool(args.procs, initializer=_init) as pool:
+    with mp.get_context('spawn').Pool(args.procs, initializer=_init, initargs=(args.perm,)) as pool:
         for k, (lo, csv_sha, d, c, per) in enumerate(pool.imap(_chunk, range(0, n, CHUNK))):   # document order
             b = lo // DBLOCK
             dig[b:b + len(d)] = d
@@ -228,7 +240,7 @@ def main():
         total = f'{int(dig.sum(dtype=np.uint64)):016x}'
     meta = {'generator': 'tests/golden/make_n1_digests.py (CPU oracle ticker_matches + append_to_csv rows by '
                          'pandas; sort by the reference sort_matched_csv)',
-            'seed': SEED, 'n_docs': n, 'chunk_rows': CHUNK, 'docs_per_block': DBLOCK, 'span_docs': SPAN_DOCS,
+            'seed': SEED, 'n_docs': n, 'chunk_rows': CHUNK, 'date_perm': list(DATE_PERM) if args.perm else None, 'docs_per_block': DBLOCK, 'span_docs': SPAN_DOCS,
             'kb': 'tests/golden/kb_processed.json.gz', 'csv_chain_sha256': chain.hexdigest(),
             'total_rows': int(cnt.sum()), 'rows_digest': total, 'n_files': len(files),
             'files_sorted_unchanged': sum(f['sorted_sha256'] == f['appended_sha256'] for f in files.values()),
