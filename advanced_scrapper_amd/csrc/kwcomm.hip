@@ -94,7 +94,7 @@ __global__ void kw_rebase_kernel(const kw_hit *__restrict__ src, kw_hit *__restr
 struct kw_comm {
     int nranks = 1, rank = 0, device = 0;
     ncclComm_t comm = nullptr;
-    int64_t *d_counts = nullptr;   // [2 nranks + 2]: own values at [2 nranks, 2 nranks + 2), gathered at [0, 2 nranks)
+    int64_t *d_counts = nullptr;   // [3 nranks + 3]: own values at [3 nranks, 3 nranks + 3), gathered at [0, 3 nranks)
     kw_hit *d_stage = nullptr;     // this rank's records, rebased
     size_t stage_cap = 0;
     kw_hit *d_spill = nullptr;     // a receiver's records when its destination is short (planned exchange)
@@ -139,14 +139,15 @@ extern "C" int kw_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, int
     ncclUniqueId uid;
     memcpy(uid.internal, id, KW_COMM_ID_BYTES);
     NCHK(c, g_rccl.CommInitRank(&c->comm, nranks, uid, rank));
-    CCHK(c, hipMalloc(&c->d_counts, sizeof(int64_t) * (2 * nranks + 2)));
+    CCHK(c, hipMalloc(&c->d_counts, sizeof(int64_t) * (3 * nranks + 3)));
     return KW_OK;
 }
 
-// all-gather k (1 or 2) int64 per rank into out[r * k + j] (blocking: the host needs the values)
+// all-gather k (1 to 3) int64 per rank into out[r * k + j] (blocking: the host needs the values)
 static int gather_values(kw_comm *c, const int64_t *mine, int k, int64_t *out, hipStream_t st)
 {
-    int64_t *own = c->d_counts + 2 * c->nranks;
+    if (k < 1 || k > 3) { c->err = "gather_values: 1 to 3 values"; return KW_EINVAL; }
+    int64_t *own = c->d_counts + 3 * c->nranks;
     CCHK(c, hipMemcpyAsync(own, mine, sizeof(int64_t) * k, hipMemcpyHostToDevice, st));
     NCHK(c, g_rccl.AllGather(own, c->d_counts, (size_t)k, nccl_int64, c->comm, st));
     CCHK(c, hipMemcpyAsync(out, c->d_counts, sizeof(int64_t) * k * c->nranks, hipMemcpyDeviceToHost, st));
