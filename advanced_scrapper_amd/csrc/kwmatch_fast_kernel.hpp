@@ -1392,13 +1392,11 @@ __device__ __forceinline__ uint32_t hb8(uint64_t z)
 
 constexpr int LV_WIN = 23;   // dwords of text per lane in LDS (stride 23: no bank conflicts between lanes)
 
-// 8 text bytes at text position s (relative to the lane's window start A, 4-aligned)
+// 8 text bytes at byte d of the lane's window: one ds_read_b64 at any byte address (LDS runs in unaligned mode on
+// gfx950: scripts/probe/lds_unaligned.hip)
 __device__ __forceinline__ uint64_t lv_text8(const uint32_t *win, int64_t d)
 {
-    const int k = (int)(d >> 2);
-    const uint32_t sh = (uint32_t)(d & 3);
-    const uint32_t x0 = win[k], x1 = win[k + 1], x2 = win[k + 2];
-    return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32);
+    return *(const uint64_t *)((const uint8_t *)win + d);
 }
 
 // positions of byte c in the name (bit i = name[i] == c), name in 8 little-endian words
@@ -1413,7 +1411,9 @@ __device__ __forceinline__ uint64_t lv_match(const uint64_t (&NW)[8], uint32_t c
 
 // Band test of one lane's verify task (the text [base - 2k, base + m + 2k) staged in the lane's
 // LDS window): every name byte matched by a passing full window lies within +-2k of its aligned
-// text byte.  Returns the number of full windows [pmin, pmin + nwj) left to evaluate.
+// text byte.  Returns the number of full windows [pmin, pmin + nwj) left to evaluate.  The window's bytes
+// outside the field are staged as 0 (no name byte is 0; a 0 could only let a task through to the exact window
+// jobs), so the shifts need no field-bound masks.
 __device__ uint32_t lv_band(const uint8_t *__restrict__ arena, int64_t fb, uint32_t n, const uint64_t (&NW)[8],
                             uint32_t m, int64_t base, uint32_t k, uint32_t *win, int64_t &pmin)
 {
@@ -1424,24 +1424,20 @@ __device__ uint32_t lv_band(const uint8_t *__restrict__ arena, int64_t fb, uint3
     const int64_t A = (fb + lo) & ~(int64_t)3;
     const int64_t fe = fb + n;
 #pragma unroll
-    for (int j = 0; j < LV_WIN; ++j) {   // only dwords that overlap the field (the rest never matches)
+    for (int j = 0; j < LV_WIN; ++j) {   // only dwords that overlap the field; their bytes outside it cleared
         const int64_t ad = A + 4 * j;
-        win[j] = (ad + 4 > fb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+        uint32_t x = (ad + 4 > fb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+        if (ad < fb) x &= ~0u << (8 * (uint32_t)(fb - ad) & 31u);
+        if (ad + 4 > fe) x &= fe > ad ? ~(~0u << (8 * (uint32_t)(fe - ad) & 31u)) : 0u;
+        win[j] = x;
     }
     uint64_t hit[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t d0 = fb + base - A;   // window byte of name byte 0 at shift 0
     for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) {
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
             if (8 * w >= (int)m) break;
-            const int64_t s = base + 8 * w + t;   // field position of name byte 8w
-            const uint64_t z = zb64(lv_text8(win, fb + s - A) ^ NW[w]);
-            // bytes outside the field never match
-            const int64_t first = s < 0 ? -s : 0, last = (int64_t)n - s;   // valid byte range [first, last)
-            if (first >= 8 || last <= 0) continue;
-            uint64_t vm = ~0ull;
-            if (first > 0) vm &= ~0ull << (8 * first);
-            if (last < 8) vm &= (1ull << (8 * last)) - 1;
-            hit[w] |= z & vm;
+            hit[w] |= zb64(lv_text8(win, d0 + 8 * w + t) ^ NW[w]);
         }
     }
     uint32_t cnt = 0;
@@ -1606,9 +1602,15 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
         uint32_t nwj = 0, pre = 0, cj = 0;
         if (lanewise) {
             ++nver;
+#if defined(VK_TIMING_SKIP)   // (timing variants only, results void: 1 no band test, 2 no band test and no jobs)
+            nwj = 0;
+            pre = VK_TIMING_SKIP == 1 && q + pl + 1 <= m ? 1u : 0u;
+            cj = VK_TIMING_SKIP == 1 ? nwj + pre + (q + m > n ? 1u : 0u) : 0u;
+#else
             nwj = lv_band(la, fb, n, NW, m, (int64_t)q - (int64_t)o, kfull(m), win, pmin);
             pre = q + pl + 1 <= m ? 1u : 0u;
             cj = nwj + pre + (q + m > n ? 1u : 0u);
+#endif
         }
         int J = 0;
         const int ex = wave_excl_scan((int)cj, &J);
