@@ -1351,7 +1351,11 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
         for (int i = 0; i < 11; ++i) atomicAdd(&S.stats[21 + i], ekt[i]);
     // the workgroup's big documents: wave 0 with the whole workgroup's LDS as one 4096 + 512-item buffer
     __syncthreads();
+#if defined(EK_TIMING_SKIP_BIG)   // (timing variant only, results void: the big documents are not finished)
+    const uint32_t nb = 0;
+#else
     const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
+#endif
     if (wib == 0 && nb) {
         for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC) & 1u;
         if (lane == 0) atomicAdd(&S.stats[16], (unsigned long long)nb);
@@ -1722,7 +1726,11 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
     }
     // the workgroup's big documents: wave 0 with the whole workgroup's LDS as one 4096 + 512-item buffer
     __syncthreads();
+#if defined(EK_TIMING_SKIP_BIG)   // (timing variant only, results void: the big documents are not finished)
+    const uint32_t nb = 0;
+#else
     const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
+#endif
     if (wib == 0 && nb) {
         for (uint32_t i = 0; i < nb; ++i) {
             const uint32_t r = epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC);
