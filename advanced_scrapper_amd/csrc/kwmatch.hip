@@ -1133,7 +1133,7 @@ extern "C" int kw_compile(const uint8_t *pat_bytes, const int64_t *pat_off, cons
         HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, (sp & 1) ? hi : lo));
         HIPCHK(h, hipStreamCreateWithPriority(&h->side2, hipStreamNonBlocking, (sp & 2) ? hi : lo));
-        HIPCHK(h, hipStreamCreateWithPriority(&h->side3, hipStreamNonBlocking, lo));
+        HIPCHK(h, hipStreamCreateWithPriority(&h->side3, hipStreamNonBlocking, (sp & 4) ? hi : lo));
     }
     HIPCHK(h, hipEventCreateWithFlags(&h->eve, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->evq, hipEventDisableTiming));
