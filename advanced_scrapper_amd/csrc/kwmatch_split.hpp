@@ -33,6 +33,11 @@ namespace kw {
 #ifndef FS_MINW
 #define FS_MINW 1
 #endif
+#ifndef FS_EQ_TRIGGER
+#define FS_EQ_TRIGGER 32   // queued entries that start a stage-2 round: a round then takes ~2 tiles of survivors
+                           // while their bytes are still in L2 (64: filter reads 4.03 GB a launch, 48: 3.59, 32: 3.08
+                           // for 1.103 / 1.111 / 1.112 ms; 24: 1.145 ms, 16: 1.238 ms)
+#endif
 #ifndef FS_AHEAD
 #define FS_AHEAD 3       // 1 KiB tiles each filter wave keeps in flight
 #endif
@@ -363,7 +368,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             if (!em) return;
             if (sm != 0u) sent[(eh + en + mbcnt(em)) & (2u * WAVE - 1u)] = make_uint2(rel, sm);
             en += (uint32_t)__popcll(em);
-            while (en >= (uint32_t)WAVE) round();
+            while (en >= (uint32_t)FS_EQ_TRIGGER) round();
         };
         uint4 v[FS_AHEAD];
         uint32_t w[FS_AHEAD];
