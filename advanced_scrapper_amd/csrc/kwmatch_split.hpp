@@ -809,12 +809,18 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
         const int jlo = r0 <= 0 ? 0 : (r0 >= 16 ? 16 : (int)r0);
         const int jhi = r2 <= 0 ? 0 : (r2 >= 16 ? 16 : (int)r2);
         const uint32_t valid = (jhi > jlo) ? (((1u << jhi) - 1u) & ~((1u << jlo) - 1u)) : 0u;
-        uint32_t lead = 0, high = 0;
+        // a lane whose 16 bytes are ASCII (most of them: a non-ASCII field has a few multi-byte characters) has
+        // every byte a lead byte and copies them with one 16-byte LDS store below
+        const bool asc = ((W[0] | W[1] | W[2] | W[3]) & 0x80808080u) == 0u;
+        uint32_t lead = 0xFFFFu, high = 0;
+        if (!asc) {
+            lead = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t b = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-            lead |= (uint32_t)((b & 0xC0u) != 0x80u) << j;
-            high |= (uint32_t)(b >= 0x80u) << j;
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t b = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                lead |= (uint32_t)((b & 0xC0u) != 0x80u) << j;
+                high |= (uint32_t)(b >= 0x80u) << j;
+            }
         }
         lead &= valid;
         high &= valid;
@@ -829,9 +835,13 @@ __device__ uint32_t tx_field(const uint32_t *txk, const uint32_t *txv, const uin
         // every lead byte's output at its rank among the lane's lead bytes: the ASCII ones unrolled (one
         // predicated store each), then a loop over the lane's few multi-byte characters only (decode, marker)
         const uint32_t hl = lead & high;
+        if (asc && valid == 0xFFFFu) {
+            *(uint4 *)(stg + k) = v;   // (any byte address: LDS runs in unaligned mode, scripts/probe/lds_unaligned.hip)
+        } else {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (((lead & ~hl) >> j) & 1u) stg[k + (uint32_t)__popc(lead & ((1u << j) - 1u))] = (uint8_t)(W[j >> 2] >> (8 * (j & 3)));
+            for (int j = 0; j < 16; ++j)
+                if (((lead & ~hl) >> j) & 1u) stg[k + (uint32_t)__popc(lead & ((1u << j) - 1u))] = (uint8_t)(W[j >> 2] >> (8 * (j & 3)));
+        }
         for (uint32_t lm = hl; lm; lm &= lm - 1) {
             const int j = __ffs(lm) - 1;
             const uint32_t b0 = (W[j >> 2] >> (8 * (j & 3))) & 0xFFu;
