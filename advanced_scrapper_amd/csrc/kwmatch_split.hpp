@@ -1588,13 +1588,21 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
                 if (cnt <= (uint32_t)WAVE) {
                     const int64_t fb = f ? t1 : t0, a0 = fb & ~(int64_t)3;
                     const uint32_t sh0 = (uint32_t)(fb - a0);
+                    // the field's <= 67 bytes as dwords loaded six at a time (three round trips, not one per dword;
+                    // the arena is padded; more at once spills the epilogue's registers), then the names'
+                    // signatures four at a time
                     uint64_t fsig = 0;
-                    for (uint32_t w = 0; 4 * w < n + sh0; ++w) {
-                        const uint32_t x = *(const uint32_t *)(arena + a0 + 4 * w);   // (the arena is padded)
+                    for (uint32_t w0 = 0; 4 * w0 < n + sh0; w0 += 6) {
+                        uint32_t xw[6];
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const uint32_t p = 4 * w + (uint32_t)k;
-                            if (p >= sh0 && p < n + sh0) fsig |= 1ull << ((x >> (8 * k)) & 63u);
+                        for (int w = 0; w < 6; ++w) xw[w] = *(const uint32_t *)(arena + a0 + 4 * (w0 + (uint32_t)w));
+#pragma unroll
+                        for (int w = 0; w < 6; ++w) {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const uint32_t p = 4 * (w0 + (uint32_t)w) + (uint32_t)k;
+                                if (p >= sh0 && p < n + sh0) fsig |= 1ull << ((xw[w] >> (8 * k)) & 63u);
+                            }
                         }
                     }
                     const uint32_t allow = (2 * n - 1) / 20;
