@@ -545,7 +545,12 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
             }
         }
         uint32_t tcur = rb[0], tend = re[0], b1 = rb[1], e1 = re[1], b2 = rb[2], e2 = re[2];
+#if defined(PK_TIMING_SKIP) && PK_TIMING_SKIP == 2
+        bool more = false;
+        if (__ballot(valid && (tcur | b1 | b2) == 0xFFFFFFFFu)) nanchor += 1;   // (keeps the lookups)
+#else
         bool more = valid;
+#endif
         uint32_t pn = 0;                    // items in the pool (wave-uniform)
         while (__ballot(more)) {
             // stage A: up to two matching anchors of this lane's candidate
@@ -583,6 +588,9 @@ __global__ __launch_bounds__(PK_BLOCK, PK_MINW) void kw_probe_kernel(FastTables 
             // stage B: (candidate, use) pairs over the lanes
             int total;
             const int ex = wave_excl_scan_dpp((int)(uc + uc1), &total);
+#if defined(PK_TIMING_SKIP)   // (timing variants only, results void: 1 no stage B, 2 no stage A or B)
+            total = 0;
+#endif
             for (int g0 = 0; g0 < total; g0 += WAVE) {
                 const int g = g0 + lane;
                 bool pass = false;
