@@ -1351,6 +1351,8 @@ static int launch_scan(kw_handle *h)
         h->FS.item_cap = (uint32_t)icap;
         h->FS.item_grow = icap == h->caps.item_cap && !h->item_clamped ? 1u : 0u;
     }
+    h->FS.bigq = EK_BIGQ;   // (KW_TEST_BIGQ lowers it: tests send the big documents to the resolve kernel)
+    if (const char *e = kw_env("KW_TEST_BIGQ")) h->FS.bigq = (uint32_t)std::min(std::max(0, atoi(e)), EK_BIGQ);
     h->FS.dyn = dyn_groups ? 1 : 0;
     h->FS.chunk_groups = kchunk;
     const int nk = h->nk;   // the allocation may be larger than this launch needs: every region is cleared
@@ -1736,13 +1738,18 @@ extern "C" int kw_doc_routes(kw_handle *h, uint8_t *routes, int64_t n)
     if (rc) return rc;
     if (n != h->n_docs) { h->err = "kw_doc_routes: n differs from the scanned document count"; return KW_EINVAL; }
     std::vector<uint2> hdr((size_t)n);
-    if (n > 0) HIPCHK(h, hipMemcpy(hdr.data(), h->FS.hdr, (size_t)n * sizeof(uint2), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> dfl((size_t)n);
+    if (n > 0) {
+        HIPCHK(h, hipMemcpy(hdr.data(), h->FS.hdr, (size_t)n * sizeof(uint2), hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy(dfl.data(), h->FS.dflags, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
     for (int64_t d = 0; d < n; ++d) {
         const uint32_t y = hdr[d].y;
-        routes[d] = (y & DH_DEFER)                ? KW_ROUTE_GENERIC
-                    : (y & DH_TX)                 ? KW_ROUTE_TRANSCODE
-                    : (y & (DH_NA0 | DH_NA1))     ? KW_ROUTE_RESOLVE
-                                                  : KW_ROUTE_SCAN;
+        // (dflags: DH_RESOLVE also marks the all-ASCII big documents an epilogue workgroup had no room for)
+        routes[d] = (y & DH_DEFER)                                       ? KW_ROUTE_GENERIC
+                    : (y & DH_TX)                                        ? KW_ROUTE_TRANSCODE
+                    : ((y & (DH_NA0 | DH_NA1)) || (dfl[d] & DH_RESOLVE)) ? KW_ROUTE_RESOLVE
+                                                                         : KW_ROUTE_SCAN;
     }
     return KW_OK;
 }

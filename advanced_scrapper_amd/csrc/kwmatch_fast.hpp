@@ -174,6 +174,7 @@ struct FastTables {
 struct FastScratch {
     uint64_t *items;            // per filter region: item_cap items (the probe's), indexed by 32-bit hdr.x
     uint32_t item_cap;          // regions x item_cap < 2^32 (launch_scan clamps it)
+    uint32_t bigq;              // big documents an epilogue workgroup queues for itself (<= EK_BIGQ; more: resolve)
     uint32_t item_grow;         // 1: a region whose items overflow asks the host for larger regions (rescan);
                                 // 0 (item_cap clamped): its batches' documents only defer to the generic kernel
     uint2 *hdr;                 // per document

@@ -60,7 +60,7 @@ constexpr int PK_POOL = PK_POOL_CFG;     // items one batch of 64 candidates may
 #define PK_MINW 5   // <= 102 VGPRs: the probe and the transcoding kernel beside it share the CUs better
 #endif
 constexpr int EK_WAVES = 8;              // waves per epilogue workgroup
-constexpr int EK_BIGQ = 64;              // big documents one epilogue workgroup finishes itself (more: generic)
+constexpr int EK_BIGQ = 64;              // big documents one epilogue workgroup finishes itself (more: resolve)
 constexpr int EK_BLOCK = EK_WAVES * WAVE;
 
 constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range; 5 bits of a candidate)
@@ -1314,9 +1314,18 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
                     if (lane == 0) bi = atomicAdd(&blk_n, 1u);
                     bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
                 }
-                if (bi < (uint32_t)EK_BIGQ) {
+                if (bi < S.bigq) {
                     if (lane == 0) blk_docs[bi] = (uint32_t)d;
                     queued = true;
+                } else if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG0) {
+                    // the workgroup's queue is full (or the title is past FK_BIG1): the resolve kernel's big documents
+                    ++nres;
+                    queued = true;
+                    if (lane == 0) {
+                        S.dflags[d] = flags | DH_RESOLVE;
+                        const uint32_t i = atomicAdd(S.res_cnt, 1u);
+                        if (i < S.defer_cap) S.res_list[i] = (uint32_t)d;
+                    }
                 } else {
                     defer = true;
                     ++ndef_items;
@@ -1377,7 +1386,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
 #if defined(EK_TIMING_SKIP_BIG)   // (timing variant only, results void: the big documents are not finished)
     const uint32_t nb = 0;
 #else
-    const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
+    const uint32_t nb = min(blk_n, S.bigq);
 #endif
     if (wib == 0 && nb) {
         for (uint32_t i = 0; i < nb; ++i) ndefer += epi_big_doc(FT, S, GS, arena, off, blk_docs[i], items_all, wave, O, TC) & 1u;
@@ -1674,7 +1683,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
                     uint32_t bi = 0;
                     if (lane == 0) bi = atomicAdd(&blk_n, 1u);
                     bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
-                    if (bi < (uint32_t)EK_BIGQ) {
+                    if (bi < S.bigq) {
                         if (lane == 0) blk_docs[bi] = (uint32_t)dd | EK_TXBIG;
                         wave_sync();
                         continue;
@@ -1712,13 +1721,21 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
             bool defer = (dflags & DH_DEFER) != 0 || D.t1 - D.t0 > MAX_FIELD_BYTES || D.t2 - D.t1 > MAX_FIELD_BYTES;
             if (defer && lane == 0) atomicAdd(&S.stats[15], 1ull);
             if (!defer && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1)) {
-                uint32_t bi = 0xFFFFFFFFu;
-                if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG1) {
-                    if (lane == 0) bi = atomicAdd(&blk_n, 1u);
+                if (n0 <= (uint32_t)FK_BIG0 && n1 <= (uint32_t)FK_BIG0) {
+                    // the workgroup's big documents; with its queue full (or the title past FK_BIG1) the resolve
+                    // kernel's big documents
+                    uint32_t bi = 0xFFFFFFFFu;
+                    if (lane == 0 && n1 <= (uint32_t)FK_BIG1) bi = atomicAdd(&blk_n, 1u);
                     bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)bi);
-                }
-                if (bi < (uint32_t)EK_BIGQ) {
-                    if (lane == 0) blk_docs[bi] = (uint32_t)dd;
+                    if (lane == 0) {
+                        if (bi < S.bigq) {
+                            blk_docs[bi] = (uint32_t)dd;
+                        } else {
+                            S.dflags[dd] = dflags | DH_RESOLVE;
+                            const uint32_t i = atomicAdd(S.res_cnt, 1u);
+                            if (i < S.defer_cap) S.res_list[i] = (uint32_t)dd;
+                        }
+                    }
                     continue;
                 }
                 defer = true;
@@ -1760,7 +1777,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
 #if defined(EK_TIMING_SKIP_BIG)   // (timing variant only, results void: the big documents are not finished)
     const uint32_t nb = 0;
 #else
-    const uint32_t nb = min(blk_n, (uint32_t)EK_BIGQ);
+    const uint32_t nb = min(blk_n, S.bigq);
 #endif
     if (wib == 0 && nb) {
         for (uint32_t i = 0; i < nb; ++i) {

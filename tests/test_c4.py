@@ -179,6 +179,28 @@ def test_c4_whole_corpus_vs_oracle_digests():
     assert not len(bad), f'{len(bad)} of {n} documents differ from the oracle; first: {bad[:20].tolist()}'
     assert int(cnt.sum()) == meta['total_records']
     assert cd.total(dig) == meta['hits_digest'] == bench.hits_digest(hits)
+    st = m.stats()
+    assert st['big_docs'] > 1000 and st['deferred_item_caps'] == 0
+    # the same corpus with no room in any epilogue workgroup's big-document queue (KW_TEST_BIGQ=0): every
+    # all-ASCII big document takes the resolve kernel's big-document path instead (what a workgroup past its
+    # 64 queued documents does at 10M), same records
+    from advanced_scrapper_amd import _native
+    import os as _os
+    _os.environ['KW_TEST_BIGQ'] = '0'
+    try:
+        m.scan(d_arena, d_off, n)
+        hits2 = m.hits_device()
+        st2 = m.stats()
+        routes = m.doc_routes(n)
+    finally:
+        del _os.environ['KW_TEST_BIGQ']
+    dig2, cnt2 = cd.per_doc(records_from_tensor(hits2), n)
+    bad2 = np.flatnonzero((dig2 != z['digest']) | (cnt2 != z['count'].astype(np.int64)))
+    assert not len(bad2), f'KW_TEST_BIGQ=0: {len(bad2)} documents differ; first: {bad2[:20].tolist()}'
+    # (big_docs counts both kernels' big documents)
+    assert st2['deferred_item_caps'] == 0 and st2['deferred_docs'] == st['deferred_docs']
+    assert st2['resolved_docs'] >= st['resolved_docs'] + st['big_docs'] // 2
+    assert int((routes == _native.KW_ROUTE_RESOLVE).sum()) >= st2['resolved_docs'] - st['resolved_docs']
     m.close()
 
 
