@@ -256,7 +256,11 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             const bool act = (uint32_t)lane < n;
             // the 4-byte key at the position (the group's bytes were just streamed: a cache hit; taking it from
             // the owner lane's registers when queued was measured slower in round 5: the selects cost more VALU)
+#if defined(FS_TIMING_SKIP) && FS_TIMING_SKIP == 2   // (traffic calibration only, results void: no key re-read)
+            const uint32_t key = act ? r * 0x9E3779B1u : 0u;
+#else
             const uint32_t key = act ? ld_u32_unaligned(arena, gb + (int64_t)r) : 0u;
+#endif
             const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
             const uint32_t pr = (uint32_t)lds_bit(L.p2, fk_b2_index(key));
             const uint32_t b3 = pr & t3on & (uint32_t)lds_bit(t3, fk_t3_index(key));
@@ -368,6 +372,9 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             if (!em) return;
             if (sm != 0u) sent[(eh + en + mbcnt(em)) & (2u * WAVE - 1u)] = make_uint2(rel, sm);
             en += (uint32_t)__popcll(em);
+#if defined(FS_TIMING_SKIP) && FS_TIMING_SKIP == 1   // (traffic calibration only, results void: no stage 2)
+            en = 0;
+#endif
             while (en >= (uint32_t)FS_EQ_TRIGGER) round();
         };
         uint4 v[FS_AHEAD];
