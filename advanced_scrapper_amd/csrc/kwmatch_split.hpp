@@ -252,15 +252,9 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         // keys behind the exact pair table); the final survivors ("candidates") ranked by ballot and written
         // with their document
         // (r: the lane's survivor position, lanes < n)
-        auto round_at = [&](uint32_t n, uint32_t r) {
+        // (key: the 4-byte key at the position, loaded when the round was formed; see round())
+        auto round_at = [&](uint32_t n, uint32_t r, uint32_t key) {
             const bool act = (uint32_t)lane < n;
-            // the 4-byte key at the position (the group's bytes were just streamed: a cache hit; taking it from
-            // the owner lane's registers when queued was measured slower in round 5: the selects cost more VALU)
-#if defined(FS_TIMING_SKIP) && FS_TIMING_SKIP == 2   // (traffic calibration only, results void: no key re-read)
-            const uint32_t key = act ? r * 0x9E3779B1u : 0u;
-#else
-            const uint32_t key = act ? ld_u32_unaligned(arena, gb + (int64_t)r) : 0u;
-#endif
             const uint32_t b4 = (uint32_t)lds_bit(l2, fk_l2_index(key));
             const uint32_t pr = (uint32_t)lds_bit(L.p2, fk_b2_index(key));
             const uint32_t b3 = pr & t3on & (uint32_t)lds_bit(t3, fk_t3_index(key));
@@ -294,6 +288,9 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
         };
         uint2 *sent = L.sent[wib];
         uint32_t eh = 0, en = 0;   // the entry ring's head and length (wave-uniform)
+        // the round formed last: its survivors' keys are in flight while the next tiles' stage 1 runs (the
+        // re-read of bytes streamed a few tiles earlier often misses L2), it finishes when the next round forms
+        uint32_t qn = 0, qr = 0, qx0 = 0, qx1 = 0;
         // one round: lane = entry, the ring's first E entries whose survivors add up to <= 64 (E >= 1: an entry
         // holds <= 16); each expands its survivors in position order into spos at its rank, then lane = survivor
         auto round = [&]() {
@@ -319,7 +316,22 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             wave_sync();
             const uint32_t r = spos[lane];
             wave_sync();
-            round_at(n, r);
+            // the key's two aligned words (joined when the round finishes: no wait for them here)
+            uint32_t x0 = 0, x1 = 0;
+#if defined(FS_TIMING_SKIP) && FS_TIMING_SKIP == 2   // (traffic calibration only, results void: no key re-read)
+            x0 = r * 0x9E3779B1u;
+#else
+            if ((uint32_t)lane < n) {
+                const int64_t a0 = (gb + (int64_t)r) & ~(int64_t)3;
+                x0 = *(const uint32_t *)(arena + a0);
+                x1 = *(const uint32_t *)(arena + a0 + 4);
+            }
+#endif
+            if (qn) round_at(qn, qr, __builtin_amdgcn_alignbyte(qx1, qx0, (uint32_t)(gb + qr) & 3u));
+            qn = n;
+            qr = r;
+            qx0 = x0;
+            qx1 = x1;
         };
         auto tile = [&](const uint4 &v, uint32_t w4, uint32_t tb) {
             const uint32_t lp = tb + 16u * (uint32_t)lane;
@@ -394,6 +406,7 @@ __device__ __forceinline__ void fk_filter_groups(const FastTables &FT, FilterLds
             }
         }
         while (en) round();   // the group's last survivors
+        if (qn) round_at(qn, qr, __builtin_amdgcn_alignbyte(qx1, qx0, (uint32_t)(gb + qr) & 3u));
     }
 }
 
