@@ -17,8 +17,8 @@
 //   kw_epi_kernel     one wave per document: all-ASCII documents are finished by the epilogue
 //                     (fk_scan_epilogue: sort, emit, queue the verify / short / regex tasks), the others get
 //                     their header for the resolve kernel; documents with more items than a wave's LDS
-//                     holds are finished after the workgroup's loop with the whole workgroup's LDS
-//                     (epi_big_doc), oversize ones go to the generic kernel.
+//                     holds are finished after the workgroup's loop with the whole workgroup's LDS (epi_big_doc;
+//                     up to EK_BIGQ, the rest: kw_resolve_big_kernel), oversize ones go to the generic kernel.
 //
 // Reference: the per-article x per-name loop of match_keywords.py:159-180 (see kwmatch_fast.hpp for the
 // anchors and filters).

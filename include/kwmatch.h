@@ -151,8 +151,8 @@ int kw_last_kernel_times(kw_handle *h, float *ms, int32_t n);
 /* Which kernel finished each document of the last scan (after kw_hits):
  * routes[d] = KW_ROUTE_SCAN (the scan kernel's epilogue and its task kernels),
  * KW_ROUTE_TRANSCODE (a non-ASCII field: the epilogue on the document's
- * transcoded view, then the task kernels), KW_ROUTE_RESOLVE (the resolve
- * kernel: non-ASCII fields the view cannot take) or KW_ROUTE_GENERIC (deferred
+ * transcoded view, then the task kernels), KW_ROUTE_RESOLVE (the resolve kernels: non-ASCII
+ * fields the view cannot take, big documents past an epilogue queue) or KW_ROUTE_GENERIC (deferred
  * to the generic kernel: capacity limits).  For tests and tuning. */
 #define KW_ROUTE_SCAN 0
 #define KW_ROUTE_RESOLVE 1
