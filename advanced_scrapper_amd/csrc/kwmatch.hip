@@ -1388,9 +1388,15 @@ static int launch_scan(kw_handle *h)
     if (n_docs > 0) {
         // the group epilogue (lane = item across 32 documents); KW_EPI_FLAT=0: one wave per document
         static const bool flat = !kw_env("KW_EPI_FLAT") || atoi(kw_env("KW_EPI_FLAT")) != 0;
-        if (flat)
-            hipLaunchKernelGGL(kw_epi_flat_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off,
-                               n_docs, h->FS, h->S);
+        // its transcoded documents in the batches too when no name is PI_TXUNSAFE (KW_TEST_EPI_TXB=0, read per
+        // scan: one at a time, as with such names)
+        const bool txb = EF_TX_FLAT && (!kw_env("KW_TEST_EPI_TXB") || atoi(kw_env("KW_TEST_EPI_TXB")) != 0);
+        if (flat && txb && h->FT.n_txu == 0)
+            hipLaunchKernelGGL(kw_epi_flat_kernel<true>, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena,
+                               h->doc_off, n_docs, h->FS, h->S);
+        else if (flat)
+            hipLaunchKernelGGL(kw_epi_flat_kernel<false>, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena,
+                               h->doc_off, n_docs, h->FS, h->S);
         else
             hipLaunchKernelGGL(kw_epi_kernel, dim3(neb), dim3(EK_BLOCK), 0, st, h->FT, h->arena, h->doc_off, n_docs,
                                h->FS, h->S);

@@ -64,6 +64,9 @@ constexpr int EK_BIGQ = 64;              // big documents one epilogue workgroup
 constexpr int EK_BLOCK = EK_WAVES * WAVE;
 
 constexpr int FG_DOCS = 32;              // documents per filter group (one flat byte range; 5 bits of a candidate)
+#ifndef EF_TX_FLAT
+#define EF_TX_FLAT 1   // kw_epi_flat_kernel<true> batches the transcoded documents too (KBs without PI_TXUNSAFE names)
+#endif
 
 struct __attribute__((aligned(16))) FilterLds {
     uint32_t s1[FK_S1_WORDS];
@@ -1443,12 +1446,14 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_kernel(FastTables FT
 // documents (non-ASCII, big, deferred) take the per-document code after the batches.
 __device__ __forceinline__ uint32_t ep_n(const uint32_t (&v)[2], uint32_t f) { return f ? v[1] : v[0]; }
 
+template <bool TXB>
 __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTables FT, const uint8_t *__restrict__ arena,
                                                                const int64_t *__restrict__ off, int64_t n_docs,
                                                                FastScratch S, DevScratch GS)
 {
     __shared__ uint64_t items_all[EK_WAVES * (FK_ITEMS0 + FK_ITEMS1)];
     __shared__ uint32_t blk_docs[EK_BIGQ];
+    __shared__ uint4 segtx_all[TXB ? EK_WAVES * WAVE : 1];   // TXB: the segments' arena start, chunk table
     __shared__ uint32_t blk_n;
     if (threadIdx.x == 0) blk_n = 0;
     __syncthreads();
@@ -1457,6 +1462,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
     const int64_t wave = (int64_t)blockIdx.x * EK_WAVES + wib;
     const int64_t n_waves = (int64_t)gridDim.x * EK_WAVES;
     uint64_t *items = items_all + wib * (FK_ITEMS0 + FK_ITEMS1);
+    uint4 *segtx = segtx_all + (TXB ? wib * WAVE : 0);
     uint32_t ndefer = 0, ndef_items = 0, ntx = 0, nres = 0;
     OutCtx O;
     O.shared = nullptr;
@@ -1491,9 +1497,34 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         }
         const uint32_t flags = fl | ef;
         const int64_t l0 = t1 - t0, l1 = t2 - t1;
-        const bool flat = act && !(fl & (DH_NA0 | DH_NA1 | DH_DEFER)) && l0 <= MAX_FIELD_BYTES &&
+        // TXB: a document with a non-ASCII field joins the batches on its transcoded view (the transcoding
+        // kernel's record V: the view's place, the fields' code point counts; its items' positions become code
+        // points).  The host picks TXB only when no name is PI_TXUNSAFE (kw_epi_kernel's per-document tests)
+        const bool na = (fl & (DH_NA0 | DH_NA1)) != 0;
+        uint32_t c0 = (uint32_t)l0, c1 = (uint32_t)l1;   // the fields' code points
+        bool txd = false;
+        uint4 V = make_uint4(0u, TX_NONE, 0u, 0u);
+        if (TXB && act && na) {
+            V = S.vrec[d];
+            txd = V.y != TX_NONE;
+            if (txd) { c0 = V.z; c1 = V.w; }
+        }
+        const bool flat = act && !(fl & DH_DEFER) && (!na || txd) && l0 <= MAX_FIELD_BYTES &&
                           l1 <= MAX_FIELD_BYTES && nc.x <= (uint32_t)WAVE && nc.y <= (uint32_t)WAVE;
         const uint64_t flatm = __ballot(flat);
+        const uint64_t txm = TXB ? __ballot(flat && txd) : 0ull;   // (wave-uniform: 0 for an all-ASCII group)
+        if (txm) {   // segment 2 l + f's arena start and chunk table of code point counts (tarena offset; tx_pos)
+            wave_sync();
+            if (flat && txd) {
+                const int64_t ch0 = (int64_t)(((uint64_t)(V.y & 0x7FFFFFFFu) << 32) | V.x) + (int64_t)tx_bytes(l0, l1);
+                const int64_t ch1 = ch0 + 2 * (int64_t)((fl & DH_NA0) ? tx_nchunks(t0, t1) : 0u);
+                segtx[2 * lane] = make_uint4((uint32_t)t0, (uint32_t)((uint64_t)t0 >> 32), (uint32_t)ch0,
+                                             (uint32_t)((uint64_t)ch0 >> 32));
+                segtx[2 * lane + 1] = make_uint4((uint32_t)t1, (uint32_t)((uint64_t)t1 >> 32), (uint32_t)ch1,
+                                                 (uint32_t)((uint64_t)ch1 >> 32));
+            }
+            wave_sync();
+        }
         // ---- lane = segment s = 2 * document + field of the plain documents: size, first item, batch offset
         const int sd = lane >> 1, sf = lane & 1;
         const uint32_t s_n0 = (uint32_t)__shfl((int)nc.x, sd, WAVE), s_n1 = (uint32_t)__shfl((int)nc.y, sd, WAVE);
@@ -1503,8 +1534,14 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         const uint32_t st = s_beg + (sf ? s_n0 : 0u);
         int stot;
         const uint32_t soff = (uint32_t)wave_excl_scan_dpp((int)sz, &stot);
-        const uint32_t s_l0 = (uint32_t)__shfl((int)(uint32_t)l0, sd, WAVE), s_l1 = (uint32_t)__shfl((int)(uint32_t)l1, sd, WAVE);
-        const uint32_t s_len = sf ? s_l1 : s_l0;   // the segment's field bytes (= code points: ASCII)
+        const uint32_t s_l0 = (uint32_t)__shfl((int)c0, sd, WAVE), s_l1 = (uint32_t)__shfl((int)c1, sd, WAVE);
+        const uint32_t s_len = sf ? s_l1 : s_l0;   // the segment's field length in code points
+        // the segments of non-ASCII fields (transcoded documents)
+        uint64_t snam = 0;
+        if (txm) {
+            const uint32_t s_fl = (uint32_t)__shfl((int)fl, sd, WAVE);
+            snam = __ballot(s_flat && ((txm >> sd) & 1ull) && (s_fl & (sf ? DH_NA1 : DH_NA0)));
+        }
         // ---- batches of whole segments, <= 64 items each
         for (uint32_t base = 0; base < (uint32_t)stot;) {
             // the segments that fit: soff + sz - base <= 64 (soff ascending)
@@ -1522,7 +1559,12 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
             }
             const bool valid = (uint32_t)lane < cnt;
             const uint32_t sgo = (uint32_t)__shfl((int)soff, sg, WAVE), sgs = (uint32_t)__shfl((int)st, sg, WAVE);
-            const uint64_t it0 = valid ? S.items[sgs + (base + (uint32_t)lane - sgo)] : 0ull;
+            uint64_t it0 = valid ? S.items[sgs + (base + (uint32_t)lane - sgo)] : 0ull;
+            if (snam && valid && ((snam >> sg) & 1ull)) {   // (an item of a non-ASCII field: its position in code points)
+                const uint4 e = segtx[sg];
+                const int64_t fbs = (int64_t)(((uint64_t)e.y << 32) | e.x), chs = (int64_t)(((uint64_t)e.w << 32) | e.z);
+                it0 = it_with_pos(it0, tx_pos(arena, fbs, (const uint16_t *)(S.tarena + chs), it_pos(it0)));
+            }
             base = bend;
             // sort by (segment, name, position, kind); the use rides along
             uint32_t use = it_use(it0);
@@ -1540,7 +1582,8 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
             const uint32_t rxl = valid ? FT.pat_rxl[pat] : 0u;
             const uint32_t uinfo = (valid && kind == FU_PIECE) ? FT.use_info1[use] : 0u;
             const uint32_t m = pi_m(pi);
-            const bool rxi = rxk == RXK_REGEX && rxl != 0u;   // (plain documents: every field is ASCII)
+            // (RXM items are exact regex matches in an ASCII field only; a transcoded field's regex names are searched)
+            const bool rxi = rxk == RXK_REGEX && rxl != 0u && !((snam >> seg) & 1ull);
             const uint32_t mlen = rxi ? rxl : m;
             const bool fuzzy = (pi & PI_FUZZY) != 0;
             const uint64_t gkey = key >> 38;   // (segment, name)
@@ -1618,9 +1661,10 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         // KB's) first takes the short kernel's signature test here: without a candidate name it needs no task.
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-            const int64_t lf = f ? l1 : l0;
+            const int64_t lf = f ? (int64_t)c1 : (int64_t)c0;
             bool sh = flat && lf <= (int64_t)MAXM;
-            if (EPI_SHORT_PREF && sh && lf > (int64_t)SHORT_EXACT_MAX) {
+            // (a transcoded document's short field takes its task untested: a superset, the short kernel decides)
+            if (EPI_SHORT_PREF && sh && !txd && lf > (int64_t)SHORT_EXACT_MAX) {
                 const uint32_t n = (uint32_t)lf, cnt = (uint32_t)FT.f_count_ge[n];
                 if (cnt <= (uint32_t)WAVE) {
                     const int64_t fb = f ? t1 : t0, a0 = fb & ~(int64_t)3;
@@ -1663,19 +1707,29 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
             const int l = __builtin_ctzll(edm);
             edm &= edm - 1;
             FastDoc D;
-            D.arena = arena;
-            D.t0 = rdlane64(t0, l);
-            D.t1 = rdlane64(t1, l);
-            D.t2 = rdlane64(t2, l);
+            if ((txm >> l) & 1ull) {   // (a transcoded document: its windows on the view)
+                const uint4 Vl = S.vrec[d0 + l];
+                D.arena = S.tarena;
+                D.t0 = (int64_t)(((uint64_t)(Vl.y & 0x7FFFFFFFu) << 32) | Vl.x);
+                D.t1 = D.t0 + Vl.z;
+                D.t2 = D.t1 + Vl.w;
+            } else {
+                D.arena = arena;
+                D.t0 = rdlane64(t0, l);
+                D.t1 = rdlane64(t1, l);
+                D.t2 = rdlane64(t2, l);
+            }
             D.doc = (uint32_t)(d0 + l);
             D.l1 = (int32_t)(D.t1 - D.t0);
             D.l2 = (int32_t)(D.t2 - D.t0);
             fk_epi_edge(FT, S, GS, D, (uint32_t)__builtin_amdgcn_readlane((int)flags, l), O, TC, xq);
         }
         if (flat) {
-            S.hdr[d] = make_uint2(hd.x, nc.x | (nc.y << DH_N1_SHIFT) | flags);
-            S.vrec[d] = make_uint4((uint32_t)t0, (uint32_t)((uint64_t)t0 >> 32), (uint32_t)l0, (uint32_t)l1);
+            S.hdr[d] = make_uint2(hd.x, nc.x | (nc.y << DH_N1_SHIFT) | flags | (txd ? DH_TX : 0u));
+            if (!txd)   // (a transcoded document's view record is the transcoding kernel's)
+                S.vrec[d] = make_uint4((uint32_t)t0, (uint32_t)((uint64_t)t0 >> 32), (uint32_t)l0, (uint32_t)l1);
         }
+        ntx += (uint32_t)__popcll(txm);
         // ---- the other documents, one at a time (kw_epi_kernel's per-document code)
         uint64_t slow = __ballot(act && !flat);
         while (slow) {
@@ -1695,6 +1749,16 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
             const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)nc.y, l);
             const uint32_t dfl = (uint32_t)__builtin_amdgcn_readlane((int)fl, l);
             const uint32_t dflags = (uint32_t)__builtin_amdgcn_readlane((int)flags, l);
+            if (TXB && (dfl & (DH_NA0 | DH_NA1))) {   // (no view, or more than 64 items in a field)
+                ++nres;
+                if (lane == 0) {
+                    S.dflags[dd] = dfl | DH_RESOLVE;
+                    const uint32_t i = atomicAdd(S.res_cnt, 1u);
+                    if (i < S.defer_cap) S.res_list[i] = (uint32_t)dd;
+                }
+                wave_sync();
+                continue;
+            }
             if (dfl & (DH_NA0 | DH_NA1)) {
                 bool done = false;
                 if (FK_TX && (n0 > (uint32_t)FK_ITEMS0 || n1 > (uint32_t)FK_ITEMS1) && n0 <= (uint32_t)FK_BIG0 &&

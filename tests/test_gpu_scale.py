@@ -136,6 +136,34 @@ def test_whole_corpus_vs_oracle_digests(bench_scan):
     assert cd.total(dig) == meta['hits_digest'] == bench.hits_digest(b['hits'])
 
 
+def test_transcoded_batches_equal_per_document(bench_scan):
+    """The epilogue batches the transcoded documents with the all-ASCII ones (kw_epi_flat_kernel<true>, KBs
+    without PI_TXUNSAFE names, as here); KW_TEST_EPI_TXB=0 finishes them one wave per document on the same view
+    (the path KBs with such names take).  Same records for every document of the 1M corpus, and the batched
+    documents report the transcode route."""
+    import os
+    from advanced_scrapper_amd import _native
+    from advanced_scrapper_amd.matcher import records_from_tensor
+    from tests import corpus_digest as cd
+    from tests.golden_data import HERE
+    b = bench_scan
+    z = np.load(os.path.join(HERE, 'c2_digests.npz'))
+    n_tx = int((b['routes'] == _native.KW_ROUTE_TRANSCODE).sum())
+    assert n_tx > 100_000
+    os.environ['KW_TEST_EPI_TXB'] = '0'
+    try:
+        b['m'].scan(b['d_arena'], b['d_off'], N_DOCS)
+        rec = records_from_tensor(b['m'].hits_device())
+        routes = b['m'].doc_routes(N_DOCS)
+    finally:
+        del os.environ['KW_TEST_EPI_TXB']
+    dig, cnt = cd.per_doc(rec, N_DOCS)
+    bad = np.flatnonzero((dig != z['digest']) | (cnt != z['count'].astype(np.int64)))
+    assert not len(bad), f'KW_TEST_EPI_TXB=0: {len(bad)} documents differ; first: {bad[:20].tolist()}'
+    # (batched: the documents with a view and <= 64 items a field; the others take the resolve kernel there)
+    assert int((routes == _native.KW_ROUTE_TRANSCODE).sum()) >= n_tx
+
+
 def test_sharded_scans_equal_one_shot(bench_scan):
     import bench
     from advanced_scrapper_amd import dist
