@@ -524,6 +524,8 @@ def pmc_step_traffic(path: str, prefix: str = 'kw', **workload):
     tot = 0.0
     for k, v in j.get('kernels', {}).items():
         name = k.split('(')[0]
+        if name.startswith('void '):   # (a template instance's demangled name carries its return type)
+            name = name[5:]
         if name.startswith(prefix) or name.startswith(prefix.rstrip('_') + '::'):
             # a kernel launched twice a step (the regex tasks' two phases) counts twice
             tot += v['hbm_bytes_per_launch'] * v.get('launches_per_step', 1)

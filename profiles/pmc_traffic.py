@@ -3,7 +3,9 @@
     python profiles/pmc_traffic.py OUT.json FETCH_DIR WRITE_DIR [scans=N] [workload-key=value ...]
 
 scans=N: the passes ran N whole scans each (bench steps + warmup), so each kernel's launches per step are
-its dispatches / N.  The workload keys (bench.py matches them) include the sha256 of the library profiled.
+its dispatches / N; scans=auto:NAME counts the scans as the dispatches of the kernel whose name contains NAME
+(once per scan, rescans included: a warmup scan that grows the scratch runs the kernels again).  The workload
+keys (bench.py matches them) include the sha256 of the library profiled.
 
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (they do not fit one
 TCC pass on gfx950).  Both are in KiB.  The MI355X guide's gfx950 correction is
@@ -34,9 +36,16 @@ def per_kernel(d: str, counter: str):
 def main():
     out, fdir, wdir = sys.argv[1:4]
     extra = dict(a.split('=', 1) for a in sys.argv[4:])
-    scans = int(extra.pop('scans', 0))       # whole scans (steps + warmup) each pass ran: launches per step
+    scans_arg = extra.pop('scans', '0')      # whole scans (steps + warmup) each pass ran: launches per step
     fetch = per_kernel(fdir, 'FETCH_SIZE')
     write = per_kernel(wdir, 'WRITE_SIZE')
+    if scans_arg.startswith('auto:'):
+        name = scans_arg[5:]
+        hits = [max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1]) for k in set(fetch) | set(write) if name in k]
+        assert hits, f'scans=auto: no kernel named like {name}'
+        scans = max(hits)
+    else:
+        scans = int(scans_arg)
     res = {}
     for k in sorted(set(fetch) | set(write)):
         fk, nf = fetch.get(k, (0.0, 0))

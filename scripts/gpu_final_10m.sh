@@ -6,4 +6,5 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 bash scripts/gpu_final_check.sh || exit $?
 timeout -k 10 500 python bench.py --total-docs 10000000 --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/final_c3.log 2>&1 || exit $?
-timeout -k 10 500 python bench.py --workload kb50k --total-docs 10000000 --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/final_c4_10m.log 2>&1
+timeout -k 10 500 python bench.py --workload kb50k --total-docs 10000000 --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/final_c4_10m.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --workload kb50k > gpurun_out/final_c4.log 2>&1

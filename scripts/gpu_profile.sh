@@ -19,7 +19,7 @@ if [ -z "$SKIP_MAIN" ]; then
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$R -o run -- \
       python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/bench_write_$R.log 2>&1 || exit $?
   python3 profiles/pmc_traffic.py gpurun_out/traffic_$R.json gpurun_out/prof_fetch_$R gpurun_out/prof_write_$R \
-      scans=4 docs_per_gpu=1000000 seed=20250905 library_sha256=$LIBSHA > gpurun_out/traffic_$R.log 2>&1 || exit $?
+      scans=auto:kw_filter_kernel docs_per_gpu=1000000 seed=20250905 library_sha256=$LIBSHA > gpurun_out/traffic_$R.log 2>&1 || exit $?
   timeout -k 10 600 python bench.py --traffic-json gpurun_out/traffic_$R.json > gpurun_out/bench_$R.log 2>&1
   echo "rc=$?" >> gpurun_out/bench_$R.log
 fi
@@ -32,7 +32,7 @@ if [ -z "$SKIP_DEDUP" ]; then
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_dedup_$R -o run -- \
       python3 bench.py --workload dedup --steps 1 --warmup 0 --cpu-sample 0 > gpurun_out/bench_write_dedup_$R.log 2>&1 || exit $?
   python3 profiles/pmc_traffic.py gpurun_out/traffic_dedup_$R.json gpurun_out/prof_fetch_dedup_$R gpurun_out/prof_write_dedup_$R \
-      scans=1 rows_per_gpu=500000000 seed=20250905 library_sha256=$LIBSHA > gpurun_out/traffic_dedup_$R.log 2>&1 || exit $?
+      scans=auto:dd_transform_kernel rows_per_gpu=500000000 seed=20250905 library_sha256=$LIBSHA > gpurun_out/traffic_dedup_$R.log 2>&1 || exit $?
   timeout -k 10 600 python bench.py --workload dedup --traffic-json gpurun_out/traffic_dedup_$R.json > gpurun_out/bench_dedup_$R.log 2>&1
   echo "rc=$?" >> gpurun_out/bench_dedup_$R.log
 fi

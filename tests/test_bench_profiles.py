@@ -20,6 +20,11 @@ def test_default_traffic_profiles_resolve():
     assert dd and dd > 40_000_000_000
     step = bench.pmc_step_traffic(bench.TRAFFIC_KW, docs_per_gpu=1_000_000, seed=20250905, library_sha256=kw_sha)
     assert step and step > kw
+    # every kernel of the library counts, template instances included ("void kw::kw_epi_flat_kernel<true>(...)")
+    ks = json.load(open(bench.TRAFFIC_KW))['kernels']
+    want = sum(v['hbm_bytes_per_launch'] * v.get('launches_per_step', 1) for k, v in ks.items() if 'kw::' in k)
+    assert any(k.startswith('void kw::') for k in ks) and step == int(want)
+    assert all(v.get('launches_per_step', 1) in (1.0, 2.0) for k, v in ks.items() if 'kw::' in k)
     c4 = bench.pmc_traffic(bench.TRAFFIC_C4, 'kw_filter_kernel', docs_per_gpu=1_000_000, seed=20250905,
                            workload='kb50k', library_sha256=_sha(bench.TRAFFIC_C4))
     assert c4 and c4 > 2_000_000_000
