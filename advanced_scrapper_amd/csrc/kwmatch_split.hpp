@@ -1663,11 +1663,19 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
         for (int f = 0; f < 2; ++f) {
             const int64_t lf = f ? (int64_t)c1 : (int64_t)c0;
             bool sh = flat && lf <= (int64_t)MAXM;
-            // (a transcoded document's short field takes its task untested: a superset, the short kernel decides)
-            if (EPI_SHORT_PREF && sh && !txd && lf > (int64_t)SHORT_EXACT_MAX) {
+            if (EPI_SHORT_PREF && sh && lf > (int64_t)SHORT_EXACT_MAX) {
                 const uint32_t n = (uint32_t)lf, cnt = (uint32_t)FT.f_count_ge[n];
                 if (cnt <= (uint32_t)WAVE) {
-                    const int64_t fb = f ? t1 : t0, a0 = fb & ~(int64_t)3;
+                    // (a transcoded document's field: its view bytes; the reads past the field stay in tarena's
+                    // document record or its 64-byte tail)
+                    int64_t fb = f ? t1 : t0;
+                    const uint8_t *fa = arena;
+                    if (txd) {
+                        const uint4 Vs = S.vrec[d];
+                        fb = (int64_t)(((uint64_t)(Vs.y & 0x7FFFFFFFu) << 32) | Vs.x) + (f ? (int64_t)Vs.z : 0);
+                        fa = S.tarena;
+                    }
+                    const int64_t a0 = fb & ~(int64_t)3;
                     const uint32_t sh0 = (uint32_t)(fb - a0);
                     // the field's <= 67 bytes as dwords loaded six at a time (three round trips, not one per dword;
                     // the arena is padded; more at once spills the epilogue's registers), then the names'
@@ -1676,7 +1684,7 @@ __global__ __launch_bounds__(EK_BLOCK, EK_MINW) void kw_epi_flat_kernel(FastTabl
                     for (uint32_t w0 = 0; 4 * w0 < n + sh0; w0 += 6) {
                         uint32_t xw[6];
 #pragma unroll
-                        for (int w = 0; w < 6; ++w) xw[w] = *(const uint32_t *)(arena + a0 + 4 * (w0 + (uint32_t)w));
+                        for (int w = 0; w < 6; ++w) xw[w] = *(const uint32_t *)(fa + a0 + 4 * (w0 + (uint32_t)w));
 #pragma unroll
                         for (int w = 0; w < 6; ++w) {
 #pragma unroll
