@@ -26,6 +26,9 @@
 #define VK_U 8
 #endif
 // task kernels' minimum waves per SIMD (register budget: 4 -> 128 VGPRs, 5 -> 102, 6 -> 84, 8 -> 64)
+#ifndef VK_PRETEST
+#define VK_PRETEST 1   // the verify kernel's band-test pretest with a queue of the tasks it cannot rule out
+#endif
 #ifndef VK_MINW
 #define VK_MINW 4
 #endif
@@ -1451,6 +1454,35 @@ __device__ uint32_t lv_band(const uint8_t *__restrict__ arena, int64_t fb, uint3
     return pmax >= pmin ? (uint32_t)(pmax - pmin + 1) : 0u;
 }
 
+// The band test on the name's first 16 bytes alone (m > 16): those bytes matched within +-2k of their aligned text
+// bytes must number >= 16 - k, or the whole test fails (the other m - 16 bytes can add at most m - 16).  Stages
+// only the window's first dwords.  A task failing it has no full window to evaluate.
+__device__ bool lv_pretest(const uint8_t *__restrict__ arena, int64_t fb, uint32_t n, uint64_t w0, uint64_t w1,
+                           int64_t base, uint32_t k, uint32_t *win)
+{
+    const int64_t lo = base - 2 * (int64_t)k;
+    const int64_t A = (fb + lo) & ~(int64_t)3;
+    const int64_t fe = fb + n;
+    const int nd = (int)((4 * k + 3 + 16 + 7) / 4) + 1;   // dwords the shifts read (<= 12 for k <= 3)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        if (j >= nd) break;
+        const int64_t ad = A + 4 * j;
+        uint32_t x = (ad + 4 > fb && ad < fe) ? *(const uint32_t *)(arena + ad) : 0u;
+        if (ad < fb) x &= ~0u << (8 * (uint32_t)(fb - ad) & 31u);
+        if (ad + 4 > fe) x &= fe > ad ? ~(~0u << (8 * (uint32_t)(fe - ad) & 31u)) : 0u;
+        win[j] = x;
+    }
+    uint64_t h0 = 0, h1 = 0;
+    const int64_t d0 = fb + base - A;
+    for (int t = -2 * (int)k; t <= 2 * (int)k; ++t) {
+        h0 |= zb64(lv_text8(win, d0 + t) ^ w0);
+        h1 |= zb64(lv_text8(win, d0 + 8 + t) ^ w1);
+    }
+    const uint32_t cnt = (uint32_t)__popcll(hb8(h0)) + (uint32_t)__popcll(hb8(h1));
+    return cnt + k >= 16u;
+}
+
 // regex-class names decided in the task kernels -> the region's regex queue (xq), lane-parallel;
 // several waves may append to one region (atomic count)
 struct XPush {
@@ -1551,6 +1583,7 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
     __shared__ uint32_t lvwin_all[RK_BLOCK * LV_WIN];
     __shared__ uint16_t jobs_all[RK_BLOCK * LV_MAXJ];
     __shared__ uint32_t okf_all[RK_BLOCK];
+    __shared__ uint32_t vsel_all[RK_BLOCK * 2];   // per wave: a ring of 128 task indices that passed the pretest
     const int lane = lane_id();
     const int wib = threadIdx.x / WAVE;
     const int64_t gw = (int64_t)blockIdx.x * RK_WAVES + wib;   // G waves per region
@@ -1565,9 +1598,8 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
     unsigned long long nver = 0, nwin = 0, nver_w = 0, nwin_w = 0;
     const uint32_t nv = min(S.vcnt[t], S.vcap);
     const uint4 *vq = S.vq + (size_t)t * S.vcap;
-    for (uint32_t k0 = sub * WAVE; k0 < nv; k0 += (uint32_t)G * WAVE) {
-        const uint32_t kk = k0 + (uint32_t)lane;
-        const bool valid = kk < nv;
+    uint32_t *vsel = vsel_all + wib * 2 * WAVE;
+    auto run = [&](uint32_t kk, bool valid) {
         const uint4 tk = valid ? vq[kk] : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t doc = tk.x, P = tk.y >> 1, field = tk.y & 1u;
         const bool todo = valid && !dset_contains(S, dset_key(doc, P, field));
@@ -1702,7 +1734,59 @@ __global__ __launch_bounds__(RK_BLOCK, VK_MINW) void kw_verify_kernel(FastTables
         const bool rx = first && FT.pat_rxk[P] == RXK_REGEX;
         emit_hits(O, GS, first && !rx, doc, P, KW_NOPOS, field);
         xq_push(X, rx, doc, P, field);
+    };
+#if VK_PRETEST
+    // the tasks 64 at a time through the pretest; the ones it cannot rule out queue up and run the full test (and
+    // their window jobs) 64 at a time, so those rounds run on full waves (~90 % of the tasks fail the band test)
+    uint32_t qh = 0, qn = 0;
+    for (uint32_t k0 = sub * WAVE; k0 < nv; k0 += (uint32_t)G * WAVE) {
+        const uint32_t kk = k0 + (uint32_t)lane;
+        bool keep = kk < nv;
+        if (keep) {
+            const uint4 tk = vq[kk];
+            const uint32_t P = tk.y >> 1, field = tk.y & 1u;
+            const uint32_t pi = FT.pat_info[P];
+            const uint32_t m = pi_m(pi);
+            if ((pi & PI_ASCII) != 0) {
+                const uint4 v = S.vrec[tk.x];
+                const bool tx = (v.y >> 31) != 0;
+                const int64_t fb = (int64_t)(((uint64_t)(v.y & 0x7FFFFFFFu) << 32) | v.x) + (field ? (int64_t)v.z : 0);
+                const uint32_t n = field ? v.w : v.z;
+                const uint32_t q = tk.z, o = tk.w & 0xFFu, pl = (tk.w >> 8) & 0xFFu;
+                const uint32_t k = kfull(m);
+                // (a prefix or suffix job runs whatever the band test says; k = 0: no full window at all, m <= 20)
+                if (q + pl + 1 > m && q + m <= n) {
+                    if (k == 0) {
+                        keep = false;
+                    } else if (m > 16u) {
+                        const int64_t nb = FT.pat_boff[P];
+                        keep = lv_pretest(tx ? S.tarena : arena, fb, n, load8(FT.pat_bytes, nb),
+                                          load8(FT.pat_bytes, nb + 8), (int64_t)q - (int64_t)o, k, win);
+                    }
+                    if (!keep) ++nver;   // (verified: no full window passes)
+                }
+            }
+        }
+        const uint64_t km = __ballot(keep);
+        wave_sync();
+        if (keep) vsel[(qh + qn + mbcnt(km)) & (2u * WAVE - 1u)] = kk;
+        qn += (uint32_t)__popcll(km);
+        wave_sync();
+        if (qn >= (uint32_t)WAVE) {
+            const uint32_t kq = vsel[(qh + (uint32_t)lane) & (2u * WAVE - 1u)];
+            qh = (qh + WAVE) & (2u * WAVE - 1u);
+            qn -= WAVE;
+            run(kq, true);
+        }
     }
+    if (qn) {
+        wave_sync();
+        const uint32_t kq = vsel[(qh + (uint32_t)lane) & (2u * WAVE - 1u)];
+        run(kq, (uint32_t)lane < qn);
+    }
+#else
+    for (uint32_t k0 = sub * WAVE; k0 < nv; k0 += (uint32_t)G * WAVE) run(k0 + (uint32_t)lane, k0 + (uint32_t)lane < nv);
+#endif
     task_stats(S, wave_sum64(nver) + nver_w, wave_sum64(nwin) + nwin_w, 0, 0, 0, 0);
 }
 
